@@ -1,0 +1,302 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X.
+
+metric : device-resident GiB/s, float32 FI_SUM reduce, 256 MiB buffers
+step   : one pass of the hot path — ofi_atomic_write_handler(FI_SUM, FI_FLOAT,
+         dst, src, 67,108,864) (prov/coll/src/coll_coll.c:763) — over one
+         256 MiB (dst, src) pair already resident in HBM, launched through the
+         C ABI (lfa_atomic_write_async, liblfa.so).
+value  : whole-job traffic rate, 3·S bytes per step (read dst, read src,
+         write dst) × steps × ranks ÷ the max-over-ranks wall time, in GiB/s.
+         The buffer rate S/t is reported beside it.
+N > 1  : one process per GPU, each rank combines its own 256 MiB buckets (the
+         bucket reduction shards with no data-path exchange): weak scaling.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel (combine_vec<SUM,float>): algorithmic bytes per
+                launch (3·S) ÷ its average duration from HIP events on the
+                launch stream; peak 8.0 TB/s (MI355X HBM3E spec); ``traffic``
+                from the committed rocprofv3 PMC pass (profiles/) when present.
+  cpu_baseline  rank 0, N=1 only: the reference combine on 1 pinned host core,
+                same shape (256 MiB float SUM), median of a bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu]
+       python bench.py --tune      # kernel-variant sweep (dev tool)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+S_BYTES = 256 * 1024 * 1024            # BASELINE config 2: 256 MiB buffers
+COUNT = S_BYTES // 4                   # 67,108,864 float
+BUFFER_SETS = 4                        # rotate: 2 GiB of inputs >> 256 MiB MALL
+PEAK_GBPS = 8000.0                     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FI_SUM, FI_FLOAT = 2, 8
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def init_dist(n_gpus: int):
+    if n_gpus > 1 or "RANK" in os.environ:
+        rank = int(os.environ.get("RANK", 0))
+        world = int(os.environ.get("WORLD_SIZE", 1))
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+        return rank, world, local
+    torch.cuda.set_device(0)
+    return 0, 1, 0
+
+
+def barrier(world: int) -> None:
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_buffers(dev, seed: int):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    sets = []
+    for _ in range(BUFFER_SETS):
+        src = torch.rand(COUNT, device=dev, generator=g) * 2 - 1
+        dst = torch.rand(COUNT, device=dev, generator=g) * 2 - 1
+        sets.append((dst, src))
+    return sets
+
+
+def read_traffic():
+    """Per-launch HBM bytes of the headline kernel from the committed PMC pass."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def cpu_baseline(sample_reps: int = 5):
+    """The reference combine timed on ONE pinned host core (rank 0, N=1).
+
+    Primary: our restatement of the shipping HAVE_BUILTIN_MM_ATOMICS handler
+    (per-element seq_cst CAS, util_atomic.c:266-289) — kind "port".  Beside
+    it: the open-coded variant (util_atomic.c:119-153) and the reference's own
+    fabtests restatement compiled from /root/reference (oracle/_ref).
+    """
+    import numpy as np
+    import oracle
+
+    rng = np.random.default_rng(1)
+    src = rng.uniform(-1, 1, COUNT).astype(np.float32)
+    dst0 = rng.uniform(-1, 1, COUNT).astype(np.float32)
+    dst = dst0.copy()
+    try:
+        prev = os.sched_getaffinity(0)
+        core = sorted(prev)[-1]
+        os.sched_setaffinity(0, {core})
+    except (AttributeError, OSError):
+        prev, core = None, None
+
+    def timeit(fn):
+        ts = []
+        for _ in range(sample_reps):
+            dst[:] = dst0
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    res = {}
+    try:
+        res["cas"] = timeit(lambda: oracle.write(FI_SUM, FI_FLOAT, dst, src, oracle.CAS))
+        res["plain"] = timeit(lambda: oracle.write(FI_SUM, FI_FLOAT, dst, src, oracle.PLAIN))
+        if oracle.ref_available():
+            res["ref"] = timeit(lambda: oracle.ref_write(FI_SUM, FI_FLOAT, dst, src))
+    finally:
+        if prev is not None:
+            os.sched_setaffinity(0, prev)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+
+    def gib(t):
+        return round(3 * S_BYTES / t / 2**30, 3)
+
+    out = {
+        "value": gib(res["cas"]), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": (f"256 MiB float FI_SUM combine (67,108,864 elements), median of "
+                   f"{sample_reps} runs, 1 pinned core (cpu {core}) of {os.cpu_count()} "
+                   f"({cpu}); shipping CAS handler restated in oracle/"),
+        "ms_per_combine": round(res["cas"] * 1e3, 2),
+        "plain_loop": {"value": gib(res["plain"]), "kind": "port",
+                       "ms_per_combine": round(res["plain"] * 1e3, 2)},
+    }
+    if "ref" in res:
+        out["reference_fabtests"] = {
+            "value": gib(res["ref"]), "kind": "reference",
+            "ms_per_combine": round(res["ref"] * 1e3, 2),
+            "what": "fabtests/common/ofi_atomic.c plain loop, built from /root/reference"}
+    return out
+
+
+def tune(args) -> None:
+    """Interleaved A/B of the combine_vec variants (guide §5.4 rule 24)."""
+    from libfabric_amd import _native
+    L = _native.lib()
+    torch.cuda.set_device(0)
+    sets = make_buffers("cuda", 7)
+    stream = torch.cuda.current_stream()
+    h = stream.cuda_stream
+    nvec = COUNT // 4
+    variants = list(range(12))
+    times = {v: [] for v in variants}
+    for _ in range(3):
+        for v in variants:
+            for i in range(4):
+                d, s = sets[i % BUFFER_SETS]
+                assert L.lfa__tune_sum_f32(v, d.data_ptr(), s.data_ptr(), nvec, h) == 0
+    torch.cuda.synchronize()
+    for rnd in range(args.tune_rounds):
+        for v in variants:
+            evs = [(torch.cuda.Event(enable_timing=True),
+                    torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+            for i, (a, b) in enumerate(evs):
+                d, s = sets[i % BUFFER_SETS]
+                a.record(stream)
+                L.lfa__tune_sum_f32(v, d.data_ptr(), s.data_ptr(), nvec, h)
+                b.record(stream)
+            torch.cuda.synchronize()
+            times[v].extend(a.elapsed_time(b) for a, b in evs)
+    rows = []
+    for v in variants:
+        ms = statistics.median(times[v])
+        rows.append({"variant": v, "median_us": round(ms * 1e3, 2),
+                     "min_us": round(min(times[v]) * 1e3, 2),
+                     "tbps": round(3 * S_BYTES / (ms * 1e-3) / 1e12, 3),
+                     "frac": round(3 * S_BYTES / (ms * 1e-3) / 1e9 / PEAK_GBPS, 4)})
+    print(json.dumps({"tune": rows}))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--tune-rounds", type=int, default=10)
+    args = ap.parse_args()
+
+    if args.tune:
+        tune(args)
+        return
+
+    rank, world, local = init_dist(args.gpus)
+    from libfabric_amd import atomic, lib
+    lib()  # no fallback: raises if liblfa.so is missing
+    dev = torch.device("cuda", local)
+    sets = make_buffers(dev, 1000 + rank)
+    stream = torch.cuda.current_stream()
+
+    def step(i):
+        d, s = sets[i % BUFFER_SETS]
+        atomic.write(FI_SUM, FI_FLOAT, d, s, COUNT, stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # kernel-duration events: one pair per launch, on the launch stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step(i)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(t1 - t0, world)
+    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    kern_ms = max_over_ranks(kern_ms, world)
+
+    total_bytes = 3 * S_BYTES * args.steps * world
+    value = total_bytes / elapsed / 2**30
+    achieved = 3 * S_BYTES / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = read_traffic()
+
+    line = {
+        "metric": "device-resident GiB/s, float32 FI_SUM reduce, 256 MiB buffers",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (uniform[-1,1) float32, torch.Generator seeds 1000+rank)",
+        "config": {
+            "workload": "float32 FI_SUM local combine, 256 MiB device-resident per GPU "
+                        "(BASELINE.json configs[1]); dst += src through "
+                        "lfa_atomic_write_async",
+            "count": COUNT, "buffer_bytes": S_BYTES, "buffer_sets": BUFFER_SETS,
+            "bytes_per_step_per_gpu": 3 * S_BYTES,
+            "buffer_rate_gib_s": round(S_BYTES * args.steps * world / elapsed / 2**30, 2),
+            "parallelism": f"shard{world} (independent buckets per GPU, no exchange)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / PEAK_GBPS, 4),
+            "traffic": traffic,
+            "kernel": "combine_vec<FI_SUM,float,U=4,nt,nt>",
+            "kernel_us": round(kern_ms * 1e3, 2),
+            "algorithmic_bytes_per_launch": 3 * S_BYTES,
+            "traffic_source": traffic_src,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

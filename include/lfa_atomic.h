@@ -1,0 +1,79 @@
+/*
+ * lfa_atomic.h — C ABI of the MI355X combine kernels (liblfa.so).
+ *
+ * Drop-in for libfabric's element-wise combine tables, the L4 layer that
+ * prov/coll's REDUCE work items call (prov/coll/src/coll_coll.c:758-768):
+ *
+ *   lfa_datatype_size()          replaces ofi_datatype_size()
+ *                                  prov/util/src/util_atomic.c:58-64,
+ *                                  include/ofi_atomic.h:45
+ *   lfa_atomic_valid()           replaces ofi_atomic_valid() (write table)
+ *                                  prov/util/src/util_atomic.c:1088-1140
+ *   lfa_atomic_write_handlers    replaces ofi_atomic_write_handlers[op][dt]
+ *                                  prov/util/src/util_atomic.c:907-922,
+ *                                  include/ofi_atomic.h:73-82
+ *                                (same signature; dst/src are DEVICE
+ *                                 pointers; synchronous on the null stream)
+ *   lfa_atomic_write_async()     the GPU form: same semantics, enqueued on a
+ *                                  HIP stream, returns 0 / negative errno
+ *   lfa_reduce_tree_async()      N-input fused combine in prov/coll's
+ *                                  recursive-doubling association order
+ *                                  (coll_coll.c:349-449), one pass over HBM
+ *
+ * Semantics are the shipping (HAVE_BUILTIN_MM_ATOMICS) table's, bit-exact:
+ * dst-biased MIN/MAX, wrapping integer SUM/PROD, IEEE float/double with no
+ * denormal flush, 0/1 logical results, bitwise ops on integers only, int128
+ * columns as built with HAVE_BUILTIN_MM_INT128_ATOMICS.
+ *
+ * Buffers: any alignment (16-byte co-aligned buffers take the vector path),
+ * dst updated in place, src read-only, no allocation.  Streams are passed as
+ * `void *` (a hipStream_t; NULL = the null stream), so this header needs no
+ * HIP include.
+ */
+#ifndef LFA_ATOMIC_H
+#define LFA_ATOMIC_H
+
+#include "lfa_fabric.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void (*lfa_write_fn)(void *dst, const void *src, size_t cnt);
+
+/* 0 and errno = EINVAL for datatype >= LFA_DATATYPE_CNT. */
+size_t lfa_datatype_size(enum lfa_datatype datatype);
+
+/* 0, -LFA_EOPNOTSUPP, -LFA_EBADFLAGS or -LFA_ENOSYS, as ofi_atomic_valid. */
+int lfa_atomic_valid(enum lfa_datatype datatype, enum lfa_op op, uint64_t flags);
+
+/* Synchronous table form: [op][datatype], NULL where unsupported. */
+extern lfa_write_fn const lfa_atomic_write_handlers[LFA_WRITE_OP_CNT][LFA_DATATYPE_CNT];
+
+/*
+ * dst[i] = dst[i] OP src[i] for i < cnt, on `stream`.
+ * Returns 0, -LFA_EOPNOTSUPP (no handler), -LFA_EINVAL (bad pointer/args),
+ * -LFA_EIO (launch failure).
+ */
+int lfa_atomic_write_async(enum lfa_op op, enum lfa_datatype datatype,
+			   void *dst, const void *src, size_t cnt, void *stream);
+
+/*
+ * dst[i] = tree(srcs[0][i], …, srcs[nsrc-1][i]) where tree is prov/coll's
+ * recursive-doubling association for nsrc ranks (every pairwise step is
+ * `higher-rank partial OP lower-rank partial`).  `srcs` is a HOST array of
+ * DEVICE pointers; dst may alias any srcs[k].  1 <= nsrc <= LFA_TREE_MAX.
+ */
+#define LFA_TREE_MAX 32
+int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype datatype,
+			  void *dst, const void *const *srcs, int nsrc,
+			  size_t cnt, void *stream);
+
+/* Version string of the kernel library (build id, target arch). */
+const char *lfa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LFA_ATOMIC_H */

@@ -1,0 +1,61 @@
+"""ctypes binding of the native libraries.  Fails loudly when missing.
+
+``import torch`` happens first on purpose: torch bundles its own
+libamdhip64.so / librccl.so with the same SONAMEs as /opt/rocm's.  Loading
+torch first makes liblfa*.so bind to the already-loaded runtime, so device
+pointers from torch's allocator and our kernels share one HIP context.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL loads below)
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+_LIBS = {"lfa": "liblfa.so", "coll": "liblfa_coll.so"}
+_loaded = {}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib_path(name: str = "lfa") -> str:
+    return os.path.join(PKG, _LIBS[name])
+
+
+def _bind_lfa(L):
+    c_int, c_size_t, c_void_p, c_uint64 = (ctypes.c_int, ctypes.c_size_t,
+                                           ctypes.c_void_p, ctypes.c_uint64)
+    L.lfa_datatype_size.restype = c_size_t
+    L.lfa_datatype_size.argtypes = [c_int]
+    L.lfa_atomic_valid.restype = c_int
+    L.lfa_atomic_valid.argtypes = [c_int, c_int, c_uint64]
+    L.lfa_atomic_write_async.restype = c_int
+    L.lfa_atomic_write_async.argtypes = [c_int, c_int, c_void_p, c_void_p,
+                                         c_size_t, c_void_p]
+    L.lfa_reduce_tree_async.restype = c_int
+    L.lfa_reduce_tree_async.argtypes = [c_int, c_int, c_void_p,
+                                        ctypes.POINTER(c_void_p), c_int,
+                                        c_size_t, c_void_p]
+    L.lfa_version.restype = ctypes.c_char_p
+    L.lfa__tune_sum_f32.restype = c_int
+    L.lfa__tune_sum_f32.argtypes = [c_int, c_void_p, c_void_p, c_size_t,
+                                    c_void_p]
+
+
+def lib(name: str = "lfa") -> ctypes.CDLL:
+    """The loaded native library; raises NativeLibraryMissing if not built."""
+    if name in _loaded:
+        return _loaded[name]
+    path = lib_path(name)
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} is not built: run `python -m libfabric_amd.build` "
+            "(there is no CPU fallback for the combine path)")
+    if name == "coll":
+        lib("lfa")
+    L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    if name == "lfa":
+        _bind_lfa(L)
+    _loaded[name] = L
+    return L

@@ -1,0 +1,106 @@
+"""Tensor-level access to the gfx950 combine kernels (liblfa.so).
+
+Mirrors the reference's L4 combine interface (include/ofi_atomic.h:45-90):
+
+  datatype_size(dt)                 ofi_datatype_size        util_atomic.c:58
+  atomic_valid(dt, op, flags)       ofi_atomic_valid         util_atomic.c:1088
+  write_handler(op, dt)             ofi_atomic_write_handlers[op][dt]
+  write(op, dt, dst, src, cnt)      ofi_atomic_write_handler(op, dt, dst, src, cnt)
+                                    — asynchronous on a HIP stream
+  reduce_tree(op, dt, dst, srcs)    prov/coll's log2(N) REDUCE items fused into
+                                    one pass (coll_coll.c:349-449 order)
+
+Tensors are raw device storage: ``dt`` says how the bytes are interpreted,
+``cnt`` defaults to ``dst.nbytes // datatype_size(dt)``.  Errors raise
+``LfaError`` carrying the negative errno the C ABI returned.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._native import lib
+from .enums import DT, OP
+
+LFA_EOPNOTSUPP = 95
+LFA_EINVAL = 22
+
+
+class LfaError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} failed: {rc}")
+        self.rc = rc
+
+
+def datatype_size(dt: int) -> int:
+    return int(lib().lfa_datatype_size(int(dt)))
+
+
+def atomic_valid(dt: int, op: int, flags: int = 0) -> int:
+    return int(lib().lfa_atomic_valid(int(dt), int(op), int(flags)))
+
+
+_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
+def write_handler(op: int, dt: int):
+    """The synchronous table entry lfa_atomic_write_handlers[op][dt] or None."""
+    tbl = (ctypes.c_void_p * (12 * 16)).in_dll(lib(), "lfa_atomic_write_handlers")
+    p = tbl[int(op) * 16 + int(dt)]
+    return _FN(p) if p else None
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _check_dev(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def write(op: int, dt: int, dst: torch.Tensor, src: torch.Tensor,
+          cnt: int | None = None, stream=None) -> None:
+    """dst[i] = dst[i] OP src[i] on the GPU (enqueued, not waited for)."""
+    _check_dev(dst, "dst")
+    _check_dev(src, "src")
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    if cnt * esz > dst.nbytes or cnt * esz > src.nbytes:
+        raise ValueError("cnt exceeds buffer size")
+    rc = lib().lfa_atomic_write_async(int(op), int(dt), dst.data_ptr(),
+                                      src.data_ptr(), cnt,
+                                      _stream_handle(stream))
+    if rc:
+        raise LfaError(rc, f"lfa_atomic_write_async({OP(op).name},{DT(dt).name})")
+
+
+def write_ptr(op: int, dt: int, dst: int, src: int, cnt: int,
+              stream=None) -> int:
+    """Raw-pointer form (returns the C return code)."""
+    return int(lib().lfa_atomic_write_async(int(op), int(dt), dst, src, cnt,
+                                            _stream_handle(stream)))
+
+
+def reduce_tree(op: int, dt: int, dst: torch.Tensor, srcs: list[torch.Tensor],
+                cnt: int | None = None, stream=None) -> None:
+    """dst = recursive-doubling tree of srcs (rank order = list order)."""
+    _check_dev(dst, "dst")
+    for i, s in enumerate(srcs):
+        _check_dev(s, f"srcs[{i}]")
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    if any(cnt * esz > s.nbytes for s in srcs) or cnt * esz > dst.nbytes:
+        raise ValueError("cnt exceeds buffer size")
+    arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    rc = lib().lfa_reduce_tree_async(int(op), int(dt), dst.data_ptr(), arr,
+                                     len(srcs), cnt, _stream_handle(stream))
+    if rc:
+        raise LfaError(rc, f"lfa_reduce_tree_async({OP(op).name},{DT(dt).name})")

@@ -1,0 +1,107 @@
+"""Build the in-tree native libraries for gfx950.
+
+  libfabric_amd/liblfa.so       combine kernels + C ABI (include/lfa_atomic.h)
+  libfabric_amd/liblfa_coll.so  C host provider (include/lfa_coll.h), links
+                                liblfa.so + RCCL
+
+hipcc cross-compiles gfx950 without a GPU.  Objects are cached under
+build/ by source mtime; the kernel file is compiled once per write op in
+parallel (-DLFA_OP=<op>).  Run:  python -m libfabric_amd.build
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+BUILD = os.path.join(ROOT, "build", "lfa")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+WRITE_OPS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]
+
+HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fPIC",
+             "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + INC]
+
+LIB_LFA = os.path.join(PKG, "liblfa.so")
+LIB_COLL = os.path.join(PKG, "liblfa_coll.so")
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} … {cmd[-1]}")
+
+
+def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    kern = os.path.join(CSRC, "lfa_combine.hip")
+    hdrs = [os.path.join(CSRC, "lfa_ops.hpp"), os.path.join(INC, "lfa_atomic.h"),
+            os.path.join(INC, "lfa_fabric.h")]
+    steps = []
+    objs = []
+    for op in WRITE_OPS:
+        o = os.path.join(BUILD, f"combine_op{op}.o")
+        objs.append(o)
+        if _newer(o, [kern] + hdrs):
+            steps.append([HIPCC, *HIP_FLAGS, f"-DLFA_OP={op}", "-c", kern, "-o", o])
+    capi = os.path.join(CSRC, "lfa_capi.cpp")
+    o = os.path.join(BUILD, "lfa_capi.o")
+    objs.append(o)
+    if _newer(o, [capi] + hdrs):
+        # host-only C++ (hipcc would compile .cpp as HIP): g++ + HIP C API
+        steps.append(["g++", "-O2", "-fPIC", "-std=c++17", "-Wall",
+                      "-D__HIP_PLATFORM_AMD__", "-I" + INC,
+                      "-I" + os.path.join(ROCM, "include"), "-c", capi, "-o", o])
+    if steps:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for f in [ex.submit(_run, s) for s in steps]:
+                f.result()
+    if steps or _newer(LIB_LFA, objs):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_LFA,
+              *objs, "-Wl,-soname,liblfa.so"])
+    if verbose:
+        print(f"built {LIB_LFA} ({len(steps)} objects recompiled)")
+    return LIB_LFA
+
+
+def build_coll(verbose: bool = False) -> str | None:
+    src = os.path.join(CSRC, "lfa_coll.c")
+    if not os.path.exists(src):
+        return None
+    hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "lfa_atomic.h"),
+            os.path.join(INC, "lfa_fabric.h"), LIB_LFA]
+    if _newer(LIB_COLL, [src] + hdrs):
+        # Plain C (the reference's host language), calling HIP's and RCCL's
+        # C APIs; no HIP device code in this library.
+        _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
+              "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__", "-I" + INC,
+              "-I" + os.path.join(ROCM, "include"), "-shared", "-o", LIB_COLL, src,
+              "-L" + PKG, "-llfa", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64",
+              "-lrccl", "-lpthread", "-Wl,-rpath,$ORIGIN",
+              "-Wl,-soname,liblfa_coll.so"])
+        if verbose:
+            print(f"built {LIB_COLL}")
+    return LIB_COLL
+
+
+def build_all(verbose: bool = False) -> None:
+    build_lfa(verbose=verbose)
+    build_coll(verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True)

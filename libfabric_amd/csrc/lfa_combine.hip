@@ -1,0 +1,453 @@
+// lfa_combine.hip — MI355X (gfx950) combine kernels + their C ABI (liblfa.so).
+//
+// What runs on the GPU for libfabric's L4 combine layer
+// (ofi_atomic_write_handlers, prov/util/src/util_atomic.c:907-922, called by
+// prov/coll's REDUCE items, prov/coll/src/coll_coll.c:758-768):
+//
+//   combine_vec    dst[i] = dst[i] OP src[i] over 16-byte vectors.  The work is a
+//                  pure HBM stream (2 reads + 1 write per element, ~0.1 flop/B):
+//                  no MFMA, no LDS — the roofline is HBM.  Each
+//                  thread keeps UNROLL independent 16-B loads of each operand in
+//                  flight; each workgroup sweeps one contiguous chunk so every
+//                  wave-instruction touches 1 KiB of consecutive bytes.
+//   combine_elem   the same op for misaligned heads/tails and for buffers that
+//                  are not co-aligned mod 16 (one element per lane, coalesced).
+//   reduce_tree    N inputs → 1 output in ONE pass, in prov/coll's
+//                  recursive-doubling association order (coll_coll.c:349-449):
+//                  replaces log2(N) pairwise REDUCE+COPY items, traffic
+//                  (N+1)·S instead of ~3·log2(N)·S.
+//
+// Semantics: lfa_ops.hpp.  Build: hipcc --offload-arch=gfx950 -O3
+// -ffp-contract=off -DLFA_OP=<op> (see libfabric_amd/build.py).
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <type_traits>
+
+#include "lfa_ops.hpp"
+#include "../../include/lfa_atomic.h"
+
+namespace lfa {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// memory access helpers
+// ---------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// OP applied lane-wise to the 16/sizeof(T) elements packed in a 16-B vector.
+template <int OP, typename T>
+__device__ __forceinline__ u32x4 apply_vec(u32x4 d, u32x4 s) {
+  constexpr int N = 16 / sizeof(T);
+  T a[N], b[N];
+  __builtin_memcpy(a, &d, 16);
+  __builtin_memcpy(b, &s, 16);
+#pragma unroll
+  for (int i = 0; i < N; i++) a[i] = apply<OP, T>(a[i], b[i]);
+  u32x4 r;
+  __builtin_memcpy(&r, a, 16);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// binary combine, vector body
+// ---------------------------------------------------------------------------
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// Chunked: workgroup b owns vectors [b·kBlock·U, (b+1)·kBlock·U); step u of
+// thread t touches base + u·kBlock + t, i.e. each wave-instruction reads 1 KiB
+// of consecutive bytes.  All 2·U loads issue before the first op.
+template <int OP, typename T, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void combine_vec(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+  if (base + (size_t)(U - 1) * kBlock < nvec) {  // full chunk: no guards
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<NTL>(dst + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++) b[u] = ld<NTL>(src + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<NTS>(dst + base + u * kBlock, apply_vec<OP, T>(a[u], b[u]));
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec)
+        st<NTS>(dst + i, apply_vec<OP, T>(ld<NTL>(dst + i), ld<NTL>(src + i)));
+    }
+  }
+}
+
+// Grid-stride variant (for the tuning sweep): a fixed grid of G workgroups
+// walks the buffer; each thread holds U vectors spaced kBlock apart.
+template <int OP, typename T, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void combine_vec_gs(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  const size_t step = (size_t)gridDim.x * kBlock * U;
+  size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+  for (; base + (size_t)(U - 1) * kBlock < nvec; base += step) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<NTL>(dst + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++) b[u] = ld<NTL>(src + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<NTS>(dst + base + u * kBlock, apply_vec<OP, T>(a[u], b[u]));
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec)
+      st<NTS>(dst + i, apply_vec<OP, T>(ld<NTL>(dst + i), ld<NTL>(src + i)));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// binary combine, element-wise (heads, tails, non-co-aligned buffers)
+// ---------------------------------------------------------------------------
+// Up to two index ranges [0, n0) and [off1, off1 + n1) in one launch, so a
+// misaligned head and tail cost a single extra dispatch.
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void combine_elem(
+    T *__restrict__ dst, const T *__restrict__ src, size_t n0, size_t off1,
+    size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    dst[k] = apply<OP, T>(dst[k], src[k]);
+  }
+}
+
+// Element pointers not even aligned to sizeof(T): byte-wise access.
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void combine_unaligned(
+    unsigned char *dst, const unsigned char *src, size_t n) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n; i += stride) {
+    T a, b;
+    __builtin_memcpy(&a, dst + i * sizeof(T), sizeof(T));
+    __builtin_memcpy(&b, src + i * sizeof(T), sizeof(T));
+    a = apply<OP, T>(a, b);
+    __builtin_memcpy(dst + i * sizeof(T), &a, sizeof(T));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// N-input tree reduction in recursive-doubling order
+// ---------------------------------------------------------------------------
+// Leaf k (k < nleaf, nleaf = largest power of two <= nsrc) is either a pair
+// (in[hi] OP in[lo]) — the non-power-of-two pre-step, coll_coll.c:366-389 —
+// or a single input.  Leaves are then combined pairwise, higher-index
+// partial OP lower-index partial, level by level (coll_coll.c:392-433).
+// The kernel evaluates that tree with a stack: push leaves left to right and
+// merge the two top entries while they cover equal-size groups, so only
+// log2(nleaf)+1 partials are live per element.
+constexpr int kMaxLeaf = 16;
+
+struct TreeArgs {
+  const void *in[2 * kMaxLeaf];
+  signed char hi[kMaxLeaf];  // input index of the leaf's (higher-rank) value
+  signed char lo[kMaxLeaf];  // paired lower-rank input, or -1
+};
+
+template <int OP, typename T, typename V>
+__device__ __forceinline__ V apply_any(V d, V s) {
+  if constexpr (sizeof(V) == 16 && sizeof(T) <= 16 && !__is_same(V, T))
+    return apply_vec<OP, T>(d, s);
+  else
+    return apply<OP, T>(d, s);
+}
+
+template <int OP, typename T, typename V, int NLEAF>
+__device__ __forceinline__ V tree_eval(const TreeArgs &a, size_t i) {
+  V stack[6];
+  int depth = 0;
+#pragma unroll
+  for (int k = 0; k < NLEAF; k++) {
+    const V *h = (const V *)a.in[a.hi[k]];
+    V v = h[i];
+    if (a.lo[k] >= 0) {  // wave-uniform: kernel-argument branch
+      const V *l = (const V *)a.in[a.lo[k]];
+      v = apply_any<OP, T, V>(v, l[i]);
+    }
+    stack[depth++] = v;
+    // merge while the two top groups are the same size: after leaf k the
+    // number of merges is the count of trailing one bits of (k + 1) - 1…
+    // i.e. of trailing zero bits of (k + 1).
+#pragma unroll
+    for (int m = 1; m < NLEAF; m <<= 1) {
+      if (((k + 1) & (2 * m - 1)) == 0) {
+        V hi = stack[--depth];
+        V lo = stack[--depth];
+        stack[depth++] = apply_any<OP, T, V>(hi, lo);
+      }
+    }
+  }
+  return stack[0];
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_vec(TreeArgs a,
+                                                          u32x4 *dst,
+                                                          size_t nvec) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < nvec; i += stride)
+    st<true>(dst + i, tree_eval<OP, T, u32x4, NLEAF>(a, i));
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
+                                                           size_t n0,
+                                                           size_t off1,
+                                                           size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    dst[k] = tree_eval<OP, T, T, NLEAF>(a, k);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+// Product configuration of the vector body (chosen by the on-GPU sweep in
+// bench.py --tune; see DESIGN.md "Kernel tuning").
+constexpr int kUnroll = 4;
+constexpr bool kNtLoad = true;
+constexpr bool kNtStore = true;
+
+static inline unsigned grid_for(size_t work, size_t per_block, unsigned cap) {
+  size_t g = (work + per_block - 1) / per_block;
+  if (g == 0) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+constexpr unsigned kElemGridCap = 256 * 8;  // 8 workgroups per CU, grid-stride
+
+template <int OP, typename T>
+static int launch_write(void *dst, const void *src, size_t cnt,
+                        hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
+    if (cnt == 0) return 0;
+    if (pd % E || ps % E) {
+      hipLaunchKernelGGL((combine_unaligned<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock),
+                         0, s, (unsigned char *)dst, (const unsigned char *)src,
+                         cnt);
+    } else if ((pd ^ ps) % 16 == 0 && E <= 16) {
+      size_t head = ((16 - pd % 16) % 16) / E;
+      if (head > cnt) head = cnt;
+      size_t nvec = (cnt - head) * E / 16;
+      size_t body = nvec * 16 / E;
+      size_t tail = cnt - head - body;
+      if (nvec) {
+        u32x4 *d = (u32x4 *)((char *)dst + head * E);
+        const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
+        hipLaunchKernelGGL((combine_vec<OP, T, kUnroll, kNtLoad, kNtStore>),
+                           dim3(grid_for(nvec, (size_t)kBlock * kUnroll, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, d, v, nvec);
+      }
+      if (head + tail)
+        hipLaunchKernelGGL((combine_elem<OP, T>),
+                           dim3(grid_for(head + tail, kBlock, kElemGridCap)),
+                           dim3(kBlock), 0, s, (T *)dst, (const T *)src, head,
+                           head + body, tail);
+    } else {
+      hipLaunchKernelGGL((combine_elem<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock),
+                         0, s, (T *)dst, (const T *)src, cnt, (size_t)0,
+                         (size_t)0);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+static int launch_tree_n(const TreeArgs &a, void *dst, size_t cnt, bool vec,
+                         size_t head, size_t nvec, hipStream_t s) {
+  constexpr size_t E = sizeof(T);
+  if (vec && nvec) {
+    TreeArgs b = a;
+    for (int k = 0; k < 2 * kMaxLeaf; k++)
+      if (b.in[k]) b.in[k] = (const char *)b.in[k] + head * E;
+    hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
+                       dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
+                       s, b, (u32x4 *)((char *)dst + head * E), nvec);
+  }
+  size_t body = vec ? nvec * 16 / E : 0;
+  size_t n0 = vec ? head : cnt;
+  size_t tail = vec ? cnt - head - body : 0;
+  if (n0 + tail)
+    hipLaunchKernelGGL((reduce_tree_elem<OP, T, NLEAF>),
+                       dim3(grid_for(n0 + tail, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, a, (T *)dst, n0, head + body, tail);
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T>
+static int launch_tree(void *dst, const void *const *srcs, int nsrc,
+                       size_t cnt, hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    if (nsrc < 1 || nsrc > 2 * kMaxLeaf) return -LFA_EINVAL;
+    if (cnt == 0) return 0;
+    if (nsrc == 1) {
+      if (dst == srcs[0]) return 0;
+      return hipMemcpyAsync(dst, srcs[0], cnt * E, hipMemcpyDeviceToDevice,
+                            s) == hipSuccess ? 0 : -LFA_EIO;
+    }
+    int pof2 = 1;
+    while (pof2 * 2 <= nsrc) pof2 *= 2;
+    int rem = nsrc - pof2;
+    TreeArgs a;
+    memset(&a, 0, sizeof(a));
+    uintptr_t mis = (uintptr_t)dst % 16, anyelem = (uintptr_t)dst % E;
+    for (int k = 0; k < nsrc; k++) {
+      a.in[k] = srcs[k];
+      mis |= ((uintptr_t)srcs[k] % 16) ^ ((uintptr_t)dst % 16);
+      anyelem |= (uintptr_t)srcs[k] % E;
+    }
+    if (anyelem) return -LFA_EINVAL;  // element-misaligned inputs: unsupported
+    for (int k = 0; k < pof2; k++) {
+      if (k < rem) {
+        a.hi[k] = (signed char)(2 * k + 1);
+        a.lo[k] = (signed char)(2 * k);
+      } else {
+        a.hi[k] = (signed char)(k + rem);
+        a.lo[k] = -1;
+      }
+    }
+    bool vec = (mis == 0) && E <= 16;
+    size_t head = vec ? ((16 - (uintptr_t)dst % 16) % 16) / E : 0;
+    if (head > cnt) head = cnt;
+    size_t nvec = vec ? (cnt - head) * E / 16 : 0;
+    switch (pof2) {
+      case 2: return launch_tree_n<OP, T, 2>(a, dst, cnt, vec, head, nvec, s);
+      case 4: return launch_tree_n<OP, T, 4>(a, dst, cnt, vec, head, nvec, s);
+      case 8: return launch_tree_n<OP, T, 8>(a, dst, cnt, vec, head, nvec, s);
+      case 16: return launch_tree_n<OP, T, 16>(a, dst, cnt, vec, head, nvec, s);
+      default: return -LFA_EINVAL;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-op entry points
+// ---------------------------------------------------------------------------
+// This file is compiled once per write op (-DLFA_OP=<enum fi_op value>) so the
+// ~100 (op, datatype) kernel families build in parallel; each object exports
+//   lfa__write_op<N>(dt, dst, src, cnt, stream)
+//   lfa__tree_op<N>(dt, dst, srcs, nsrc, cnt, stream)
+// which lfa_capi.cpp dispatches to.  Return 0 or a negative LFA_E* code.
+template <int OP, typename F>
+static int by_type(int dt, F &&f) {
+  switch (dt) {
+    case LFA_INT8: return f((int8_t *)0);
+    case LFA_UINT8: return f((uint8_t *)0);
+    case LFA_INT16: return f((int16_t *)0);
+    case LFA_UINT16: return f((uint16_t *)0);
+    case LFA_INT32: return f((int32_t *)0);
+    case LFA_UINT32: return f((uint32_t *)0);
+    case LFA_INT64: return f((int64_t *)0);
+    case LFA_UINT64: return f((uint64_t *)0);
+    case LFA_FLOAT: return f((float *)0);
+    case LFA_DOUBLE: return f((double *)0);
+    case LFA_FLOAT_COMPLEX: return f((cf32 *)0);
+    case LFA_INT128: return f((i128 *)0);
+    case LFA_UINT128: return f((u128 *)0);
+    default: return -LFA_EOPNOTSUPP;
+  }
+}
+
+}  // namespace lfa
+
+#ifndef LFA_OP
+#error "compile with -DLFA_OP=<op>"
+#endif
+
+#define LFA_CAT2(a, b) a##b
+#define LFA_CAT(a, b) LFA_CAT2(a, b)
+
+extern "C" int LFA_CAT(lfa__write_op, LFA_OP)(int dt, void *dst,
+                                              const void *src, size_t cnt,
+                                              void *stream) {
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_write<LFA_OP, T>(dst, src, cnt, (hipStream_t)stream);
+  });
+}
+
+extern "C" int LFA_CAT(lfa__tree_op, LFA_OP)(int dt, void *dst,
+                                             const void *const *srcs, int nsrc,
+                                             size_t cnt, void *stream) {
+#if LFA_OP <= 9
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_tree<LFA_OP, T>(dst, srcs, nsrc, cnt,
+                                       (hipStream_t)stream);
+  });
+#else
+  (void)dt; (void)dst; (void)srcs; (void)nsrc; (void)cnt; (void)stream;
+  return -LFA_EOPNOTSUPP;
+#endif
+}
+
+#if LFA_OP == 2
+// Tuning sweep for the headline kernel (float SUM): the variants bench.py
+// --tune times against each other in one process (guide §5.4 rule 24).
+// Returns -LFA_EINVAL for an unknown variant id.
+extern "C" int lfa__tune_sum_f32(int variant, void *dst, const void *src,
+                                 size_t nvec, void *stream) {
+  using namespace lfa;
+  hipStream_t s = (hipStream_t)stream;
+  u32x4 *d = (u32x4 *)dst;
+  const u32x4 *v = (const u32x4 *)src;
+  auto chunk = [&](auto kern, int u) {
+    hipLaunchKernelGGL(kern, dim3(grid_for(nvec, (size_t)kBlock * u, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, d, v, nvec);
+  };
+  auto gs = [&](auto kern, unsigned grid) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, d, v, nvec);
+  };
+  switch (variant) {
+    case 0: chunk(combine_vec<OP_SUM, float, 4, true, true>, 4); break;
+    case 1: chunk(combine_vec<OP_SUM, float, 1, true, true>, 1); break;
+    case 2: chunk(combine_vec<OP_SUM, float, 2, true, true>, 2); break;
+    case 3: chunk(combine_vec<OP_SUM, float, 8, true, true>, 8); break;
+    case 4: chunk(combine_vec<OP_SUM, float, 4, false, false>, 4); break;
+    case 5: chunk(combine_vec<OP_SUM, float, 4, true, false>, 4); break;
+    case 6: chunk(combine_vec<OP_SUM, float, 4, false, true>, 4); break;
+    case 7: gs(combine_vec_gs<OP_SUM, float, 4, true, true>, 2048); break;
+    case 8: gs(combine_vec_gs<OP_SUM, float, 4, true, true>, 1024); break;
+    case 9: gs(combine_vec_gs<OP_SUM, float, 2, true, true>, 4096); break;
+    case 10: gs(combine_vec_gs<OP_SUM, float, 8, true, true>, 1024); break;
+    case 11: chunk(combine_vec<OP_SUM, float, 8, false, false>, 8); break;
+    default: return -LFA_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+#endif

@@ -1,0 +1,90 @@
+"""CPU-side checks of the native boundary (no GPU compute calls).
+
+* liblfa.so / liblfa_coll.so load and export every function and table that
+  include/*.h declares;
+* the host-only entry points (datatype size, atomic_valid, table membership)
+  agree with the oracle restatement of util_atomic.c;
+* argument validation errors come back as negative errno values.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+import oracle
+from libfabric_amd import _native
+from libfabric_amd.enums import DT
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+
+
+def _declared(header: str) -> list[str]:
+    text = open(os.path.join(INC, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(lfa_[a-z0-9_]+)\s*\(", text)
+    names += re.findall(r"extern\s+[^;]*?\b(lfa_[a-z0-9_]+)\s*\[", text)
+    return sorted(set(n for n in names if not n.endswith("_fn")))
+
+
+def _lib_or_skip(name):
+    try:
+        return _native.lib(name)
+    except _native.NativeLibraryMissing as e:
+        pytest.fail(str(e))
+
+
+def test_lfa_exports_every_declared_symbol():
+    L = _lib_or_skip("lfa")
+    for sym in _declared("lfa_atomic.h"):
+        assert hasattr(L, sym), sym
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(INC, "lfa_coll.h")),
+                    reason="no lfa_coll.h yet")
+def test_coll_exports_every_declared_symbol():
+    L = _lib_or_skip("coll")
+    for sym in _declared("lfa_coll.h"):
+        assert hasattr(L, sym), sym
+
+
+def test_table_membership_matches_oracle():
+    from libfabric_amd import atomic
+    for op in range(12):
+        for dt in range(16):
+            assert (atomic.write_handler(op, dt) is not None) == \
+                oracle.has_handler(op, dt), (op, dt)
+
+
+def test_valid_and_size_match_oracle():
+    from libfabric_amd import atomic
+    flags_set = [0, 1 << 3, 1 << 58, 1 << 59, (1 << 58) | (1 << 59),
+                 (1 << 3) | (1 << 58), 1 << 40]
+    for op in range(13):
+        for dt in range(18):
+            for fl in flags_set:
+                assert atomic.atomic_valid(dt, op, fl) == \
+                    oracle.atomic_valid(dt, op, fl), (op, dt, fl)
+    for dt in range(17):
+        assert atomic.datatype_size(dt) == oracle.datatype_size(dt)
+
+
+def test_async_argument_errors():
+    L = _lib_or_skip("lfa")
+    # unsupported (op, dt): float BOR → -EOPNOTSUPP, before touching the GPU
+    assert L.lfa_atomic_write_async(6, int(DT.FLOAT), None, None, 0, None) == -95
+    # null buffers with cnt > 0 → -EINVAL
+    assert L.lfa_atomic_write_async(2, int(DT.FLOAT), None, None, 4, None) == -22
+    # tree: nsrc out of range → -EINVAL
+    arr = (ctypes.c_void_p * 1)(None)
+    assert L.lfa_reduce_tree_async(2, int(DT.FLOAT), None, arr, 0, 0, None) == -22
+    assert L.lfa_reduce_tree_async(2, int(DT.FLOAT), None, arr, 33, 0, None) == -22
+    assert L.lfa_reduce_tree_async(11, int(DT.FLOAT), None, arr, 1, 0, None) == -95
+    # cnt == 0 is a no-op success
+    assert L.lfa_atomic_write_async(2, int(DT.FLOAT), None, None, 0, None) == 0
+
+
+def test_version_string():
+    L = _lib_or_skip("lfa")
+    assert b"gfx950" in L.lfa_version()

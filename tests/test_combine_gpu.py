@@ -1,0 +1,207 @@
+"""GPU parity of the gfx950 combine kernels (liblfa.so) against the oracle.
+
+Every test calls through the C ABI (lfa_atomic_write_async /
+lfa_reduce_tree_async / the synchronous lfa_atomic_write_handlers table).
+Bar: bit-exact for integer ops; float/double/complex bit-exact on every
+non-NaN lane with NaN-class agreement on NaN lanes (tests/_cmp.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests._cmp import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def lfa():
+    from libfabric_amd import atomic, lib
+    lib()  # raises if liblfa.so is missing: no fallback
+    assert torch.cuda.is_available()
+    return atomic
+
+
+@pytest.fixture(scope="module")
+def manifest(golden_dir):
+    with open(os.path.join(golden_dir, "manifest.json")) as f:
+        return json.load(f)
+
+
+def _dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(DEV)
+
+
+def test_golden_fixtures_async(lfa, manifest, golden_dir):
+    """All 132 (op, datatype) handlers on the reference-generated fixtures."""
+    for case in manifest["combine"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        d, s = _dev(z["dst"]), _dev(z["src"])
+        lfa.write(case["op"], case["dt"], d, s)
+        torch.cuda.synchronize()
+        assert_parity(case["dt"], d.cpu().numpy(), z["out"], case["file"])
+
+
+def test_golden_fixtures_sync_table(lfa, manifest, golden_dir):
+    """The ofi_atomic_write_handlers-shaped synchronous table entries."""
+    for case in manifest["combine"]:
+        fn = lfa.write_handler(case["op"], case["dt"])
+        assert fn is not None
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        d, s = _dev(z["dst"]), _dev(z["src"])
+        torch.cuda.synchronize()
+        fn(d.data_ptr(), s.data_ptr(), case["n"])
+        assert_parity(case["dt"], d.cpu().numpy(), z["out"], case["file"])
+
+
+def _rand(dt: int, n: int, rng) -> np.ndarray:
+    nd = oracle.DT_NP[dt]
+    if nd.kind == "V":
+        return rng.integers(0, 256, size=n * 16, dtype=np.uint8).view(nd)
+    if nd.kind == "c":
+        return rng.uniform(-2, 2, size=2 * n).astype(np.float32).view(np.complex64)
+    if nd.kind == "f":
+        return rng.uniform(-2, 2, size=n).astype(nd)
+    info = np.iinfo(nd)
+    return rng.integers(info.min, info.max, size=n, dtype=nd, endpoint=True)
+
+
+CASES = [("SUM", "FLOAT"), ("MIN", "INT64"), ("BOR", "INT64"),
+         ("PROD", "DOUBLE"), ("SUM", "INT8"), ("MAX", "UINT16"),
+         ("PROD", "FLOAT_COMPLEX"), ("BXOR", "UINT128"), ("LXOR", "FLOAT"),
+         ("ATOMIC_WRITE", "INT32"), ("MIN", "FLOAT"), ("SUM", "INT128")]
+SIZES = [0, 1, 7, 1000, 4099, (1 << 20) + 5]
+OFFSETS = [(0, 0), (1, 1), (3, 3), (1, 2), (0, 5)]
+
+
+@pytest.mark.parametrize("opname,dtname", CASES)
+def test_sizes_and_alignment(lfa, opname, dtname):
+    """Heads, tails, vector body, non-co-aligned and element-misaligned."""
+    op, dt = oracle.OPS[opname], oracle.DT_CODE[dtname]
+    esz = oracle.datatype_size(dt)
+    rng = np.random.default_rng(op * 31 + dt)
+    for n in SIZES:
+        for od, os_ in OFFSETS:
+            d = _rand(dt, n + 8, rng)
+            s = _rand(dt, n + 8, rng)
+            want = d.copy()
+            oracle.write(op, dt, want[od:od + n], s[os_:os_ + n].copy())
+            dd, sd = _dev(d), _dev(s)
+            rc = lfa.write_ptr(op, dt, dd.data_ptr() + od * esz,
+                               sd.data_ptr() + os_ * esz, n)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert_parity(dt, dd.cpu().numpy(), want, f"{opname} {dtname} n={n} off={od},{os_}")
+
+
+def test_byte_misaligned_elements(lfa):
+    """Element pointers not aligned to sizeof(T) (the reference allows any)."""
+    op, dt = oracle.OPS["SUM"], oracle.DT_CODE["DOUBLE"]
+    rng = np.random.default_rng(5)
+    n = 3001
+    raw_d = rng.integers(0, 256, n * 8 + 16, dtype=np.uint8)
+    raw_s = rng.integers(0, 256, n * 8 + 16, dtype=np.uint8)
+    raw_s[3:3 + n * 8] = rng.uniform(-1, 1, n).astype(np.float64).view(np.uint8)
+    raw_d[5:5 + n * 8] = rng.uniform(-1, 1, n).astype(np.float64).view(np.uint8)
+    want = raw_d.copy()
+    a = want[5:5 + n * 8].copy().view(np.float64)
+    oracle.write(op, dt, a, raw_s[3:3 + n * 8].copy().view(np.float64))
+    want[5:5 + n * 8] = a.view(np.uint8)
+    dd, sd = _dev(raw_d), _dev(raw_s)
+    assert lfa.write_ptr(op, dt, dd.data_ptr() + 5, sd.data_ptr() + 3, n) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(dd.cpu().numpy(), want)
+
+
+def test_denormals_not_flushed(lfa):
+    d = torch.tensor([1, 3, 0x00400000], dtype=torch.int32).view(torch.float32).to(DEV)
+    s = torch.tensor([1, 0x80000001, 0x00400000], dtype=torch.int32).view(torch.float32).to(DEV)
+    lfa.write(2, 8, d, s)
+    torch.cuda.synchronize()
+    assert d.view(torch.int32).cpu().tolist() == [2, 2, 0x00800000]
+
+
+def test_full_size_float_sum_256mib(lfa):
+    """BASELINE config 2 at full size: 67,108,864 float, bit-exact vs numpy
+    (one IEEE add per element — the same op the reference performs)."""
+    n = 256 * 1024 * 1024 // 4
+    g = torch.Generator(device=DEV).manual_seed(1)
+    src = torch.rand(n, device=DEV, generator=g) * 2 - 1
+    dst = torch.rand(n, device=DEV, generator=g) * 2 - 1
+    want = dst.cpu().numpy() + src.cpu().numpy()
+    lfa.write(2, 8, dst, src)
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_full_size_int64_bor_min_64mib(lfa):
+    """BASELINE config 3 at full size: 8,388,608 int64, BOR and MIN."""
+    n = 64 * 1024 * 1024 // 8
+    rng = np.random.default_rng(3)
+    a = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    b = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    lanes = rng.integers(0, n, n // 100)
+    a[lanes] = rng.choice(np.array([-2**63, 2**63 - 1, 0, -1], np.int64), lanes.size)
+    for op, ref in ((6, np.bitwise_or(a, b)), (0, np.where(a > b, b, a))):
+        d, s = torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV)
+        lfa.write(op, 6, d, s)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------- tree ----
+
+def test_tree_allreduce_fixtures(lfa, manifest, golden_dir):
+    """N-input fused combine == prov/coll recursive-doubling result."""
+    for case in manifest["allreduce"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        srcs = [torch.from_numpy(x.copy()).to(DEV) for x in z["sends"]]
+        out = torch.empty_like(srcs[0])
+        lfa.reduce_tree(case["op"], case["dt"], out, srcs)
+        torch.cuda.synchronize()
+        assert_parity(case["dt"], out.cpu().numpy(), z["out"], case["file"])
+        # in place into the highest rank's buffer
+        lfa.reduce_tree(case["op"], case["dt"], srcs[-1], srcs)
+        torch.cuda.synchronize()
+        assert_parity(case["dt"], srcs[-1].cpu().numpy(), z["out"], case["file"] + " inplace")
+
+
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16, 17, 31, 32])
+def test_tree_vs_oracle_allreduce(lfa, nsrc):
+    op, dt = 2, 8
+    rng = np.random.default_rng(nsrc)
+    n = 10_003
+    sends = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(nsrc)]
+    want = oracle.allreduce(op, dt, sends)[0]
+    srcs = [torch.from_numpy(x).to(DEV) for x in sends]
+    out = torch.empty_like(srcs[0])
+    lfa.reduce_tree(op, dt, out, srcs)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_tree_misaligned_and_minmax_zero_sign(lfa):
+    """Dst-biased MIN over signed zeros makes the association order visible."""
+    op, dt = 0, 8
+    n = 4099
+    rng = np.random.default_rng(9)
+    sends = []
+    for r in range(8):
+        x = rng.choice(np.array([0.0, -0.0, 1.0, np.nan], np.float32), n + 1)
+        sends.append(x)
+    want = oracle.allreduce(op, dt, [s[1:].copy() for s in sends])[0]
+    srcs = [torch.from_numpy(x).to(DEV) for x in sends]
+    out = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+    from libfabric_amd import _native
+    import ctypes
+    arr = (ctypes.c_void_p * 8)(*[s.data_ptr() + 4 for s in srcs])
+    rc = _native.lib().lfa_reduce_tree_async(op, dt, out.data_ptr() + 4, arr, 8, n, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert_parity(dt, out.cpu().numpy()[1:], want, "tree min zeros")
