@@ -174,13 +174,28 @@ def tune(args) -> None:
     stream = torch.cuda.current_stream()
     h = stream.cuda_stream
     nvec = COUNT // 4
-    variants = list(range(12))
+    variants = [int(v) for v in args.variants.split(',')] if args.variants else list(range(30))
+
+    def run(v, d, s, n):
+        fn = L.lfa__tune_sum_f32 if v < 12 or v == 30 else L.lfa__tune2_sum_f32
+        return fn(v, d.data_ptr(), s.data_ptr(), n, h)
+
+    # correctness of every variant first (odd size: exercises the tail path)
+    nchk = (1 << 20) + 77
+    for v in variants:
+        a = torch.rand(nchk * 4, device="cuda")
+        b = torch.rand(nchk * 4, device="cuda")
+        want = a + b
+        assert run(v, a, b, nchk) == 0
+        torch.cuda.synchronize()
+        if not torch.equal(a, want):
+            raise SystemExit(f"tune variant {v} is WRONG")
     times = {v: [] for v in variants}
     for _ in range(3):
         for v in variants:
             for i in range(4):
                 d, s = sets[i % BUFFER_SETS]
-                assert L.lfa__tune_sum_f32(v, d.data_ptr(), s.data_ptr(), nvec, h) == 0
+                assert run(v, d, s, nvec) == 0
     torch.cuda.synchronize()
     for rnd in range(args.tune_rounds):
         for v in variants:
@@ -189,7 +204,7 @@ def tune(args) -> None:
             for i, (a, b) in enumerate(evs):
                 d, s = sets[i % BUFFER_SETS]
                 a.record(stream)
-                L.lfa__tune_sum_f32(v, d.data_ptr(), s.data_ptr(), nvec, h)
+                run(v, d, s, nvec)
                 b.record(stream)
             torch.cuda.synchronize()
             times[v].extend(a.elapsed_time(b) for a, b in evs)
@@ -212,6 +227,7 @@ def main() -> None:
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--tune-rounds", type=int, default=10)
+    ap.add_argument("--variants", default="", help="comma list for --tune")
     args = ap.parse_args()
 
     if args.tune:
@@ -284,7 +300,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "combine_vec<FI_SUM,float,U=4,nt,nt>",
+            "kernel": "combine_lds<FI_SUM,float,U=4> (LDS-DMA staged, nt)",
             "kernel_us": round(kern_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": 3 * S_BYTES,
             "traffic_source": traffic_src,

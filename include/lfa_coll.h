@@ -1,0 +1,234 @@
+/*
+ * lfa_coll.h — C ABI of the MI355X collective provider (liblfa_coll.so).
+ *
+ * The host side of libfabric's software-collective path (prov/coll), in C,
+ * driving RCCL over xGMI for transport and the gfx950 combine kernels of
+ * liblfa.so (include/lfa_atomic.h) for every reduction.
+ *
+ * Reference interfaces each entry point replaces:
+ *
+ *   lfa_barrier / lfa_broadcast / lfa_allreduce / lfa_allgather /
+ *   lfa_reduce_scatter / lfa_reduce
+ *       struct fi_ops_collective slots, include/rdma/fi_collective.h:92-139;
+ *       prov/coll implementations coll_ep_barrier (coll_coll.c:1035),
+ *       coll_ep_allreduce (:1040-1085), coll_ep_allgather (:1087),
+ *       coll_ep_broadcast (:1158-1216); reduce / reduce_scatter are
+ *       fi_coll_no_* in the reference (coll_ep.c:75-76) — new here, with the
+ *       semantics of man/fi_collective.3.md:354-404.
+ *   lfa_query_collective   coll_query_collective, coll_coll.c:1267-1318
+ *   lfa_join_collective    coll_join_collective, coll_coll.c:912-995
+ *                          (group id = lowest common free id of the 256-bit
+ *                          cid masks, agreed by a UINT8 BAND allreduce)
+ *   lfa_cq_read / lfa_cq_readerr / lfa_eq_read
+ *                          the completions the reference writes to the peer
+ *                          CQ (coll_collective_comp, :722-756) and EQ
+ *                          (coll_join_comp, :690-720)
+ *   lfa_coll_plan          the schedule builder (coll_do_allreduce,
+ *                          :349-449, and friends): a rank's work queue of
+ *                          SEND/RECV/REDUCE/TREE/COPY items, as data
+ *
+ * Argument meaning and errors follow libfabric: calls return 0 (work queued,
+ * completion reported later through lfa_cq_read with the caller's context)
+ * or a negative LFA_E* errno; -LFA_EAGAIN is retryable.
+ *
+ * Buffers: `buf`/`result` may be device memory (hipMalloc, the data path of
+ * this provider) or host memory (staged through HBM in pipelined chunks).
+ * `desc`/`result_desc` are accepted and ignored, as in prov/coll.
+ */
+#ifndef LFA_COLL_H
+#define LFA_COLL_H
+
+#include <sys/types.h>
+#include "lfa_fabric.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct lfa_coll_domain;
+struct lfa_coll_ep;
+struct lfa_coll_mc;
+
+/* Algorithms for reducing collectives. */
+enum lfa_coll_algo {
+	/* default: per-rank block exchange over RCCL grouped send/recv, ONE
+	 * fused N-input combine kernel per block in prov/coll's
+	 * recursive-doubling association order, then block all-gather.
+	 * Bit-identical to the reference for every op and datatype. */
+	LFA_ALGO_TREE = 0,
+	/* the reference's own schedule (coll_coll.c:349-449): log2(N)
+	 * full-buffer pairwise exchanges, each followed by the binary combine
+	 * kernel (and COPY), exactly as prov/coll orders its work items. */
+	LFA_ALGO_RD = 1,
+	/* RCCL's own reduction (ncclAllReduce / ncclReduceScatter /
+	 * ncclReduce) for SUM/PROD/MIN/MAX on RCCL datatypes: fastest, but
+	 * ring association order (float results within the documented
+	 * tolerance, not bit-identical); other ops fall back to TREE. */
+	LFA_ALGO_RCCL = 2,
+};
+
+/* ---- bootstrap (replaces fi_getinfo/fi_fabric/fi_domain/fi_endpoint
+ *      and AV insertion for this path) ---------------------------------- */
+
+/* Bytes of the opaque unique id rank 0 creates and every rank passes in. */
+#define LFA_UNIQUE_ID_BYTES 128
+int lfa_coll_get_unique_id(void *id, size_t len);
+
+int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
+			 size_t id_len, struct lfa_coll_domain **domain);
+int lfa_coll_domain_close(struct lfa_coll_domain *domain);
+
+/* An endpoint owns one HIP stream (its progress context), a work-item
+ * workspace in HBM and a completion queue. */
+int lfa_coll_ep_open(struct lfa_coll_domain *domain, struct lfa_coll_ep **ep);
+int lfa_coll_ep_close(struct lfa_coll_ep *ep);
+/* The endpoint's HIP stream (hipStream_t), for callers that order work. */
+void *lfa_coll_ep_stream(struct lfa_coll_ep *ep);
+int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo);
+/* Host-staging chunk size in bytes (0 = default 64 MiB). */
+int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
+
+/* ---- groups (fi_join_collective) -------------------------------------- */
+
+/* coll_addr = LFA_ADDR_NOTAVAIL joins the world group.  `ranks` (sorted,
+ * `nmembers` entries) selects the members; NULL = all ranks.  Every listed
+ * rank must call it; non-members pass their own rank absent and get
+ * -LFA_EINVAL.  Completion: an LFA_JOIN_COMPLETE event on lfa_eq_read. */
+#define LFA_JOIN_COMPLETE 6
+int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+			const int *ranks, size_t nmembers, uint64_t flags,
+			struct lfa_coll_mc **mc, void *context);
+lfa_addr_t lfa_mc_addr(struct lfa_coll_mc *mc);
+int lfa_mc_close(struct lfa_coll_mc *mc);
+/* The world group, usable without a join (the reference's av_set coll_mc). */
+lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep);
+
+/* ---- fi_ops_collective ------------------------------------------------ */
+
+ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context);
+ssize_t lfa_broadcast(struct lfa_coll_ep *ep, void *buf, size_t count,
+		      void *desc, lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		      enum lfa_datatype datatype, uint64_t flags, void *context);
+ssize_t lfa_allreduce(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		      void *desc, void *result, void *result_desc,
+		      lfa_addr_t coll_addr, enum lfa_datatype datatype,
+		      enum lfa_op op, uint64_t flags, void *context);
+ssize_t lfa_allgather(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		      void *desc, void *result, void *result_desc,
+		      lfa_addr_t coll_addr, enum lfa_datatype datatype,
+		      uint64_t flags, void *context);
+/* `count` = elements each rank contributes; rank r receives the block
+ * [off(r), off(r+1)) of the reduced vector, off() splitting `count` into
+ * nranks contiguous blocks, the first count % nranks one element longer
+ * (lfa_coll_block). */
+ssize_t lfa_reduce_scatter(struct lfa_coll_ep *ep, const void *buf,
+			   size_t count, void *desc, void *result,
+			   void *result_desc, lfa_addr_t coll_addr,
+			   enum lfa_datatype datatype, enum lfa_op op,
+			   uint64_t flags, void *context);
+/* Full reduced vector lands in `result` at root_addr (a group rank) only. */
+ssize_t lfa_reduce(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		   void *desc, void *result, void *result_desc,
+		   lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		   enum lfa_datatype datatype, enum lfa_op op, uint64_t flags,
+		   void *context);
+
+int lfa_query_collective(struct lfa_coll_domain *domain,
+			 enum lfa_collective_op coll,
+			 struct lfa_collective_attr *attr, uint64_t flags);
+
+/* ---- completions ------------------------------------------------------ */
+
+/* Mirrors struct fi_cq_data_entry (include/rdma/fi_eq.h:215-222). */
+struct lfa_cq_entry {
+	void *op_context;
+	uint64_t flags;      /* LFA_COLLECTIVE */
+	size_t len;
+	void *buf;
+	uint64_t data;
+};
+struct lfa_cq_err_entry {
+	void *op_context;
+	uint64_t flags;
+	int err;             /* positive LFA_E* */
+	int prov_errno;      /* hipError_t / ncclResult_t */
+};
+struct lfa_eq_entry {        /* mirrors struct fi_eq_entry */
+	void *fid;           /* the lfa_coll_mc */
+	void *context;
+	uint64_t data;
+};
+
+/* Progresses the endpoint and returns completed entries (>0), or
+ * -LFA_EAGAIN when none are ready, or -LFA_EIO when an error entry waits
+ * (read it with lfa_cq_readerr). */
+ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
+		    size_t count);
+ssize_t lfa_cq_readerr(struct lfa_coll_ep *ep, struct lfa_cq_err_entry *buf);
+ssize_t lfa_eq_read(struct lfa_coll_ep *ep, uint32_t *event,
+		    struct lfa_eq_entry *entry);
+/* Blocks until every queued operation has completed (convenience). */
+int lfa_coll_ep_flush(struct lfa_coll_ep *ep);
+
+/* ---- schedules as data ------------------------------------------------ */
+
+enum lfa_step_type {
+	LFA_STEP_SEND = 0,     /* bytes from src to peer                     */
+	LFA_STEP_RECV = 1,     /* bytes from peer into dst                   */
+	LFA_STEP_GROUP_END = 2,/* the SEND/RECVs since the last GROUP_END run
+				  concurrently (one RCCL group)              */
+	LFA_STEP_REDUCE = 3,   /* dst[i] = dst[i] OP src[i], count elements  */
+	LFA_STEP_TREE = 4,     /* dst = tree(refs[first..first+nsrc)), count */
+	LFA_STEP_COPY = 5,     /* bytes from src to dst                      */
+};
+enum lfa_buf_id { LFA_BUF_SEND = 0, LFA_BUF_RESULT = 1, LFA_BUF_TMP = 2 };
+
+struct lfa_ref {
+	int32_t buf;           /* enum lfa_buf_id */
+	uint32_t pad;
+	uint64_t off;          /* byte offset */
+};
+struct lfa_step {
+	int32_t type;          /* enum lfa_step_type */
+	int32_t peer;          /* SEND/RECV: group rank */
+	uint64_t count;        /* bytes (SEND/RECV/COPY) or elements */
+	struct lfa_ref dst;
+	struct lfa_ref src;
+	uint32_t first;        /* TREE: first index into the refs array */
+	uint32_t nsrc;         /* TREE: number of inputs (rank order) */
+};
+
+/*
+ * Build rank `rank`'s schedule for one collective of `count` elements of
+ * `esz` bytes in an `nranks` group (root: group rank, or -1).  Writes up to
+ * *nsteps steps / *nrefs refs and returns the counts in them, and the HBM
+ * workspace the schedule needs in *tmp_bytes.  Host-only, no GPU needed.
+ * Returns 0, -LFA_EINVAL, -LFA_ENOSYS (collective/algo not planned) or
+ * -LFA_ETOOSMALL (arrays too short; *nsteps/*nrefs = sizes needed).
+ */
+#define LFA_ETOOSMALL 257
+int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
+		  int rank, int nranks, int root, size_t count, size_t esz,
+		  struct lfa_step *steps, size_t *nsteps,
+		  struct lfa_ref *refs, size_t *nrefs, size_t *tmp_bytes);
+
+/* Block [off, off + len) of rank r when `count` splits over `nranks`. */
+void lfa_coll_block(size_t count, int nranks, int r, size_t *off, size_t *len);
+
+/*
+ * Single-GPU multi-rank execution of the schedules: runs the plans of all
+ * `nranks` ranks on this device, matching every SEND with its RECV by a
+ * device-to-device copy, with the real combine kernels.  send[r]/result[r]
+ * are device pointers.  For testing the schedule+kernel data path at N>1 on
+ * one GPU; the RCCL transport is used by lfa_allreduce & co.
+ */
+int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
+		      int nranks, int root, enum lfa_datatype datatype,
+		      enum lfa_op op, size_t count, void *const *send,
+		      void *const *result, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LFA_COLL_H */

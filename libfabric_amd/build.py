@@ -58,6 +58,11 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
         objs.append(o)
         if _newer(o, [kern] + hdrs):
             steps.append([HIPCC, *HIP_FLAGS, f"-DLFA_OP={op}", "-c", kern, "-o", o])
+    tune = os.path.join(CSRC, "lfa_tune.hip")
+    o = os.path.join(BUILD, "lfa_tune.o")
+    objs.append(o)
+    if _newer(o, [tune] + hdrs):
+        steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", o])
     capi = os.path.join(CSRC, "lfa_capi.cpp")
     o = os.path.join(BUILD, "lfa_capi.o")
     objs.append(o)

@@ -1,0 +1,389 @@
+"""ctypes front end of the collective provider (liblfa_coll.so, include/lfa_coll.h).
+
+The provider is C; this module only marshals arguments:
+
+  plan(...)        lfa_coll_plan — a rank's schedule as data (host only)
+  block(...)       lfa_coll_block — reduce_scatter block bounds
+  loopback(...)    lfa_coll_loopback — all ranks' schedules on ONE GPU
+  Endpoint         domain + endpoint over RCCL; fi_ops_collective calls
+                   (allreduce, reduce_scatter, reduce, allgather, broadcast,
+                   barrier), join, query, cq_read — prov/coll's surface
+                   (include/rdma/fi_collective.h:92-139).
+
+Bootstrap: rank 0 creates the RCCL unique id (lfa_coll_get_unique_id) and
+ships it to the other ranks over torch.distributed's store/gloo group.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from ._native import lib as _lib
+from .enums import COLL, DT, OP, SIZES
+
+c_int, c_size_t, c_void_p, c_uint64, c_uint32, c_int32 = (
+    ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64,
+    ctypes.c_uint32, ctypes.c_int32)
+c_ssize_t = ctypes.c_ssize_t
+
+ALGO_TREE, ALGO_RD, ALGO_RCCL = 0, 1, 2
+STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY = range(6)
+BUF_SEND, BUF_RESULT, BUF_TMP = 0, 1, 2
+ADDR_NOTAVAIL = (1 << 64) - 1
+EAGAIN, EIO = 11, 5
+JOIN_COMPLETE = 6
+UNIQUE_ID_BYTES = 128
+
+
+class Ref(ctypes.Structure):
+    _fields_ = [("buf", c_int32), ("pad", c_uint32), ("off", c_uint64)]
+
+
+class Step(ctypes.Structure):
+    _fields_ = [("type", c_int32), ("peer", c_int32), ("count", c_uint64),
+                ("dst", Ref), ("src", Ref), ("first", c_uint32),
+                ("nsrc", c_uint32)]
+
+
+class AtomicAttr(ctypes.Structure):
+    _fields_ = [("count", c_size_t), ("size", c_size_t)]
+
+
+class CollectiveAttr(ctypes.Structure):
+    _fields_ = [("op", c_int), ("datatype", c_int),
+                ("datatype_attr", AtomicAttr), ("max_members", c_size_t),
+                ("mode", c_uint64)]
+
+
+class CqEntry(ctypes.Structure):
+    _fields_ = [("op_context", c_void_p), ("flags", c_uint64), ("len", c_size_t),
+                ("buf", c_void_p), ("data", c_uint64)]
+
+
+class CqErrEntry(ctypes.Structure):
+    _fields_ = [("op_context", c_void_p), ("flags", c_uint64), ("err", c_int),
+                ("prov_errno", c_int)]
+
+
+class EqEntry(ctypes.Structure):
+    _fields_ = [("fid", c_void_p), ("context", c_void_p), ("data", c_uint64)]
+
+
+_bound = False
+
+
+def lib() -> ctypes.CDLL:
+    global _bound
+    L = _lib("coll")
+    if _bound:
+        return L
+    P = ctypes.POINTER
+    L.lfa_coll_plan.restype = c_int
+    L.lfa_coll_plan.argtypes = [c_int, c_int, c_int, c_int, c_int, c_size_t,
+                                c_size_t, P(Step), P(c_size_t), P(Ref),
+                                P(c_size_t), P(c_size_t)]
+    L.lfa_coll_block.restype = None
+    L.lfa_coll_block.argtypes = [c_size_t, c_int, c_int, P(c_size_t), P(c_size_t)]
+    L.lfa_coll_loopback.restype = c_int
+    L.lfa_coll_loopback.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_size_t, P(c_void_p), P(c_void_p), c_void_p]
+    L.lfa_coll_get_unique_id.restype = c_int
+    L.lfa_coll_get_unique_id.argtypes = [c_void_p, c_size_t]
+    L.lfa_coll_domain_open.restype = c_int
+    L.lfa_coll_domain_open.argtypes = [c_int, c_int, c_int, c_void_p, c_size_t,
+                                       P(c_void_p)]
+    L.lfa_coll_domain_close.restype = c_int
+    L.lfa_coll_domain_close.argtypes = [c_void_p]
+    L.lfa_coll_ep_open.restype = c_int
+    L.lfa_coll_ep_open.argtypes = [c_void_p, P(c_void_p)]
+    L.lfa_coll_ep_close.restype = c_int
+    L.lfa_coll_ep_close.argtypes = [c_void_p]
+    L.lfa_coll_ep_stream.restype = c_void_p
+    L.lfa_coll_ep_stream.argtypes = [c_void_p]
+    L.lfa_coll_ep_set_algo.restype = c_int
+    L.lfa_coll_ep_set_algo.argtypes = [c_void_p, c_int]
+    L.lfa_coll_ep_set_chunk.restype = c_int
+    L.lfa_coll_ep_set_chunk.argtypes = [c_void_p, c_size_t]
+    L.lfa_coll_ep_flush.restype = c_int
+    L.lfa_coll_ep_flush.argtypes = [c_void_p]
+    L.lfa_coll_world_addr.restype = c_uint64
+    L.lfa_coll_world_addr.argtypes = [c_void_p]
+    L.lfa_join_collective.restype = c_int
+    L.lfa_join_collective.argtypes = [c_void_p, c_uint64, P(c_int), c_size_t,
+                                      c_uint64, P(c_void_p), c_void_p]
+    L.lfa_mc_addr.restype = c_uint64
+    L.lfa_mc_addr.argtypes = [c_void_p]
+    L.lfa_mc_close.restype = c_int
+    L.lfa_mc_close.argtypes = [c_void_p]
+    for name in ("lfa_allreduce", "lfa_reduce_scatter", "lfa_allgather"):
+        f = getattr(L, name)
+        f.restype = c_ssize_t
+    L.lfa_allreduce.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                c_void_p, c_uint64, c_int, c_int, c_uint64, c_void_p]
+    L.lfa_reduce_scatter.argtypes = L.lfa_allreduce.argtypes
+    L.lfa_reduce.restype = c_ssize_t
+    L.lfa_reduce.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                             c_void_p, c_uint64, c_uint64, c_int, c_int, c_uint64,
+                             c_void_p]
+    L.lfa_allgather.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                c_void_p, c_uint64, c_int, c_uint64, c_void_p]
+    L.lfa_broadcast.restype = c_ssize_t
+    L.lfa_broadcast.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_uint64,
+                                c_uint64, c_int, c_uint64, c_void_p]
+    L.lfa_barrier.restype = c_ssize_t
+    L.lfa_barrier.argtypes = [c_void_p, c_uint64, c_void_p]
+    L.lfa_query_collective.restype = c_int
+    L.lfa_query_collective.argtypes = [c_void_p, c_int, P(CollectiveAttr), c_uint64]
+    L.lfa_cq_read.restype = c_ssize_t
+    L.lfa_cq_read.argtypes = [c_void_p, P(CqEntry), c_size_t]
+    L.lfa_cq_readerr.restype = c_ssize_t
+    L.lfa_cq_readerr.argtypes = [c_void_p, P(CqErrEntry)]
+    L.lfa_eq_read.restype = c_ssize_t
+    L.lfa_eq_read.argtypes = [c_void_p, P(c_uint32), P(EqEntry)]
+    _bound = True
+    return L
+
+
+class CollError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} -> {rc}")
+        self.rc = rc
+
+
+def _chk(rc: int, what: str) -> int:
+    if rc < 0:
+        raise CollError(rc, what)
+    return rc
+
+
+# ------------------------------------------------------------- schedules --
+
+@dataclass
+class Plan:
+    steps: list
+    refs: list
+    tmp_bytes: int
+
+
+def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
+         esz: int) -> Plan:
+    L = lib()
+    ns, nr, tmp = c_size_t(0), c_size_t(0), c_size_t(0)
+    _chk(L.lfa_coll_plan(coll, algo, rank, nranks, root, count, esz, None,
+                         ctypes.byref(ns), None, ctypes.byref(nr),
+                         ctypes.byref(tmp)), "lfa_coll_plan(size)")
+    steps = (Step * max(ns.value, 1))()
+    refs = (Ref * max(nr.value, 1))()
+    _chk(L.lfa_coll_plan(coll, algo, rank, nranks, root, count, esz, steps,
+                         ctypes.byref(ns), refs, ctypes.byref(nr),
+                         ctypes.byref(tmp)), "lfa_coll_plan")
+    out = []
+    for s in steps[:ns.value]:
+        out.append({"type": s.type, "peer": s.peer, "count": s.count,
+                    "dst": (s.dst.buf, s.dst.off), "src": (s.src.buf, s.src.off),
+                    "first": s.first, "nsrc": s.nsrc})
+    return Plan(out, [(r.buf, r.off) for r in refs[:nr.value]], tmp.value)
+
+
+def block(count: int, nranks: int, r: int) -> tuple[int, int]:
+    off, ln = c_size_t(0), c_size_t(0)
+    lib().lfa_coll_block(count, nranks, r, ctypes.byref(off), ctypes.byref(ln))
+    return off.value, ln.value
+
+
+def loopback(coll: int, algo: int, nranks: int, root: int, dt: int, op: int,
+             count: int, sends: list[torch.Tensor], results: list[torch.Tensor],
+             stream=None) -> None:
+    """Run all ranks' schedules on the current GPU (device tensors)."""
+    sp = (c_void_p * nranks)(*[t.data_ptr() if t is not None else None for t in sends])
+    rp = (c_void_p * nranks)(*[t.data_ptr() if t is not None else None for t in results])
+    h = (stream or torch.cuda.current_stream()).cuda_stream
+    _chk(lib().lfa_coll_loopback(coll, algo, nranks, root, dt, op, count, sp, rp, h),
+         "lfa_coll_loopback")
+
+
+# -------------------------------------------------------------- endpoint --
+
+def _ptr(x) -> int | None:
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return int(x)
+
+
+class Endpoint:
+    """One rank's domain + endpoint.  Buffers: torch tensors (device or host)
+    or numpy arrays (host).  Calls return after enqueueing; completions come
+    from cq_read()/wait() with the context value passed in."""
+
+    def __init__(self, rank: int, nranks: int, device: int, uid: bytes):
+        L = lib()
+        self.rank, self.nranks, self.device = rank, nranks, device
+        self.dom, self.ep = c_void_p(), c_void_p()
+        buf = ctypes.create_string_buffer(uid, UNIQUE_ID_BYTES)
+        _chk(L.lfa_coll_domain_open(device, rank, nranks, buf, UNIQUE_ID_BYTES,
+                                    ctypes.byref(self.dom)), "domain_open")
+        _chk(L.lfa_coll_ep_open(self.dom, ctypes.byref(self.ep)), "ep_open")
+        self.world = L.lfa_coll_world_addr(self.ep)
+        self._ctx = 0
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+        _chk(lib().lfa_coll_get_unique_id(buf, UNIQUE_ID_BYTES), "get_unique_id")
+        return buf.raw
+
+    @classmethod
+    def from_torch_dist(cls, device: int | None = None) -> "Endpoint":
+        """Bootstrap over an initialised torch.distributed group."""
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            return cls(0, 1, device or 0, cls.unique_id())
+        rank, world = dist.get_rank(), dist.get_world_size()
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(rank, world, torch.cuda.current_device() if device is None
+                   else device, obj[0])
+
+    def close(self) -> None:
+        L = lib()
+        if self.ep:
+            L.lfa_coll_ep_close(self.ep)
+            self.ep = c_void_p()
+        if self.dom:
+            L.lfa_coll_domain_close(self.dom)
+            self.dom = c_void_p()
+
+    # configuration
+    def set_algo(self, algo: int) -> None:
+        _chk(lib().lfa_coll_ep_set_algo(self.ep, algo), "set_algo")
+
+    def set_chunk(self, nbytes: int) -> None:
+        _chk(lib().lfa_coll_ep_set_chunk(self.ep, nbytes), "set_chunk")
+
+    @property
+    def stream_handle(self) -> int:
+        return lib().lfa_coll_ep_stream(self.ep)
+
+    def _next_ctx(self) -> int:
+        self._ctx += 1
+        return self._ctx
+
+    # fi_ops_collective
+    def allreduce(self, buf, result, count: int, dt: int, op: int,
+                  coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_allreduce(self.ep, _ptr(buf), count, None, _ptr(result),
+                                 None, coll_addr or self.world, dt, op, 0, ctx),
+             "lfa_allreduce")
+        return ctx
+
+    def reduce_scatter(self, buf, result, count: int, dt: int, op: int,
+                       coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_reduce_scatter(self.ep, _ptr(buf), count, None, _ptr(result),
+                                      None, coll_addr or self.world, dt, op, 0, ctx),
+             "lfa_reduce_scatter")
+        return ctx
+
+    def reduce(self, buf, result, count: int, root: int, dt: int, op: int,
+               coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_reduce(self.ep, _ptr(buf), count, None, _ptr(result), None,
+                              coll_addr or self.world, root, dt, op, 0, ctx),
+             "lfa_reduce")
+        return ctx
+
+    def allgather(self, buf, result, count: int, dt: int,
+                  coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_allgather(self.ep, _ptr(buf), count, None, _ptr(result),
+                                 None, coll_addr or self.world, dt, 0, ctx),
+             "lfa_allgather")
+        return ctx
+
+    def broadcast(self, buf, count: int, root: int, dt: int,
+                  coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_broadcast(self.ep, _ptr(buf), count, None,
+                                 coll_addr or self.world, root, dt, 0, ctx),
+             "lfa_broadcast")
+        return ctx
+
+    def barrier(self, coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_barrier(self.ep, coll_addr or self.world, ctx), "lfa_barrier")
+        return ctx
+
+    def query(self, coll: int, op: int = OP.SUM, dt: int = DT.FLOAT,
+              flags: int = 0, mode: int = 0) -> tuple[int, CollectiveAttr]:
+        a = CollectiveAttr(op=op, datatype=dt, mode=mode)
+        rc = lib().lfa_query_collective(self.dom, coll, ctypes.byref(a), flags)
+        return rc, a
+
+    def join(self, ranks: list[int] | None = None, context: int | None = None,
+             coll_addr: int | None = None):
+        mc = c_void_p()
+        arr = (c_int * len(ranks))(*ranks) if ranks is not None else None
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_join_collective(self.ep, coll_addr or ADDR_NOTAVAIL, arr,
+                                       len(ranks) if ranks else 0, 0,
+                                       ctypes.byref(mc), ctx), "lfa_join_collective")
+        return mc.value, ctx
+
+    def mc_addr(self, mc: int) -> int:
+        return lib().lfa_mc_addr(mc)
+
+    # completions
+    def cq_read(self, max_entries: int = 16) -> list[int]:
+        ents = (CqEntry * max_entries)()
+        n = lib().lfa_cq_read(self.ep, ents, max_entries)
+        if n == -EAGAIN:
+            return []
+        if n == -EIO:
+            err = CqErrEntry()
+            lib().lfa_cq_readerr(self.ep, ctypes.byref(err))
+            raise CollError(-err.err, f"completion error (prov_errno {err.prov_errno})")
+        _chk(n, "lfa_cq_read")
+        return [ents[i].op_context for i in range(n)]
+
+    def eq_read(self):
+        ev, ent = c_uint32(0), EqEntry()
+        n = lib().lfa_eq_read(self.ep, ctypes.byref(ev), ctypes.byref(ent))
+        if n == -EAGAIN:
+            return None
+        _chk(n, "lfa_eq_read")
+        return ev.value, ent.fid, ent.context
+
+    def wait(self, ctx: int, timeout_s: float = 120.0) -> None:
+        """Poll the CQ (the progress call) until `ctx` completes."""
+        import time
+        t0 = time.time()
+        while True:
+            if ctx in self.cq_read():
+                return
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError(f"collective {ctx} did not complete")
+
+    def wait_join(self, timeout_s: float = 120.0):
+        import time
+        t0 = time.time()
+        while True:
+            e = self.eq_read()
+            if e is not None:
+                return e
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError("join did not complete")
+
+
+def esz(dt: int) -> int:
+    return SIZES[DT(dt)]
+
+
+__all__ = ["plan", "block", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
+           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "esz"]

@@ -127,7 +127,7 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
 }
 
 const char *lfa_version(void) {
-  return "lfa-combine 0.1 gfx950 (U=4, nt loads/stores, 256-thread chunks)";
+  return "lfa-combine 0.2 gfx950 (LDS-DMA staged, 4 KiB/operand/wave, nt loads/stores)";
 }
 
 }  // extern "C"

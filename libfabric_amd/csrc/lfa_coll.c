@@ -1,0 +1,1681 @@
+/*
+ * lfa_coll.c — MI355X collective provider: the host side of libfabric's
+ * software-collective path (prov/coll), in C.
+ *
+ * Reference structure this restates (not copies):
+ *   prov/coll builds, per operation, a work queue of SEND / RECV / REDUCE /
+ *   COPY / COMP items (include/ofi_coll.h:64-119, coll_coll.c:229-343) and
+ *   drains it from the application's progress thread (coll_ep_progress,
+ *   coll_coll.c:816-890), with transport delegated to the host provider
+ *   through FI_PEER_TRANSFER tagged messages (coll_coll.c:770-814) and every
+ *   REDUCE item calling ofi_atomic_write_handler (coll_coll.c:758-768).
+ *
+ * The MI355X design keeps that split — schedule / transport / combine — but:
+ *   - the schedule is built once per call as an array of lfa_step items
+ *     (lfa_coll_plan, host-only, testable on CPU);
+ *   - the executor enqueues the whole schedule on the endpoint's HIP stream:
+ *     SEND/RECV groups become RCCL grouped ncclSend/ncclRecv over xGMI,
+ *     REDUCE / TREE items launch the gfx950 combine kernels (liblfa.so),
+ *     COPY items are D2D copies; nothing blocks the host;
+ *   - completion is a HIP event per operation, reaped by lfa_cq_read (the
+ *     progress call, like fi_cq_read driving coll_ep_progress).
+ *
+ * Default algorithm (LFA_ALGO_TREE): rank r receives block r of every
+ * rank's input (one grouped exchange, (N-1)/N·S bytes out per rank), reduces
+ * the N blocks in ONE fused kernel in the reference's recursive-doubling
+ * association order — so every rank's result is bit-identical to prov/coll's
+ * — and all-gathers the reduced blocks.  Bandwidth-optimal like RS+AG, and
+ * valid for every op including the bitwise/logical ones RCCL lacks.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "lfa_atomic.h"
+#include "lfa_coll.h"
+
+#define LFA_MAX_GROUP_ID 256            /* OFI_MAX_GROUP_ID, ofi_coll.h:44 */
+#define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
+#define LFA_DEFAULT_CHUNK (64u << 20)
+#define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
+
+/* ====================================================================== */
+/* schedule builder                                                        */
+/* ====================================================================== */
+
+void lfa_coll_block(size_t count, int nranks, int r, size_t *off, size_t *len)
+{
+	size_t base = count / (size_t)nranks, extra = count % (size_t)nranks;
+	size_t rr = (size_t)r;
+
+	*len = base + (rr < extra ? 1 : 0);
+	*off = rr * base + (rr < extra ? rr : extra);
+}
+
+struct planner {
+	struct lfa_step *steps;
+	size_t cap, n;
+	struct lfa_ref *refs;
+	size_t rcap, nr;
+	int pending_comm;       /* SEND/RECV since the last GROUP_END */
+};
+
+static struct lfa_ref ref(int buf, uint64_t off)
+{
+	struct lfa_ref r;
+
+	r.buf = buf;
+	r.pad = 0;
+	r.off = off;
+	return r;
+}
+
+static struct lfa_step *push(struct planner *p, int type)
+{
+	struct lfa_step *s;
+
+	if (p->n < p->cap) {
+		s = &p->steps[p->n];
+		memset(s, 0, sizeof(*s));
+		s->type = type;
+	} else {
+		s = NULL;
+	}
+	p->n++;
+	return s;
+}
+
+static void p_xfer(struct planner *p, int type, int peer, struct lfa_ref r,
+		   uint64_t bytes)
+{
+	struct lfa_step *s;
+
+	if (!bytes)
+		return;
+	s = push(p, type);
+	if (s) {
+		s->peer = peer;
+		s->count = bytes;
+		if (type == LFA_STEP_SEND)
+			s->src = r;
+		else
+			s->dst = r;
+	}
+	p->pending_comm = 1;
+}
+
+static void p_group_end(struct planner *p)
+{
+	if (!p->pending_comm)
+		return;
+	push(p, LFA_STEP_GROUP_END);
+	p->pending_comm = 0;
+}
+
+static void p_reduce(struct planner *p, struct lfa_ref dst, struct lfa_ref src,
+		     uint64_t count)
+{
+	struct lfa_step *s;
+
+	p_group_end(p);
+	if (!count)
+		return;
+	s = push(p, LFA_STEP_REDUCE);
+	if (s) {
+		s->dst = dst;
+		s->src = src;
+		s->count = count;
+	}
+}
+
+static void p_copy(struct planner *p, struct lfa_ref dst, struct lfa_ref src,
+		   uint64_t bytes)
+{
+	struct lfa_step *s;
+
+	p_group_end(p);
+	if (!bytes || (dst.buf == src.buf && dst.off == src.off))
+		return;
+	s = push(p, LFA_STEP_COPY);
+	if (s) {
+		s->dst = dst;
+		s->src = src;
+		s->count = bytes;
+	}
+}
+
+/* TREE over refs pushed by the caller with p_tree_src() right before. */
+static uint32_t p_tree_begin(struct planner *p)
+{
+	p_group_end(p);
+	return (uint32_t)p->nr;
+}
+
+static void p_tree_src(struct planner *p, struct lfa_ref r)
+{
+	if (p->nr < p->rcap)
+		p->refs[p->nr] = r;
+	p->nr++;
+}
+
+static void p_tree_end(struct planner *p, uint32_t first, struct lfa_ref dst,
+		       uint64_t count)
+{
+	struct lfa_step *s;
+
+	if (!count)
+		return;
+	s = push(p, LFA_STEP_TREE);
+	if (s) {
+		s->dst = dst;
+		s->first = first;
+		s->nsrc = (uint32_t)(p->nr - first);
+		s->count = count;
+	}
+}
+
+/*
+ * Tree algorithm, phase 1: rank r collects block r of every rank's input.
+ * TMP slot p (block-r sized) receives rank p's block; rank r's own block is
+ * read in place from SEND.  Returns the ref list start for the TREE item.
+ */
+static void plan_gather_blocks(struct planner *p, int r, int n, size_t count,
+			       size_t esz)
+{
+	size_t off, len, moff, mlen;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	for (int k = 1; k < n; k++) {
+		/* pairwise order (r+k, r-k) spreads the peers over xGMI links */
+		int to = (r + k) % n, from = (r - k + n) % n;
+
+		lfa_coll_block(count, n, to, &off, &len);
+		p_xfer(p, LFA_STEP_SEND, to, ref(LFA_BUF_SEND, off * esz), len * esz);
+		p_xfer(p, LFA_STEP_RECV, from,
+		       ref(LFA_BUF_TMP, (uint64_t)from * mlen * esz), mlen * esz);
+	}
+	p_group_end(p);
+}
+
+static void plan_tree_block(struct planner *p, int r, int n, size_t count,
+			    size_t esz, struct lfa_ref dst)
+{
+	size_t moff, mlen;
+	uint32_t first;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	first = p_tree_begin(p);
+	for (int k = 0; k < n; k++)
+		p_tree_src(p, k == r ? ref(LFA_BUF_SEND, moff * esz) :
+			   ref(LFA_BUF_TMP, (uint64_t)k * mlen * esz));
+	p_tree_end(p, first, dst, mlen);
+}
+
+static void plan_allgather_blocks(struct planner *p, int r, int n,
+				  size_t count, size_t esz)
+{
+	size_t off, len, moff, mlen;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	for (int k = 1; k < n; k++) {
+		int to = (r + k) % n, from = (r - k + n) % n;
+
+		lfa_coll_block(count, n, from, &off, &len);
+		p_xfer(p, LFA_STEP_SEND, to, ref(LFA_BUF_RESULT, moff * esz),
+		       mlen * esz);
+		p_xfer(p, LFA_STEP_RECV, from, ref(LFA_BUF_RESULT, off * esz),
+		       len * esz);
+	}
+	p_group_end(p);
+}
+
+/* Small messages: everyone gets everyone's full input, one tree per rank.
+ * One exchange phase instead of two; TMP holds N full inputs. */
+static void plan_allreduce_small(struct planner *p, int r, int n, size_t count,
+				 size_t esz, struct lfa_ref dst)
+{
+	uint32_t first;
+
+	for (int k = 1; k < n; k++) {
+		int to = (r + k) % n, from = (r - k + n) % n;
+
+		p_xfer(p, LFA_STEP_SEND, to, ref(LFA_BUF_SEND, 0), count * esz);
+		p_xfer(p, LFA_STEP_RECV, from,
+		       ref(LFA_BUF_TMP, (uint64_t)from * count * esz), count * esz);
+	}
+	p_group_end(p);
+	first = p_tree_begin(p);
+	for (int k = 0; k < n; k++)
+		p_tree_src(p, k == r ? ref(LFA_BUF_SEND, 0) :
+			   ref(LFA_BUF_TMP, (uint64_t)k * count * esz));
+	p_tree_end(p, first, dst, count);
+}
+
+static uint64_t pof2_floor(uint64_t v)
+{
+	uint64_t q = 1;
+
+	while (q * 2 <= v)
+		q *= 2;
+	return q;
+}
+
+/*
+ * The reference's recursive-doubling schedule, item for item
+ * (coll_do_allreduce, coll_coll.c:349-449), into `res` with `tmp` scratch.
+ */
+static void plan_rd_allreduce(struct planner *p, uint64_t local, uint64_t n,
+			      size_t count, size_t esz, struct lfa_ref res,
+			      struct lfa_ref tmp)
+{
+	uint64_t pof2 = pof2_floor(n), rem = n - pof2, newid, mask;
+	uint64_t bytes = (uint64_t)count * esz;
+
+	p_copy(p, res, ref(LFA_BUF_SEND, 0), bytes);        /* :364 memcpy */
+	if (local < 2 * rem) {
+		if (local % 2 == 0) {
+			p_xfer(p, LFA_STEP_SEND, (int)local + 1, res, bytes);
+			p_group_end(p);
+			newid = (uint64_t)-1;
+		} else {
+			p_xfer(p, LFA_STEP_RECV, (int)local - 1, tmp, bytes);
+			p_group_end(p);
+			p_reduce(p, res, tmp, count);       /* result = result OP tmp */
+			newid = local / 2;
+		}
+	} else {
+		newid = local - rem;
+	}
+	if (newid != (uint64_t)-1) {
+		for (mask = 1; mask < pof2; mask <<= 1) {
+			uint64_t nr = newid ^ mask;
+			uint64_t remote = nr < rem ? nr * 2 + 1 : nr + rem;
+
+			p_xfer(p, LFA_STEP_RECV, (int)remote, tmp, bytes);
+			p_xfer(p, LFA_STEP_SEND, (int)remote, res, bytes);
+			p_group_end(p);
+			if (remote < local) {
+				p_reduce(p, res, tmp, count);
+			} else {
+				p_reduce(p, tmp, res, count);
+				p_copy(p, res, tmp, bytes);
+			}
+		}
+	}
+	if (local < 2 * rem) {
+		if (local % 2)
+			p_xfer(p, LFA_STEP_SEND, (int)local - 1, res, bytes);
+		else
+			p_xfer(p, LFA_STEP_RECV, (int)local + 1, res, bytes);
+		p_group_end(p);
+	}
+}
+
+int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
+		  int rank, int nranks, int root, size_t count, size_t esz,
+		  struct lfa_step *steps, size_t *nsteps, struct lfa_ref *refs,
+		  size_t *nrefs, size_t *tmp_bytes)
+{
+	struct planner p;
+	size_t moff, mlen, bytes = count * esz;
+	int r = rank, n = nranks;
+
+	if (!nsteps || !nrefs || !tmp_bytes || n < 1 || r < 0 || r >= n || !esz)
+		return -LFA_EINVAL;
+	if ((coll == LFA_REDUCE || coll == LFA_BROADCAST || coll == LFA_SCATTER) &&
+	    (root < 0 || root >= n))
+		return -LFA_EINVAL;
+	memset(&p, 0, sizeof(p));
+	p.steps = steps;
+	p.cap = steps ? *nsteps : 0;
+	p.refs = refs;
+	p.rcap = refs ? *nrefs : 0;
+	*tmp_bytes = 0;
+	lfa_coll_block(count, n, r, &moff, &mlen);
+
+	if (algo == LFA_ALGO_RCCL)
+		algo = LFA_ALGO_TREE;   /* the RCCL algo is not a schedule */
+	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD)
+		return -LFA_ENOSYS;
+
+	switch (coll) {
+	case LFA_ALLREDUCE:
+		if (algo == LFA_ALGO_RD) {
+			plan_rd_allreduce(&p, (uint64_t)r, (uint64_t)n, count, esz,
+					  ref(LFA_BUF_RESULT, 0), ref(LFA_BUF_TMP, 0));
+			*tmp_bytes = n > 1 ? bytes : 0;
+		} else if (n > 1 && bytes * (size_t)n <= LFA_SMALL_AG_BYTES) {
+			plan_allreduce_small(&p, r, n, count, esz,
+					     ref(LFA_BUF_RESULT, 0));
+			*tmp_bytes = (size_t)n * bytes;
+		} else {
+			plan_gather_blocks(&p, r, n, count, esz);
+			plan_tree_block(&p, r, n, count, esz,
+					ref(LFA_BUF_RESULT, moff * esz));
+			plan_allgather_blocks(&p, r, n, count, esz);
+			*tmp_bytes = n > 1 ? (size_t)n * mlen * esz : 0;
+		}
+		break;
+	case LFA_REDUCE_SCATTER:
+		if (algo == LFA_ALGO_RD) {
+			plan_rd_allreduce(&p, (uint64_t)r, (uint64_t)n, count, esz,
+					  ref(LFA_BUF_TMP, bytes), ref(LFA_BUF_TMP, 0));
+			p_copy(&p, ref(LFA_BUF_RESULT, 0),
+			       ref(LFA_BUF_TMP, bytes + moff * esz), mlen * esz);
+			*tmp_bytes = 2 * bytes;
+		} else {
+			plan_gather_blocks(&p, r, n, count, esz);
+			plan_tree_block(&p, r, n, count, esz, ref(LFA_BUF_RESULT, 0));
+			*tmp_bytes = n > 1 ? (size_t)n * mlen * esz : 0;
+		}
+		break;
+	case LFA_REDUCE:
+		if (algo == LFA_ALGO_RD) {
+			plan_rd_allreduce(&p, (uint64_t)r, (uint64_t)n, count, esz,
+					  ref(LFA_BUF_TMP, bytes), ref(LFA_BUF_TMP, 0));
+			if (r == root)
+				p_copy(&p, ref(LFA_BUF_RESULT, 0),
+				       ref(LFA_BUF_TMP, bytes), bytes);
+			*tmp_bytes = 2 * bytes;
+		} else {
+			size_t off, len;
+
+			plan_gather_blocks(&p, r, n, count, esz);
+			plan_tree_block(&p, r, n, count, esz,
+					r == root ? ref(LFA_BUF_RESULT, moff * esz) :
+					ref(LFA_BUF_TMP, (uint64_t)r * mlen * esz));
+			if (r != root) {
+				p_xfer(&p, LFA_STEP_SEND, root,
+				       ref(LFA_BUF_TMP, (uint64_t)r * mlen * esz),
+				       mlen * esz);
+			} else {
+				for (int k = 0; k < n; k++) {
+					if (k == root)
+						continue;
+					lfa_coll_block(count, n, k, &off, &len);
+					p_xfer(&p, LFA_STEP_RECV, k,
+					       ref(LFA_BUF_RESULT, off * esz), len * esz);
+				}
+			}
+			p_group_end(&p);
+			*tmp_bytes = n > 1 ? (size_t)n * mlen * esz : 0;
+		}
+		break;
+	case LFA_ALLGATHER:
+		for (int k = 1; k < n; k++) {
+			int to = (r + k) % n, from = (r - k + n) % n;
+
+			p_xfer(&p, LFA_STEP_SEND, to, ref(LFA_BUF_SEND, 0), bytes);
+			p_xfer(&p, LFA_STEP_RECV, from,
+			       ref(LFA_BUF_RESULT, (uint64_t)from * bytes), bytes);
+		}
+		p_group_end(&p);
+		p_copy(&p, ref(LFA_BUF_RESULT, (uint64_t)r * bytes),
+		       ref(LFA_BUF_SEND, 0), bytes);
+		break;
+	case LFA_BROADCAST:
+		/* buf is in/out: the executor binds SEND and RESULT to it */
+		if (r == root) {
+			for (int k = 1; k < n; k++)
+				p_xfer(&p, LFA_STEP_SEND, (root + k) % n,
+				       ref(LFA_BUF_RESULT, 0), bytes);
+		} else {
+			p_xfer(&p, LFA_STEP_RECV, root, ref(LFA_BUF_RESULT, 0), bytes);
+		}
+		p_group_end(&p);
+		break;
+	case LFA_SCATTER: {
+		/* root's buf holds n blocks of `count`; everyone gets block r */
+		if (r == root) {
+			for (int k = 1; k < n; k++) {
+				int to = (root + k) % n;
+
+				p_xfer(&p, LFA_STEP_SEND, to,
+				       ref(LFA_BUF_SEND, (uint64_t)to * bytes), bytes);
+			}
+		} else {
+			p_xfer(&p, LFA_STEP_RECV, root, ref(LFA_BUF_RESULT, 0), bytes);
+		}
+		p_group_end(&p);
+		if (r == root)
+			p_copy(&p, ref(LFA_BUF_RESULT, 0),
+			       ref(LFA_BUF_SEND, (uint64_t)r * bytes), bytes);
+		break;
+	}
+	default:
+		return -LFA_ENOSYS;
+	}
+	p_group_end(&p);
+
+	*nsteps = p.n;
+	*nrefs = p.nr;
+	if (!steps || !refs)
+		return 0;               /* size query */
+	if (p.n > p.cap || p.nr > p.rcap)
+		return -LFA_ETOOSMALL;
+	return 0;
+}
+
+/* A heap-allocated plan. */
+struct plan {
+	struct lfa_step *steps;
+	struct lfa_ref *refs;
+	size_t nsteps, nrefs, tmp;
+};
+
+static void plan_free(struct plan *pl)
+{
+	free(pl->steps);
+	free(pl->refs);
+	memset(pl, 0, sizeof(*pl));
+}
+
+static int plan_make(struct plan *pl, enum lfa_collective_op coll,
+		     enum lfa_coll_algo algo, int rank, int n, int root,
+		     size_t count, size_t esz)
+{
+	size_t ns = 0, nr = 0;
+	int ret;
+
+	memset(pl, 0, sizeof(*pl));
+	ret = lfa_coll_plan(coll, algo, rank, n, root, count, esz, NULL, &ns,
+			    NULL, &nr, &pl->tmp);
+	if (ret)
+		return ret;
+	pl->steps = calloc(ns ? ns : 1, sizeof(*pl->steps));
+	pl->refs = calloc(nr ? nr : 1, sizeof(*pl->refs));
+	if (!pl->steps || !pl->refs) {
+		plan_free(pl);
+		return -LFA_ENOMEM;
+	}
+	pl->nsteps = ns;
+	pl->nrefs = nr;
+	ret = lfa_coll_plan(coll, algo, rank, n, root, count, esz, pl->steps,
+			    &pl->nsteps, pl->refs, &pl->nrefs, &pl->tmp);
+	if (ret)
+		plan_free(pl);
+	return ret;
+}
+
+/* ====================================================================== */
+/* device helpers                                                          */
+/* ====================================================================== */
+
+static void *resolve(void *const base[3], struct lfa_ref r)
+{
+	return (char *)base[r.buf] + r.off;
+}
+
+/* Non-communication step on `stream`. */
+static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
+		     void *const base[3], enum lfa_op op,
+		     enum lfa_datatype dt, hipStream_t stream)
+{
+	switch (s->type) {
+	case LFA_STEP_REDUCE:
+		return lfa_atomic_write_async(op, dt, resolve(base, s->dst),
+					      resolve(base, s->src), s->count,
+					      stream);
+	case LFA_STEP_TREE: {
+		const void *srcs[LFA_TREE_MAX];
+
+		if (s->nsrc > LFA_TREE_MAX)
+			return -LFA_EINVAL;
+		for (uint32_t k = 0; k < s->nsrc; k++)
+			srcs[k] = resolve(base, refs[s->first + k]);
+		return lfa_reduce_tree_async(op, dt, resolve(base, s->dst), srcs,
+					     (int)s->nsrc, s->count, stream);
+	}
+	case LFA_STEP_COPY:
+		return hipMemcpyAsync(resolve(base, s->dst), resolve(base, s->src),
+				      s->count, hipMemcpyDeviceToDevice,
+				      stream) == hipSuccess ? 0 : -LFA_EIO;
+	default:
+		return -LFA_EINVAL;
+	}
+}
+
+static int is_device_ptr(const void *p)
+{
+	hipPointerAttribute_t a;
+
+	if (!p)
+		return 0;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+/* ====================================================================== */
+/* domain / endpoint                                                       */
+/* ====================================================================== */
+
+struct lfa_coll_mc {
+	struct lfa_coll_ep *ep;
+	ncclComm_t comm;
+	int owns_comm;
+	int rank, size;
+	uint16_t group_id;
+	uint16_t seq;
+	int is_world;
+	/* join in flight */
+	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
+	void *join_context;
+};
+
+struct lfa_coll_domain {
+	int device, rank, nranks;
+	ncclComm_t comm;
+};
+
+struct pending {
+	hipEvent_t ev;
+	void *context;
+	int kind;               /* 0 collective, 1 join */
+	struct lfa_coll_mc *mc;
+};
+
+struct lfa_coll_ep {
+	struct lfa_coll_domain *dom;
+	pthread_mutex_t lock;
+	hipStream_t stream;         /* executor stream (RCCL + kernels) */
+	hipStream_t copy_stream;    /* host staging copies */
+	enum lfa_coll_algo algo;
+	size_t chunk;
+	void *ws;                   /* device workspace */
+	size_t ws_size;
+	void *hs[2];                /* device staging for host buffers */
+	size_t hs_size;
+	uint64_t *barrier_host;     /* pinned ~rank for barrier */
+	void *barrier_dev;          /* 2 x uint64 */
+	uint8_t cid_mask[LFA_CID_BYTES];
+	struct lfa_coll_mc world;
+	struct pending *q;          /* FIFO ring of in-flight ops */
+	size_t qcap, qhead, qlen;
+	struct lfa_cq_err_entry err;
+	int have_err;
+	struct { uint32_t event; struct lfa_eq_entry entry; } eq[64];
+	size_t eqh, eqn;
+};
+
+int lfa_coll_get_unique_id(void *id, size_t len)
+{
+	ncclUniqueId uid;
+
+	if (!id || len < sizeof(uid) || sizeof(uid) > LFA_UNIQUE_ID_BYTES)
+		return -LFA_EINVAL;
+	if (ncclGetUniqueId(&uid) != ncclSuccess)
+		return -LFA_EIO;
+	memset(id, 0, len);
+	memcpy(id, &uid, sizeof(uid));
+	return 0;
+}
+
+int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
+			 size_t id_len, struct lfa_coll_domain **domain)
+{
+	struct lfa_coll_domain *d;
+	ncclUniqueId uid;
+
+	if (!domain || !id || id_len < sizeof(uid) || nranks < 1 || rank < 0 ||
+	    rank >= nranks)
+		return -LFA_EINVAL;
+	if (hipSetDevice(device) != hipSuccess)
+		return -LFA_EINVAL;
+	d = calloc(1, sizeof(*d));
+	if (!d)
+		return -LFA_ENOMEM;
+	memcpy(&uid, id, sizeof(uid));
+	d->device = device;
+	d->rank = rank;
+	d->nranks = nranks;
+	if (ncclCommInitRank(&d->comm, nranks, uid, rank) != ncclSuccess) {
+		free(d);
+		return -LFA_EIO;
+	}
+	*domain = d;
+	return 0;
+}
+
+int lfa_coll_domain_close(struct lfa_coll_domain *d)
+{
+	if (!d)
+		return -LFA_EINVAL;
+	ncclCommDestroy(d->comm);
+	free(d);
+	return 0;
+}
+
+int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
+{
+	struct lfa_coll_ep *ep;
+
+	if (!d || !out)
+		return -LFA_EINVAL;
+	hipSetDevice(d->device);
+	ep = calloc(1, sizeof(*ep));
+	if (!ep)
+		return -LFA_ENOMEM;
+	ep->dom = d;
+	pthread_mutex_init(&ep->lock, NULL);
+	ep->algo = LFA_ALGO_TREE;
+	ep->chunk = LFA_DEFAULT_CHUNK;
+	if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
+	    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess) {
+		free(ep);
+		return -LFA_EIO;
+	}
+	ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
+	memset(ep->cid_mask, 0xff, sizeof(ep->cid_mask));
+	ep->cid_mask[0] &= (uint8_t)~1u;            /* world group id 0 taken */
+	ep->world.ep = ep;
+	ep->world.comm = d->comm;
+	ep->world.rank = d->rank;
+	ep->world.size = d->nranks;
+	ep->world.is_world = 1;
+	ep->qcap = 256;
+	ep->q = calloc(ep->qcap, sizeof(*ep->q));
+	if (!ep->q) {
+		free(ep);
+		return -LFA_ENOMEM;
+	}
+	*out = ep;
+	return 0;
+}
+
+int lfa_coll_ep_close(struct lfa_coll_ep *ep)
+{
+	if (!ep)
+		return -LFA_EINVAL;
+	lfa_coll_ep_flush(ep);
+	for (size_t i = 0; i < ep->qlen; i++)
+		hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
+	free(ep->q);
+	if (ep->ws)
+		hipFree(ep->ws);
+	for (int i = 0; i < 2; i++)
+		if (ep->hs[i])
+			hipFree(ep->hs[i]);
+	hipFree(ep->barrier_dev);
+	hipHostFree(ep->barrier_host);
+	hipStreamDestroy(ep->stream);
+	hipStreamDestroy(ep->copy_stream);
+	pthread_mutex_destroy(&ep->lock);
+	free(ep);
+	return 0;
+}
+
+void *lfa_coll_ep_stream(struct lfa_coll_ep *ep)
+{
+	return ep ? (void *)ep->stream : NULL;
+}
+
+int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo)
+{
+	if (!ep || (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
+		    algo != LFA_ALGO_RCCL))
+		return -LFA_EINVAL;
+	ep->algo = algo;
+	return 0;
+}
+
+int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes)
+{
+	if (!ep)
+		return -LFA_EINVAL;
+	ep->chunk = bytes ? bytes : LFA_DEFAULT_CHUNK;
+	return 0;
+}
+
+lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep)
+{
+	return ep ? (lfa_addr_t)(uintptr_t)&ep->world : LFA_ADDR_NOTAVAIL;
+}
+
+lfa_addr_t lfa_mc_addr(struct lfa_coll_mc *mc)
+{
+	return (lfa_addr_t)(uintptr_t)mc;
+}
+
+static struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a)
+{
+	if (a == LFA_ADDR_NOTAVAIL || a == 0)
+		return &ep->world;
+	return (struct lfa_coll_mc *)(uintptr_t)a;
+}
+
+/* Grow-only device buffer, stream-ordered so in-flight users stay valid. */
+static int grow(void **buf, size_t *size, size_t need, hipStream_t s)
+{
+	void *nb;
+
+	if (need <= *size)
+		return 0;
+	need = (need + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+	if (hipMallocAsync(&nb, need, s) != hipSuccess)
+		return -LFA_ENOMEM;
+	if (*buf)
+		hipFreeAsync(*buf, s);
+	*buf = nb;
+	*size = need;
+	return 0;
+}
+
+/* Both host-staging slots, always the same size. */
+static int grow_staging(struct lfa_coll_ep *ep, size_t need)
+{
+	void *nb[2];
+
+	if (need <= ep->hs_size)
+		return 0;
+	need = (need + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+	for (int i = 0; i < 2; i++) {
+		if (hipMallocAsync(&nb[i], need, ep->stream) != hipSuccess) {
+			if (i)
+				hipFreeAsync(nb[0], ep->stream);
+			return -LFA_ENOMEM;
+		}
+	}
+	for (int i = 0; i < 2; i++) {
+		if (ep->hs[i])
+			hipFreeAsync(ep->hs[i], ep->stream);
+		ep->hs[i] = nb[i];
+	}
+	ep->hs_size = need;
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* completion queue                                                        */
+/* ---------------------------------------------------------------------- */
+
+static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
+			      void *context, int kind, struct lfa_coll_mc *mc)
+{
+	struct pending *p;
+
+	if (ep->qlen == ep->qcap) {
+		struct pending *nq = calloc(ep->qcap * 2, sizeof(*nq));
+
+		if (!nq)
+			return -LFA_ENOMEM;
+		for (size_t i = 0; i < ep->qlen; i++)
+			nq[i] = ep->q[(ep->qhead + i) % ep->qcap];
+		free(ep->q);
+		ep->q = nq;
+		ep->qhead = 0;
+		ep->qcap *= 2;
+	}
+	p = &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
+	if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess)
+		return -LFA_EIO;
+	if (hipEventRecord(p->ev, s) != hipSuccess) {
+		hipEventDestroy(p->ev);
+		return -LFA_EIO;
+	}
+	p->context = context;
+	p->kind = kind;
+	p->mc = mc;
+	ep->qlen++;
+	return 0;
+}
+
+static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
+{
+	/* coll_join_comp (coll_coll.c:690-720): group id = lowest set bit of the
+	 * BAND of every member's free-id mask; mark it used locally. */
+	int gid = -1;
+
+	for (int b = 0; b < LFA_MAX_GROUP_ID; b++) {
+		if (mc->mask_host[b / 8] & (1u << (b % 8))) {
+			gid = b;
+			break;
+		}
+	}
+	if (gid >= 0) {
+		mc->group_id = (uint16_t)gid;
+		ep->cid_mask[gid / 8] &= (uint8_t)~(1u << (gid % 8));
+	}
+	mc->seq = 0;
+	hipHostFree(mc->mask_host);
+	mc->mask_host = NULL;
+	if (ep->eqn < 64) {
+		size_t i = (ep->eqh + ep->eqn) % 64;
+
+		ep->eq[i].event = LFA_JOIN_COMPLETE;
+		ep->eq[i].entry.fid = mc;
+		ep->eq[i].entry.context = mc->join_context;
+		ep->eq[i].entry.data = 0;
+		ep->eqn++;
+	}
+}
+
+/* Reap completed operations in issue order. */
+static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
+		     size_t count, size_t *nout)
+{
+	*nout = 0;
+	while (ep->qlen && !ep->have_err) {
+		struct pending *p = &ep->q[ep->qhead];
+		hipError_t e = hipEventQuery(p->ev);
+
+		if (e == hipErrorNotReady)
+			break;
+		if (p->kind == 0 && e == hipSuccess && *nout >= count)
+			break;
+		if (e != hipSuccess) {
+			ep->err.op_context = p->context;
+			ep->err.flags = LFA_COLLECTIVE;
+			ep->err.err = LFA_EIO;
+			ep->err.prov_errno = (int)e;
+			ep->have_err = 1;
+		} else if (p->kind == 1) {
+			join_finish(ep, p->mc);
+		} else {
+			struct lfa_cq_entry *c = &out[(*nout)++];
+
+			memset(c, 0, sizeof(*c));
+			c->op_context = p->context;
+			c->flags = LFA_COLLECTIVE;
+		}
+		hipEventDestroy(p->ev);
+		ep->qhead = (ep->qhead + 1) % ep->qcap;
+		ep->qlen--;
+	}
+}
+
+ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
+		    size_t count)
+{
+	size_t n;
+	ncclResult_t async;
+
+	if (!ep || (!buf && count))
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	progress(ep, buf, count, &n);
+	if (!n && !ep->have_err &&
+	    ncclCommGetAsyncError(ep->dom->comm, &async) == ncclSuccess &&
+	    async != ncclSuccess && async != ncclInProgress) {
+		ep->err.op_context = ep->qlen ? ep->q[ep->qhead].context : NULL;
+		ep->err.flags = LFA_COLLECTIVE;
+		ep->err.err = LFA_EIO;
+		ep->err.prov_errno = (int)async;
+		ep->have_err = 1;
+	}
+	pthread_mutex_unlock(&ep->lock);
+	if (n)
+		return (ssize_t)n;
+	return ep->have_err ? -LFA_EIO : -LFA_EAGAIN;
+}
+
+ssize_t lfa_cq_readerr(struct lfa_coll_ep *ep, struct lfa_cq_err_entry *buf)
+{
+	ssize_t ret = -LFA_EAGAIN;
+
+	if (!ep || !buf)
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	if (ep->have_err) {
+		*buf = ep->err;
+		ep->have_err = 0;
+		ret = 1;
+	}
+	pthread_mutex_unlock(&ep->lock);
+	return ret;
+}
+
+ssize_t lfa_eq_read(struct lfa_coll_ep *ep, uint32_t *event,
+		    struct lfa_eq_entry *entry)
+{
+	struct lfa_cq_entry tmp[1];
+	size_t n;
+	ssize_t ret = -LFA_EAGAIN;
+
+	if (!ep || !event || !entry)
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	/* progress joins only up to the first collective completion */
+	while (ep->qlen && ep->q[ep->qhead].kind == 1 && !ep->have_err) {
+		progress(ep, tmp, 0, &n);
+		if (ep->qlen && ep->q[ep->qhead].kind == 1 &&
+		    hipEventQuery(ep->q[ep->qhead].ev) == hipErrorNotReady)
+			break;
+	}
+	if (ep->eqn) {
+		*event = ep->eq[ep->eqh].event;
+		*entry = ep->eq[ep->eqh].entry;
+		ep->eqh = (ep->eqh + 1) % 64;
+		ep->eqn--;
+		ret = (ssize_t)sizeof(*entry);
+	}
+	pthread_mutex_unlock(&ep->lock);
+	return ret;
+}
+
+int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
+{
+	if (!ep)
+		return -LFA_EINVAL;
+	return hipStreamSynchronize(ep->stream) == hipSuccess &&
+	       hipStreamSynchronize(ep->copy_stream) == hipSuccess ? 0 : -LFA_EIO;
+}
+
+/* ---------------------------------------------------------------------- */
+/* executor: schedule -> RCCL + kernels on the endpoint stream             */
+/* ---------------------------------------------------------------------- */
+
+static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
+		     void *const base[3], enum lfa_op op, enum lfa_datatype dt,
+		     hipStream_t s)
+{
+	int in_group = 0, ret = 0;
+
+	for (size_t i = 0; i < pl->nsteps && !ret; i++) {
+		const struct lfa_step *st = &pl->steps[i];
+
+		switch (st->type) {
+		case LFA_STEP_SEND:
+		case LFA_STEP_RECV:
+			if (!in_group) {
+				if (ncclGroupStart() != ncclSuccess)
+					return -LFA_EIO;
+				in_group = 1;
+			}
+			if (st->type == LFA_STEP_SEND)
+				ret = ncclSend(resolve(base, st->src), st->count, ncclUint8,
+					       st->peer, mc->comm, s) == ncclSuccess ?
+				      0 : -LFA_EIO;
+			else
+				ret = ncclRecv(resolve(base, st->dst), st->count, ncclUint8,
+					       st->peer, mc->comm, s) == ncclSuccess ?
+				      0 : -LFA_EIO;
+			break;
+		case LFA_STEP_GROUP_END:
+			if (in_group && ncclGroupEnd() != ncclSuccess)
+				return -LFA_EIO;
+			in_group = 0;
+			break;
+		default:
+			ret = run_local(st, pl->refs, base, op, dt, s);
+		}
+	}
+	if (in_group && ncclGroupEnd() != ncclSuccess && !ret)
+		ret = -LFA_EIO;
+	return ret;
+}
+
+static int rccl_type(enum lfa_datatype dt, ncclDataType_t *t)
+{
+	switch (dt) {
+	case LFA_INT8: *t = ncclInt8; return 1;
+	case LFA_UINT8: *t = ncclUint8; return 1;
+	case LFA_INT32: *t = ncclInt32; return 1;
+	case LFA_UINT32: *t = ncclUint32; return 1;
+	case LFA_INT64: *t = ncclInt64; return 1;
+	case LFA_UINT64: *t = ncclUint64; return 1;
+	case LFA_FLOAT: *t = ncclFloat32; return 1;
+	case LFA_DOUBLE: *t = ncclFloat64; return 1;
+	default: return 0;
+	}
+}
+
+static int rccl_op(enum lfa_op op, ncclRedOp_t *o)
+{
+	switch (op) {
+	case LFA_SUM: *o = ncclSum; return 1;
+	case LFA_PROD: *o = ncclProd; return 1;
+	case LFA_MIN: *o = ncclMin; return 1;
+	case LFA_MAX: *o = ncclMax; return 1;
+	default: return 0;
+	}
+}
+
+/* LFA_ALGO_RCCL for one device-resident operation; 1 = handled. */
+static int try_rccl(struct lfa_coll_mc *mc, enum lfa_collective_op coll,
+		    const void *buf, void *result, size_t count, int root,
+		    enum lfa_datatype dt, enum lfa_op op, hipStream_t s, int *ret)
+{
+	ncclDataType_t t;
+	ncclRedOp_t o;
+	ncclResult_t r;
+
+	if (!rccl_type(dt, &t) || !rccl_op(op, &o))
+		return 0;
+	switch (coll) {
+	case LFA_ALLREDUCE:
+		r = ncclAllReduce(buf, result, count, t, o, mc->comm, s);
+		break;
+	case LFA_REDUCE_SCATTER:
+		if (count % (size_t)mc->size)
+			return 0;   /* ragged blocks: use the tree schedule */
+		r = ncclReduceScatter(buf, result, count / (size_t)mc->size, t, o,
+				      mc->comm, s);
+		break;
+	case LFA_REDUCE:
+		r = ncclReduce(buf, result, count, t, o, root, mc->comm, s);
+		break;
+	default:
+		return 0;
+	}
+	*ret = r == ncclSuccess ? 0 : -LFA_EIO;
+	return 1;
+}
+
+/*
+ * One operation on device buffers, enqueued on ep->stream.
+ */
+static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+		      enum lfa_collective_op coll, const void *buf, void *result,
+		      size_t count, int root, enum lfa_datatype dt,
+		      enum lfa_op op, hipStream_t s)
+{
+	struct plan pl;
+	size_t esz = lfa_datatype_size(dt);
+	void *base[3];
+	int ret;
+
+	if (ep->algo == LFA_ALGO_RCCL && mc->size > 1 &&
+	    try_rccl(mc, coll, buf, result, count, root, dt, op, s, &ret))
+		return ret;
+	ret = plan_make(&pl, coll, ep->algo, mc->rank, mc->size, root, count, esz);
+	if (ret)
+		return ret;
+	ret = grow(&ep->ws, &ep->ws_size, pl.tmp, s);
+	if (!ret) {
+		base[LFA_BUF_SEND] = (void *)buf;
+		base[LFA_BUF_RESULT] = result;
+		base[LFA_BUF_TMP] = ep->ws;
+		ret = exec_plan(mc, &pl, base, op, dt, s);
+	}
+	plan_free(&pl);
+	return ret;
+}
+
+/*
+ * Host buffers: stream chunks through HBM.  Chunk c's H2D (copy stream)
+ * overlaps chunk c-1's collective (executor stream) and its D2H; two staging
+ * slots, ordered with events.  Valid for the element-wise collectives
+ * (allreduce, broadcast), where chunks are independent.
+ */
+static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			    enum lfa_collective_op coll, const void *buf,
+			    void *result, size_t count, int root,
+			    enum lfa_datatype dt, enum lfa_op op)
+{
+	size_t esz = lfa_datatype_size(dt);
+	size_t per = ep->chunk / esz, off = 0;
+	hipEvent_t h2d[2], done[2];
+	int ret = 0, slot = 0;
+
+	if (!per)
+		per = 1;
+	if (per > count)
+		per = count;
+	if (grow_staging(ep, 2 * per * esz))
+		return -LFA_ENOMEM;
+	for (int i = 0; i < 2; i++) {
+		hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming);
+		hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
+		hipEventRecord(done[i], ep->stream);
+	}
+	while (off < count && !ret) {
+		size_t n = count - off < per ? count - off : per;
+		char *din = ep->hs[slot], *dout = din + per * esz;
+
+		/* slot reuse: wait until chunk c-2's D2H finished */
+		hipStreamWaitEvent(ep->copy_stream, done[slot], 0);
+		if (coll != LFA_BROADCAST || mc->rank == root)
+			hipMemcpyAsync(din, (const char *)buf + off * esz, n * esz,
+				       hipMemcpyHostToDevice, ep->copy_stream);
+		hipEventRecord(h2d[slot], ep->copy_stream);
+		hipStreamWaitEvent(ep->stream, h2d[slot], 0);
+		if (coll == LFA_BROADCAST)
+			ret = run_device(ep, mc, coll, din, din, n, root, dt, op,
+					 ep->stream);
+		else
+			ret = run_device(ep, mc, coll, din, dout, n, root, dt, op,
+					 ep->stream);
+		hipEventRecord(h2d[slot], ep->stream);
+		hipStreamWaitEvent(ep->copy_stream, h2d[slot], 0);
+		hipMemcpyAsync((char *)result + off * esz,
+			       coll == LFA_BROADCAST ? din : dout, n * esz,
+			       hipMemcpyDeviceToHost, ep->copy_stream);
+		hipEventRecord(done[slot], ep->copy_stream);
+		off += n;
+		slot ^= 1;
+	}
+	/* the operation completes when the last D2H lands */
+	hipStreamWaitEvent(ep->stream, done[slot ^ 1], 0);
+	for (int i = 0; i < 2; i++) {
+		hipEventDestroy(h2d[i]);
+		hipEventDestroy(done[i]);
+	}
+	return ret;
+}
+
+/* Host buffers for non-elementwise collectives: whole-buffer staging. */
+static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			  enum lfa_collective_op coll, const void *buf,
+			  size_t in_bytes, void *result, size_t out_bytes,
+			  size_t count, int root, enum lfa_datatype dt,
+			  enum lfa_op op)
+{
+	char *din, *dout;
+	int ret;
+
+	if (grow_staging(ep, in_bytes + out_bytes + 32))
+		return -LFA_ENOMEM;
+	din = ep->hs[0];
+	dout = din + ((in_bytes + 15) & ~(size_t)15);
+	if (buf && in_bytes)
+		hipMemcpyAsync(din, buf, in_bytes, hipMemcpyHostToDevice, ep->stream);
+	ret = run_device(ep, mc, coll, din, dout, count, root, dt, op, ep->stream);
+	if (!ret && result && out_bytes)
+		hipMemcpyAsync(result, dout, out_bytes, hipMemcpyDeviceToHost,
+			       ep->stream);
+	return ret;
+}
+
+static int check_reduce_args(enum lfa_datatype dt, enum lfa_op op)
+{
+	if (op < LFA_MIN || op > LFA_BXOR)
+		return -LFA_ENOSYS;   /* coll_process_reduce_item :760-761 */
+	if (lfa_atomic_valid(dt, op, 0))
+		return -LFA_EOPNOTSUPP;
+	return 0;
+}
+
+static int group_rank(struct lfa_coll_mc *mc, lfa_addr_t a)
+{
+	/* root_addr is a group rank (the reference indexes fi_addr_array by
+	 * rank, coll_coll.c:782) */
+	if (a >= (lfa_addr_t)mc->size)
+		return -1;
+	return (int)a;
+}
+
+static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
+		      const void *buf, size_t count, void *result,
+		      lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		      enum lfa_datatype dt, enum lfa_op op, void *context)
+{
+	struct lfa_coll_mc *mc;
+	size_t esz;
+	int root = -1, ret, host;
+
+	if (!ep)
+		return -LFA_EINVAL;
+	mc = mc_of(ep, coll_addr);
+	if (!mc || !mc->comm)
+		return -LFA_EINVAL;
+	esz = lfa_datatype_size(dt);
+	if (!esz)
+		return -LFA_EINVAL;
+	if (coll == LFA_REDUCE || coll == LFA_BROADCAST || coll == LFA_SCATTER) {
+		root = group_rank(mc, root_addr);
+		if (root < 0)
+			return -LFA_EINVAL;
+	}
+	if (coll == LFA_ALLREDUCE || coll == LFA_REDUCE ||
+	    coll == LFA_REDUCE_SCATTER) {
+		ret = check_reduce_args(dt, op);
+		if (ret)
+			return ret;
+	}
+	pthread_mutex_lock(&ep->lock);
+	hipSetDevice(ep->dom->device);
+	mc->seq++;                              /* coll_get_next_id :48-52 */
+	host = (buf && count && !is_device_ptr(buf)) ||
+	       (result && count && !is_device_ptr(result));
+	if (!count) {
+		ret = 0;
+	} else if (!host) {
+		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
+				 ep->stream);
+	} else if (coll == LFA_ALLREDUCE || coll == LFA_BROADCAST) {
+		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
+				       op);
+	} else {
+		size_t moff, mlen, in_b = count * esz, out_b = count * esz;
+
+		lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
+		if (coll == LFA_REDUCE_SCATTER)
+			out_b = mlen * esz;
+		else if (coll == LFA_ALLGATHER)
+			out_b = (size_t)mc->size * count * esz;
+		else if (coll == LFA_SCATTER)
+			in_b = mc->rank == root ? (size_t)mc->size * count * esz : 0;
+		else if (coll == LFA_REDUCE && mc->rank != root)
+			out_b = 0;
+		ret = run_host_whole(ep, mc, coll, buf, in_b, result, out_b, count,
+				     root, dt, op);
+	}
+	if (!ret)
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+	pthread_mutex_unlock(&ep->lock);
+	return ret;
+}
+
+ssize_t lfa_allreduce(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		      void *desc, void *result, void *result_desc,
+		      lfa_addr_t coll_addr, enum lfa_datatype datatype,
+		      enum lfa_op op, uint64_t flags, void *context)
+{
+	(void)desc; (void)result_desc; (void)flags;
+	if (count && (!buf || !result))
+		return -LFA_EINVAL;
+	return submit(ep, LFA_ALLREDUCE, buf, count, result, coll_addr, 0,
+		      datatype, op, context);
+}
+
+ssize_t lfa_reduce_scatter(struct lfa_coll_ep *ep, const void *buf,
+			   size_t count, void *desc, void *result,
+			   void *result_desc, lfa_addr_t coll_addr,
+			   enum lfa_datatype datatype, enum lfa_op op,
+			   uint64_t flags, void *context)
+{
+	(void)desc; (void)result_desc; (void)flags;
+	if (count && (!buf || !result))
+		return -LFA_EINVAL;
+	return submit(ep, LFA_REDUCE_SCATTER, buf, count, result, coll_addr, 0,
+		      datatype, op, context);
+}
+
+ssize_t lfa_reduce(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		   void *desc, void *result, void *result_desc,
+		   lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		   enum lfa_datatype datatype, enum lfa_op op, uint64_t flags,
+		   void *context)
+{
+	(void)desc; (void)result_desc; (void)flags;
+	if (count && !buf)
+		return -LFA_EINVAL;
+	return submit(ep, LFA_REDUCE, buf, count, result, coll_addr, root_addr,
+		      datatype, op, context);
+}
+
+ssize_t lfa_allgather(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		      void *desc, void *result, void *result_desc,
+		      lfa_addr_t coll_addr, enum lfa_datatype datatype,
+		      uint64_t flags, void *context)
+{
+	(void)desc; (void)result_desc; (void)flags;
+	if (count && (!buf || !result))
+		return -LFA_EINVAL;
+	return submit(ep, LFA_ALLGATHER, buf, count, result, coll_addr, 0,
+		      datatype, LFA_NOOP, context);
+}
+
+ssize_t lfa_broadcast(struct lfa_coll_ep *ep, void *buf, size_t count,
+		      void *desc, lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		      enum lfa_datatype datatype, uint64_t flags, void *context)
+{
+	(void)desc; (void)flags;
+	if (count && !buf)
+		return -LFA_EINVAL;
+	return submit(ep, LFA_BROADCAST, buf, count, buf, coll_addr, root_addr,
+		      datatype, LFA_NOOP, context);
+}
+
+ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
+{
+	/* coll_ep_barrier2 (coll_coll.c:997-1033): an allreduce of ~rank with
+	 * FI_BAND over one uint64. */
+	struct lfa_coll_mc *mc;
+	int ret;
+
+	if (!ep)
+		return -LFA_EINVAL;
+	mc = mc_of(ep, coll_addr);
+	pthread_mutex_lock(&ep->lock);
+	hipSetDevice(ep->dom->device);
+	ep->barrier_host[0] = ~(uint64_t)mc->rank;
+	ret = hipMemcpyAsync(ep->barrier_dev, ep->barrier_host, sizeof(uint64_t),
+			     hipMemcpyHostToDevice, ep->stream) == hipSuccess ?
+	      0 : -LFA_EIO;
+	if (!ret)
+		ret = run_device(ep, mc, LFA_ALLREDUCE, ep->barrier_dev,
+				 (uint64_t *)ep->barrier_dev + 1, 1, -1, LFA_UINT64,
+				 LFA_BAND, ep->stream);
+	if (!ret)
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+	pthread_mutex_unlock(&ep->lock);
+	return ret;
+}
+
+/* ---------------------------------------------------------------------- */
+/* join                                                                    */
+/* ---------------------------------------------------------------------- */
+
+int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+			const int *ranks, size_t nmembers, uint64_t flags,
+			struct lfa_coll_mc **mcp, void *context)
+{
+	struct lfa_coll_mc *parent, *mc;
+	int member = 0, pos = -1, ret;
+	void *dmask;
+
+	if (!ep || !mcp)
+		return -LFA_EINVAL;
+	if (flags & ~LFA_COLLECTIVE)
+		return -LFA_EBADFLAGS;
+	parent = mc_of(ep, coll_addr);
+	if (ranks) {
+		for (size_t i = 0; i < nmembers; i++) {
+			if (ranks[i] < 0 || ranks[i] >= parent->size ||
+			    (i && ranks[i] <= ranks[i - 1]))
+				return -LFA_EINVAL;
+			if (ranks[i] == parent->rank) {
+				member = 1;
+				pos = (int)i;
+			}
+		}
+	} else {
+		member = 1;
+		pos = parent->rank;
+		nmembers = (size_t)parent->size;
+	}
+	mc = calloc(1, sizeof(*mc));
+	if (!mc)
+		return -LFA_ENOMEM;
+	mc->ep = ep;
+	mc->join_context = context;
+	pthread_mutex_lock(&ep->lock);
+	hipSetDevice(ep->dom->device);
+	if (!ranks) {
+		mc->comm = parent->comm;
+		mc->rank = parent->rank;
+		mc->size = parent->size;
+	} else {
+		/* every parent rank takes part in the split (non-members with
+		 * NCCL_SPLIT_NOCOLOR) */
+		ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+
+		if (ncclCommSplit(parent->comm, member ? 0 : NCCL_SPLIT_NOCOLOR,
+				  parent->rank, &mc->comm, &cfg) != ncclSuccess) {
+			pthread_mutex_unlock(&ep->lock);
+			free(mc);
+			return -LFA_EIO;
+		}
+		mc->owns_comm = 1;
+		mc->rank = pos;
+		mc->size = (int)nmembers;
+	}
+	if (!member) {
+		pthread_mutex_unlock(&ep->lock);
+		free(mc);
+		*mcp = NULL;
+		return 0;
+	}
+	/* agree on the group id: BAND of the free-id masks over the PARENT
+	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 */
+	ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) == hipSuccess ?
+	      0 : -LFA_ENOMEM;
+	if (!ret && grow_staging(ep, 4 * LFA_CID_BYTES))
+		ret = -LFA_ENOMEM;
+	if (!ret) {
+		dmask = ep->hs[0];
+		memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
+		hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
+			       hipMemcpyHostToDevice, ep->stream);
+		ret = run_device(ep, parent, LFA_ALLREDUCE, dmask,
+				 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
+				 LFA_UINT8, LFA_BAND, ep->stream);
+		if (!ret)
+			hipMemcpyAsync(mc->mask_host, (char *)dmask + LFA_CID_BYTES,
+				       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
+	}
+	if (!ret)
+		ret = enqueue_completion(ep, ep->stream, context, 1, mc);
+	pthread_mutex_unlock(&ep->lock);
+	if (ret) {
+		if (mc->owns_comm)
+			ncclCommDestroy(mc->comm);
+		if (mc->mask_host)
+			hipHostFree(mc->mask_host);
+		free(mc);
+		return ret;
+	}
+	*mcp = mc;
+	return 0;
+}
+
+int lfa_mc_close(struct lfa_coll_mc *mc)
+{
+	if (!mc)
+		return -LFA_EINVAL;
+	if (mc->is_world)
+		return -LFA_EINVAL;
+	lfa_coll_ep_flush(mc->ep);
+	if (mc->owns_comm)
+		ncclCommDestroy(mc->comm);
+	if (mc->group_id < LFA_MAX_GROUP_ID)
+		mc->ep->cid_mask[mc->group_id / 8] |= (uint8_t)(1u << (mc->group_id % 8));
+	free(mc);
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* query (coll_query_collective, coll_coll.c:1267-1318)                     */
+/* ---------------------------------------------------------------------- */
+
+int lfa_query_collective(struct lfa_coll_domain *domain,
+			 enum lfa_collective_op coll,
+			 struct lfa_collective_attr *attr, uint64_t flags)
+{
+	int ret;
+	size_t esz;
+
+	(void)domain;
+	if (!attr || attr->mode != 0)
+		return -LFA_EINVAL;
+	switch (coll) {
+	case LFA_BARRIER:
+	case LFA_ALLGATHER:
+	case LFA_SCATTER:
+	case LFA_BROADCAST:
+		ret = 0;
+		break;
+	case LFA_ALLREDUCE:
+	case LFA_REDUCE_SCATTER:   /* new here: -FI_ENOSYS in the reference */
+	case LFA_REDUCE:
+		if (attr->op < LFA_MIN || attr->op > LFA_BXOR)
+			return -LFA_ENOSYS;
+		if (flags & LFA_TAGGED)
+			return -LFA_EINVAL;          /* rxm_atomic.c:505-509 */
+		ret = lfa_atomic_valid(attr->datatype, attr->op, flags);
+		if (ret)
+			return ret;
+		esz = lfa_datatype_size(attr->datatype);
+		attr->datatype_attr.size = esz;
+		/* limited by HBM, not by an eager buffer: 64 GiB per buffer */
+		attr->datatype_attr.count = (size_t)(64ULL << 30) / esz;
+		break;
+	case LFA_ALLTOALL:
+	case LFA_GATHER:
+	default:
+		return -LFA_ENOSYS;
+	}
+	attr->max_members = ~(0x80000000u);
+	return 0;
+}
+
+/* ====================================================================== */
+/* single-GPU multi-rank executor (loopback transport)                     */
+/* ====================================================================== */
+
+struct lb_msg {
+	struct lb_msg *next;
+	void *data;
+	size_t bytes;
+};
+
+int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
+		      int n, int root, enum lfa_datatype dt, enum lfa_op op,
+		      size_t count, void *const *send, void *const *result,
+		      void *stream)
+{
+	hipStream_t s = (hipStream_t)stream;
+	size_t esz = lfa_datatype_size(dt);
+	struct plan *pl = NULL;
+	size_t *pc = NULL;
+	void **tmp = NULL;
+	struct lb_msg **box = NULL;
+	int ret = 0, done, progressed;
+
+	if (n < 1 || n > 64 || !send || !result || !esz)
+		return -LFA_EINVAL;
+	if ((coll == LFA_ALLREDUCE || coll == LFA_REDUCE ||
+	     coll == LFA_REDUCE_SCATTER) && (ret = check_reduce_args(dt, op)))
+		return ret;
+	if (algo == LFA_ALGO_RCCL)
+		algo = LFA_ALGO_TREE;
+	pl = calloc((size_t)n, sizeof(*pl));
+	pc = calloc((size_t)n, sizeof(*pc));
+	tmp = calloc((size_t)n, sizeof(*tmp));
+	box = calloc((size_t)n * (size_t)n, sizeof(*box));
+	if (!pl || !pc || !tmp || !box) {
+		ret = -LFA_ENOMEM;
+		goto out;
+	}
+	for (int r = 0; r < n && !ret; r++) {
+		ret = plan_make(&pl[r], coll, algo, r, n, root, count, esz);
+		if (!ret && pl[r].tmp &&
+		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)
+			ret = -LFA_ENOMEM;
+	}
+	/*
+	 * Lockstep: a rank runs local steps freely; at a comm group it posts
+	 * all its SENDs (snapshot copies) and completes once every RECV of the
+	 * group has a message waiting — RCCL group semantics.
+	 */
+	do {
+		done = 1;
+		progressed = 0;
+		for (int r = 0; r < n && !ret; r++) {
+			void *base[3] = {send[r], result[r], tmp[r]};
+
+			if (coll == LFA_BROADCAST)
+				base[LFA_BUF_SEND] = result[r];
+			while (pc[r] < pl[r].nsteps && !ret) {
+				struct lfa_step *st = &pl[r].steps[pc[r]];
+
+				if (st->type != LFA_STEP_SEND && st->type != LFA_STEP_RECV &&
+				    st->type != LFA_STEP_GROUP_END) {
+					ret = run_local(st, pl[r].refs, base, op, dt, s);
+					pc[r]++;
+					progressed = 1;
+					continue;
+				}
+				/* a group: [pc, end) up to GROUP_END */
+				size_t end = pc[r];
+				int ready = 1;
+
+				while (end < pl[r].nsteps &&
+				       pl[r].steps[end].type != LFA_STEP_GROUP_END)
+					end++;
+				/* post sends once (mark by negating peer) */
+				for (size_t i = pc[r]; i < end; i++) {
+					struct lfa_step *x = &pl[r].steps[i];
+
+					if (x->type != LFA_STEP_SEND || x->peer < 0)
+						continue;
+					struct lb_msg *m = calloc(1, sizeof(*m)), **t;
+
+					if (!m || hipMallocAsync(&m->data, x->count, s) != hipSuccess) {
+						free(m);
+						ret = -LFA_ENOMEM;
+						break;
+					}
+					m->bytes = x->count;
+					hipMemcpyAsync(m->data, resolve(base, x->src), x->count,
+						       hipMemcpyDeviceToDevice, s);
+					t = &box[(size_t)r * n + x->peer];
+					while (*t)
+						t = &(*t)->next;
+					*t = m;
+					x->peer = -x->peer - 1;
+					progressed = 1;
+				}
+				/* every recv matched? (count per peer in order) */
+				for (size_t i = pc[r]; i < end && ready; i++) {
+					struct lfa_step *x = &pl[r].steps[i];
+					int need = 0;
+
+					if (x->type != LFA_STEP_RECV)
+						continue;
+					for (size_t j = pc[r]; j <= i; j++)
+						if (pl[r].steps[j].type == LFA_STEP_RECV &&
+						    pl[r].steps[j].peer == x->peer)
+							need++;
+					struct lb_msg *m = box[(size_t)x->peer * n + r];
+
+					while (m && --need)
+						m = m->next;
+					if (!m)
+						ready = 0;
+				}
+				if (!ready || ret)
+					break;
+				for (size_t i = pc[r]; i < end; i++) {
+					struct lfa_step *x = &pl[r].steps[i];
+					struct lb_msg *m;
+
+					if (x->type == LFA_STEP_SEND) {
+						x->peer = -x->peer - 1;  /* restore */
+						continue;
+					}
+					m = box[(size_t)x->peer * n + r];
+					box[(size_t)x->peer * n + r] = m->next;
+					if (m->bytes != x->count)
+						ret = -LFA_EIO;
+					hipMemcpyAsync(resolve(base, x->dst), m->data, x->count,
+						       hipMemcpyDeviceToDevice, s);
+					hipFreeAsync(m->data, s);
+					free(m);
+				}
+				pc[r] = end < pl[r].nsteps ? end + 1 : end;
+				progressed = 1;
+			}
+			if (pc[r] < pl[r].nsteps)
+				done = 0;
+		}
+		if (!done && !progressed && !ret)
+			ret = -LFA_EIO;   /* schedule deadlock: a bug */
+	} while (!done && !ret);
+out:
+	if (box) {
+		for (size_t k = 0; k < (size_t)n * (size_t)n; k++)
+			while (box[k]) {
+				struct lb_msg *m = box[k];
+
+				box[k] = m->next;
+				hipFreeAsync(m->data, s);
+				free(m);
+			}
+	}
+	if (tmp)
+		for (int r = 0; r < n; r++)
+			if (tmp[r])
+				hipFreeAsync(tmp[r], s);
+	if (pl)
+		for (int r = 0; r < n; r++)
+			plan_free(&pl[r]);
+	free(pl);
+	free(pc);
+	free(tmp);
+	free(box);
+	return ret;
+}

@@ -4,12 +4,13 @@
 // (ofi_atomic_write_handlers, prov/util/src/util_atomic.c:907-922, called by
 // prov/coll's REDUCE items, prov/coll/src/coll_coll.c:758-768):
 //
-//   combine_vec    dst[i] = dst[i] OP src[i] over 16-byte vectors.  The work is a
-//                  pure HBM stream (2 reads + 1 write per element, ~0.1 flop/B):
-//                  no MFMA, no LDS — the roofline is HBM.  Each
-//                  thread keeps UNROLL independent 16-B loads of each operand in
-//                  flight; each workgroup sweeps one contiguous chunk so every
-//                  wave-instruction touches 1 KiB of consecutive bytes.
+//   combine_lds    dst[i] = dst[i] OP src[i] over 16-byte vectors (the product
+//                  body).  A pure HBM stream (2 reads + 1 write per element,
+//                  ~0.1 op/B): no MFMA — the roofline is HBM.  Each
+//                  wave DMAs 4 KiB of each operand into LDS (global_load_lds,
+//                  nt), reads it back with ds_read_b128, applies OP and stores
+//                  nt; every wave-instruction moves 1 KiB of consecutive bytes.
+//   combine_vec    the register-staged form of the same (tuning reference).
 //   combine_elem   the same op for misaligned heads/tails and for buffers that
 //                  are not co-aligned mod 16 (one element per lane, coalesced).
 //   reduce_tree    N inputs → 1 output in ONE pass, in prov/coll's
@@ -92,6 +93,48 @@ __global__ __launch_bounds__(kBlock) void combine_vec(
   }
 }
 
+// LDS-DMA staged form — the PRODUCT body (bench.py --tune, DESIGN.md
+// "Kernel tuning": 1-2 % faster than register staging at 256 MiB).  Each wave
+// owns U consecutive KiB of both operands and moves them HBM -> LDS with
+// global_load_lds_dwordx4 (aux = nt, no VGPR round trip; 2·U KiB in flight per
+// wave), waits on its own vmcnt, reads its lane's 16 B back with
+// ds_read_b128, applies OP and streams the result out with nt stores.  Waves
+// never share LDS, so there is no barrier; a wave whose chunk runs past nvec
+// takes the guarded register path.
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kLdsWaves = 4;
+
+template <int OP, typename T, int U>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base =
+      (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0,
+                                       /*aux: nt*/ 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<true>(dst + base + u * 64 + l,
+               apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]));
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, apply_vec<OP, T>(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
 // Grid-stride variant (for the tuning sweep): a fixed grid of G workgroups
 // walks the buffer; each thread holds U vectors spaced kBlock apart.
 template <int OP, typename T, int U, bool NTL, bool NTS>
@@ -159,10 +202,10 @@ __global__ __launch_bounds__(kBlock) void combine_unaligned(
 // The kernel evaluates that tree with a stack: push leaves left to right and
 // merge the two top entries while they cover equal-size groups, so only
 // log2(nleaf)+1 partials are live per element.
-constexpr int kMaxLeaf = 16;
+constexpr int kMaxLeaf = 32;
 
 struct TreeArgs {
-  const void *in[2 * kMaxLeaf];
+  const void *in[kMaxLeaf];  // nsrc <= 32 inputs (LFA_TREE_MAX)
   signed char hi[kMaxLeaf];  // input index of the leaf's (higher-rank) value
   signed char lo[kMaxLeaf];  // paired lower-rank input, or -1
 };
@@ -230,10 +273,9 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
 // host-side launchers
 // ---------------------------------------------------------------------------
 // Product configuration of the vector body (chosen by the on-GPU sweep in
-// bench.py --tune; see DESIGN.md "Kernel tuning").
+// bench.py --tune; see DESIGN.md "Kernel tuning"): LDS-DMA staging, 4 KiB of
+// each operand per wave, nt loads and stores.
 constexpr int kUnroll = 4;
-constexpr bool kNtLoad = true;
-constexpr bool kNtStore = true;
 
 static inline unsigned grid_for(size_t work, size_t per_block, unsigned cap) {
   size_t g = (work + per_block - 1) / per_block;
@@ -265,9 +307,10 @@ static int launch_write(void *dst, const void *src, size_t cnt,
       if (nvec) {
         u32x4 *d = (u32x4 *)((char *)dst + head * E);
         const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
-        hipLaunchKernelGGL((combine_vec<OP, T, kUnroll, kNtLoad, kNtStore>),
-                           dim3(grid_for(nvec, (size_t)kBlock * kUnroll, 0x7fffffffu)),
-                           dim3(kBlock), 0, s, d, v, nvec);
+        hipLaunchKernelGGL((combine_lds<OP, T, kUnroll>),
+                           dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll,
+                                         0x7fffffffu)),
+                           dim3(kLdsWaves * 64), 0, s, d, v, nvec);
       }
       if (head + tail)
         hipLaunchKernelGGL((combine_elem<OP, T>),
@@ -290,7 +333,7 @@ static int launch_tree_n(const TreeArgs &a, void *dst, size_t cnt, bool vec,
   constexpr size_t E = sizeof(T);
   if (vec && nvec) {
     TreeArgs b = a;
-    for (int k = 0; k < 2 * kMaxLeaf; k++)
+    for (int k = 0; k < kMaxLeaf; k++)
       if (b.in[k]) b.in[k] = (const char *)b.in[k] + head * E;
     hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
                        dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
@@ -313,7 +356,7 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
     return -LFA_EOPNOTSUPP;
   } else {
     constexpr size_t E = sizeof(T);
-    if (nsrc < 1 || nsrc > 2 * kMaxLeaf) return -LFA_EINVAL;
+    if (nsrc < 1 || nsrc > kMaxLeaf) return -LFA_EINVAL;
     if (cnt == 0) return 0;
     if (nsrc == 1) {
       if (dst == srcs[0]) return 0;
@@ -350,6 +393,7 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
       case 4: return launch_tree_n<OP, T, 4>(a, dst, cnt, vec, head, nvec, s);
       case 8: return launch_tree_n<OP, T, 8>(a, dst, cnt, vec, head, nvec, s);
       case 16: return launch_tree_n<OP, T, 16>(a, dst, cnt, vec, head, nvec, s);
+      case 32: return launch_tree_n<OP, T, 32>(a, dst, cnt, vec, head, nvec, s);
       default: return -LFA_EINVAL;
     }
   }
@@ -435,6 +479,8 @@ extern "C" int lfa__tune_sum_f32(int variant, void *dst, const void *src,
   };
   switch (variant) {
     case 0: chunk(combine_vec<OP_SUM, float, 4, true, true>, 4); break;
+    case 30:  // the product launch itself
+      return launch_write<OP_SUM, float>(dst, src, nvec * 4, s);
     case 1: chunk(combine_vec<OP_SUM, float, 1, true, true>, 1); break;
     case 2: chunk(combine_vec<OP_SUM, float, 2, true, true>, 2); break;
     case 3: chunk(combine_vec<OP_SUM, float, 8, true, true>, 8); break;

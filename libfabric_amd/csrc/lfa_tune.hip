@@ -1,0 +1,175 @@
+// lfa_tune.hip — alternative schedules of the headline kernel (float FI_SUM
+// combine) for the on-GPU A/B sweep (bench.py --tune).  Not on the product
+// path: the winner is folded back into combine_vec (lfa_combine.hip).
+//
+// Each variant is the same dst[i] += src[i] stream over 16-byte vectors; they
+// differ only in how work maps to lanes, cache policy and staging:
+//   layout 0  block-strided: step u of thread t -> base + u*B + t
+//   layout 1  wave-contiguous: wave w owns U consecutive KiB
+//   XCD       blockIdx remapped so XCD x sweeps one contiguous 1/8 of the buffer
+//   LDSDMA    operands land in LDS through global_load_lds_dwordx4 (no VGPR
+//             round trip), then ds_read_b128 -> add -> global store
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lfa_fabric.h"
+
+namespace lfa_tune {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ u32x4 addf(u32x4 a, u32x4 b) {
+  f32x4 x = __builtin_bit_cast(f32x4, a), y = __builtin_bit_cast(f32x4, b);
+  return __builtin_bit_cast(u32x4, x + y);
+}
+
+__device__ __forceinline__ unsigned block_id(bool xcd) {
+  unsigned b = blockIdx.x, nb = gridDim.x;
+  if (xcd && nb % 8 == 0) b = (b % 8) * (nb / 8) + b / 8;
+  return b;
+}
+
+template <int B, int U, bool NTL, bool NTS, int LAYOUT, bool XCD, bool INTERLEAVE>
+__global__ __launch_bounds__(B) void sum_vec(u32x4 *__restrict__ dst,
+                                             const u32x4 *__restrict__ src,
+                                             size_t nvec) {
+  const size_t blk = (size_t)block_id(XCD) * (B * U);
+  const unsigned t = threadIdx.x;
+  size_t idx[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if constexpr (LAYOUT == 0) idx[u] = blk + (size_t)u * B + t;
+    else idx[u] = blk + (size_t)(t / 64) * 64 * U + (size_t)u * 64 + (t % 64);
+  }
+  if (blk + (size_t)B * U <= nvec) {
+    u32x4 a[U], b[U];
+    if constexpr (INTERLEAVE) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        a[u] = ld<NTL>(dst + idx[u]);
+        b[u] = ld<NTL>(src + idx[u]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) a[u] = ld<NTL>(dst + idx[u]);
+#pragma unroll
+      for (int u = 0; u < U; u++) b[u] = ld<NTL>(src + idx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) st<NTS>(dst + idx[u], addf(a[u], b[u]));
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (idx[u] < nvec)
+        st<NTS>(dst + idx[u], addf(ld<NTL>(dst + idx[u]), ld<NTL>(src + idx[u])));
+  }
+}
+
+// LDS-DMA staged: every wave pulls its U KiB of dst and src straight into
+// LDS (global_load_lds_dwordx4, aux=nt), waits on its own vmcnt, reads back
+// with ds_read_b128 and stores the sum.  No cross-wave sharing, no barrier.
+// MODE 0: all dst then all src; 1: interleaved per step; 2: dst via LDS-DMA,
+// src via register loads.
+template <int W, int U, int AUX, int MODE>
+__global__ __launch_bounds__(W * 64) void sum_ldsdma(u32x4 *__restrict__ dst,
+                                                     const u32x4 *__restrict__ src,
+                                                     size_t nvec) {
+  __shared__ u32x4 lds[2][W][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (W * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+    u32x4 b[U];
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, AUX);
+        __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                         (lds_void *)&lds[1][w][u][0], 16, 0, AUX);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, AUX);
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int u = 0; u < U; u++) b[u] = ld<true>(src + base + u * 64 + l);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                           (lds_void *)&lds[1][w][u][0], 16, 0, AUX);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      u32x4 y = MODE == 2 ? b[u] : lds[1][w][u][l];
+      st<true>(dst + base + u * 64 + l, addf(lds[0][w][u][l], y));
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + u * 64 + l;
+      if (i < nvec) st<true>(dst + i, addf(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
+static inline unsigned blocks(size_t nvec, size_t per) {
+  return (unsigned)((nvec + per - 1) / per);
+}
+
+}  // namespace lfa_tune
+
+using namespace lfa_tune;
+
+// Variants 12.. (0..11 live in lfa_combine.hip next to the product kernel).
+extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
+                                  size_t nvec, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  u32x4 *d = (u32x4 *)dst;
+  const u32x4 *v = (const u32x4 *)src;
+#define RUN(B, U, NTL, NTS, L, X, I)                                             \
+  hipLaunchKernelGGL((sum_vec<B, U, NTL, NTS, L, X, I>), dim3(blocks(nvec, B * U)), \
+                     dim3(B), 0, s, d, v, nvec)
+  switch (variant) {
+    case 12: RUN(512, 4, true, true, 0, false, false); break;
+    case 13: RUN(1024, 2, true, true, 0, false, false); break;
+    case 14: RUN(256, 4, true, true, 1, false, false); break;
+    case 15: RUN(256, 8, true, true, 1, false, false); break;
+    case 16: RUN(256, 4, true, true, 0, true, false); break;
+    case 17: RUN(256, 4, true, true, 0, false, true); break;
+    case 18: RUN(64, 16, true, true, 1, false, false); break;
+    case 19: RUN(256, 4, true, true, 0, false, false); break;  // = product, in this TU
+#define LDSDMA(W, U, AUX, MODE)                                                  \
+  hipLaunchKernelGGL((sum_ldsdma<W, U, AUX, MODE>), dim3(blocks(nvec, W * 64 * U)), \
+                     dim3(W * 64), 0, s, d, v, nvec)
+    case 20: LDSDMA(4, 4, 2, 0); break;
+    case 21: LDSDMA(4, 4, 0, 0); break;
+    case 22: LDSDMA(4, 8, 2, 0); break;
+    case 24: LDSDMA(4, 2, 2, 0); break;
+    case 25: LDSDMA(8, 4, 2, 0); break;
+    case 26: LDSDMA(4, 4, 2, 2); break;
+    case 27: LDSDMA(4, 4, 2, 1); break;
+    case 28: LDSDMA(2, 4, 2, 0); break;
+    case 29: LDSDMA(1, 4, 2, 0); break;
+    case 23: RUN(256, 4, true, true, 1, true, true); break;
+    default: return -LFA_EINVAL;
+  }
+#undef RUN
+#undef LDSDMA
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}

@@ -1,0 +1,90 @@
+"""Host simulation of lfa_coll_plan schedules (test infrastructure).
+
+Executes every rank's schedule — built by the C provider, liblfa_coll.so —
+with numpy byte buffers: SEND/RECV groups matched FIFO per (src, dst) pair
+exactly as the GPU loopback executor and RCCL groups match them; REDUCE via
+the oracle's combine; TREE via the oracle's recursive-doubling allreduce of
+the listed inputs (which IS the tree association order).
+"""
+import numpy as np
+
+import oracle
+from libfabric_amd import coll
+
+SEND, RECV, GEND, REDUCE, TREE, COPY = range(6)
+
+
+def _view(bufs, ref, nbytes):
+    b, off = ref
+    return bufs[b][off:off + nbytes]
+
+
+def run(coll_op, algo, n, root, dt, op, count, sends, results):
+    """sends/results: per-rank uint8 arrays (results modified in place)."""
+    esz = oracle.datatype_size(dt)
+    nd = oracle.DT_NP[dt]
+    plans = [coll.plan(coll_op, algo, r, n, root, count, esz) for r in range(n)]
+    bufs = []
+    for r in range(n):
+        tmp = np.zeros(plans[r].tmp_bytes, np.uint8)
+        send = sends[r] if coll_op != 1 else results[r]   # broadcast: in/out
+        bufs.append({0: send, 1: results[r], 2: tmp})
+    pc = [0] * n
+    box = {}
+    posted = [set() for _ in range(n)]
+    while True:
+        progressed, done = False, True
+        for r in range(n):
+            st = plans[r].steps
+            while pc[r] < len(st):
+                s = st[pc[r]]
+                if s["type"] not in (SEND, RECV, GEND):
+                    if s["type"] == REDUCE:
+                        d = _view(bufs[r], s["dst"], s["count"] * esz).view(nd)
+                        x = _view(bufs[r], s["src"], s["count"] * esz).view(nd).copy()
+                        oracle.write(op, dt, d, x)
+                    elif s["type"] == COPY:
+                        src = _view(bufs[r], s["src"], s["count"]).copy()
+                        _view(bufs[r], s["dst"], s["count"])[:] = src
+                    else:
+                        ins = [_view(bufs[r], plans[r].refs[s["first"] + k],
+                                     s["count"] * esz).view(nd).copy()
+                               for k in range(s["nsrc"])]
+                        out = oracle.allreduce(op, dt, ins)[0]
+                        _view(bufs[r], s["dst"], s["count"] * esz)[:] = out.view(np.uint8)
+                    pc[r] += 1
+                    progressed = True
+                    continue
+                end = pc[r]
+                while end < len(st) and st[end]["type"] != GEND:
+                    end += 1
+                for i in range(pc[r], end):
+                    x = st[i]
+                    if x["type"] == SEND and i not in posted[r]:
+                        box.setdefault((r, x["peer"]), []).append(
+                            _view(bufs[r], x["src"], x["count"]).copy())
+                        posted[r].add(i)
+                        progressed = True
+                need = {}
+                for i in range(pc[r], end):
+                    if st[i]["type"] == RECV:
+                        need[st[i]["peer"]] = need.get(st[i]["peer"], 0) + 1
+                if any(len(box.get((p, r), [])) < k for p, k in need.items()):
+                    break
+                for i in range(pc[r], end):
+                    x = st[i]
+                    if x["type"] == RECV:
+                        m = box[(x["peer"], r)].pop(0)
+                        assert m.nbytes == x["count"]
+                        _view(bufs[r], x["dst"], x["count"])[:] = m
+                pc[r] = min(end + 1, len(st))
+                posted[r].clear()
+                progressed = True
+            if pc[r] < len(st):
+                done = False
+        if done:
+            break
+        if not progressed:
+            raise RuntimeError("schedule deadlock")
+    assert all(not v for v in box.values()), "unmatched sends"
+    return results

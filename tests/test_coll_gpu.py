@@ -1,0 +1,215 @@
+"""GPU tests of the collective provider (liblfa_coll.so).
+
+* loopback: the schedules of N = 2..16 ranks run on ONE MI355X with the real
+  combine kernels (lfa_coll_loopback), compared with the oracle's prov/coll
+  recursive-doubling results — bit-exact;
+* a real RCCL domain + endpoint at world size 1 (the box has one GPU):
+  every fi_ops_collective call on device and host buffers, completions,
+  join, query and error codes through the C ABI.
+The N>1 RCCL transport runs in the driver's 8-GPU bench; its schedules are
+covered across processes by tests/test_coll_gloo.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests._cmp import assert_parity
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+ALLREDUCE, BROADCAST, ALLGATHER, REDUCE_SCATTER, REDUCE, SCATTER = 3, 1, 4, 5, 6, 7
+
+
+@pytest.fixture(scope="module")
+def coll():
+    from libfabric_amd import coll as c
+    c.lib()
+    return c
+
+
+def _inputs(dt, n, count, seed, lo=-1.0, hi=1.0):
+    rng = np.random.default_rng(seed)
+    nd = oracle.DT_NP[dt]
+    if nd.kind == "f":
+        return [rng.uniform(lo, hi, count).astype(nd) for _ in range(n)]
+    info = np.iinfo(nd)
+    return [rng.integers(info.min, info.max, count, dtype=nd, endpoint=True)
+            for _ in range(n)]
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(DEV)
+
+
+CASES = [(8, 2), (9, 3), (6, 0), (6, 6), (1, 7), (4, 9), (8, 1)]
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
+def test_loopback_allreduce(coll, algo, n):
+    for dt, op in CASES:
+        for count in (1, 777, 100_003):
+            sends = _inputs(dt, n, count, n + count + op,
+                            *((0.9, 1.1) if op == 3 else (-1, 1)))
+            want = oracle.allreduce(op, dt, sends)[0]
+            sd = [_dev(s) for s in sends]
+            rd = [torch.zeros_like(x) for x in sd]
+            coll.loopback(ALLREDUCE, algo, n, -1, dt, op, count, sd, rd)
+            torch.cuda.synchronize()
+            for r in range(n):
+                assert_parity(dt, rd[r].cpu().numpy(), want, f"n={n} dt={dt} op={op} r={r}")
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_loopback_reduce_scatter_and_reduce(coll, algo, n):
+    dt, op, count = 9, 3, 50_001
+    sends = _inputs(dt, n, count, 99 + n, 0.9, 1.1)
+    want = oracle.allreduce(op, dt, sends)[0]
+    sd = [_dev(s) for s in sends]
+    rd = []
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        rd.append(torch.zeros(ln * 8, dtype=torch.uint8, device=DEV))
+    coll.loopback(REDUCE_SCATTER, algo, n, -1, dt, op, count, sd, rd)
+    torch.cuda.synchronize()
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        assert_parity(dt, rd[r].cpu().numpy(), want[off:off + ln], f"rs r={r}")
+    root = n - 1
+    rd = [torch.zeros(count * 8, dtype=torch.uint8, device=DEV) for _ in range(n)]
+    coll.loopback(REDUCE, algo, n, root, dt, op, count, sd, rd)
+    torch.cuda.synchronize()
+    assert_parity(dt, rd[root].cpu().numpy(), want, "reduce root")
+
+
+def test_loopback_moves(coll):
+    n, count = 5, 12_345
+    sends = _inputs(6, n, count, 5)
+    sd = [_dev(s) for s in sends]
+    rd = [torch.zeros(n * count * 8, dtype=torch.uint8, device=DEV) for _ in range(n)]
+    coll.loopback(ALLGATHER, 0, n, -1, 6, 2, count, sd, rd)
+    torch.cuda.synchronize()
+    want = np.concatenate(sends).view(np.uint8)
+    for r in range(n):
+        assert np.array_equal(rd[r].cpu().numpy(), want)
+    bufs = [x.clone() for x in sd]
+    coll.loopback(BROADCAST, 0, n, 2, 6, 2, count, [None] * n, bufs)
+    torch.cuda.synchronize()
+    for r in range(n):
+        assert np.array_equal(bufs[r].cpu().numpy(), sends[2].view(np.uint8))
+
+
+def test_loopback_16_ranks_int_bitwise(coll):
+    n, count = 16, 4099
+    for dt, op in ((7, 6), (7, 9), (2, 2)):
+        sends = _inputs(dt, n, count, op)
+        want = oracle.allreduce(op, dt, sends)[0]
+        sd = [_dev(s) for s in sends]
+        rd = [torch.zeros_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, 0, n, -1, dt, op, count, sd, rd)
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert np.array_equal(rd[r].cpu().numpy(), want.view(np.uint8))
+
+
+# ------------------------------------------------ RCCL domain, world = 1 ----
+
+@pytest.fixture(scope="module")
+def ep(coll):
+    e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    yield e
+    e.close()
+
+
+def test_rccl_allreduce_device_and_host(coll, ep):
+    count = 1 << 20
+    x = torch.rand(count, device=DEV)
+    y = torch.empty_like(x)
+    ctx = ep.allreduce(x, y, count, 8, 2)
+    ep.wait(ctx)
+    assert torch.equal(x, y)
+    # host buffers, chunked through HBM (small chunks: several pipeline steps)
+    ep.set_chunk(1 << 18)
+    hx = np.random.default_rng(1).uniform(-1, 1, count).astype(np.float32)
+    hy = np.zeros_like(hx)
+    ctx = ep.allreduce(hx, hy, count, 8, 2)
+    ep.wait(ctx)
+    assert np.array_equal(hx, hy)
+    ep.set_chunk(0)
+
+
+def test_rccl_other_collectives(coll, ep):
+    count = 10_000
+    x = torch.arange(count, dtype=torch.int64, device=DEV)
+    out = torch.zeros_like(x)
+    ep.wait(ep.reduce_scatter(x, out, count, 6, 2))
+    assert torch.equal(out, x)
+    out.zero_()
+    ep.wait(ep.reduce(x, out, count, 0, 6, 0))
+    assert torch.equal(out, x)
+    out.zero_()
+    ep.wait(ep.allgather(x, out, count, 6))
+    assert torch.equal(out, x)
+    b = x.clone()
+    ep.wait(ep.broadcast(b, count, 0, 6))
+    assert torch.equal(b, x)
+    ep.wait(ep.barrier())
+    # host-buffer reduce_scatter (whole-buffer staging)
+    hx = np.arange(count, dtype=np.int64)
+    ho = np.zeros_like(hx)
+    ep.wait(ep.reduce_scatter(hx, ho, count, 6, 2))
+    assert np.array_equal(ho, hx)
+
+
+def test_rccl_algorithms_selectable(coll, ep):
+    count = 4096
+    x = torch.rand(count, device=DEV, dtype=torch.float64)
+    for algo in (coll.ALGO_RD, coll.ALGO_RCCL, coll.ALGO_TREE):
+        ep.set_algo(algo)
+        y = torch.zeros_like(x)
+        ep.wait(ep.allreduce(x, y, count, 9, 3))
+        assert torch.equal(x, y)
+    ep.set_algo(coll.ALGO_TREE)
+
+
+def test_join_world_and_completion_order(coll, ep):
+    mc, ctx = ep.join(None)
+    ev, fid, context = ep.wait_join()
+    assert ev == coll.JOIN_COMPLETE and fid == mc and context == ctx
+    addr = ep.mc_addr(mc)
+    x = torch.ones(1000, device=DEV)
+    y = torch.zeros_like(x)
+    c1 = ep.allreduce(x, y, 1000, 8, 2, coll_addr=addr)
+    c2 = ep.barrier(coll_addr=addr)
+    got = []
+    import time
+    t0 = time.time()
+    while len(got) < 2 and time.time() - t0 < 60:
+        got += ep.cq_read()
+    assert got == [c1, c2]            # completions in issue order
+    assert ep.cq_read() == []         # -EAGAIN when nothing is pending
+    assert torch.equal(x, y)
+
+
+def test_errors_and_query(coll, ep):
+    x = torch.ones(16, device=DEV)
+    with pytest.raises(coll.CollError) as e:
+        ep.allreduce(x, x, 16, 8, 6)                # float BOR
+    assert e.value.rc == -95
+    with pytest.raises(coll.CollError) as e:
+        ep.allreduce(x, x, 16, 8, 11)               # ATOMIC_WRITE: not a reduce op
+    assert e.value.rc == -38
+    with pytest.raises(coll.CollError) as e:
+        ep.reduce(x, x, 16, 3, 8, 2)                # root outside the group
+    assert e.value.rc == -22
+    rc, a = ep.query(3, 2, 8)
+    assert rc == 0 and a.max_members == 0x7fffffff and a.datatype_attr.size == 4
+    assert ep.query(3, 6, 8)[0] == -95              # BOR on float
+    assert ep.query(3, 12, 8)[0] == -38             # CSWAP: not a reduction
+    assert ep.query(3, 2, 8, mode=1)[0] == -22      # mode must be 0
+    assert ep.query(2, 2, 8)[0] == -38              # ALLTOALL
+    assert ep.query(8, 2, 8)[0] == -38              # GATHER
+    assert ep.query(0, 256, 256)[0] == 0            # BARRIER
+    assert ep.query(5, 2, 8)[0] == 0                # REDUCE_SCATTER (new here)

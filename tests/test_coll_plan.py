@@ -1,0 +1,128 @@
+"""The C schedule builder (lfa_coll_plan) executed on the host for N ranks.
+
+Every collective × algorithm × rank count × ragged count: the schedules the
+GPU executor runs must produce the reference results — allreduce bit-exact
+with prov/coll's recursive doubling (coll_coll.c:349-449), reduce_scatter
+slice r of it, reduce at root, allgather / broadcast / scatter moves.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from libfabric_amd import coll
+from tests import _plansim
+
+ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BROADCAST, SCATTER = 3, 5, 6, 4, 1, 7
+F32, I64, U8, F64 = 8, 6, 1, 9
+SUM, MIN, BOR, BAND, PROD = 2, 0, 6, 7, 3
+
+
+def _inputs(dt, n, count, seed):
+    rng = np.random.default_rng(seed)
+    nd = oracle.DT_NP[dt]
+    if nd.kind == "f":
+        return [rng.uniform(-1, 1, count).astype(nd) for _ in range(n)]
+    info = np.iinfo(nd)
+    return [rng.integers(info.min, info.max, count, dtype=nd, endpoint=True)
+            for _ in range(n)]
+
+
+NS = [1, 2, 3, 4, 5, 7, 8]
+COUNTS = [0, 1, 5, 1000, 70_001]
+
+
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("n", NS)
+@pytest.mark.parametrize("count", COUNTS)
+def test_allreduce_schedule(algo, n, count):
+    for dt, op in ((F32, SUM), (I64, MIN)):
+        sends = _inputs(dt, n, count, n * 1000 + count)
+        want = oracle.allreduce(op, dt, sends)[0] if count else sends[0]
+        res = [np.zeros(count * sends[0].itemsize, np.uint8) for _ in range(n)]
+        _plansim.run(ALLREDUCE, algo, n, -1, dt, op, count,
+                     [s.view(np.uint8) for s in sends], res)
+        for r in range(n):
+            assert res[r].tobytes() == want.view(np.uint8).tobytes(), (r, dt)
+
+
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("n", NS)
+@pytest.mark.parametrize("count", COUNTS)
+def test_reduce_scatter_schedule(algo, n, count):
+    dt, op = F64, PROD
+    sends = _inputs(dt, n, count, 7 + n + count)
+    full = oracle.allreduce(op, dt, sends)[0] if count else np.zeros(0)
+    res = []
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        res.append(np.zeros(ln * 8, np.uint8))
+    _plansim.run(REDUCE_SCATTER, algo, n, -1, dt, op, count,
+                 [s.view(np.uint8) for s in sends], res)
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        assert res[r].tobytes() == full[off:off + ln].tobytes()
+
+
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+def test_reduce_schedule(algo, n):
+    dt, op, count = U8, BAND, 4099
+    for root in sorted({0, n - 1, n // 2}):
+        sends = _inputs(dt, n, count, root + 31 * n)
+        want = oracle.allreduce(op, dt, sends)[0]
+        res = [np.zeros(count, np.uint8) for _ in range(n)]
+        _plansim.run(REDUCE, algo, n, root, dt, op, count,
+                     [s.view(np.uint8) for s in sends], res)
+        assert res[root].tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 6])
+def test_allgather_broadcast_scatter_schedules(n):
+    count = 333
+    sends = _inputs(I64, n, count, n)
+    res = [np.zeros(n * count * 8, np.uint8) for _ in range(n)]
+    _plansim.run(ALLGATHER, 0, n, -1, I64, SUM, count,
+                 [s.view(np.uint8) for s in sends], res)
+    want = np.concatenate(sends).view(np.uint8)
+    for r in range(n):
+        assert res[r].tobytes() == want.tobytes()
+    root = n - 1
+    bufs = [s.view(np.uint8).copy() for s in sends]
+    _plansim.run(BROADCAST, 0, n, root, I64, SUM, count, [None] * n, bufs)
+    for r in range(n):
+        assert bufs[r].tobytes() == sends[root].view(np.uint8).tobytes()
+    big = np.concatenate(sends).view(np.uint8)
+    res = [np.zeros(count * 8, np.uint8) for _ in range(n)]
+    _plansim.run(SCATTER, 0, n, 0, I64, SUM, count,
+                 [big if r == 0 else np.zeros(0, np.uint8) for r in range(n)], res)
+    for r in range(n):
+        assert res[r].tobytes() == sends[r].view(np.uint8).tobytes()
+
+
+def test_tree_schedule_traffic_is_bandwidth_optimal():
+    """Per rank: (N-1)/N·S out in each of the two exchange phases."""
+    n, count, esz = 8, 8 * 1_000_000, 4
+    p = coll.plan(ALLREDUCE, coll.ALGO_TREE, 3, n, -1, count, esz)
+    sent = sum(s["count"] for s in p.steps if s["type"] == 0)
+    assert sent == 2 * (n - 1) * count * esz // n
+    trees = [s for s in p.steps if s["type"] == 4]
+    assert len(trees) == 1 and trees[0]["nsrc"] == n
+
+
+def test_plan_errors():
+    with pytest.raises(coll.CollError) as e:
+        coll.plan(8, 0, 0, 2, -1, 10, 4)         # FI_GATHER: not planned
+    assert e.value.rc == -38
+    with pytest.raises(coll.CollError):
+        coll.plan(ALLREDUCE, 0, 2, 2, -1, 10, 4)  # rank out of range
+    with pytest.raises(coll.CollError):
+        coll.plan(REDUCE, 0, 0, 2, 5, 10, 4)      # root out of range
+
+
+def test_block_split():
+    for count in (0, 1, 7, 8, 1001):
+        for n in (1, 3, 8):
+            offs = [coll.block(count, n, r) for r in range(n)]
+            assert [o for o, _ in offs] == list(np.cumsum([0] + [ln for _, ln in offs])[:-1])
+            assert sum(ln for _, ln in offs) == count
+            assert [(a, b - a) for a, b in oracle.slice_bounds(count, n)] == offs

@@ -120,11 +120,13 @@ def test_byte_misaligned_elements(lfa):
 
 
 def test_denormals_not_flushed(lfa):
-    d = torch.tensor([1, 3, 0x00400000], dtype=torch.int32).view(torch.float32).to(DEV)
-    s = torch.tensor([1, 0x80000001, 0x00400000], dtype=torch.int32).view(torch.float32).to(DEV)
-    lfa.write(2, 8, d, s)
+    d = _dev(np.array([1, 3, 0x00400000, 0x80000002], np.uint32))
+    s = _dev(np.array([1, 0x80000001, 0x00400000, 0x00000001], np.uint32))
+    lfa.write(2, 8, d, s, 4)
     torch.cuda.synchronize()
-    assert d.view(torch.int32).cpu().tolist() == [2, 2, 0x00800000]
+    # 2 ulp-denormals add exactly; 3 - 1 = 2; two halves of FLT_MIN make FLT_MIN;
+    # -2 + 1 = -1 (denormal results are kept, never flushed to ±0)
+    assert d.cpu().numpy().view(np.uint32).tolist() == [2, 2, 0x00800000, 0x80000001]
 
 
 def test_full_size_float_sum_256mib(lfa):
