@@ -165,6 +165,138 @@ def cpu_baseline(sample_reps: int = 5):
     return out
 
 
+
+# ------------------------------------------------------------------ extras --
+
+def _kernel_events(fn, reps, stream):
+    """Mean per-launch duration (ms) of fn(i) from HIP events on `stream`."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for i, (a, b) in enumerate(evs):
+        a.record(stream)
+        fn(i)
+        b.record(stream)
+    torch.cuda.synchronize()
+    return statistics.mean(a.elapsed_time(b) for a, b in evs)
+
+
+def extra_config3(dev, stream):
+    """BASELINE configs[2]: int64 FI_BOR and FI_MIN, 64 MiB, bit-exact path.
+    8 rotating buffer pairs (1 GiB) so the 256 MiB MALL cannot serve reruns."""
+    from libfabric_amd import atomic
+    n = 64 * 1024 * 1024 // 8
+    g = torch.Generator(device=dev).manual_seed(3)
+    sets = []
+    for _ in range(8):
+        a = torch.randint(-2**63, 2**63 - 1, (n,), device=dev, dtype=torch.int64, generator=g)
+        b = torch.randint(-2**63, 2**63 - 1, (n,), device=dev, dtype=torch.int64, generator=g)
+        sets.append((a, b))
+    out = {}
+    for name, op in (("bor", 6), ("min", 0)):
+        def fn(i, op=op):
+            d, s = sets[i % 8]
+            atomic.write(op, 6, d, s, n, stream)
+        for i in range(8):
+            fn(i)
+        ms = _kernel_events(fn, 40, stream)
+        gbps = 3 * n * 8 / (ms * 1e-3) / 1e9
+        out[name] = {"kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
+                     "frac": round(gbps / PEAK_GBPS, 4),
+                     "gib_s": round(3 * n * 8 / (ms * 1e-3) / 2**30, 1)}
+    return out
+
+
+def extra_tree(dev, stream, nsrc=8):
+    """N-input fused combine (the allreduce's local step): 8 x 32 MiB float
+    blocks -> 1, recursive-doubling order.  Traffic (N+1)·B per launch."""
+    from libfabric_amd import atomic
+    blk = 32 * 1024 * 1024 // 4
+    sets = []
+    for k in range(2):
+        srcs = [torch.rand(blk, device=dev) for _ in range(nsrc)]
+        sets.append((srcs, torch.empty(blk, device=dev)))
+
+    def fn(i):
+        srcs, out = sets[i % 2]
+        atomic.reduce_tree(2, 8, out, srcs, blk, stream)
+    for i in range(4):
+        fn(i)
+    ms = _kernel_events(fn, 30, stream)
+    gbps = (nsrc + 1) * blk * 4 / (ms * 1e-3) / 1e9
+    return {"nsrc": nsrc, "block_bytes": blk * 4, "kernel_us": round(ms * 1e3, 2),
+            "achieved_gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
+
+
+def extra_e2e_host(dev, stream, reps=5):
+    """The same 256 MiB float SUM combine when the buffers start and end in
+    pinned host memory (what a libfabric caller hands over): H2D dst and src,
+    combine, D2H dst — the PCIe-inclusive rate (never the headline value)."""
+    from libfabric_amd import atomic
+    hd = torch.rand(COUNT).pin_memory()
+    hs = torch.rand(COUNT).pin_memory()
+    d = torch.empty(COUNT, device=dev)
+    s = torch.empty(COUNT, device=dev)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.copy_(hd, non_blocking=True)
+        s.copy_(hs, non_blocking=True)
+        atomic.write(FI_SUM, FI_FLOAT, d, s, COUNT, stream)
+        hd.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts[1:])
+    return {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
+            "traffic_gib_s": round(3 * S_BYTES / t / 2**30, 2),
+            "note": "pinned host buffers; 2x256 MiB H2D + combine + 256 MiB D2H, serial"}
+
+
+def extra_collectives(rank, world, stream):
+    """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
+    and a double PROD reduce_scatter bucket sweep, through the C provider
+    (liblfa_coll.so) over RCCL.  algbw = S/t, busbw = 2(N-1)/N·S/t."""
+    from libfabric_amd import coll
+    ep = coll.Endpoint.from_torch_dist()
+    out = {}
+    try:
+        x = torch.rand(COUNT, device="cuda")
+        y = torch.empty_like(x)
+        for name, algo in (("allreduce_tree_exact", coll.ALGO_TREE),
+                           ("allreduce_rccl", coll.ALGO_RCCL)):
+            ep.set_algo(algo)
+            ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
+            barrier(world)
+            reps = 10
+            t0 = time.perf_counter()
+            ctxs = [ep.allreduce(x, y, COUNT, 8, 2) for _ in range(reps)]
+            ep.wait(ctxs[-1])
+            t = max_over_ranks(time.perf_counter() - t0, world) / reps
+            out[name] = {"ms": round(t * 1e3, 3),
+                         "algbw_gbs": round(S_BYTES / t / 1e9, 1),
+                         "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)}
+        ep.set_algo(coll.ALGO_TREE)
+        sweep = {}
+        for nbytes in (4096, 65536, 1 << 20, 16 << 20, 256 << 20):
+            cnt = nbytes // 8
+            a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
+            off, ln = coll.block(cnt, world, rank)
+            b = torch.empty(max(ln, 1), device="cuda", dtype=torch.float64)
+            ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
+            barrier(world)
+            reps = 20 if nbytes < (16 << 20) else 5
+            t0 = time.perf_counter()
+            ctxs = [ep.reduce_scatter(a, b, cnt, 9, 3) for _ in range(reps)]
+            ep.wait(ctxs[-1])
+            t = max_over_ranks(time.perf_counter() - t0, world) / reps
+            sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
+                                  "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+        out["reduce_scatter_double_prod_tree"] = sweep
+    finally:
+        ep.close()
+    return out
+
+
 def tune(args) -> None:
     """Interleaved A/B of the combine_vec variants (guide §5.4 rule 24)."""
     from libfabric_amd import _native
@@ -218,6 +350,53 @@ def tune(args) -> None:
     print(json.dumps({"tune": rows}))
 
 
+def tune_tree(args) -> None:
+    """A/B of the N-input tree kernel forms (float SUM), interleaved."""
+    import ctypes
+    from libfabric_amd import _native
+    L = _native.lib()
+    torch.cuda.set_device(0)
+    h = torch.cuda.current_stream().cuda_stream
+    rows = []
+    for nsrc in (2, 4, 8, 16):
+        blk = (256 * 1024 * 1024 // 4) // nsrc           # 256 MiB of inputs
+        sets = []
+        for _ in range(2):
+            srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
+            sets.append((srcs, torch.empty(blk, device="cuda"),
+                         (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs])))
+        variants = [0, 1, 2, 3, -1]
+        ref = None
+        for v in variants:  # correctness: every form equals the product's bits
+            srcs, out, arr = sets[0]
+            assert L.lfa__tune_tree_f32(v, out.data_ptr(), arr, nsrc, blk, h) == 0
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.clone()
+            elif not torch.equal(ref, out):
+                raise SystemExit(f"tree variant {v} nsrc={nsrc} WRONG")
+        times = {v: [] for v in variants}
+        for _ in range(args.tune_rounds):
+            for v in variants:
+                evs = [(torch.cuda.Event(enable_timing=True),
+                        torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+                for i, (a, b) in enumerate(evs):
+                    srcs, out, arr = sets[i % 2]
+                    a.record()
+                    L.lfa__tune_tree_f32(v, out.data_ptr(), arr, nsrc, blk, h)
+                    b.record()
+                torch.cuda.synchronize()
+                times[v].extend(a.elapsed_time(b) for a, b in evs[2:])
+        for v in variants:
+            ms = statistics.median(times[v])
+            gbps = (nsrc + 1) * blk * 4 / (ms * 1e-3) / 1e9
+            rows.append({"nsrc": nsrc, "variant": v, "median_us": round(ms * 1e3, 2),
+                         "gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)})
+        del sets
+        torch.cuda.empty_cache()
+    print(json.dumps({"tune_tree": rows}))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,10 +407,18 @@ def main() -> None:
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--tune-rounds", type=int, default=10)
     ap.add_argument("--variants", default="", help="comma list for --tune")
+    ap.add_argument("--tune-tree", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--extras-coll", action="store_true",
+                    help="run the collective extras at N=1 too (testing)")
+    ap.add_argument("--extras-timeout", type=float, default=300.0)
     args = ap.parse_args()
 
     if args.tune:
         tune(args)
+        return
+    if args.tune_tree:
+        tune_tree(args)
         return
 
     rank, world, local = init_dist(args.gpus)
@@ -263,7 +450,14 @@ def main() -> None:
     barrier(world)
     t1 = time.perf_counter()
     elapsed = max_over_ranks(t1 - t0, world)
-    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    # Kernel duration: mean over the steady-state launches.  The first few
+    # pairs after the synchronize open while the launch queue is still
+    # empty, so their start event fires before the kernel is even submitted
+    # (host launch latency lands inside the pair); skip them.
+    durs = [a.elapsed_time(b) for a, b in evs]
+    skip = min(3, max(0, len(durs) - 1))
+    kern_ms = statistics.mean(durs[skip:])
+    kern_med = statistics.median(durs[skip:])
     kern_ms = max_over_ranks(kern_ms, world)
 
     total_bytes = 3 * S_BYTES * args.steps * world
@@ -302,14 +496,46 @@ def main() -> None:
             "traffic": traffic,
             "kernel": "combine_lds<FI_SUM,float,U=4> (LDS-DMA staged, nt)",
             "kernel_us": round(kern_ms * 1e3, 2),
+            "kernel_us_median": round(kern_med * 1e3, 2),
+            "kernel_us_all_launches": round(statistics.mean(durs) * 1e3, 2),
+            "timing": "HIP events around each launch on the launch stream; mean "
+                      "over steady-state launches (first 3 skipped)",
             "algorithmic_bytes_per_launch": 3 * S_BYTES,
             "traffic_source": traffic_src,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+
+    # Extras (never the headline).  A watchdog prints the line collected so
+    # far and exits if an extra stalls, so the metric is always reported.
+    import threading
+
+    def _emit(note=None):
+        if note:
+            line.setdefault("extras", {})["status"] = note
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+
+    if not args.no_extras:
+        del sets
+        torch.cuda.empty_cache()
+        wd = threading.Timer(args.extras_timeout, lambda: (_emit("extras timed out"),
+                                                           os._exit(0)))
+        wd.daemon = True
+        wd.start()
+        ex = line.setdefault("extras", {})
+        try:
+            if world == 1:
+                ex["config3_int64_64mib"] = extra_config3(dev, stream)
+                ex["tree8_fused_combine"] = extra_tree(dev, stream)
+                ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
+            if world > 1 or args.extras_coll:
+                ex.update(extra_collectives(rank, world, stream))
+        except Exception as e:  # noqa: BLE001 — extras must not hide the metric
+            ex["error"] = f"{type(e).__name__}: {e}"[:300]
+        wd.cancel()
+    _emit()
     if world > 1:
         dist.destroy_process_group()
 

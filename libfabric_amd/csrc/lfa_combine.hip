@@ -218,22 +218,21 @@ __device__ __forceinline__ V apply_any(V d, V s) {
     return apply<OP, T>(d, s);
 }
 
-template <int OP, typename T, typename V, int NLEAF>
-__device__ __forceinline__ V tree_eval(const TreeArgs &a, size_t i) {
+// Evaluate the tree for one element (or one 16-B vector); load(k) fetches
+// input k.  Leaf order, pairing and merge order are compile-time except the
+// kernel-argument (wave-uniform) pair test.
+template <int OP, typename T, typename V, int NLEAF, typename L>
+__device__ __forceinline__ V tree_eval_with(const TreeArgs &a, L &&load) {
   V stack[6];
   int depth = 0;
 #pragma unroll
   for (int k = 0; k < NLEAF; k++) {
-    const V *h = (const V *)a.in[a.hi[k]];
-    V v = h[i];
-    if (a.lo[k] >= 0) {  // wave-uniform: kernel-argument branch
-      const V *l = (const V *)a.in[a.lo[k]];
-      v = apply_any<OP, T, V>(v, l[i]);
-    }
+    V v = load(a.hi[k]);
+    if (a.lo[k] >= 0)  // wave-uniform: kernel-argument branch
+      v = apply_any<OP, T, V>(v, load(a.lo[k]));
     stack[depth++] = v;
-    // merge while the two top groups are the same size: after leaf k the
-    // number of merges is the count of trailing one bits of (k + 1) - 1…
-    // i.e. of trailing zero bits of (k + 1).
+    // after leaf k, merge the two top partials once per trailing zero bit
+    // of (k + 1): that is when they cover equal-size rank groups
 #pragma unroll
     for (int m = 1; m < NLEAF; m <<= 1) {
       if (((k + 1) & (2 * m - 1)) == 0) {
@@ -246,6 +245,13 @@ __device__ __forceinline__ V tree_eval(const TreeArgs &a, size_t i) {
   return stack[0];
 }
 
+template <int OP, typename T, typename V, int NLEAF>
+__device__ __forceinline__ V tree_eval(const TreeArgs &a, size_t i) {
+  return tree_eval_with<OP, T, V, NLEAF>(
+      a, [&](int k) { return ((const V *)a.in[k])[i]; });
+}
+
+// Grid-stride form (tuning reference): plain loads, one vector per lane.
 template <int OP, typename T, int NLEAF>
 __global__ __launch_bounds__(kBlock) void reduce_tree_vec(TreeArgs a,
                                                           u32x4 *dst,
@@ -254,6 +260,52 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_vec(TreeArgs a,
   size_t stride = (size_t)gridDim.x * kBlock;
   for (; i < nvec; i += stride)
     st<true>(dst + i, tree_eval<OP, T, u32x4, NLEAF>(a, i));
+}
+
+// Chunked register form: workgroup b owns [b·kBlock·U, (b+1)·kBlock·U),
+// every input read with nt loads (U·nsrc 16-B loads in flight per lane).
+template <int OP, typename T, int NLEAF, int U>
+__global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
+                                                            u32x4 *dst,
+                                                            size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec)
+      st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+                 return ld<true>((const u32x4 *)a.in[k] + i);
+               }));
+  }
+}
+
+// LDS-DMA form (the product body for <= 16 inputs): each wave DMAs 1 KiB of
+// every input into its own LDS slots (global_load_lds_dwordx4, nt), waits on
+// its vmcnt, then evaluates the tree from LDS and stores nt.  Dynamic LDS:
+// nin · 4 waves · 1 KiB per workgroup.
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kLdsWaves * 64) void reduce_tree_lds(TreeArgs a,
+                                                                  int nin,
+                                                                  u32x4 *dst,
+                                                                  size_t nvec) {
+  extern __shared__ u32x4 tlds[];  // [nin][kLdsWaves][64]
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64) + (size_t)w * 64;
+  if (base + 64 <= nvec) {
+    for (int k = 0; k < nin; k++)  // uniform loop over the inputs
+      __builtin_amdgcn_global_load_lds(
+          (const void *)((const u32x4 *)a.in[k] + base + l),
+          (lds_void *)&tlds[(k * kLdsWaves + w) * 64], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st<true>(dst + base + l,
+             tree_eval_with<OP, T, u32x4, NLEAF>(
+                 a, [&](int k) { return tlds[(k * kLdsWaves + w) * 64 + l]; }));
+  } else if (base + l < nvec) {
+    size_t i = base + l;
+    st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+               return ld<true>((const u32x4 *)a.in[k] + i);
+             }));
+  }
 }
 
 template <int OP, typename T, int NLEAF>
@@ -327,17 +379,44 @@ static int launch_write(void *dst, const void *src, size_t cnt,
   }
 }
 
+// Vector body of the tree: LDS-DMA form while the per-workgroup LDS
+// (nsrc · 4 KiB) fits comfortably, else the chunked register form.
 template <int OP, typename T, int NLEAF>
-static int launch_tree_n(const TreeArgs &a, void *dst, size_t cnt, bool vec,
-                         size_t head, size_t nvec, hipStream_t s) {
+static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
+                             size_t nvec, hipStream_t s, int variant = -1) {
+  const bool use_lds = variant < 0 ? nsrc <= 16 : variant == 3;
+  if (variant == 0) {
+    hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
+                       dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
+                       s, b, dst, nvec);
+  } else if (variant == 2) {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2>),
+                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+  } else if (use_lds) {
+    hipLaunchKernelGGL((reduce_tree_lds<OP, T, NLEAF>),
+                       dim3(grid_for(nvec, (size_t)kLdsWaves * 64, 0x7fffffffu)),
+                       dim3(kLdsWaves * 64),
+                       (size_t)nsrc * kLdsWaves * 64 * sizeof(u32x4), s, b, nsrc,
+                       dst, nvec);
+  } else {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
+                       dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+static int launch_tree_n(const TreeArgs &a, int nsrc, void *dst, size_t cnt,
+                         bool vec, size_t head, size_t nvec, hipStream_t s,
+                         int variant) {
   constexpr size_t E = sizeof(T);
   if (vec && nvec) {
     TreeArgs b = a;
     for (int k = 0; k < kMaxLeaf; k++)
       if (b.in[k]) b.in[k] = (const char *)b.in[k] + head * E;
-    hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
-                       dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
-                       s, b, (u32x4 *)((char *)dst + head * E), nvec);
+    launch_tree_body<OP, T, NLEAF>(b, nsrc, (u32x4 *)((char *)dst + head * E),
+                                   nvec, s, variant);
   }
   size_t body = vec ? nvec * 16 / E : 0;
   size_t n0 = vec ? head : cnt;
@@ -351,7 +430,7 @@ static int launch_tree_n(const TreeArgs &a, void *dst, size_t cnt, bool vec,
 
 template <int OP, typename T>
 static int launch_tree(void *dst, const void *const *srcs, int nsrc,
-                       size_t cnt, hipStream_t s) {
+                       size_t cnt, hipStream_t s, int variant = -1) {
   if constexpr (!supported<OP, T>()) {
     return -LFA_EOPNOTSUPP;
   } else {
@@ -389,11 +468,11 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
     if (head > cnt) head = cnt;
     size_t nvec = vec ? (cnt - head) * E / 16 : 0;
     switch (pof2) {
-      case 2: return launch_tree_n<OP, T, 2>(a, dst, cnt, vec, head, nvec, s);
-      case 4: return launch_tree_n<OP, T, 4>(a, dst, cnt, vec, head, nvec, s);
-      case 8: return launch_tree_n<OP, T, 8>(a, dst, cnt, vec, head, nvec, s);
-      case 16: return launch_tree_n<OP, T, 16>(a, dst, cnt, vec, head, nvec, s);
-      case 32: return launch_tree_n<OP, T, 32>(a, dst, cnt, vec, head, nvec, s);
+      case 2: return launch_tree_n<OP, T, 2>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 4: return launch_tree_n<OP, T, 4>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 8: return launch_tree_n<OP, T, 8>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 16: return launch_tree_n<OP, T, 16>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 32: return launch_tree_n<OP, T, 32>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
       default: return -LFA_EINVAL;
     }
   }
@@ -495,5 +574,17 @@ extern "C" int lfa__tune_sum_f32(int variant, void *dst, const void *src,
     default: return -LFA_EINVAL;
   }
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+#endif
+
+#if LFA_OP == 2
+// Tree-kernel sweep: float SUM over `nsrc` device inputs.  variant 0 grid-
+// stride plain loads, 1 chunked nt U=1, 2 chunked nt U=2, 3 LDS-DMA,
+// -1 the product choice.
+extern "C" int lfa__tune_tree_f32(int variant, void *dst,
+                                  const void *const *srcs, int nsrc,
+                                  size_t cnt, void *stream) {
+  return lfa::launch_tree<lfa::OP_SUM, float>(dst, srcs, nsrc, cnt,
+                                              (hipStream_t)stream, variant);
 }
 #endif
