@@ -252,6 +252,25 @@ def extra_e2e_host(dev, stream, reps=5):
             "note": "pinned host buffers; 2x256 MiB H2D + combine + 256 MiB D2H, serial"}
 
 
+def cpu_model_allreduce(world: int):
+    """Modelled reference compute for a 256 MiB float SUM allreduce at N
+    ranks: log2(N) x (CAS combine [+ COPY]) — prov/coll's per-rank REDUCE
+    items (coll_coll.c:409-430).  The reference itself cannot run this
+    (eager-size hang); transport is excluded.  Measured on a 16 MiB
+    slice on 1 core and scaled linearly."""
+    import numpy as np
+    import oracle
+    n = 4 * 1024 * 1024
+    rng = np.random.default_rng(0)
+    d, s = rng.uniform(-1, 1, n).astype(np.float32), rng.uniform(-1, 1, n).astype(np.float32)
+    t0 = time.perf_counter()
+    oracle.write(FI_SUM, FI_FLOAT, d, s, oracle.CAS)
+    t = (time.perf_counter() - t0) * (COUNT / n)
+    steps = max(1, (world - 1).bit_length())
+    return {"ms": round(t * steps * 1e3, 1), "steps": steps, "kind": "modelled",
+            "note": "log2(N) CAS combines of 256 MiB on 1 host core; transport excluded"}
+
+
 def extra_collectives(rank, world, stream):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
@@ -277,7 +296,7 @@ def extra_collectives(rank, world, stream):
                          "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)}
         ep.set_algo(coll.ALGO_TREE)
         sweep = {}
-        for nbytes in (4096, 65536, 1 << 20, 16 << 20, 256 << 20):
+        for nbytes in [4096 * 4 ** k for k in range(9)]:   # 4 KiB .. 256 MiB
             cnt = nbytes // 8
             a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
             off, ln = coll.block(cnt, world, rank)
@@ -292,6 +311,18 @@ def extra_collectives(rank, world, stream):
             sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
                                   "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
         out["reduce_scatter_double_prod_tree"] = sweep
+        # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
+        a = torch.rand(1024, device="cuda")
+        b = torch.empty_like(a)
+        ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(200):
+            ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+        t = max_over_ranks(time.perf_counter() - t0, world) / 200
+        out["allreduce_4kib_float_sum_us"] = round(t * 1e6, 1)
+        if rank == 0:
+            out["cpu_model_allreduce_256mib"] = cpu_model_allreduce(world)
     finally:
         ep.close()
     return out

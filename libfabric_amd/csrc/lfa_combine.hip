@@ -379,12 +379,13 @@ static int launch_write(void *dst, const void *src, size_t cnt,
   }
 }
 
-// Vector body of the tree: LDS-DMA form while the per-workgroup LDS
-// (nsrc · 4 KiB) fits comfortably, else the chunked register form.
+// Vector body of the tree (bench.py --tune-tree): LDS-DMA for
+// 2 inputs, chunked nt register loads for more (U=2 above 8 inputs).
 template <int OP, typename T, int NLEAF>
 static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                              size_t nvec, hipStream_t s, int variant = -1) {
-  const bool use_lds = variant < 0 ? nsrc <= 16 : variant == 3;
+  const bool use_lds = variant < 0 ? nsrc <= 2 : variant == 3;
+  if (variant < 0 && nsrc > 8) variant = 2;
   if (variant == 0) {
     hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
                        dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,

@@ -166,6 +166,11 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
     case 27: LDSDMA(4, 4, 2, 1); break;
     case 28: LDSDMA(2, 4, 2, 0); break;
     case 29: LDSDMA(1, 4, 2, 0); break;
+    case 31: LDSDMA(8, 2, 2, 0); break;
+    case 32: LDSDMA(16, 1, 2, 0); break;
+    case 33: LDSDMA(4, 3, 2, 0); break;
+    case 34: LDSDMA(8, 1, 2, 0); break;
+    case 35: LDSDMA(4, 4, 2, 2); break;
     case 23: RUN(256, 4, true, true, 1, true, true); break;
     default: return -LFA_EINVAL;
   }
