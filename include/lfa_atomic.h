@@ -16,6 +16,12 @@
  *                                 pointers; synchronous on the null stream)
  *   lfa_atomic_write_async()     the GPU form: same semantics, enqueued on a
  *                                  HIP stream, returns 0 / negative errno
+ *   lfa_atomic_readwrite_handlers / lfa_atomic_readwrite_async
+ *                                replace ofi_atomic_readwrite_handlers
+ *                                  (util_atomic.c:924-950)
+ *   lfa_atomic_swap_handlers / lfa_atomic_swap_async
+ *                                replace ofi_atomic_swap_handlers
+ *                                  (util_atomic.c:952-980)
  *   lfa_reduce_tree_async()      N-input fused combine in prov/coll's
  *                                  recursive-doubling association order
  *                                  (coll_coll.c:349-449), one pass over HBM
@@ -44,7 +50,9 @@ typedef void (*lfa_write_fn)(void *dst, const void *src, size_t cnt);
 /* 0 and errno = EINVAL for datatype >= LFA_DATATYPE_CNT. */
 size_t lfa_datatype_size(enum lfa_datatype datatype);
 
-/* 0, -LFA_EOPNOTSUPP, -LFA_EBADFLAGS or -LFA_ENOSYS, as ofi_atomic_valid. */
+/* 0, -LFA_EOPNOTSUPP, -LFA_EBADFLAGS or -LFA_ENOSYS, as ofi_atomic_valid
+ * (write table; LFA_FETCH_ATOMIC → fetch table; LFA_COMPARE_ATOMIC → compare
+ * table). */
 int lfa_atomic_valid(enum lfa_datatype datatype, enum lfa_op op, uint64_t flags);
 
 /* Synchronous table form: [op][datatype], NULL where unsupported. */
@@ -68,6 +76,35 @@ int lfa_atomic_write_async(enum lfa_op op, enum lfa_datatype datatype,
 int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype datatype,
 			  void *dst, const void *const *srcs, int nsrc,
 			  size_t cnt, void *stream);
+
+/*
+ * Fetch table — replaces ofi_atomic_readwrite_handlers (util_atomic.c:924-950):
+ * res[i] = dst[i], then dst[i] = dst[i] OP src[i] (ATOMIC_READ: load only,
+ * ATOMIC_WRITE: exchange).
+ */
+typedef void (*lfa_readwrite_fn)(void *dst, const void *src, void *res,
+				 size_t cnt);
+extern lfa_readwrite_fn const
+	lfa_atomic_readwrite_handlers[LFA_READWRITE_OP_CNT][LFA_DATATYPE_CNT];
+int lfa_atomic_readwrite_async(enum lfa_op op, enum lfa_datatype datatype,
+			       void *dst, const void *src, void *res,
+			       size_t cnt, void *stream);
+
+/*
+ * Compare table — replaces ofi_atomic_swap_handlers (util_atomic.c:952-980),
+ * indexed [op - LFA_CSWAP][datatype]: res[i] = dst[i]; dst[i] = src[i] when
+ * the compare holds.  LFA_CSWAP compares BITS, as the shipping
+ * __atomic_compare_exchange does (-0.0 != +0.0; a NaN equals its own bits);
+ * CSWAP_NE/LE/LT/GE/GT compare values (cmp OP dst); MSWAP writes
+ * (src & cmp) | (dst & ~cmp).
+ */
+typedef void (*lfa_swap_fn)(void *dst, const void *src, const void *cmp,
+			    void *res, size_t cnt);
+extern lfa_swap_fn const
+	lfa_atomic_swap_handlers[LFA_SWAP_OP_CNT][LFA_DATATYPE_CNT];
+int lfa_atomic_swap_async(enum lfa_op op, enum lfa_datatype datatype,
+			  void *dst, const void *src, const void *cmp,
+			  void *res, size_t cnt, void *stream);
 
 /* Version string of the kernel library (build id, target arch). */
 const char *lfa_version(void);

@@ -88,6 +88,37 @@ def write_ptr(op: int, dt: int, dst: int, src: int, cnt: int,
                                             _stream_handle(stream)))
 
 
+def readwrite(op: int, dt: int, dst: torch.Tensor, src: torch.Tensor | None,
+              res: torch.Tensor, cnt: int | None = None, stream=None) -> None:
+    """res = dst; dst = dst OP src (ofi_atomic_readwrite_handler; ATOMIC_READ
+    ignores src, ATOMIC_WRITE exchanges)."""
+    _check_dev(dst, "dst")
+    _check_dev(res, "res")
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    rc = lib().lfa_atomic_readwrite_async(
+        int(op), int(dt), dst.data_ptr(), src.data_ptr() if src is not None else None,
+        res.data_ptr(), cnt, _stream_handle(stream))
+    if rc:
+        raise LfaError(rc, f"lfa_atomic_readwrite_async({op},{DT(dt).name})")
+
+
+def swap(op: int, dt: int, dst: torch.Tensor, src: torch.Tensor, cmp: torch.Tensor,
+         res: torch.Tensor, cnt: int | None = None, stream=None) -> None:
+    """res = dst; dst = src where (cmp OP dst) (ofi_atomic_swap_handler)."""
+    for name, t in (("dst", dst), ("src", src), ("cmp", cmp), ("res", res)):
+        _check_dev(t, name)
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    rc = lib().lfa_atomic_swap_async(int(op), int(dt), dst.data_ptr(), src.data_ptr(),
+                                     cmp.data_ptr(), res.data_ptr(), cnt,
+                                     _stream_handle(stream))
+    if rc:
+        raise LfaError(rc, f"lfa_atomic_swap_async({op},{DT(dt).name})")
+
+
 def reduce_tree(op: int, dt: int, dst: torch.Tensor, srcs: list[torch.Tensor],
                 cnt: int | None = None, stream=None) -> None:
     """dst = recursive-doubling tree of srcs (rank order = list order)."""

@@ -23,7 +23,8 @@ BUILD = os.path.join(ROOT, "build", "lfa")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"
-WRITE_OPS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]
+# every enum fi_op row of the three tables: write+fetch 0..11, compare 12..18
+WRITE_OPS = list(range(19))
 
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fPIC",
              "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + INC]

@@ -1,7 +1,8 @@
 // lfa_capi.cpp — the public C ABI of liblfa.so (include/lfa_atomic.h).
 //
 // Host-only C++: argument validation, the ofi_atomic_valid restatement, the
-// synchronous [op][datatype] table, and dispatch to the per-op kernel
+// synchronous [op][datatype] tables (write, fetch, compare), and dispatch to
+// the per-op kernel
 // objects built from lfa_combine.hip.  No CPU compute path exists: every
 // combine runs on the GPU.
 #include <hip/hip_runtime_api.h>
@@ -11,12 +12,29 @@
 #include "../../include/lfa_atomic.h"
 
 extern "C" {
-#define LFA_DECL(N)                                                            \
-  int lfa__write_op##N(int, void *, const void *, size_t, void *);             \
+#define LFA_DECL_W(N)                                                          \
+  int lfa__write_op##N(int, void *, const void *, size_t, void *);
+#define LFA_DECL_T(N)                                                          \
   int lfa__tree_op##N(int, void *, const void *const *, int, size_t, void *);
-LFA_DECL(0) LFA_DECL(1) LFA_DECL(2) LFA_DECL(3) LFA_DECL(4) LFA_DECL(5)
-LFA_DECL(6) LFA_DECL(7) LFA_DECL(8) LFA_DECL(9) LFA_DECL(11)
-#undef LFA_DECL
+#define LFA_DECL_RW(N)                                                         \
+  int lfa__readwrite_op##N(int, void *, const void *, void *, size_t, void *);
+#define LFA_DECL_SW(N)                                                         \
+  int lfa__swap_op##N(int, void *, const void *, const void *, void *, size_t, \
+                      void *);
+LFA_DECL_W(0) LFA_DECL_W(1) LFA_DECL_W(2) LFA_DECL_W(3) LFA_DECL_W(4)
+LFA_DECL_W(5) LFA_DECL_W(6) LFA_DECL_W(7) LFA_DECL_W(8) LFA_DECL_W(9)
+LFA_DECL_W(11)
+LFA_DECL_T(0) LFA_DECL_T(1) LFA_DECL_T(2) LFA_DECL_T(3) LFA_DECL_T(4)
+LFA_DECL_T(5) LFA_DECL_T(6) LFA_DECL_T(7) LFA_DECL_T(8) LFA_DECL_T(9)
+LFA_DECL_RW(0) LFA_DECL_RW(1) LFA_DECL_RW(2) LFA_DECL_RW(3) LFA_DECL_RW(4)
+LFA_DECL_RW(5) LFA_DECL_RW(6) LFA_DECL_RW(7) LFA_DECL_RW(8) LFA_DECL_RW(9)
+LFA_DECL_RW(10) LFA_DECL_RW(11)
+LFA_DECL_SW(12) LFA_DECL_SW(13) LFA_DECL_SW(14) LFA_DECL_SW(15)
+LFA_DECL_SW(16) LFA_DECL_SW(17) LFA_DECL_SW(18)
+#undef LFA_DECL_W
+#undef LFA_DECL_T
+#undef LFA_DECL_RW
+#undef LFA_DECL_SW
 }
 
 namespace {
@@ -29,6 +47,18 @@ const write_launch_t kWrite[LFA_WRITE_OP_CNT] = {
     lfa__write_op0, lfa__write_op1, lfa__write_op2, lfa__write_op3,
     lfa__write_op4, lfa__write_op5, lfa__write_op6, lfa__write_op7,
     lfa__write_op8, lfa__write_op9, nullptr,        lfa__write_op11};
+typedef int (*rw_launch_t)(int, void *, const void *, void *, size_t, void *);
+typedef int (*swap_launch_t)(int, void *, const void *, const void *, void *,
+                             size_t, void *);
+const rw_launch_t kReadWrite[LFA_READWRITE_OP_CNT] = {
+    lfa__readwrite_op0, lfa__readwrite_op1, lfa__readwrite_op2,
+    lfa__readwrite_op3, lfa__readwrite_op4, lfa__readwrite_op5,
+    lfa__readwrite_op6, lfa__readwrite_op7, lfa__readwrite_op8,
+    lfa__readwrite_op9, lfa__readwrite_op10, lfa__readwrite_op11};
+const swap_launch_t kSwap[LFA_SWAP_OP_CNT] = {
+    lfa__swap_op12, lfa__swap_op13, lfa__swap_op14, lfa__swap_op15,
+    lfa__swap_op16, lfa__swap_op17, lfa__swap_op18};
+
 const tree_launch_t kTree[LFA_BXOR + 1] = {
     lfa__tree_op0, lfa__tree_op1, lfa__tree_op2, lfa__tree_op3, lfa__tree_op4,
     lfa__tree_op5, lfa__tree_op6, lfa__tree_op7, lfa__tree_op8, lfa__tree_op9};
@@ -47,6 +77,55 @@ constexpr bool in_table(int op, int dt) {
     case LFA_BOR: case LFA_BAND: case LFA_BXOR: return ints;
     default: return false;
   }
+}
+
+// Fetch table (util_atomic.c:924-950): the write rows plus an ALL-types
+// ATOMIC_READ row; ATOMIC_WRITE is an exchange.
+constexpr bool in_rw_table(int op, int dt) {
+  return op == LFA_ATOMIC_READ ? in_table(LFA_ATOMIC_WRITE, dt) : in_table(op, dt);
+}
+
+// Compare table (util_atomic.c:952-980): CSWAP / CSWAP_NE over ALL types,
+// LE/LT/GE/GT over REALNO, MSWAP over INT.
+constexpr bool in_swap_table(int op, int dt) {
+  switch (op) {
+    case LFA_CSWAP: case LFA_CSWAP_NE: return in_table(LFA_SUM, dt);
+    case LFA_CSWAP_LE: case LFA_CSWAP_LT: case LFA_CSWAP_GE: case LFA_CSWAP_GT:
+      return in_table(LFA_MIN, dt);
+    case LFA_MSWAP: return in_table(LFA_BOR, dt);
+    default: return false;
+  }
+}
+
+template <int OP, int DT>
+void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
+  int rc = kReadWrite[OP](DT, dst, src, res, cnt, nullptr);
+  hipError_t e = hipStreamSynchronize(nullptr);
+  if (rc || e != hipSuccess)
+    fprintf(stderr, "lfa: fetch op=%d dt=%d failed (%d, %s)\n", OP, DT, rc,
+            hipGetErrorString(e));
+}
+
+template <int OP, int DT>
+void sync_swap_entry(void *dst, const void *src, const void *cmp, void *res,
+                     size_t cnt) {
+  int rc = kSwap[OP - LFA_CSWAP](DT, dst, src, cmp, res, cnt, nullptr);
+  hipError_t e = hipStreamSynchronize(nullptr);
+  if (rc || e != hipSuccess)
+    fprintf(stderr, "lfa: swap op=%d dt=%d failed (%d, %s)\n", OP, DT, rc,
+            hipGetErrorString(e));
+}
+
+template <int OP, int DT>
+constexpr lfa_readwrite_fn rw_entry() {
+  if constexpr (in_rw_table(OP, DT)) return &sync_rw_entry<OP, DT>;
+  else return nullptr;
+}
+
+template <int OP, int DT>
+constexpr lfa_swap_fn swap_entry() {
+  if constexpr (in_swap_table(OP, DT)) return &sync_swap_entry<OP, DT>;
+  else return nullptr;
 }
 
 template <int OP, int DT>
@@ -72,7 +151,52 @@ constexpr lfa_write_fn entry() {
     entry<OP, 8>(), entry<OP, 9>(), entry<OP, 10>(), entry<OP, 11>(),    \
     entry<OP, 12>(), entry<OP, 13>(), entry<OP, 14>(), entry<OP, 15>() }
 
+#define LFA_RW_ROW(OP)                                                         \
+  { rw_entry<OP, 0>(), rw_entry<OP, 1>(), rw_entry<OP, 2>(), rw_entry<OP, 3>(), \
+    rw_entry<OP, 4>(), rw_entry<OP, 5>(), rw_entry<OP, 6>(), rw_entry<OP, 7>(), \
+    rw_entry<OP, 8>(), rw_entry<OP, 9>(), rw_entry<OP, 10>(),                   \
+    rw_entry<OP, 11>(), rw_entry<OP, 12>(), rw_entry<OP, 13>(),                 \
+    rw_entry<OP, 14>(), rw_entry<OP, 15>() }
+#define LFA_SW_ROW(OP)                                                         \
+  { swap_entry<OP, 0>(), swap_entry<OP, 1>(), swap_entry<OP, 2>(),             \
+    swap_entry<OP, 3>(), swap_entry<OP, 4>(), swap_entry<OP, 5>(),             \
+    swap_entry<OP, 6>(), swap_entry<OP, 7>(), swap_entry<OP, 8>(),             \
+    swap_entry<OP, 9>(), swap_entry<OP, 10>(), swap_entry<OP, 11>(),           \
+    swap_entry<OP, 12>(), swap_entry<OP, 13>(), swap_entry<OP, 14>(),          \
+    swap_entry<OP, 15>() }
+
 extern "C" {
+
+lfa_readwrite_fn const
+    lfa_atomic_readwrite_handlers[LFA_READWRITE_OP_CNT][LFA_DATATYPE_CNT] = {
+        LFA_RW_ROW(0), LFA_RW_ROW(1), LFA_RW_ROW(2), LFA_RW_ROW(3),
+        LFA_RW_ROW(4), LFA_RW_ROW(5), LFA_RW_ROW(6), LFA_RW_ROW(7),
+        LFA_RW_ROW(8), LFA_RW_ROW(9), LFA_RW_ROW(10), LFA_RW_ROW(11)};
+
+lfa_swap_fn const lfa_atomic_swap_handlers[LFA_SWAP_OP_CNT][LFA_DATATYPE_CNT] = {
+    LFA_SW_ROW(12), LFA_SW_ROW(13), LFA_SW_ROW(14), LFA_SW_ROW(15),
+    LFA_SW_ROW(16), LFA_SW_ROW(17), LFA_SW_ROW(18)};
+
+int lfa_atomic_readwrite_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
+                               const void *src, void *res, size_t cnt,
+                               void *stream) {
+  if ((unsigned)op >= LFA_READWRITE_OP_CNT || (unsigned)dt >= LFA_DATATYPE_CNT ||
+      !in_rw_table(op, dt))
+    return -LFA_EOPNOTSUPP;
+  if (cnt && (!dst || !res || (op != LFA_ATOMIC_READ && !src)))
+    return -LFA_EINVAL;
+  return kReadWrite[op](dt, dst, src, res, cnt, stream);
+}
+
+int lfa_atomic_swap_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
+                          const void *src, const void *cmp, void *res,
+                          size_t cnt, void *stream) {
+  if (op < LFA_CSWAP || op > LFA_MSWAP || (unsigned)dt >= LFA_DATATYPE_CNT ||
+      !in_swap_table(op, dt))
+    return -LFA_EOPNOTSUPP;
+  if (cnt && (!dst || !src || !cmp || !res)) return -LFA_EINVAL;
+  return kSwap[op - LFA_CSWAP](dt, dst, src, cmp, res, cnt, stream);
+}
 
 lfa_write_fn const lfa_atomic_write_handlers[LFA_WRITE_OP_CNT][LFA_DATATYPE_CNT] = {
     LFA_ROW(0), LFA_ROW(1), LFA_ROW(2), LFA_ROW(3), LFA_ROW(4),  LFA_ROW(5),
@@ -97,8 +221,11 @@ int lfa_atomic_valid(enum lfa_datatype dt, enum lfa_op op, uint64_t flags) {
     return -LFA_EBADFLAGS;
   }
   if ((unsigned)dt >= LFA_DATATYPE_CNT) return -LFA_EOPNOTSUPP;
-  if (flags & (LFA_FETCH_ATOMIC | LFA_COMPARE_ATOMIC))
-    return -LFA_EOPNOTSUPP;  // fetch / compare tables are not provided
+  if (flags & LFA_FETCH_ATOMIC)
+    return (unsigned)op < LFA_READWRITE_OP_CNT && in_rw_table(op, dt)
+               ? 0 : -LFA_EOPNOTSUPP;
+  if (flags & LFA_COMPARE_ATOMIC)
+    return in_swap_table(op, dt) ? 0 : -LFA_EOPNOTSUPP;
   if ((unsigned)op >= LFA_WRITE_OP_CNT || op == LFA_ATOMIC_READ)
     return -LFA_EOPNOTSUPP;
   return in_table(op, dt) ? 0 : -LFA_EOPNOTSUPP;

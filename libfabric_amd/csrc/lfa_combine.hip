@@ -322,6 +322,114 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
 }
 
 // ---------------------------------------------------------------------------
+// fetch (readwrite) and compare-swap tables
+// ---------------------------------------------------------------------------
+// One launch shape for both: a functor F carries the operand pointers and
+// knows how to process one 16-B vector (vec) or one element (elem); the
+// kernels only map indices.  res[] receives the old destination, as every
+// shipping readwrite / swap handler returns it (util_atomic.c:345-760).
+template <int OP, typename T, bool ALIGNED>
+struct RwF {
+  char *d;
+  const char *s;
+  char *r;
+  u32x4 *dv;
+  const u32x4 *sv;
+  u32x4 *rv;
+  __device__ __forceinline__ void vec(size_t i) const {
+    u32x4 a = ld<true>(dv + i);
+    st<true>(rv + i, a);
+    if constexpr (OP != OP_READ)
+      st<true>(dv + i, apply_vec<OP, T>(a, ld<true>(sv + i)));
+  }
+  __device__ __forceinline__ void elem(size_t k) const {
+    T a;
+    if constexpr (ALIGNED) a = ((T *)d)[k];
+    else __builtin_memcpy(&a, d + k * sizeof(T), sizeof(T));
+    if constexpr (ALIGNED) ((T *)r)[k] = a;
+    else __builtin_memcpy(r + k * sizeof(T), &a, sizeof(T));
+    if constexpr (OP != OP_READ) {
+      T b;
+      if constexpr (ALIGNED) b = ((const T *)s)[k];
+      else __builtin_memcpy(&b, s + k * sizeof(T), sizeof(T));
+      a = apply<OP, T>(a, b);
+      if constexpr (ALIGNED) ((T *)d)[k] = a;
+      else __builtin_memcpy(d + k * sizeof(T), &a, sizeof(T));
+    }
+  }
+};
+
+template <int OP, typename T>
+__device__ __forceinline__ u32x4 swap_vec(u32x4 a, u32x4 b, u32x4 c) {
+  constexpr int N = 16 / sizeof(T);
+  T x[N], y[N], z[N];
+  __builtin_memcpy(x, &a, 16);
+  __builtin_memcpy(y, &b, 16);
+  __builtin_memcpy(z, &c, 16);
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = swap_apply<OP, T>(x[i], y[i], z[i]);
+  u32x4 out;
+  __builtin_memcpy(&out, x, 16);
+  return out;
+}
+
+template <int OP, typename T, bool ALIGNED>
+struct SwapF {
+  char *d;
+  const char *s;
+  const char *c;
+  char *r;
+  u32x4 *dv;
+  const u32x4 *sv;
+  const u32x4 *cv;
+  u32x4 *rv;
+  __device__ __forceinline__ void vec(size_t i) const {
+    u32x4 a = ld<true>(dv + i);
+    u32x4 b = ld<true>(sv + i);
+    u32x4 m = ld<true>(cv + i);
+    st<true>(rv + i, a);
+    st<true>(dv + i, swap_vec<OP, T>(a, b, m));
+  }
+  __device__ __forceinline__ void elem(size_t k) const {
+    T a, b, m;
+    if constexpr (ALIGNED) {
+      a = ((T *)d)[k];
+      b = ((const T *)s)[k];
+      m = ((const T *)c)[k];
+      ((T *)r)[k] = a;
+      ((T *)d)[k] = swap_apply<OP, T>(a, b, m);
+    } else {
+      __builtin_memcpy(&a, d + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(&b, s + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(&m, c + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(r + k * sizeof(T), &a, sizeof(T));
+      a = swap_apply<OP, T>(a, b, m);
+      __builtin_memcpy(d + k * sizeof(T), &a, sizeof(T));
+    }
+  }
+};
+
+constexpr int kFetchUnroll = 2;
+
+template <typename F>
+__global__ __launch_bounds__(kBlock) void fetch_vec(F f, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * kFetchUnroll) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kFetchUnroll; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec) f.vec(i);
+  }
+}
+
+template <typename F>
+__global__ __launch_bounds__(kBlock) void fetch_elem(F f, size_t n0, size_t off1,
+                                                     size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) f.elem(i < n0 ? i : off1 + (i - n0));
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
 // Product configuration of the vector body (chosen by the on-GPU sweep in
@@ -479,6 +587,81 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
   }
 }
 
+// Shared launcher for the fetch / swap tables: vector body when every operand
+// is co-aligned mod 16, element path for heads, tails and the rest.
+template <typename T, typename MakeF>
+static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
+                        hipStream_t s, MakeF &&make) {
+  constexpr size_t E = sizeof(T);
+  if (cnt == 0) return 0;
+  uintptr_t p0 = (uintptr_t)ptrs[0], mis = 0, elem_mis = 0;
+  for (int k = 0; k < nptr; k++) {
+    mis |= ((uintptr_t)ptrs[k] ^ p0) % 16;
+    elem_mis |= (uintptr_t)ptrs[k] % E;
+  }
+  if (elem_mis) {
+    auto f = make(std::integral_constant<bool, false>(), (size_t)0);
+    hipLaunchKernelGGL(fetch_elem<decltype(f)>, dim3(grid_for(cnt, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, f, cnt, (size_t)0, (size_t)0);
+  } else if (mis == 0 && E <= 16) {
+    size_t head = ((16 - p0 % 16) % 16) / E;
+    if (head > cnt) head = cnt;
+    size_t nvec = (cnt - head) * E / 16, body = nvec * 16 / E;
+    size_t tail = cnt - head - body;
+    auto f = make(std::integral_constant<bool, true>(), head);
+    if (nvec)
+      hipLaunchKernelGGL(fetch_vec<decltype(f)>,
+                         dim3(grid_for(nvec, (size_t)kBlock * kFetchUnroll, 0x7fffffffu)),
+                         dim3(kBlock), 0, s, f, nvec);
+    if (head + tail)
+      hipLaunchKernelGGL(fetch_elem<decltype(f)>,
+                         dim3(grid_for(head + tail, kBlock, kElemGridCap)),
+                         dim3(kBlock), 0, s, f, head, head + body, tail);
+  } else {
+    auto f = make(std::integral_constant<bool, true>(), (size_t)0);
+    hipLaunchKernelGGL(fetch_elem<decltype(f)>, dim3(grid_for(cnt, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, f, cnt, (size_t)0, (size_t)0);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T>
+static int launch_readwrite(void *dst, const void *src, void *res, size_t cnt,
+                            hipStream_t s) {
+  if constexpr (!rw_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    const void *ptrs[3] = {dst, res, OP == OP_READ ? dst : src};
+    return launch_fetch<T>(ptrs, 3, cnt, s, [&](auto aligned, size_t head) {
+      constexpr bool A = decltype(aligned)::value;
+      const size_t hb = head * sizeof(T);
+      return RwF<OP, T, A>{(char *)dst, (const char *)src, (char *)res,
+                           (u32x4 *)((char *)dst + hb),
+                           (const u32x4 *)((const char *)src + hb),
+                           (u32x4 *)((char *)res + hb)};
+    });
+  }
+}
+
+template <int OP, typename T>
+static int launch_swap(void *dst, const void *src, const void *cmp, void *res,
+                       size_t cnt, hipStream_t s) {
+  if constexpr (!swap_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    const void *ptrs[4] = {dst, src, cmp, res};
+    return launch_fetch<T>(ptrs, 4, cnt, s, [&](auto aligned, size_t head) {
+      constexpr bool A = decltype(aligned)::value;
+      const size_t hb = head * sizeof(T);
+      return SwapF<OP, T, A>{(char *)dst, (const char *)src, (const char *)cmp,
+                             (char *)res, (u32x4 *)((char *)dst + hb),
+                             (const u32x4 *)((const char *)src + hb),
+                             (const u32x4 *)((const char *)cmp + hb),
+                             (u32x4 *)((char *)res + hb)};
+    });
+  }
+}
+
 // ---------------------------------------------------------------------------
 // per-op entry points
 // ---------------------------------------------------------------------------
@@ -516,6 +699,8 @@ static int by_type(int dt, F &&f) {
 #define LFA_CAT2(a, b) a##b
 #define LFA_CAT(a, b) LFA_CAT2(a, b)
 
+#if LFA_OP <= 11
+#if LFA_OP != 10
 extern "C" int LFA_CAT(lfa__write_op, LFA_OP)(int dt, void *dst,
                                               const void *src, size_t cnt,
                                               void *stream) {
@@ -524,21 +709,40 @@ extern "C" int LFA_CAT(lfa__write_op, LFA_OP)(int dt, void *dst,
     return lfa::launch_write<LFA_OP, T>(dst, src, cnt, (hipStream_t)stream);
   });
 }
+#endif
 
+#if LFA_OP <= 9
 extern "C" int LFA_CAT(lfa__tree_op, LFA_OP)(int dt, void *dst,
                                              const void *const *srcs, int nsrc,
                                              size_t cnt, void *stream) {
-#if LFA_OP <= 9
   return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
     typedef typename std::remove_pointer<decltype(tag)>::type T;
     return lfa::launch_tree<LFA_OP, T>(dst, srcs, nsrc, cnt,
                                        (hipStream_t)stream);
   });
-#else
-  (void)dt; (void)dst; (void)srcs; (void)nsrc; (void)cnt; (void)stream;
-  return -LFA_EOPNOTSUPP;
-#endif
 }
+#endif
+
+extern "C" int LFA_CAT(lfa__readwrite_op, LFA_OP)(int dt, void *dst,
+                                                  const void *src, void *res,
+                                                  size_t cnt, void *stream) {
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_readwrite<LFA_OP, T>(dst, src, res, cnt,
+                                            (hipStream_t)stream);
+  });
+}
+#else
+extern "C" int LFA_CAT(lfa__swap_op, LFA_OP)(int dt, void *dst, const void *src,
+                                             const void *cmp, void *res,
+                                             size_t cnt, void *stream) {
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_swap<LFA_OP, T>(dst, src, cmp, res, cnt,
+                                       (hipStream_t)stream);
+  });
+}
+#endif
 
 #if LFA_OP == 2
 // Tuning sweep for the headline kernel (float SUM): the variants bench.py

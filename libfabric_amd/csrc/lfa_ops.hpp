@@ -183,3 +183,72 @@ constexpr bool supported() {
 }
 
 }  // namespace lfa
+
+namespace lfa {
+
+// ---------------------------------------------------------------------------
+// fetch (readwrite) and compare-swap tables (util_atomic.c:345-760, 924-980)
+// ---------------------------------------------------------------------------
+enum SwapOp : int {
+  OP_CSWAP = 12, OP_CSWAP_NE, OP_CSWAP_LE, OP_CSWAP_LT, OP_CSWAP_GE,
+  OP_CSWAP_GT, OP_MSWAP
+};
+
+template <int N> struct Bits;
+template <> struct Bits<1> { typedef uint8_t type; };
+template <> struct Bits<2> { typedef uint16_t type; };
+template <> struct Bits<4> { typedef uint32_t type; };
+template <> struct Bits<8> { typedef uint64_t type; };
+template <> struct Bits<16> { typedef u128 type; };
+
+// __atomic_compare_exchange compares object representations, not values:
+// the shipping CSWAP swaps on identical BITS (-0.0 != +0.0, NaN == same NaN).
+template <typename T>
+__device__ __forceinline__ bool bits_eq(T a, T b) {
+  typename Bits<sizeof(T)>::type x, y;
+  __builtin_memcpy(&x, &a, sizeof(T));
+  __builtin_memcpy(&y, &b, sizeof(T));
+  return x == y;
+}
+
+template <typename T>
+__device__ __forceinline__ bool val_ne(T c, T d) { return c != d; }
+template <>
+__device__ __forceinline__ bool val_ne<cf32>(cf32 c, cf32 d) {
+  return !(c.re == d.re && c.im == d.im);
+}
+
+// new dst for the swap row OP given dst a, src b, compare c
+template <int OP, typename T>
+__device__ __forceinline__ T swap_apply(T a, T b, T c) {
+  if constexpr (OP == OP_CSWAP) {
+    return bits_eq(a, c) ? b : a;
+  } else if constexpr (OP == OP_CSWAP_NE) {
+    return val_ne(c, a) ? b : a;
+  } else if constexpr (OP == OP_CSWAP_LE) {
+    return (c <= a) ? b : a;
+  } else if constexpr (OP == OP_CSWAP_LT) {
+    return (c < a) ? b : a;
+  } else if constexpr (OP == OP_CSWAP_GE) {
+    return (c >= a) ? b : a;
+  } else if constexpr (OP == OP_CSWAP_GT) {
+    return (c > a) ? b : a;
+  } else {  // OP_MSWAP
+    return (T)((b & c) | (a & ~c));
+  }
+}
+
+template <int OP, typename T>
+constexpr bool rw_supported() {
+  if constexpr (OP == OP_READ) return true;  // ALL handlers
+  else return supported<OP, T>();
+}
+
+template <int OP, typename T>
+constexpr bool swap_supported() {
+  if constexpr (OP == OP_CSWAP || OP == OP_CSWAP_NE) return true;
+  else if constexpr (OP == OP_MSWAP) return Class<T>::is_int;
+  else return !Class<T>::is_complex;
+}
+
+}  // namespace lfa

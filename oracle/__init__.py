@@ -82,6 +82,14 @@ def lib() -> ctypes.CDLL:
                                        ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.c_size_t]
+        L.oracle_has_readwrite.restype = ctypes.c_int
+        L.oracle_has_readwrite.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.oracle_has_swap.restype = ctypes.c_int
+        L.oracle_has_swap.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.oracle_readwrite.restype = ctypes.c_int
+        L.oracle_readwrite.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_size_t]
+        L.oracle_swap.restype = ctypes.c_int
+        L.oracle_swap.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 4 + [ctypes.c_size_t]
         L.oracle_allreduce_sched_len.restype = ctypes.c_int
         L.oracle_allreduce_sched_len.argtypes = [ctypes.c_int, ctypes.c_int]
         _lib = L
@@ -134,6 +142,48 @@ def write(op: int, dt: int, dst: np.ndarray, src: np.ndarray,
     rc = lib().oracle_write(variant, op, dt, _ptr(dst), _ptr(src), n)
     if rc:
         raise ValueError(f"oracle_write({op},{dt}) -> {rc}")
+
+
+_RW_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_size_t)
+_SW_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_size_t)
+SWAP_OPS = {"CSWAP": 12, "CSWAP_NE": 13, "CSWAP_LE": 14, "CSWAP_LT": 15,
+            "CSWAP_GE": 16, "CSWAP_GT": 17, "MSWAP": 18}
+
+
+def ref_readwrite_handler(op: int, dt: int):
+    tbl = (ctypes.c_void_p * (12 * 16)).in_dll(ref(), "ofi_atomic_readwrite_handlers")
+    p = tbl[op * 16 + dt]
+    return _RW_FN(p) if p else None
+
+
+def ref_swap_handler(op: int, dt: int):
+    tbl = (ctypes.c_void_p * (7 * 16)).in_dll(ref(), "ofi_atomic_swap_handlers")
+    p = tbl[(op - 12) * 16 + dt]
+    return _SW_FN(p) if p else None
+
+
+def has_readwrite(op: int, dt: int) -> bool:
+    return bool(lib().oracle_has_readwrite(op, dt))
+
+
+def has_swap(op: int, dt: int) -> bool:
+    return bool(lib().oracle_has_swap(op, dt))
+
+
+def readwrite(op, dt, dst, src, res, variant=PLAIN):
+    rc = lib().oracle_readwrite(variant, op, dt, _ptr(dst), _ptr(src), _ptr(res),
+                                dst.nbytes // datatype_size(dt))
+    if rc:
+        raise ValueError(f"oracle_readwrite({op},{dt}) -> {rc}")
+
+
+def swap(op, dt, dst, src, cmp, res, variant=CAS):
+    rc = lib().oracle_swap(variant, op, dt, _ptr(dst), _ptr(src), _ptr(cmp), _ptr(res),
+                           dst.nbytes // datatype_size(dt))
+    if rc:
+        raise ValueError(f"oracle_swap({op},{dt}) -> {rc}")
 
 
 def ref_write(op: int, dt: int, dst: np.ndarray, src: np.ndarray) -> None:

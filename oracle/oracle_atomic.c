@@ -14,6 +14,7 @@
  *                       :987-1020 (open-coded table)
  *   - datatype sizes    prov/util/src/util_atomic.c:37-64
  *   - ofi_atomic_valid  prov/util/src/util_atomic.c:1088-1140
+ *   - fetch / swap tbl  prov/util/src/util_atomic.c:345-760, :924-980
  *   - allreduce sched   prov/coll/src/coll_coll.c:349-449 (recursive doubling)
  *   - reduce item       prov/coll/src/coll_coll.c:758-768
  *
@@ -291,7 +292,10 @@ int oracle_write(int variant, int op, int dt, void *dst, const void *src,
 	return 0;
 }
 
-/* ofi_atomic_valid for the write table (util_atomic.c:1088-1140). */
+int oracle_has_readwrite(int op, int dt);
+int oracle_has_swap(int op, int dt);
+
+/* ofi_atomic_valid (util_atomic.c:1088-1140): write, fetch and compare tables. */
 int oracle_atomic_valid(int dt, int op, uint64_t flags)
 {
 	if (flags & LFA_TAGGED) {
@@ -304,11 +308,178 @@ int oracle_atomic_valid(int dt, int op, uint64_t flags)
 	}
 	if (dt < 0 || dt >= LFA_DATATYPE_CNT)
 		return -LFA_EOPNOTSUPP;
-	if (flags & (LFA_FETCH_ATOMIC | LFA_COMPARE_ATOMIC))
-		return -LFA_EOPNOTSUPP;  /* fetch/compare tables: not restated */
+	if (flags & LFA_FETCH_ATOMIC) {
+		if (op < LFA_MIN || op > LFA_ATOMIC_WRITE)
+			return -LFA_EOPNOTSUPP;
+		return oracle_has_readwrite(op, dt) ? 0 : -LFA_EOPNOTSUPP;
+	}
+	if (flags & LFA_COMPARE_ATOMIC) {
+		if (op < LFA_CSWAP || op > LFA_MSWAP)
+			return -LFA_EOPNOTSUPP;
+		return oracle_has_swap(op, dt) ? 0 : -LFA_EOPNOTSUPP;
+	}
 	if (op < LFA_MIN || op > LFA_ATOMIC_WRITE || op == LFA_ATOMIC_READ)
 		return -LFA_EOPNOTSUPP;
 	return table[ORACLE_PLAIN][op][dt] ? 0 : -LFA_EOPNOTSUPP;
+}
+
+/* ------------------------------------------------------------------ */
+/* fetch (readwrite) table (util_atomic.c:345-588, :924-950)           */
+/*                                                                     */
+/* Every shipping readwrite handler returns the old destination value  */
+/* in res[] and then performs the write op (READWRITEEXT CAS loops,    */
+/* __atomic_fetch_or/and/xor, __atomic_exchange for ATOMIC_WRITE); the */
+/* ATOMIC_READ row only loads.  Single-threaded that is exactly        */
+/* "res = dst; dst = dst OP src", in both variants.                    */
+/* ------------------------------------------------------------------ */
+int oracle_has_readwrite(int op, int dt)
+{
+	if (op < 0 || op >= LFA_READWRITE_OP_CNT || dt < 0 || dt >= LFA_DATATYPE_CNT)
+		return 0;
+	if (op == LFA_ATOMIC_READ)  /* ALL handlers (util_atomic.c:936) */
+		return table[ORACLE_PLAIN][LFA_ATOMIC_WRITE][dt] != NULL;
+	return table[ORACLE_PLAIN][op][dt] != NULL;
+}
+
+int oracle_readwrite(int variant, int op, int dt, void *dst, const void *src,
+		     void *res, size_t cnt)
+{
+	if (!oracle_has_readwrite(op, dt))
+		return -LFA_EOPNOTSUPP;
+	memcpy(res, dst, cnt * dt_size[dt]);
+	if (op != LFA_ATOMIC_READ)
+		table[variant][op][dt](dst, src, cnt);
+	return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* compare-swap table (util_atomic.c:590-760, :952-980)                */
+/*                                                                     */
+/* res = old dst; dst = src when the condition holds:                  */
+/*   CSWAP     CAS build: __atomic_compare_exchange — a BYTEWISE       */
+/*             compare of dst and cmp (so -0.0 != +0.0 and a NaN       */
+/*             equals itself); open-coded build: (cmp) == (dst)       */
+/*   CSWAP_NE  (cmp) != (dst)     CSWAP_LE (cmp) <= (dst)               */
+/*   CSWAP_LT  (cmp) <  (dst)     CSWAP_GE (cmp) >= (dst)               */
+/*   CSWAP_GT  (cmp) >  (dst)                                           */
+/*   MSWAP     dst = (src & cmp) | (dst & ~cmp)   (integers)            */
+/* ------------------------------------------------------------------ */
+#define SWAP_LOOP(T, COND)                                                \
+	do {                                                              \
+		T *d = (T *)dst;                                          \
+		const T *s_ = (const T *)src, *c_ = (const T *)cmp;       \
+		T *r = (T *)res;                                          \
+		for (size_t i = 0; i < cnt; i++) {                        \
+			T a = d[i], b = s_[i], c = c_[i];                 \
+			(void)b;                                          \
+			r[i] = a;                                         \
+			if (COND)                                         \
+				d[i] = b;                                 \
+		}                                                         \
+	} while (0)
+#define MSWAP_LOOP(T)                                                     \
+	do {                                                              \
+		T *d = (T *)dst;                                          \
+		const T *s_ = (const T *)src, *c_ = (const T *)cmp;       \
+		T *r = (T *)res;                                          \
+		for (size_t i = 0; i < cnt; i++) {                        \
+			r[i] = d[i];                                      \
+			d[i] = (T)((s_[i] & c_[i]) | (d[i] & ~c_[i]));    \
+		}                                                         \
+	} while (0)
+
+#define SWAP_REAL_CASES(OPV, COND)                                        \
+	switch (dt) {                                                     \
+	case LFA_INT8: SWAP_LOOP(int8_t, COND); break;                    \
+	case LFA_UINT8: SWAP_LOOP(uint8_t, COND); break;                  \
+	case LFA_INT16: SWAP_LOOP(int16_t, COND); break;                  \
+	case LFA_UINT16: SWAP_LOOP(uint16_t, COND); break;                \
+	case LFA_INT32: SWAP_LOOP(int32_t, COND); break;                  \
+	case LFA_UINT32: SWAP_LOOP(uint32_t, COND); break;                \
+	case LFA_INT64: SWAP_LOOP(int64_t, COND); break;                  \
+	case LFA_UINT64: SWAP_LOOP(uint64_t, COND); break;                \
+	case LFA_FLOAT: SWAP_LOOP(float, COND); break;                    \
+	case LFA_DOUBLE: SWAP_LOOP(double, COND); break;                  \
+	case LFA_INT128: SWAP_LOOP(i128_t, COND); break;                  \
+	case LFA_UINT128: SWAP_LOOP(u128_t, COND); break;                 \
+	default: return -LFA_EOPNOTSUPP;                                  \
+	}
+
+int oracle_has_swap(int op, int dt)
+{
+	int realno = (dt >= LFA_INT8 && dt <= LFA_DOUBLE) || dt == LFA_INT128 ||
+		     dt == LFA_UINT128;
+	int ints = (dt >= LFA_INT8 && dt <= LFA_UINT64) || dt == LFA_INT128 ||
+		   dt == LFA_UINT128;
+
+	switch (op) {
+	case LFA_CSWAP:
+	case LFA_CSWAP_NE:
+		return realno || dt == LFA_FLOAT_COMPLEX;
+	case LFA_CSWAP_LE:
+	case LFA_CSWAP_LT:
+	case LFA_CSWAP_GE:
+	case LFA_CSWAP_GT:
+		return realno;
+	case LFA_MSWAP:
+		return ints;
+	default:
+		return 0;
+	}
+}
+
+int oracle_swap(int variant, int op, int dt, void *dst, const void *src,
+		const void *cmp, void *res, size_t cnt)
+{
+	size_t esz;
+
+	if (!oracle_has_swap(op, dt))
+		return -LFA_EOPNOTSUPP;
+	esz = dt_size[dt];
+	if (op == LFA_CSWAP && variant == ORACLE_CAS) {
+		/* __atomic_compare_exchange(&d, &cmp, &src): bytewise */
+		for (size_t i = 0; i < cnt; i++) {
+			char *d = (char *)dst + i * esz;
+
+			memcpy((char *)res + i * esz, d, esz);
+			if (!memcmp(d, (const char *)cmp + i * esz, esz))
+				memcpy(d, (const char *)src + i * esz, esz);
+		}
+		return 0;
+	}
+	if (dt == LFA_FLOAT_COMPLEX) {
+		if (op == LFA_CSWAP)
+			SWAP_LOOP(cf32_t, c == a);
+		else
+			SWAP_LOOP(cf32_t, c != a);
+		return 0;
+	}
+	switch (op) {
+	case LFA_CSWAP: SWAP_REAL_CASES(op, c == a) break;
+	case LFA_CSWAP_NE: SWAP_REAL_CASES(op, c != a) break;
+	case LFA_CSWAP_LE: SWAP_REAL_CASES(op, c <= a) break;
+	case LFA_CSWAP_LT: SWAP_REAL_CASES(op, c < a) break;
+	case LFA_CSWAP_GE: SWAP_REAL_CASES(op, c >= a) break;
+	case LFA_CSWAP_GT: SWAP_REAL_CASES(op, c > a) break;
+	case LFA_MSWAP:
+		switch (dt) {
+		case LFA_INT8: MSWAP_LOOP(int8_t); break;
+		case LFA_UINT8: MSWAP_LOOP(uint8_t); break;
+		case LFA_INT16: MSWAP_LOOP(int16_t); break;
+		case LFA_UINT16: MSWAP_LOOP(uint16_t); break;
+		case LFA_INT32: MSWAP_LOOP(int32_t); break;
+		case LFA_UINT32: MSWAP_LOOP(uint32_t); break;
+		case LFA_INT64: MSWAP_LOOP(int64_t); break;
+		case LFA_UINT64: MSWAP_LOOP(uint64_t); break;
+		case LFA_INT128: MSWAP_LOOP(i128_t); break;
+		case LFA_UINT128: MSWAP_LOOP(u128_t); break;
+		default: return -LFA_EOPNOTSUPP;
+		}
+		break;
+	default:
+		return -LFA_EOPNOTSUPP;
+	}
+	return 0;
 }
 
 /* ------------------------------------------------------------------ */

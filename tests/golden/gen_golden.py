@@ -141,6 +141,54 @@ def main() -> None:
             manifest["combine"].append({"file": fn, "op": op, "dt": dt,
                                         "n": int(dst.shape[0]), "seed": seed})
 
+    # fetch (readwrite) and compare (swap) tables, also from the reference
+    manifest["readwrite"], manifest["swap"] = [], []
+    manifest["source"]["readwrite"] = ("out/res = reference fabtests "
+                                       "ofi_atomic_readwrite_handlers[op][dt]")
+    manifest["source"]["swap"] = (
+        "out/res = reference fabtests ofi_atomic_swap_handlers (open-coded: CSWAP "
+        "compares VALUES); the shipping CAS build compares BITS — see test_oracle")
+    for opname, op in oracle.OPS.items():
+        for dtname, (dt, _) in oracle.DATATYPES.items():
+            if not oracle.has_readwrite(op, dt):
+                continue
+            dst, src, _ = combine_case(op if op <= 9 else 2, dt, 5000 + 100 * op + dt)
+            out, res = dst.copy(), np.zeros_like(dst)
+            oracle.ref_readwrite_handler(op, dt)(out.ctypes.data, src.ctypes.data,
+                                                 res.ctypes.data, dst.shape[0])
+            fn = f"readwrite_{opname}_{dtname}.npz"
+            np.savez_compressed(os.path.join(OUT, fn), dst=dst.view(np.uint8),
+                                src=src.view(np.uint8), out=out.view(np.uint8),
+                                res=res.view(np.uint8))
+            manifest["readwrite"].append({"file": fn, "op": op, "dt": dt,
+                                          "n": int(dst.shape[0])})
+    for opname, op in oracle.SWAP_OPS.items():
+        for dtname, (dt, _) in oracle.DATATYPES.items():
+            if not oracle.has_swap(op, dt):
+                continue
+            rng = np.random.default_rng(7000 + 100 * op + dt)
+            dst, src, _ = combine_case(2, dt, 7000 + 100 * op + dt)
+            cmp = rand_lanes(dt, dst.shape[0], rng)
+            # a third of the lanes compare equal, a third as the other zero /
+            # the same NaN bits, the rest random
+            k = dst.shape[0]
+            eq = rng.random(k) < 0.34
+            cmp[eq] = dst[eq]
+            if oracle.DT_NP[dt].kind in "fc":
+                ft = np.float32 if oracle.DT_NP[dt].kind == "c" or dt == 8 else np.float64
+                dv, cv = dst.view(ft), cmp.view(ft)
+                dv[:16] = np.array([0.0, -0.0, np.nan, -np.nan] * 4, ft)
+                cv[:16] = np.array([-0.0, 0.0, np.nan, -np.nan, 0.0, -0.0, 1.0, np.nan] * 2, ft)
+            out, res = dst.copy(), np.zeros_like(dst)
+            oracle.ref_swap_handler(op, dt)(out.ctypes.data, src.ctypes.data,
+                                            cmp.ctypes.data, res.ctypes.data, k)
+            fn = f"swap_{opname}_{dtname}.npz"
+            np.savez_compressed(os.path.join(OUT, fn), dst=dst.view(np.uint8),
+                                src=src.view(np.uint8), cmp=cmp.view(np.uint8),
+                                out=out.view(np.uint8), res=res.view(np.uint8))
+            manifest["swap"].append({"file": fn, "op": op, "dt": dt,
+                                     "n": int(k)})
+
     manifest["source"]["allreduce"] = (
         "oracle restatement of prov/coll/src/coll_coll.c:349-449 "
         "(prov/coll itself is unbuildable here: needs configure's config.h)")
@@ -179,7 +227,8 @@ def main() -> None:
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     total = sum(os.path.getsize(os.path.join(OUT, x)) for x in os.listdir(OUT))
-    print(f"wrote {len(manifest['combine'])} combine + "
+    print(f"wrote {len(manifest['combine'])} combine + {len(manifest['readwrite'])} "
+          f"readwrite + {len(manifest['swap'])} swap + "
           f"{len(manifest['allreduce'])} allreduce fixtures, {total/1024:.0f} KiB")
 
 

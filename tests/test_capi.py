@@ -57,11 +57,23 @@ def test_table_membership_matches_oracle():
                 oracle.has_handler(op, dt), (op, dt)
 
 
+def test_fetch_compare_tables_match_oracle():
+    L = _lib_or_skip("lfa")
+    rw = (ctypes.c_void_p * (12 * 16)).in_dll(L, "lfa_atomic_readwrite_handlers")
+    sw = (ctypes.c_void_p * (7 * 16)).in_dll(L, "lfa_atomic_swap_handlers")
+    for op in range(12):
+        for dt in range(16):
+            assert bool(rw[op * 16 + dt]) == oracle.has_readwrite(op, dt), (op, dt)
+    for op in range(12, 19):
+        for dt in range(16):
+            assert bool(sw[(op - 12) * 16 + dt]) == oracle.has_swap(op, dt), (op, dt)
+
+
 def test_valid_and_size_match_oracle():
     from libfabric_amd import atomic
     flags_set = [0, 1 << 3, 1 << 58, 1 << 59, (1 << 58) | (1 << 59),
                  (1 << 3) | (1 << 58), 1 << 40]
-    for op in range(13):
+    for op in range(20):
         for dt in range(18):
             for fl in flags_set:
                 assert atomic.atomic_valid(dt, op, fl) == \

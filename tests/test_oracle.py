@@ -146,3 +146,84 @@ def test_reduce_scatter_slices():
     out = oracle.reduce_scatter(2, i64, sends)
     assert [len(o) for o in out] == [4, 3, 3]
     assert np.concatenate(out).tolist() == (np.arange(10) * 6).tolist()
+
+
+# ------------------------------------------------ fetch / compare tables --
+
+def test_fetch_and_compare_table_membership():
+    """Shipping CAS tables (util_atomic.c:924-980) vs the reference fabtests
+    tables: identical except the columns the CAS build leaves NULL
+    (double complex, long double, long double complex)."""
+    for op in range(12):
+        for dt in range(16):
+            if dt in (11, 12, 13):
+                assert not oracle.has_readwrite(op, dt)
+                continue
+            assert oracle.has_readwrite(op, dt) == \
+                (oracle.ref_readwrite_handler(op, dt) is not None), (op, dt)
+    for op in range(12, 19):
+        for dt in range(16):
+            if dt in (11, 12, 13):
+                assert not oracle.has_swap(op, dt)
+                continue
+            assert oracle.has_swap(op, dt) == \
+                (oracle.ref_swap_handler(op, dt) is not None), (op, dt)
+
+
+@pytest.mark.parametrize("variant", [oracle.CAS, oracle.PLAIN])
+def test_readwrite_fixtures(manifest, golden_dir, variant):
+    assert len(manifest["readwrite"]) == 145
+    for case in manifest["readwrite"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        nd = oracle.DT_NP[case["dt"]]
+        d = z["dst"].view(nd).copy()
+        r = np.zeros_like(d)
+        oracle.readwrite(case["op"], case["dt"], d, z["src"].view(nd).copy(), r, variant)
+        assert d.tobytes() == z["out"].tobytes(), case["file"]
+        assert r.tobytes() == z["res"].tobytes(), case["file"]
+
+
+def _bits_vs_value_lanes(dt, d, c):
+    """Lanes where a bytewise compare and a value compare disagree."""
+    nd = oracle.DT_NP[dt]
+    if nd.kind not in "fc":
+        return np.zeros(d.shape[0], bool)
+    ft = np.float32 if nd.kind == "c" or dt == 8 else np.float64
+    dv, cv = d.view(ft), c.view(ft)
+    if nd.kind == "c":
+        dv, cv = dv.reshape(-1, 2), cv.reshape(-1, 2)
+        val = (dv == cv).all(axis=1)
+        bits = (dv.view(np.uint32) == cv.view(np.uint32)).all(axis=1)
+    else:
+        ut = np.uint32 if ft == np.float32 else np.uint64
+        val = dv == cv
+        bits = dv.view(ut) == cv.view(ut)
+    return val != bits
+
+
+def test_swap_fixtures_both_builds(manifest, golden_dir):
+    """Open-coded oracle == reference fixtures everywhere.  The shipping
+    CAS build (__atomic_compare_exchange, a BYTEWISE compare) differs from
+    them on FI_CSWAP exactly where bits and values disagree: ±0 pairs and
+    identical NaNs — and nowhere else."""
+    assert len(manifest["swap"]) == 84
+    seen_divergence = 0
+    for case in manifest["swap"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        nd = oracle.DT_NP[case["dt"]]
+        d0, s, c = (z[k].view(nd).copy() for k in ("dst", "src", "cmp"))
+        for variant in (oracle.PLAIN, oracle.CAS):
+            d, r = d0.copy(), np.zeros_like(d0)
+            oracle.swap(case["op"], case["dt"], d, s, c, r, variant)
+            assert r.tobytes() == z["res"].tobytes(), case["file"]
+            if variant == oracle.PLAIN or case["op"] != 12:
+                assert d.tobytes() == z["out"].tobytes(), (case["file"], variant)
+            else:
+                esz = oracle.datatype_size(case["dt"])
+                got = d.view(np.uint8).reshape(-1, esz)
+                ref = z["out"].reshape(-1, esz)
+                differ = (got != ref).any(axis=1)
+                expect = _bits_vs_value_lanes(case["dt"], d0, c)
+                assert np.array_equal(differ, expect), case["file"]
+                seen_divergence += int(differ.sum())
+    assert seen_divergence > 0
