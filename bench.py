@@ -252,6 +252,25 @@ def extra_e2e_host(dev, stream, reps=5):
             "note": "pinned host buffers; 2x256 MiB H2D + combine + 256 MiB D2H, serial"}
 
 
+def extra_host_allreduce(ep, world, reps=3):
+    """fi_allreduce on HOST buffers (what a libfabric caller hands over):
+    the provider streams 64 MiB chunks H2D -> collective -> D2H on two HIP
+    streams.  Rate = buffer bytes / wall time, PCIe-inclusive."""
+    hx = torch.rand(COUNT).pin_memory()
+    hy = torch.empty(COUNT).pin_memory()
+    ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+    ts = []
+    for _ in range(reps):
+        barrier(world)
+        t0 = time.perf_counter()
+        ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+        ts.append(max_over_ranks(time.perf_counter() - t0, world))
+    t = statistics.median(ts)
+    return {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
+            "note": "pinned host in/out, 64 MiB chunks, H2D/D2H overlapped with the "
+                    "collective"}
+
+
 def cpu_model_allreduce(world: int):
     """Modelled reference compute for a 256 MiB float SUM allreduce at N
     ranks: log2(N) x (CAS combine [+ COPY]) — prov/coll's per-rank REDUCE
@@ -295,6 +314,7 @@ def extra_collectives(rank, world, stream):
                          "algbw_gbs": round(S_BYTES / t / 1e9, 1),
                          "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)}
         ep.set_algo(coll.ALGO_TREE)
+        out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
         sweep = {}
         for nbytes in [4096 * 4 ** k for k in range(9)]:   # 4 KiB .. 256 MiB
             cnt = nbytes // 8
@@ -440,8 +460,8 @@ def main() -> None:
     ap.add_argument("--variants", default="", help="comma list for --tune")
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--extras-coll", action="store_true",
-                    help="run the collective extras at N=1 too (testing)")
+    ap.add_argument("--no-extras-coll", action="store_true",
+                    help="skip the provider (RCCL) extras at N=1")
     ap.add_argument("--extras-timeout", type=float, default=300.0)
     args = ap.parse_args()
 
@@ -561,7 +581,7 @@ def main() -> None:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
-            if world > 1 or args.extras_coll:
+            if world > 1 or not args.no_extras_coll:
                 ex.update(extra_collectives(rank, world, stream))
         except Exception as e:  # noqa: BLE001 — extras must not hide the metric
             ex["error"] = f"{type(e).__name__}: {e}"[:300]

@@ -599,6 +599,14 @@ struct lfa_coll_ep {
 	void *barrier_dev;          /* 2 x uint64 */
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
+	hipEvent_t evpool[64];      /* recycled completion events */
+	int nev;
+	struct plan_cache {         /* last schedules built, keyed by shape */
+		int valid, coll, algo, rank, n, root;
+		size_t count, esz;
+		struct plan pl;
+	} pc[8];
+	unsigned pc_next;
 	struct pending *q;          /* FIFO ring of in-flight ops */
 	size_t qcap, qhead, qlen;
 	struct lfa_cq_err_entry err;
@@ -701,6 +709,11 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	lfa_coll_ep_flush(ep);
 	for (size_t i = 0; i < ep->qlen; i++)
 		hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
+	for (int i = 0; i < ep->nev; i++)
+		hipEventDestroy(ep->evpool[i]);
+	for (int i = 0; i < 8; i++)
+		if (ep->pc[i].valid)
+			plan_free(&ep->pc[i].pl);
 	free(ep->q);
 	if (ep->ws)
 		hipFree(ep->ws);
@@ -800,6 +813,14 @@ static int grow_staging(struct lfa_coll_ep *ep, size_t need)
 /* completion queue                                                        */
 /* ---------------------------------------------------------------------- */
 
+static void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
+{
+	if (ep->nev < (int)(sizeof(ep->evpool) / sizeof(ep->evpool[0])))
+		ep->evpool[ep->nev++] = ev;
+	else
+		hipEventDestroy(ev);
+}
+
 static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 			      void *context, int kind, struct lfa_coll_mc *mc)
 {
@@ -818,10 +839,12 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 		ep->qcap *= 2;
 	}
 	p = &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
-	if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess)
+	if (ep->nev)
+		p->ev = ep->evpool[--ep->nev];
+	else if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess)
 		return -LFA_EIO;
 	if (hipEventRecord(p->ev, s) != hipSuccess) {
-		hipEventDestroy(p->ev);
+		release_event(ep, p->ev);
 		return -LFA_EIO;
 	}
 	p->context = context;
@@ -889,7 +912,7 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			c->op_context = p->context;
 			c->flags = LFA_COLLECTIVE;
 		}
-		hipEventDestroy(p->ev);
+		release_event(ep, p->ev);
 		ep->qhead = (ep->qhead + 1) % ep->qcap;
 		ep->qlen--;
 	}
@@ -899,6 +922,7 @@ ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
 		    size_t count)
 {
 	size_t n;
+	int have_err;
 	ncclResult_t async;
 
 	if (!ep || (!buf && count))
@@ -914,10 +938,11 @@ ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
 		ep->err.prov_errno = (int)async;
 		ep->have_err = 1;
 	}
+	have_err = ep->have_err;
 	pthread_mutex_unlock(&ep->lock);
 	if (n)
 		return (ssize_t)n;
-	return ep->have_err ? -LFA_EIO : -LFA_EAGAIN;
+	return have_err ? -LFA_EIO : -LFA_EAGAIN;
 }
 
 ssize_t lfa_cq_readerr(struct lfa_coll_ep *ep, struct lfa_cq_err_entry *buf)
@@ -1073,6 +1098,43 @@ static int try_rccl(struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 	return 1;
 }
 
+/* Schedules depend only on shape: reuse the last few (repeated collectives
+ * of one size are the common case, and building one allocates). */
+static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
+		       enum lfa_collective_op coll, enum lfa_coll_algo algo,
+		       int rank, int n, int root, size_t count, size_t esz)
+{
+	struct plan_cache *c;
+	int ret;
+
+	for (int i = 0; i < 8; i++) {
+		c = &ep->pc[i];
+		if (c->valid && c->coll == (int)coll && c->algo == (int)algo &&
+		    c->rank == rank && c->n == n && c->root == root &&
+		    c->count == count && c->esz == esz) {
+			*out = &c->pl;
+			return 0;
+		}
+	}
+	c = &ep->pc[ep->pc_next++ % 8];
+	if (c->valid)
+		plan_free(&c->pl);
+	c->valid = 0;
+	ret = plan_make(&c->pl, coll, algo, rank, n, root, count, esz);
+	if (ret)
+		return ret;
+	c->valid = 1;
+	c->coll = (int)coll;
+	c->algo = (int)algo;
+	c->rank = rank;
+	c->n = n;
+	c->root = root;
+	c->count = count;
+	c->esz = esz;
+	*out = &c->pl;
+	return 0;
+}
+
 /*
  * One operation on device buffers, enqueued on ep->stream.
  */
@@ -1081,7 +1143,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		      size_t count, int root, enum lfa_datatype dt,
 		      enum lfa_op op, hipStream_t s)
 {
-	struct plan pl;
+	const struct plan *pl;
 	size_t esz = lfa_datatype_size(dt);
 	void *base[3];
 	int ret;
@@ -1089,17 +1151,17 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	if (ep->algo == LFA_ALGO_RCCL && mc->size > 1 &&
 	    try_rccl(mc, coll, buf, result, count, root, dt, op, s, &ret))
 		return ret;
-	ret = plan_make(&pl, coll, ep->algo, mc->rank, mc->size, root, count, esz);
+	ret = cached_plan(ep, &pl, coll, ep->algo, mc->rank, mc->size, root,
+			  count, esz);
 	if (ret)
 		return ret;
-	ret = grow(&ep->ws, &ep->ws_size, pl.tmp, s);
+	ret = grow(&ep->ws, &ep->ws_size, pl->tmp, s);
 	if (!ret) {
 		base[LFA_BUF_SEND] = (void *)buf;
 		base[LFA_BUF_RESULT] = result;
 		base[LFA_BUF_TMP] = ep->ws;
-		ret = exec_plan(mc, &pl, base, op, dt, s);
+		ret = exec_plan(mc, pl, base, op, dt, s);
 	}
-	plan_free(&pl);
 	return ret;
 }
 
