@@ -273,3 +273,56 @@ def test_fetch_swap_alignment(lfa, n):
         torch.cuda.synchronize()
         assert np.array_equal(dd.cpu().numpy().view(np.int32)[od:od + n], want_d)
         assert np.array_equal(rd.cpu().numpy().view(np.int32)[od:od + n], want_r)
+
+
+# ------------------------------------- size-independent properties at size ----
+
+def test_full_size_properties(lfa):
+    """At BASELINE sizes, properties the oracle need not recompute:
+    BXOR twice is the identity; MAX then MIN against the same operand
+    restores min(x, s)…max; SUM of x and -x is exactly ±0; WRITE copies;
+    the fetch-add returns the pre-image."""
+    n = 64 * 1024 * 1024 // 8
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randint(-2**63, 2**63 - 1, (n,), device=DEV, dtype=torch.int64, generator=g)
+    s = torch.randint(-2**63, 2**63 - 1, (n,), device=DEV, dtype=torch.int64, generator=g)
+    y = x.clone()
+    lfa.write(9, 6, y, s)
+    lfa.write(9, 6, y, s)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)                      # BXOR involution
+    y = x.clone()
+    lfa.write(1, 6, y, s)                         # y = max(x, s)
+    torch.cuda.synchronize()
+    assert torch.equal(y, torch.maximum(x, s))
+    lfa.write(0, 6, y, s)                         # min(max(x, s), s) == s
+    torch.cuda.synchronize()
+    assert torch.equal(y, s)
+    f = torch.rand(256 * 1024 * 1024 // 4, device=DEV, generator=g) - 0.5
+    z = f.clone()
+    lfa.write(2, 8, z, -f)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(z).item() == 0     # x + (-x) == 0 exactly
+    w = torch.empty_like(f)
+    lfa.write(11, 8, w, f)
+    torch.cuda.synchronize()
+    assert torch.equal(w, f)                      # ATOMIC_WRITE copies bits
+    r = torch.empty_like(x)
+    y = x.clone()
+    lfa.readwrite(2, 6, y, s, r)                  # fetch-add
+    torch.cuda.synchronize()
+    assert torch.equal(r, x) and torch.equal(y, x + s)
+
+
+def test_tree_full_size_8x32mib_vs_numpy(lfa):
+    """allreduce block shape at configs[3] (8 ranks x 32 MiB) against an
+    explicit numpy tree ((x7+x6)+(x5+x4))+((x3+x2)+(x1+x0))."""
+    blk = 32 * 1024 * 1024 // 4
+    g = torch.Generator(device=DEV).manual_seed(12)
+    xs = [torch.rand(blk, device=DEV, generator=g) * 2 - 1 for _ in range(8)]
+    out = torch.empty_like(xs[0])
+    lfa.reduce_tree(2, 8, out, xs)
+    torch.cuda.synchronize()
+    h = [x.cpu().numpy() for x in xs]
+    want = ((h[7] + h[6]) + (h[5] + h[4])) + ((h[3] + h[2]) + (h[1] + h[0]))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
