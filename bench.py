@@ -448,6 +448,36 @@ def tune_tree(args) -> None:
     print(json.dumps({"tune_tree": rows}))
 
 
+def sweep_ops(args) -> None:
+    """Every (op, datatype) of the write table at 256 MiB: kernel time and
+    fraction of the HBM roofline (3·S bytes per launch)."""
+    from libfabric_amd import atomic
+    import oracle
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream()
+    nbytes = S_BYTES
+    sets = [(torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda"),
+             torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda"))
+            for _ in range(3)]
+    rows = []
+    for opname, op in oracle.OPS.items():
+        for dtname, (dt, _) in oracle.DATATYPES.items():
+            if not oracle.has_handler(op, dt):
+                continue
+            cnt = nbytes // oracle.datatype_size(dt)
+
+            def fn(i, op=op, dt=dt, cnt=cnt):
+                d, s = sets[i % 3]
+                atomic.write(op, dt, d, s, cnt, stream)
+            for i in range(6):
+                fn(i)
+            ms = _kernel_events(fn, 12, stream)
+            gbps = 3 * nbytes / (ms * 1e-3) / 1e9
+            rows.append({"op": opname, "dt": dtname, "us": round(ms * 1e3, 1),
+                         "frac": round(gbps / PEAK_GBPS, 3)})
+    print(json.dumps({"sweep_ops": rows}))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -459,6 +489,7 @@ def main() -> None:
     ap.add_argument("--tune-rounds", type=int, default=10)
     ap.add_argument("--variants", default="", help="comma list for --tune")
     ap.add_argument("--tune-tree", action="store_true")
+    ap.add_argument("--sweep-ops", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
@@ -470,6 +501,9 @@ def main() -> None:
         return
     if args.tune_tree:
         tune_tree(args)
+        return
+    if args.sweep_ops:
+        sweep_ops(args)
         return
 
     rank, world, local = init_dist(args.gpus)

@@ -112,20 +112,26 @@ __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
   const size_t base =
       (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
   if (base + 64 * U <= nvec) {
+    if constexpr (OP != OP_WRITE) {  // ATOMIC_WRITE never reads dst
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
-                                       (lds_void *)&lds[0][w][u][0], 16, 0,
-                                       /*aux: nt*/ 2);
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0,
+                                         /*aux: nt*/ 2);
+    }
 #pragma unroll
     for (int u = 0; u < U; u++)
       __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
                                        (lds_void *)&lds[1][w][u][0], 16, 0, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      st<true>(dst + base + u * 64 + l,
-               apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]));
+    for (int u = 0; u < U; u++) {
+      if constexpr (OP == OP_WRITE)
+        st<true>(dst + base + u * 64 + l, lds[1][w][u][l]);
+      else
+        st<true>(dst + base + u * 64 + l,
+                 apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]));
+    }
   } else {
     for (int u = 0; u < U; u++) {
       size_t i = base + (size_t)u * 64 + l;
