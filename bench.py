@@ -301,6 +301,7 @@ def extra_collectives(rank, world, stream):
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
         for name, algo in (("allreduce_tree_exact", coll.ALGO_TREE),
+                           ("allreduce_tree_exact_rccl_xfer", coll.ALGO_TREE_COLL),
                            ("allreduce_rccl", coll.ALGO_RCCL)):
             ep.set_algo(algo)
             ep.wait(ep.allreduce(x, y, COUNT, 8, 2))

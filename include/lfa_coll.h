@@ -65,6 +65,11 @@ enum lfa_coll_algo {
 	 * ring association order (float results within the documented
 	 * tolerance, not bit-identical); other ops fall back to TREE. */
 	LFA_ALGO_RCCL = 2,
+	/* LFA_ALGO_TREE with the block exchange and the block all-gather done
+	 * by RCCL's own ncclAllToAll / in-place ncclAllGather instead of
+	 * grouped ncclSend/ncclRecv (when count divides evenly over the
+	 * group; otherwise identical to LFA_ALGO_TREE).  Same bits. */
+	LFA_ALGO_TREE_COLL = 3,
 };
 
 /* ---- bootstrap (replaces fi_getinfo/fi_fabric/fi_domain/fi_endpoint
@@ -180,6 +185,10 @@ enum lfa_step_type {
 	LFA_STEP_REDUCE = 3,   /* dst[i] = dst[i] OP src[i], count elements  */
 	LFA_STEP_TREE = 4,     /* dst = tree(refs[first..first+nsrc)), count */
 	LFA_STEP_COPY = 5,     /* bytes from src to dst                      */
+	LFA_STEP_ALLTOALL = 6, /* count bytes per rank: block p of src goes to
+				  rank p, block q of dst comes from rank q    */
+	LFA_STEP_ALLGATHER = 7,/* count bytes: src (this rank's block) to
+				  block r of dst on every rank                */
 };
 enum lfa_buf_id { LFA_BUF_SEND = 0, LFA_BUF_RESULT = 1, LFA_BUF_TMP = 2 };
 

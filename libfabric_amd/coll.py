@@ -28,7 +28,7 @@ c_int, c_size_t, c_void_p, c_uint64, c_uint32, c_int32 = (
     ctypes.c_uint32, ctypes.c_int32)
 c_ssize_t = ctypes.c_ssize_t
 
-ALGO_TREE, ALGO_RD, ALGO_RCCL = 0, 1, 2
+ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL = 0, 1, 2, 3
 STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY = range(6)
 BUF_SEND, BUF_RESULT, BUF_TMP = 0, 1, 2
 ADDR_NOTAVAIL = (1 << 64) - 1
@@ -386,4 +386,4 @@ def esz(dt: int) -> int:
 
 
 __all__ = ["plan", "block", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
-           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "esz"]
+           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "esz"]

@@ -181,6 +181,22 @@ static void p_tree_end(struct planner *p, uint32_t first, struct lfa_ref dst,
 	}
 }
 
+static void p_coll(struct planner *p, int type, struct lfa_ref dst,
+		   struct lfa_ref src, uint64_t bytes)
+{
+	struct lfa_step *s;
+
+	p_group_end(p);
+	if (!bytes)
+		return;
+	s = push(p, type);
+	if (s) {
+		s->dst = dst;
+		s->src = src;
+		s->count = bytes;
+	}
+}
+
 /*
  * Tree algorithm, phase 1: rank r collects block r of every rank's input.
  * TMP slot p (block-r sized) receives rank p's block; rank r's own block is
@@ -342,6 +358,36 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 
 	if (algo == LFA_ALGO_RCCL)
 		algo = LFA_ALGO_TREE;   /* the RCCL algo is not a schedule */
+	if (algo == LFA_ALGO_TREE_COLL) {
+		/* collective transport only for even blocks of the big path */
+		int even = n > 1 && count % (size_t)n == 0 &&
+			   !(coll == LFA_ALLREDUCE &&
+			     bytes * (size_t)n <= LFA_SMALL_AG_BYTES);
+
+		if (even && (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER)) {
+			uint32_t first;
+
+			/* TMP slot q <- block r of rank q (own block too) */
+			p_coll(&p, LFA_STEP_ALLTOALL, ref(LFA_BUF_TMP, 0),
+			       ref(LFA_BUF_SEND, 0), mlen * esz);
+			first = p_tree_begin(&p);
+			for (int k = 0; k < n; k++)
+				p_tree_src(&p, ref(LFA_BUF_TMP, (uint64_t)k * mlen * esz));
+			p_tree_end(&p, first, coll == LFA_ALLREDUCE ?
+				   ref(LFA_BUF_RESULT, moff * esz) :
+				   ref(LFA_BUF_RESULT, 0), mlen);
+			if (coll == LFA_ALLREDUCE)
+				p_coll(&p, LFA_STEP_ALLGATHER, ref(LFA_BUF_RESULT, 0),
+				       ref(LFA_BUF_RESULT, moff * esz), mlen * esz);
+			*tmp_bytes = (size_t)n * mlen * esz;
+			*nsteps = p.n;
+			*nrefs = p.nr;
+			if (!steps || !refs)
+				return 0;
+			return (p.n > p.cap || p.nr > p.rcap) ? -LFA_ETOOSMALL : 0;
+		}
+		algo = LFA_ALGO_TREE;
+	}
 	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD)
 		return -LFA_ENOSYS;
 
@@ -737,7 +783,7 @@ void *lfa_coll_ep_stream(struct lfa_coll_ep *ep)
 int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo)
 {
 	if (!ep || (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
-		    algo != LFA_ALGO_RCCL))
+		    algo != LFA_ALGO_RCCL && algo != LFA_ALGO_TREE_COLL))
 		return -LFA_EINVAL;
 	ep->algo = algo;
 	return 0;
@@ -1031,6 +1077,16 @@ static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 			if (in_group && ncclGroupEnd() != ncclSuccess)
 				return -LFA_EIO;
 			in_group = 0;
+			break;
+		case LFA_STEP_ALLTOALL:
+			ret = ncclAllToAll(resolve(base, st->src), resolve(base, st->dst),
+					   st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
+			      0 : -LFA_EIO;
+			break;
+		case LFA_STEP_ALLGATHER:
+			ret = ncclAllGather(resolve(base, st->src), resolve(base, st->dst),
+					    st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
+			      0 : -LFA_EIO;
 			break;
 		default:
 			ret = run_local(st, pl->refs, base, op, dt, s);
@@ -1574,6 +1630,77 @@ int lfa_query_collective(struct lfa_coll_domain *domain,
 	return 0;
 }
 
+/*
+ * Rewrite ALLTOALL / ALLGATHER items as the equivalent grouped SEND/RECV +
+ * COPY items, for executors without RCCL collectives (the loopback below;
+ * tests/_plansim.py does the same in Python).
+ */
+static int lower_plan(const struct plan *in, int r, int n, struct plan *out)
+{
+	size_t cap = in->nsteps + 1;
+
+	for (size_t i = 0; i < in->nsteps; i++)
+		if (in->steps[i].type == LFA_STEP_ALLTOALL ||
+		    in->steps[i].type == LFA_STEP_ALLGATHER)
+			cap += 2 * (size_t)n + 2;
+	memset(out, 0, sizeof(*out));
+	out->steps = calloc(cap, sizeof(*out->steps));
+	out->refs = calloc(in->nrefs ? in->nrefs : 1, sizeof(*out->refs));
+	if (!out->steps || !out->refs) {
+		plan_free(out);
+		return -LFA_ENOMEM;
+	}
+	memcpy(out->refs, in->refs, in->nrefs * sizeof(*in->refs));
+	out->nrefs = in->nrefs;
+	out->tmp = in->tmp;
+	for (size_t i = 0; i < in->nsteps; i++) {
+		const struct lfa_step *st = &in->steps[i];
+		int a2a = st->type == LFA_STEP_ALLTOALL;
+		struct lfa_step *o;
+
+		if (!a2a && st->type != LFA_STEP_ALLGATHER) {
+			out->steps[out->nsteps++] = *st;
+			continue;
+		}
+		for (int k = 1; k < n; k++) {
+			int to = (r + k) % n, from = (r - k + n) % n;
+
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_SEND;
+			o->peer = to;
+			o->count = st->count;
+			o->src = st->src;
+			if (a2a)
+				o->src.off += (uint64_t)to * st->count;
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_RECV;
+			o->peer = from;
+			o->count = st->count;
+			o->dst = st->dst;
+			o->dst.off += (uint64_t)from * st->count;
+		}
+		if (n > 1) {
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_GROUP_END;
+		}
+		o = &out->steps[out->nsteps++];
+		memset(o, 0, sizeof(*o));
+		o->type = LFA_STEP_COPY;
+		o->count = st->count;
+		o->dst = st->dst;
+		o->dst.off += (uint64_t)r * st->count;
+		o->src = st->src;
+		if (a2a)
+			o->src.off += (uint64_t)r * st->count;
+		if (o->dst.buf == o->src.buf && o->dst.off == o->src.off)
+			out->nsteps--;
+	}
+	return 0;
+}
+
 /* ====================================================================== */
 /* single-GPU multi-rank executor (loopback transport)                     */
 /* ====================================================================== */
@@ -1604,6 +1731,8 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		return ret;
 	if (algo == LFA_ALGO_RCCL)
 		algo = LFA_ALGO_TREE;
+	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD && algo != LFA_ALGO_TREE_COLL)
+		return -LFA_EINVAL;
 	pl = calloc((size_t)n, sizeof(*pl));
 	pc = calloc((size_t)n, sizeof(*pc));
 	tmp = calloc((size_t)n, sizeof(*tmp));
@@ -1613,7 +1742,13 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		goto out;
 	}
 	for (int r = 0; r < n && !ret; r++) {
-		ret = plan_make(&pl[r], coll, algo, r, n, root, count, esz);
+		struct plan raw;
+
+		ret = plan_make(&raw, coll, algo, r, n, root, count, esz);
+		if (ret)
+			break;
+		ret = lower_plan(&raw, r, n, &pl[r]);
+		plan_free(&raw);
 		if (!ret && pl[r].tmp &&
 		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)
 			ret = -LFA_ENOMEM;

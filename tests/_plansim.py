@@ -11,7 +11,36 @@ import numpy as np
 import oracle
 from libfabric_amd import coll
 
-SEND, RECV, GEND, REDUCE, TREE, COPY = range(6)
+SEND, RECV, GEND, REDUCE, TREE, COPY, ALLTOALL, ALLGATHER = range(8)
+
+
+def lower(steps, r, n):
+    """ALLTOALL / ALLGATHER -> grouped SEND/RECV + COPY (as lfa_coll.c's
+    lower_plan does for its loopback executor)."""
+    out = []
+    for s in steps:
+        if s["type"] not in (ALLTOALL, ALLGATHER):
+            out.append(s)
+            continue
+        a2a = s["type"] == ALLTOALL
+        c = s["count"]
+        for k in range(1, n):
+            to, frm = (r + k) % n, (r - k) % n
+            sb, so = s["src"]
+            out.append({"type": SEND, "peer": to, "count": c,
+                        "src": (sb, so + (to * c if a2a else 0)), "dst": (0, 0)})
+            db, do = s["dst"]
+            out.append({"type": RECV, "peer": frm, "count": c, "src": (0, 0),
+                        "dst": (db, do + frm * c)})
+        if n > 1:
+            out.append({"type": GEND, "peer": 0, "count": 0, "src": (0, 0), "dst": (0, 0)})
+        sb, so = s["src"]
+        db, do = s["dst"]
+        src = (sb, so + (r * c if a2a else 0))
+        dst = (db, do + r * c)
+        if src != dst:
+            out.append({"type": COPY, "count": c, "src": src, "dst": dst, "peer": 0})
+    return out
 
 
 def _view(bufs, ref, nbytes):
@@ -24,6 +53,8 @@ def run(coll_op, algo, n, root, dt, op, count, sends, results):
     esz = oracle.datatype_size(dt)
     nd = oracle.DT_NP[dt]
     plans = [coll.plan(coll_op, algo, r, n, root, count, esz) for r in range(n)]
+    for r in range(n):
+        plans[r].steps = lower(plans[r].steps, r, n)
     bufs = []
     for r in range(n):
         tmp = np.zeros(plans[r].tmp_bytes, np.uint8)

@@ -29,7 +29,8 @@ def _exec_plan(pl, bufs, op, dt, esz, nd, seq):
     """seq: per-(direction, peer) message counters — messages between a pair
     match FIFO, as RCCL's do, whatever group structure each rank has."""
     import oracle
-    st = pl.steps
+    from tests._plansim import lower
+    st = lower(pl.steps, dist.get_rank(), dist.get_world_size())
     i = 0
     while i < len(st):
         s = st[i]
@@ -82,9 +83,9 @@ def _worker(rank, world, port, q):
         import oracle
         from libfabric_amd import coll
         seq = {}
-        for algo in (coll.ALGO_TREE, coll.ALGO_RD):
+        for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL):
             for dt, op, count in ((8, 2, 70_001), (8, 2, 1000), (6, 0, 5), (1, 7, 3),
-                                  (9, 3, 4099)):
+                                  (9, 3, 4099), (8, 2, 6 * 20_000)):
                 nd = oracle.DT_NP[dt]
                 esz = nd.itemsize
                 rng = np.random.default_rng(1234)

@@ -45,11 +45,11 @@ def _dev(a):
 CASES = [(8, 2), (9, 3), (6, 0), (6, 6), (1, 7), (4, 9), (8, 1)]
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 3])
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 def test_loopback_allreduce(coll, algo, n):
     for dt, op in CASES:
-        for count in (1, 777, 100_003):
+        for count in (1, 777, 100_003, 120_000):
             sends = _inputs(dt, n, count, n + count + op,
                             *((0.9, 1.1) if op == 3 else (-1, 1)))
             want = oracle.allreduce(op, dt, sends)[0]
@@ -61,10 +61,11 @@ def test_loopback_allreduce(coll, algo, n):
                 assert_parity(dt, rd[r].cpu().numpy(), want, f"n={n} dt={dt} op={op} r={r}")
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 3])
 @pytest.mark.parametrize("n", [2, 3, 8])
-def test_loopback_reduce_scatter_and_reduce(coll, algo, n):
-    dt, op, count = 9, 3, 50_001
+@pytest.mark.parametrize("count", [50_001, 48_000])
+def test_loopback_reduce_scatter_and_reduce(coll, algo, n, count):
+    dt, op = 9, 3
     sends = _inputs(dt, n, count, 99 + n, 0.9, 1.1)
     want = oracle.allreduce(op, dt, sends)[0]
     sd = [_dev(s) for s in sends]
@@ -166,7 +167,7 @@ def test_rccl_other_collectives(coll, ep):
 def test_rccl_algorithms_selectable(coll, ep):
     count = 4096
     x = torch.rand(count, device=DEV, dtype=torch.float64)
-    for algo in (coll.ALGO_RD, coll.ALGO_RCCL, coll.ALGO_TREE):
+    for algo in (coll.ALGO_RD, coll.ALGO_RCCL, coll.ALGO_TREE_COLL, coll.ALGO_TREE):
         ep.set_algo(algo)
         y = torch.zeros_like(x)
         ep.wait(ep.allreduce(x, y, count, 9, 3))

@@ -31,9 +31,9 @@ NS = [1, 2, 3, 4, 5, 7, 8]
 COUNTS = [0, 1, 5, 1000, 70_001]
 
 
-@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL])
 @pytest.mark.parametrize("n", NS)
-@pytest.mark.parametrize("count", COUNTS)
+@pytest.mark.parametrize("count", COUNTS + [8 * 9000])
 def test_allreduce_schedule(algo, n, count):
     for dt, op in ((F32, SUM), (I64, MIN)):
         sends = _inputs(dt, n, count, n * 1000 + count)
@@ -45,9 +45,9 @@ def test_allreduce_schedule(algo, n, count):
             assert res[r].tobytes() == want.view(np.uint8).tobytes(), (r, dt)
 
 
-@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL])
 @pytest.mark.parametrize("n", NS)
-@pytest.mark.parametrize("count", COUNTS)
+@pytest.mark.parametrize("count", COUNTS + [8 * 9000])
 def test_reduce_scatter_schedule(algo, n, count):
     dt, op = F64, PROD
     sends = _inputs(dt, n, count, 7 + n + count)
@@ -107,6 +107,14 @@ def test_tree_schedule_traffic_is_bandwidth_optimal():
     assert sent == 2 * (n - 1) * count * esz // n
     trees = [s for s in p.steps if s["type"] == 4]
     assert len(trees) == 1 and trees[0]["nsrc"] == n
+
+
+def test_tree_coll_uses_rccl_collectives_when_even():
+    p = coll.plan(ALLREDUCE, coll.ALGO_TREE_COLL, 2, 8, -1, 8 * 1_000_000, 4)
+    kinds = [s["type"] for s in p.steps]
+    assert kinds == [6, 4, 7]          # ALLTOALL, TREE, ALLGATHER
+    p = coll.plan(ALLREDUCE, coll.ALGO_TREE_COLL, 2, 8, -1, 8 * 1_000_000 + 1, 4)
+    assert 6 not in [s["type"] for s in p.steps]   # ragged: grouped p2p
 
 
 def test_plan_errors():
