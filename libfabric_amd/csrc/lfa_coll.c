@@ -360,7 +360,7 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		algo = LFA_ALGO_TREE;   /* the RCCL algo is not a schedule */
 	if (algo == LFA_ALGO_TREE_COLL) {
 		/* collective transport only for even blocks of the big path */
-		int even = n > 1 && count % (size_t)n == 0 &&
+		int even = count % (size_t)n == 0 &&
 			   !(coll == LFA_ALLREDUCE &&
 			     bytes * (size_t)n <= LFA_SMALL_AG_BYTES);
 
