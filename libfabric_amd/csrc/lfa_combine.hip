@@ -285,32 +285,57 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
   }
 }
 
-// LDS-DMA form (the product body for <= 16 inputs): each wave DMAs 1 KiB of
-// every input into its own LDS slots (global_load_lds_dwordx4, nt), waits on
-// its vmcnt, then evaluates the tree from LDS and stores nt.  Dynamic LDS:
-// nin · 4 waves · 1 KiB per workgroup.
-template <int OP, typename T, int NLEAF>
-__global__ __launch_bounds__(kLdsWaves * 64) void reduce_tree_lds(TreeArgs a,
-                                                                  int nin,
-                                                                  u32x4 *dst,
-                                                                  size_t nvec) {
-  extern __shared__ u32x4 tlds[];  // [nin][kLdsWaves][64]
+// LDS-DMA form: each wave DMAs U KiB of every input into its own LDS slots
+// (global_load_lds_dwordx4, nt), waits on its vmcnt, then evaluates U trees
+// per lane from LDS and stores nt.  Dynamic LDS: nin · W · U KiB per
+// workgroup.  Waves never share LDS, so no barrier.
+template <int OP, typename T, int NLEAF, int W, int U>
+__global__ __launch_bounds__(W * 64) void reduce_tree_lds(TreeArgs a, int nin,
+                                                          u32x4 *dst,
+                                                          size_t nvec) {
+  extern __shared__ u32x4 tlds[];  // [nin][W][U][64]
   const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
-  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64) + (size_t)w * 64;
-  if (base + 64 <= nvec) {
+  const size_t base = (size_t)blockIdx.x * (W * 64 * U) + (size_t)w * 64 * U;
+  auto slot = [&](int k, int u) { return ((k * W + w) * U + u) * 64; };
+  if (base + 64 * U <= nvec) {
     for (int k = 0; k < nin; k++)  // uniform loop over the inputs
-      __builtin_amdgcn_global_load_lds(
-          (const void *)((const u32x4 *)a.in[k] + base + l),
-          (lds_void *)&tlds[(k * kLdsWaves + w) * 64], 16, 0, 2);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)((const u32x4 *)a.in[k] + base + u * 64 + l),
+            (lds_void *)&tlds[slot(k, u)], 16, 0, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st<true>(dst + base + l,
-             tree_eval_with<OP, T, u32x4, NLEAF>(
-                 a, [&](int k) { return tlds[(k * kLdsWaves + w) * 64 + l]; }));
-  } else if (base + l < nvec) {
-    size_t i = base + l;
-    st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
-               return ld<true>((const u32x4 *)a.in[k] + i);
-             }));
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<true>(dst + base + u * 64 + l,
+               tree_eval_with<OP, T, u32x4, NLEAF>(
+                   a, [&](int k) { return tlds[slot(k, u) + l]; }));
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+                   return ld<true>((const u32x4 *)a.in[k] + i);
+                 }));
+    }
+  }
+}
+
+// Wave-contiguous register form: wave w of workgroup b owns U consecutive KiB
+// of every input (longer DRAM bursts per input stream than the chunked form).
+template <int OP, typename T, int NLEAF, int U>
+__global__ __launch_bounds__(kBlock) void reduce_tree_wave(TreeArgs a,
+                                                           u32x4 *dst,
+                                                           size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U + l;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * 64;
+    if (i < nvec)
+      st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+                 return ld<true>((const u32x4 *)a.in[k] + i);
+               }));
   }
 }
 
@@ -495,11 +520,38 @@ static int launch_write(void *dst, const void *src, size_t cnt,
 
 // Vector body of the tree (bench.py --tune-tree): LDS-DMA for
 // 2 inputs, chunked nt register loads for more (U=2 above 8 inputs).
+template <int OP, typename T, int NLEAF, int W, int U>
+static void launch_tree_lds(const TreeArgs &b, int nsrc, u32x4 *dst,
+                            size_t nvec, hipStream_t s) {
+  hipLaunchKernelGGL((reduce_tree_lds<OP, T, NLEAF, W, U>),
+                     dim3(grid_for(nvec, (size_t)W * 64 * U, 0x7fffffffu)),
+                     dim3(W * 64), (size_t)nsrc * W * U * 64 * sizeof(u32x4), s,
+                     b, nsrc, dst, nvec);
+}
+
 template <int OP, typename T, int NLEAF>
 static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                              size_t nvec, hipStream_t s, int variant = -1) {
-  const bool use_lds = variant < 0 ? nsrc <= 2 : variant == 3;
-  if (variant < 0 && nsrc > 8) variant = 2;
+  if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
+  if constexpr (OP == OP_SUM && __is_same(T, float)) {
+    // tuning-only forms (bench.py --tune-tree), float SUM only
+    switch (variant) {
+      case 4: return launch_tree_lds<OP, T, NLEAF, 4, 2>(b, nsrc, dst, nvec, s);
+      case 5: return launch_tree_lds<OP, T, NLEAF, 2, 2>(b, nsrc, dst, nvec, s);
+      case 6: return launch_tree_lds<OP, T, NLEAF, 1, 4>(b, nsrc, dst, nvec, s);
+      case 7:
+        hipLaunchKernelGGL((reduce_tree_wave<OP, T, NLEAF, 2>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 8:
+        hipLaunchKernelGGL((reduce_tree_wave<OP, T, NLEAF, 4>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      default: break;
+    }
+  }
   if (variant == 0) {
     hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
                        dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
@@ -508,12 +560,8 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
     hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2>),
                        dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
                        dim3(kBlock), 0, s, b, dst, nvec);
-  } else if (use_lds) {
-    hipLaunchKernelGGL((reduce_tree_lds<OP, T, NLEAF>),
-                       dim3(grid_for(nvec, (size_t)kLdsWaves * 64, 0x7fffffffu)),
-                       dim3(kLdsWaves * 64),
-                       (size_t)nsrc * kLdsWaves * 64 * sizeof(u32x4), s, b, nsrc,
-                       dst, nvec);
+  } else if (variant == 3) {
+    launch_tree_lds<OP, T, NLEAF, kLdsWaves, 1>(b, nsrc, dst, nvec, s);
   } else {
     hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
                        dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
