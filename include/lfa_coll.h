@@ -95,10 +95,13 @@ int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
 
 /* ---- groups (fi_join_collective) -------------------------------------- */
 
-/* coll_addr = LFA_ADDR_NOTAVAIL joins the world group.  `ranks` (sorted,
- * `nmembers` entries) selects the members; NULL = all ranks.  Every listed
- * rank must call it; non-members pass their own rank absent and get
- * -LFA_EINVAL.  Completion: an LFA_JOIN_COMPLETE event on lfa_eq_read. */
+/* Form a group from the parent `coll_addr` (LFA_ADDR_NOTAVAIL = the world
+ * group).  `ranks` (sorted parent ranks, `nmembers` entries) selects the
+ * members; NULL = all.  EVERY parent rank calls it with the same list — the
+ * group id is agreed by a UINT8 BAND allreduce of the free-id masks over the
+ * parent, as coll_join_collective does (coll_coll.c:969-973).  Non-members
+ * get a handle too, but collectives on it return -LFA_EINVAL.
+ * Completion: an LFA_JOIN_COMPLETE event on lfa_eq_read. */
 #define LFA_JOIN_COMPLETE 6
 int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			const int *ranks, size_t nmembers, uint64_t flags,

@@ -1336,8 +1336,8 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	if (!ep)
 		return -LFA_EINVAL;
 	mc = mc_of(ep, coll_addr);
-	if (!mc || !mc->comm)
-		return -LFA_EINVAL;
+	if (!mc || !mc->comm || mc->rank < 0)
+		return -LFA_EINVAL;   /* not a member of this group */
 	esz = lfa_datatype_size(dt);
 	if (!esz)
 		return -LFA_EINVAL;
@@ -1457,6 +1457,8 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	if (!ep)
 		return -LFA_EINVAL;
 	mc = mc_of(ep, coll_addr);
+	if (!mc->comm || mc->rank < 0)
+		return -LFA_EINVAL;
 	pthread_mutex_lock(&ep->lock);
 	hipSetDevice(ep->dom->device);
 	ep->barrier_host[0] = ~(uint64_t)mc->rank;
@@ -1531,11 +1533,16 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		mc->rank = pos;
 		mc->size = (int)nmembers;
 	}
+	/*
+	 * A non-member (every parent rank calls join, as every rank of the
+	 * reference's parent group takes part in the join allreduce) gets a
+	 * handle with no communicator: it completes the join like the members
+	 * but cannot issue collectives on it (-LFA_EINVAL).
+	 */
 	if (!member) {
-		pthread_mutex_unlock(&ep->lock);
-		free(mc);
-		*mcp = NULL;
-		return 0;
+		mc->comm = NULL;
+		mc->rank = -1;
+		mc->size = (int)nmembers;
 	}
 	/* agree on the group id: BAND of the free-id masks over the PARENT
 	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 */
@@ -1559,7 +1566,7 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		ret = enqueue_completion(ep, ep->stream, context, 1, mc);
 	pthread_mutex_unlock(&ep->lock);
 	if (ret) {
-		if (mc->owns_comm)
+		if (mc->owns_comm && mc->comm)
 			ncclCommDestroy(mc->comm);
 		if (mc->mask_host)
 			hipHostFree(mc->mask_host);
@@ -1577,7 +1584,7 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 	if (mc->is_world)
 		return -LFA_EINVAL;
 	lfa_coll_ep_flush(mc->ep);
-	if (mc->owns_comm)
+	if (mc->owns_comm && mc->comm)
 		ncclCommDestroy(mc->comm);
 	if (mc->group_id < LFA_MAX_GROUP_ID)
 		mc->ep->cid_mask[mc->group_id / 8] |= (uint8_t)(1u << (mc->group_id % 8));

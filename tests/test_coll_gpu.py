@@ -194,6 +194,20 @@ def test_join_world_and_completion_order(coll, ep):
     assert torch.equal(x, y)
 
 
+def test_join_subset_via_comm_split(coll, ep):
+    """fi_join_collective with an explicit member list: ncclCommSplit over
+    the parent, group id from the BAND of free-id masks."""
+    mc, ctx = ep.join([0])
+    ev, fid, context = ep.wait_join()
+    assert ev == coll.JOIN_COMPLETE and fid == mc and context == ctx
+    addr = ep.mc_addr(mc)
+    x = torch.arange(4096, dtype=torch.int32, device=DEV)
+    y = torch.zeros_like(x)
+    ep.wait(ep.allreduce(x, y, 4096, 4, 9, coll_addr=addr))   # BXOR, 1 member
+    assert torch.equal(x, y)
+    assert coll.lib().lfa_mc_close(mc) == 0
+
+
 def test_errors_and_query(coll, ep):
     x = torch.ones(16, device=DEV)
     with pytest.raises(coll.CollError) as e:
