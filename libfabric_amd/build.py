@@ -104,9 +104,28 @@ def build_coll(verbose: bool = False) -> str | None:
     return LIB_COLL
 
 
+EXAMPLE = os.path.join(ROOT, "examples", "c_drop_in")
+
+
+def build_example(verbose: bool = False) -> str | None:
+    """Plain-C caller of both libraries (no torch): examples/c_drop_in."""
+    src = EXAMPLE + ".c"
+    if not os.path.exists(src):
+        return None
+    if _newer(EXAMPLE, [src, LIB_LFA, LIB_COLL]):
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-D__HIP_PLATFORM_AMD__",
+              "-I" + INC, "-I" + os.path.join(ROCM, "include"), "-o", EXAMPLE, src,
+              "-L" + PKG, "-llfa", "-llfa_coll", "-L" + os.path.join(ROCM, "lib"),
+              "-lamdhip64", "-Wl,-rpath," + PKG, "-Wl,-rpath,$ORIGIN/../libfabric_amd"])
+        if verbose:
+            print(f"built {EXAMPLE}")
+    return EXAMPLE
+
+
 def build_all(verbose: bool = False) -> None:
     build_lfa(verbose=verbose)
     build_coll(verbose=verbose)
+    build_example(verbose=verbose)
 
 
 if __name__ == "__main__":
