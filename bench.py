@@ -354,10 +354,14 @@ def tune(args) -> None:
     from libfabric_amd import _native
     L = _native.lib()
     torch.cuda.set_device(0)
-    sets = make_buffers("cuda", 7)
+    count = args.tune_bytes // 4
+    nsets = max(BUFFER_SETS, (2 << 30) // (2 * args.tune_bytes))  # >= 2 GiB rotated
+    g = torch.Generator(device="cuda").manual_seed(7)
+    sets = [(torch.rand(count, device="cuda", generator=g),
+             torch.rand(count, device="cuda", generator=g)) for _ in range(nsets)]
     stream = torch.cuda.current_stream()
     h = stream.cuda_stream
-    nvec = COUNT // 4
+    nvec = count // 4
     variants = [int(v) for v in args.variants.split(',')] if args.variants else list(range(30))
 
     def run(v, d, s, n):
@@ -378,7 +382,7 @@ def tune(args) -> None:
     for _ in range(3):
         for v in variants:
             for i in range(4):
-                d, s = sets[i % BUFFER_SETS]
+                d, s = sets[i % len(sets)]
                 assert run(v, d, s, nvec) == 0
     torch.cuda.synchronize()
     for rnd in range(args.tune_rounds):
@@ -386,7 +390,7 @@ def tune(args) -> None:
             evs = [(torch.cuda.Event(enable_timing=True),
                     torch.cuda.Event(enable_timing=True)) for _ in range(20)]
             for i, (a, b) in enumerate(evs):
-                d, s = sets[i % BUFFER_SETS]
+                d, s = sets[i % len(sets)]
                 a.record(stream)
                 run(v, d, s, nvec)
                 b.record(stream)
@@ -395,10 +399,11 @@ def tune(args) -> None:
     rows = []
     for v in variants:
         ms = statistics.median(times[v])
-        rows.append({"variant": v, "median_us": round(ms * 1e3, 2),
+        nb = args.tune_bytes
+        rows.append({"variant": v, "bytes": nb, "median_us": round(ms * 1e3, 2),
                      "min_us": round(min(times[v]) * 1e3, 2),
-                     "tbps": round(3 * S_BYTES / (ms * 1e-3) / 1e12, 3),
-                     "frac": round(3 * S_BYTES / (ms * 1e-3) / 1e9 / PEAK_GBPS, 4)})
+                     "tbps": round(3 * nb / (ms * 1e-3) / 1e12, 3),
+                     "frac": round(3 * nb / (ms * 1e-3) / 1e9 / PEAK_GBPS, 4)})
     print(json.dumps({"tune": rows}))
 
 
@@ -489,6 +494,7 @@ def main() -> None:
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--tune-rounds", type=int, default=10)
     ap.add_argument("--variants", default="", help="comma list for --tune")
+    ap.add_argument("--tune-bytes", type=int, default=S_BYTES)
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--sweep-ops", action="store_true")
     ap.add_argument("--no-extras", action="store_true")

@@ -13,13 +13,16 @@
 //   combine_vec    the register-staged form of the same (tuning reference).
 //   combine_elem   the same op for misaligned heads/tails and for buffers that
 //                  are not co-aligned mod 16 (one element per lane, coalesced).
-//   reduce_tree    N inputs → 1 output in ONE pass, in prov/coll's
+//   reduce_tree_*  N inputs → 1 output in ONE pass, in prov/coll's
 //                  recursive-doubling association order (coll_coll.c:349-449):
 //                  replaces log2(N) pairwise REDUCE+COPY items, traffic
 //                  (N+1)·S instead of ~3·log2(N)·S.
+//   fetch_vec/elem the fetch (readwrite) and compare-swap tables
+//                  (util_atomic.c:924-980): res = old dst, then the update.
 //
 // Semantics: lfa_ops.hpp.  Build: hipcc --offload-arch=gfx950 -O3
-// -ffp-contract=off -DLFA_OP=<op> (see libfabric_amd/build.py).
+// -ffp-contract=off -DLFA_OP=<op>, once per enum fi_op row (0..18; see
+// libfabric_amd/build.py).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>

@@ -128,6 +128,42 @@ __global__ __launch_bounds__(W * 64) void sum_ldsdma(u32x4 *__restrict__ dst,
   }
 }
 
+// Persistent LDS-DMA form: a grid sized to the resident capacity walks the
+// chunks in a grid-stride loop (fewer workgroup launches, one tail).
+template <int U>
+__global__ __launch_bounds__(256) void sum_ldsdma_persist(u32x4 *__restrict__ dst,
+                                                          const u32x4 *__restrict__ src,
+                                                          size_t nvec) {
+  __shared__ u32x4 lds[2][4][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  for (size_t blk = blockIdx.x;; blk += gridDim.x) {
+    const size_t base = blk * (256 * U) + (size_t)w * 64 * U;
+    if (base >= nvec) break;
+    if (base + 64 * U <= nvec) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                         (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        st<true>(dst + base + u * 64 + l, addf(lds[0][w][u][l], lds[1][w][u][l]));
+      // the next iteration overwrites this wave's LDS slots: make sure the
+      // ds_reads above have returned (their values feed the stores already)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      for (int u = 0; u < U; u++) {
+        size_t i = base + u * 64 + l;
+        if (i < nvec) st<true>(dst + i, addf(ld<true>(dst + i), ld<true>(src + i)));
+      }
+    }
+  }
+}
+
 static inline unsigned blocks(size_t nvec, size_t per) {
   return (unsigned)((nvec + per - 1) / per);
 }
@@ -171,6 +207,21 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
     case 33: LDSDMA(4, 3, 2, 0); break;
     case 34: LDSDMA(8, 1, 2, 0); break;
     case 35: LDSDMA(4, 4, 2, 2); break;
+    case 36:
+      hipLaunchKernelGGL((sum_ldsdma_persist<4>),
+                         dim3(min(blocks(nvec, 256 * 4), 256u * 5)), dim3(256), 0, s,
+                         d, v, nvec);
+      break;
+    case 37:
+      hipLaunchKernelGGL((sum_ldsdma_persist<2>),
+                         dim3(min(blocks(nvec, 256 * 2), 256u * 8)), dim3(256), 0, s,
+                         d, v, nvec);
+      break;
+    case 38:
+      hipLaunchKernelGGL((sum_ldsdma_persist<4>),
+                         dim3(min(blocks(nvec, 256 * 4), 256u * 10)), dim3(256), 0, s,
+                         d, v, nvec);
+      break;
     case 23: RUN(256, 4, true, true, 1, true, true); break;
     default: return -LFA_EINVAL;
   }
