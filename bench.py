@@ -290,6 +290,27 @@ def cpu_model_allreduce(world: int):
             "note": "log2(N) CAS combines of 256 MiB on 1 host core; transport excluded"}
 
 
+def extra_e2e_staged(reps=3):
+    """The same combine with dst/src in pinned HOST memory through the staged
+    entry point (lfa_atomic_write_staged: 32 MiB chunks, H2D of chunk c+1
+    overlapping combine + D2H of chunk c)."""
+    from libfabric_amd import _native
+    L = _native.lib()
+    hd = torch.rand(COUNT).pin_memory()
+    hs = torch.rand(COUNT).pin_memory()
+    assert L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, hd.data_ptr(), hs.data_ptr(),
+                                     COUNT, 0) == 0
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, hd.data_ptr(), hs.data_ptr(), COUNT, 0)
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    return {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
+            "traffic_gib_s": round(3 * S_BYTES / t / 2**30, 2),
+            "note": "pinned host dst/src, 32 MiB chunks, pipelined H2D / combine / D2H"}
+
+
 def extra_collectives(rank, world, stream):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
@@ -630,6 +651,7 @@ def main() -> None:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
+                ex["e2e_host_staged_float_sum_256mib"] = extra_e2e_staged()
             if world > 1 or not args.no_extras_coll:
                 ex.update(extra_collectives(rank, world, stream))
         except Exception as e:  # noqa: BLE001 — extras must not hide the metric

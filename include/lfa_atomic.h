@@ -106,6 +106,18 @@ int lfa_atomic_swap_async(enum lfa_op op, enum lfa_datatype datatype,
 			  void *dst, const void *src, const void *cmp,
 			  void *res, size_t cnt, void *stream);
 
+/*
+ * Host-resident buffers (what prov/coll's REDUCE items see, coll_coll.c:763):
+ * dst/src are streamed through HBM in `chunk_bytes` pieces (0 = 32 MiB) on
+ * two HIP streams — chunk c+1's H2D overlaps chunk c's combine and D2H — and
+ * the call returns when dst is updated.  Pinned (hipHostMalloc /
+ * hipHostRegister) buffers get full overlap; pageable ones are staged by the
+ * HIP runtime.  Returns 0 or a negative LFA_E* code.
+ */
+int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype datatype,
+			    void *dst, const void *src, size_t cnt,
+			    size_t chunk_bytes);
+
 /* Version string of the kernel library (build id, target arch). */
 const char *lfa_version(void);
 

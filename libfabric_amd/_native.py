@@ -43,6 +43,9 @@ def _bind_lfa(L):
     L.lfa_atomic_swap_async.restype = c_int
     L.lfa_atomic_swap_async.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_size_t, c_void_p]
+    L.lfa_atomic_write_staged.restype = c_int
+    L.lfa_atomic_write_staged.argtypes = [c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                          c_size_t]
     L.lfa_version.restype = ctypes.c_char_p
     L.lfa__tune_tree_f32.restype = c_int
     L.lfa__tune_tree_f32.argtypes = [c_int, c_void_p, ctypes.POINTER(c_void_p),

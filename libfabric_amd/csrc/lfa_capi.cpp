@@ -253,6 +253,63 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
   return kTree[op](dt, dst, srcs, nsrc, cnt, stream);
 }
 
+int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
+                            const void *src, size_t cnt, size_t chunk_bytes) {
+  if ((unsigned)op >= LFA_WRITE_OP_CNT || (unsigned)dt >= LFA_DATATYPE_CNT ||
+      !in_table(op, dt))
+    return -LFA_EOPNOTSUPP;
+  if (cnt && (!dst || !src)) return -LFA_EINVAL;
+  if (!cnt) return 0;
+  const size_t esz = lfa_datatype_size(dt);
+  if (!chunk_bytes) chunk_bytes = 32u << 20;
+  size_t per = chunk_bytes / esz;
+  if (!per) per = 1;
+  if (per > cnt) per = cnt;
+  // chunk slots keep 16-byte alignment so the vector body applies
+  const size_t slot = (per * esz + 255) & ~(size_t)255;
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  hipEvent_t in_done[2] = {}, out_done[2] = {};
+  char *dev = nullptr;
+  int ret = 0;
+  if (hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&dev, 4 * slot) != hipSuccess) {
+    ret = -LFA_ENOMEM;
+    goto out;
+  }
+  for (int i = 0; i < 2; i++) {
+    hipEventCreateWithFlags(&in_done[i], hipEventDisableTiming);
+    hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming);
+    hipEventRecord(out_done[i], s_out);
+  }
+  for (size_t off = 0, c = 0; off < cnt && !ret; off += per, c++) {
+    const size_t n = cnt - off < per ? cnt - off : per;
+    const int k = (int)(c & 1);
+    char *dd = dev + (size_t)k * 2 * slot, *ds = dd + slot;
+    // slot reuse: chunk c-2's D2H must have drained it
+    hipStreamWaitEvent(s_in, out_done[k], 0);
+    hipMemcpyAsync(dd, (char *)dst + off * esz, n * esz, hipMemcpyHostToDevice, s_in);
+    hipMemcpyAsync(ds, (const char *)src + off * esz, n * esz,
+                   hipMemcpyHostToDevice, s_in);
+    hipEventRecord(in_done[k], s_in);
+    hipStreamWaitEvent(s_out, in_done[k], 0);
+    ret = kWrite[op](dt, dd, ds, n, s_out);
+    hipMemcpyAsync((char *)dst + off * esz, dd, n * esz, hipMemcpyDeviceToHost, s_out);
+    hipEventRecord(out_done[k], s_out);
+  }
+  if (hipStreamSynchronize(s_out) != hipSuccess && !ret) ret = -LFA_EIO;
+  hipStreamSynchronize(s_in);
+out:
+  for (int i = 0; i < 2; i++) {
+    if (in_done[i]) hipEventDestroy(in_done[i]);
+    if (out_done[i]) hipEventDestroy(out_done[i]);
+  }
+  if (dev) hipFree(dev);
+  if (s_in) hipStreamDestroy(s_in);
+  if (s_out) hipStreamDestroy(s_out);
+  return ret;
+}
+
 const char *lfa_version(void) {
   return "lfa-combine 0.2 gfx950 (LDS-DMA staged, 4 KiB/operand/wave, nt loads/stores)";
 }
