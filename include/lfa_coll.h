@@ -140,6 +140,12 @@ ssize_t lfa_reduce(struct lfa_coll_ep *ep, const void *buf, size_t count,
 		   lfa_addr_t coll_addr, lfa_addr_t root_addr,
 		   enum lfa_datatype datatype, enum lfa_op op, uint64_t flags,
 		   void *context);
+/* coll_ep_scatter (prov/coll/src/coll_coll.c:1121-1156): root's buf holds
+ * nranks blocks of `count` elements; block r lands in rank r's result. */
+ssize_t lfa_scatter(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		    void *desc, void *result, void *result_desc,
+		    lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		    enum lfa_datatype datatype, uint64_t flags, void *context);
 
 int lfa_query_collective(struct lfa_coll_domain *domain,
 			 enum lfa_collective_op coll,
@@ -216,7 +222,7 @@ struct lfa_step {
  * *nsteps steps / *nrefs refs and returns the counts in them, and the HBM
  * workspace the schedule needs in *tmp_bytes.  Host-only, no GPU needed.
  * Returns 0, -LFA_EINVAL, -LFA_ENOSYS (collective/algo not planned) or
- * -LFA_ETOOSMALL (arrays too short; *nsteps/*nrefs = sizes needed).
+ * -LFA_ETOOSMALL (arrays too short; *nsteps and *nrefs = sizes needed).
  */
 #define LFA_ETOOSMALL 257
 int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,

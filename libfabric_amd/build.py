@@ -122,10 +122,51 @@ def build_example(verbose: bool = False) -> str | None:
     return EXAMPLE
 
 
+# libfabric's public headers: only this container has them.  The provider
+# shell and its host driver compile against them here; the built files travel
+# to the GPU box with the snapshot (as oracle/_ref does).
+FABRIC_INC = os.environ.get("LFA_FABRIC_INCLUDE", "/root/reference/include")
+LIB_OFF = os.path.join(PKG, "liboff_lfa-fi.so")
+OFF_HOST = os.path.join(ROOT, "examples", "off_lfa_host")
+
+
+def have_fabric_headers() -> bool:
+    return os.path.exists(os.path.join(FABRIC_INC, "rdma", "providers", "fi_peer.h"))
+
+
+def build_off_lfa(verbose: bool = False) -> str | None:
+    """libfabric offload-collective provider (liboff_lfa-fi.so) over
+    liblfa_coll.so, plus the rxm-shaped host driver examples/off_lfa_host."""
+    src = os.path.join(CSRC, "off_lfa.c")
+    host = OFF_HOST + ".c"
+    if not have_fabric_headers():
+        if verbose:
+            print("libfabric headers absent: off_lfa not rebuilt "
+                  f"({'prebuilt present' if os.path.exists(LIB_OFF) else 'missing'})")
+        return LIB_OFF if os.path.exists(LIB_OFF) else None
+    hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "off_lfa.h"), LIB_COLL]
+    if _newer(LIB_OFF, [src] + hdrs):
+        _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
+              "-Wno-unused-parameter", "-I" + INC, "-I" + FABRIC_INC, "-shared",
+              "-o", LIB_OFF, src, "-L" + PKG, "-llfa_coll", "-lpthread",
+              "-Wl,-rpath,$ORIGIN", "-Wl,-soname,liboff_lfa-fi.so"])
+        if verbose:
+            print(f"built {LIB_OFF}")
+    if _newer(OFF_HOST, [host, os.path.join(INC, "off_lfa.h")]):
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              "-D__HIP_PLATFORM_AMD__", "-I" + INC, "-I" + FABRIC_INC,
+              "-I" + os.path.join(ROCM, "include"), "-o", OFF_HOST, host,
+              "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-ldl"])
+        if verbose:
+            print(f"built {OFF_HOST}")
+    return LIB_OFF
+
+
 def build_all(verbose: bool = False) -> None:
     build_lfa(verbose=verbose)
     build_coll(verbose=verbose)
     build_example(verbose=verbose)
+    build_off_lfa(verbose=verbose)
 
 
 if __name__ == "__main__":

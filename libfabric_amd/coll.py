@@ -129,6 +129,9 @@ def lib() -> ctypes.CDLL:
                              c_void_p]
     L.lfa_allgather.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                 c_void_p, c_uint64, c_int, c_uint64, c_void_p]
+    L.lfa_scatter.restype = c_ssize_t
+    L.lfa_scatter.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                              c_void_p, c_uint64, c_uint64, c_int, c_uint64, c_void_p]
     L.lfa_broadcast.restype = c_ssize_t
     L.lfa_broadcast.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_uint64,
                                 c_uint64, c_int, c_uint64, c_void_p]
@@ -305,6 +308,14 @@ class Endpoint:
         _chk(lib().lfa_allgather(self.ep, _ptr(buf), count, None, _ptr(result),
                                  None, coll_addr or self.world, dt, 0, ctx),
              "lfa_allgather")
+        return ctx
+
+    def scatter(self, buf, result, count: int, root: int, dt: int,
+                coll_addr: int | None = None, context: int | None = None) -> int:
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_scatter(self.ep, _ptr(buf), count, None, _ptr(result), None,
+                               coll_addr or self.world, root, dt, 0, ctx),
+             "lfa_scatter")
         return ctx
 
     def broadcast(self, buf, count: int, root: int, dt: int,

@@ -1436,6 +1436,20 @@ ssize_t lfa_allgather(struct lfa_coll_ep *ep, const void *buf, size_t count,
 		      datatype, LFA_NOOP, context);
 }
 
+/* coll_ep_scatter (coll_coll.c:1121-1156): root's buf holds nranks blocks
+ * of `count` elements, block r lands in rank r's result. */
+ssize_t lfa_scatter(struct lfa_coll_ep *ep, const void *buf, size_t count,
+		    void *desc, void *result, void *result_desc,
+		    lfa_addr_t coll_addr, lfa_addr_t root_addr,
+		    enum lfa_datatype datatype, uint64_t flags, void *context)
+{
+	(void)desc; (void)result_desc; (void)flags;
+	if (count && !result)
+		return -LFA_EINVAL;
+	return submit(ep, LFA_SCATTER, buf, count, result, coll_addr, root_addr,
+		      datatype, LFA_NOOP, context);
+}
+
 ssize_t lfa_broadcast(struct lfa_coll_ep *ep, void *buf, size_t count,
 		      void *desc, lfa_addr_t coll_addr, lfa_addr_t root_addr,
 		      enum lfa_datatype datatype, uint64_t flags, void *context)

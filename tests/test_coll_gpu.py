@@ -153,6 +153,9 @@ def test_rccl_other_collectives(coll, ep):
     out.zero_()
     ep.wait(ep.allgather(x, out, count, 6))
     assert torch.equal(out, x)
+    out.zero_()
+    ep.wait(ep.scatter(x, out, count, 0, 6))
+    assert torch.equal(out, x)
     b = x.clone()
     ep.wait(ep.broadcast(b, count, 0, 6))
     assert torch.equal(b, x)
