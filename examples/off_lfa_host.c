@@ -502,6 +502,7 @@ int main(int argc, char **argv)
 			h_x[i] = (float)(i % 1000) * 0.25f - 7.0f;
 		hipMemcpy(d_x, h_x, n * 4, hipMemcpyHostToDevice);
 		hipMemset(d_y, 0, n * 4);
+		hipDeviceSynchronize();   /* the caller orders its own writes */
 
 		/* device buffers: allreduce -> owner CQ carries our context */
 		CHECK_RC(fi_allreduce(ep, d_x, n, NULL, d_y, NULL, world, FI_FLOAT, FI_SUM,
@@ -560,6 +561,7 @@ int main(int argc, char **argv)
 		/* the av_set's own address names the world group */
 		CHECK_RC(fi_av_set_addr(set, &setaddr), 0);
 		hipMemset(d_y, 0, n * 4);
+		hipDeviceSynchronize();   /* the caller orders its own writes */
 		CHECK_RC(fi_allreduce(ep, d_x, n, NULL, d_y, NULL, setaddr, FI_FLOAT,
 				      FI_SUM, 0, &req[11]), 0);
 		CHECK_RC(wait_comp(ep, &req[11], NULL), 0);
@@ -570,6 +572,7 @@ int main(int argc, char **argv)
 		CHECK_RC(fi_join_collective(ep, world, set, 0, &sub, &req[12]), 0);
 		CHECK_RC(wait_join(ep, sub, &req[12]), 0);
 		hipMemset(d_y, 0, n * 4);
+		hipDeviceSynchronize();   /* the caller orders its own writes */
 		CHECK_RC(fi_allreduce(ep, d_x, n, NULL, d_y, NULL, fi_mc_addr(sub),
 				      FI_FLOAT, FI_SUM, 0, &req[13]), 0);
 		CHECK_RC(wait_comp(ep, &req[13], NULL), 0);

@@ -42,7 +42,7 @@ def _run(*args, timeout=300):
     r = subprocess.run([exe, lib, *args], capture_output=True, text=True,
                        timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
-    return r.stdout
+    return r.stdout.strip().splitlines()[-1]    # RCCL prints a banner first
 
 
 def test_provider_exports():
