@@ -7,6 +7,7 @@
 // combine runs on the GPU.
 #include <hip/hip_runtime_api.h>
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 
 #include "../../include/lfa_atomic.h"
@@ -253,6 +254,46 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
   return kTree[op](dt, dst, srcs, nsrc, cnt, stream);
 }
 
+}  // extern "C"
+
+namespace {
+// Per-device staging context for lfa_atomic_write_staged: two streams, the
+// slot events and an HBM staging buffer that only grows.  Created on first
+// use and kept for the life of the process (a hipMalloc + hipFree per call
+// costs milliseconds and serialises the device).
+struct StagingCtx {
+  pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  hipEvent_t in_done[2] = {}, out_done[2] = {};
+  char *dev = nullptr;
+  size_t cap = 0;
+};
+constexpr int kMaxDevices = 64;
+StagingCtx g_staging[kMaxDevices];
+
+int staging_acquire(StagingCtx &c, size_t bytes) {
+  if (!c.s_in) {
+    if (hipStreamCreateWithFlags(&c.s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c.s_out, hipStreamNonBlocking) != hipSuccess)
+      return -LFA_ENOMEM;
+    for (int i = 0; i < 2; i++)
+      if (hipEventCreateWithFlags(&c.in_done[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c.out_done[i], hipEventDisableTiming) != hipSuccess)
+        return -LFA_ENOMEM;
+  }
+  if (c.cap < bytes) {
+    if (c.dev) hipFree(c.dev);
+    c.dev = nullptr;
+    c.cap = 0;
+    if (hipMalloc((void **)&c.dev, bytes) != hipSuccess) return -LFA_ENOMEM;
+    c.cap = bytes;
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
                             const void *src, size_t cnt, size_t chunk_bytes) {
   if ((unsigned)op >= LFA_WRITE_OP_CNT || (unsigned)dt >= LFA_DATATYPE_CNT ||
@@ -265,48 +306,36 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   size_t per = chunk_bytes / esz;
   if (!per) per = 1;
   if (per > cnt) per = cnt;
-  // chunk slots keep 16-byte alignment so the vector body applies
+  // chunk slots keep 256-byte alignment so the vector body applies
   const size_t slot = (per * esz + 255) & ~(size_t)255;
-  hipStream_t s_in = nullptr, s_out = nullptr;
-  hipEvent_t in_done[2] = {}, out_done[2] = {};
-  char *dev = nullptr;
-  int ret = 0;
-  if (hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void **)&dev, 4 * slot) != hipSuccess) {
-    ret = -LFA_ENOMEM;
-    goto out;
+  int devno = 0;
+  if (hipGetDevice(&devno) != hipSuccess || devno < 0 || devno >= kMaxDevices)
+    return -LFA_EINVAL;
+  StagingCtx &c = g_staging[devno];
+  pthread_mutex_lock(&c.lock);
+  int ret = staging_acquire(c, 4 * slot);
+  if (!ret) {
+    for (int i = 0; i < 2; i++) hipEventRecord(c.out_done[i], c.s_out);
+    for (size_t off = 0, k = 0; off < cnt && !ret; off += per, k ^= 1) {
+      const size_t n = cnt - off < per ? cnt - off : per;
+      char *dd = c.dev + k * 2 * slot, *ds = dd + slot;
+      // slot reuse: the D2H of the chunk two back must have drained it
+      hipStreamWaitEvent(c.s_in, c.out_done[k], 0);
+      hipMemcpyAsync(dd, (char *)dst + off * esz, n * esz, hipMemcpyHostToDevice,
+                     c.s_in);
+      hipMemcpyAsync(ds, (const char *)src + off * esz, n * esz,
+                     hipMemcpyHostToDevice, c.s_in);
+      hipEventRecord(c.in_done[k], c.s_in);
+      hipStreamWaitEvent(c.s_out, c.in_done[k], 0);
+      ret = kWrite[op](dt, dd, ds, n, c.s_out);
+      hipMemcpyAsync((char *)dst + off * esz, dd, n * esz, hipMemcpyDeviceToHost,
+                     c.s_out);
+      hipEventRecord(c.out_done[k], c.s_out);
+    }
+    if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
+    if (hipStreamSynchronize(c.s_in) != hipSuccess && !ret) ret = -LFA_EIO;
   }
-  for (int i = 0; i < 2; i++) {
-    hipEventCreateWithFlags(&in_done[i], hipEventDisableTiming);
-    hipEventCreateWithFlags(&out_done[i], hipEventDisableTiming);
-    hipEventRecord(out_done[i], s_out);
-  }
-  for (size_t off = 0, c = 0; off < cnt && !ret; off += per, c++) {
-    const size_t n = cnt - off < per ? cnt - off : per;
-    const int k = (int)(c & 1);
-    char *dd = dev + (size_t)k * 2 * slot, *ds = dd + slot;
-    // slot reuse: chunk c-2's D2H must have drained it
-    hipStreamWaitEvent(s_in, out_done[k], 0);
-    hipMemcpyAsync(dd, (char *)dst + off * esz, n * esz, hipMemcpyHostToDevice, s_in);
-    hipMemcpyAsync(ds, (const char *)src + off * esz, n * esz,
-                   hipMemcpyHostToDevice, s_in);
-    hipEventRecord(in_done[k], s_in);
-    hipStreamWaitEvent(s_out, in_done[k], 0);
-    ret = kWrite[op](dt, dd, ds, n, s_out);
-    hipMemcpyAsync((char *)dst + off * esz, dd, n * esz, hipMemcpyDeviceToHost, s_out);
-    hipEventRecord(out_done[k], s_out);
-  }
-  if (hipStreamSynchronize(s_out) != hipSuccess && !ret) ret = -LFA_EIO;
-  hipStreamSynchronize(s_in);
-out:
-  for (int i = 0; i < 2; i++) {
-    if (in_done[i]) hipEventDestroy(in_done[i]);
-    if (out_done[i]) hipEventDestroy(out_done[i]);
-  }
-  if (dev) hipFree(dev);
-  if (s_in) hipStreamDestroy(s_in);
-  if (s_out) hipStreamDestroy(s_out);
+  pthread_mutex_unlock(&c.lock);
   return ret;
 }
 
