@@ -353,3 +353,43 @@ def test_staged_host_buffers(lfa):
         assert L.lfa_atomic_write_staged(op, dt, dp.data_ptr(), bp.data_ptr(), n, 0) == 0
         assert dp.numpy().tobytes() == want.tobytes()
     assert L.lfa_atomic_write_staged(6, 8, None, None, 4, 0) == -95
+
+
+def _window_check(dt, got_dev, d0_dev, s_dev, op, lo, hi):
+    """Oracle check of elements [lo, hi) of a huge combine."""
+    nd = oracle.DT_NP[dt]
+    d0 = d0_dev[lo:hi].cpu().numpy().view(nd)
+    s = s_dev[lo:hi].cpu().numpy().view(nd)
+    want = d0.copy()
+    oracle.write(op, dt, want, s)
+    assert_parity(dt, got_dev[lo:hi].cpu().numpy().view(nd), want, f"[{lo},{hi})")
+
+
+def test_beyond_32bit_element_counts(lfa):
+    """Counts past 2^32 elements (the reference's REDUCE item count is an int,
+    ofi_coll.h:116; this build takes size_t): int8 BXOR over 4 GiB + 4099
+    bytes through the vector body and, with src offset by one byte, through
+    the element path; oracle windows at both ends and across the 2^32
+    boundary, plus the involution x ^ y ^ y == x over the whole buffer."""
+    free, _ = torch.cuda.mem_get_info()
+    n = (1 << 32) + 4099
+    if free < 4 * n + (1 << 30):
+        pytest.skip("needs ~17 GiB of free HBM")
+    g = torch.Generator(device=DEV).manual_seed(42)
+    d0 = torch.randint(0, 256, (n,), dtype=torch.uint8, device=DEV, generator=g)
+    s_full = torch.randint(0, 256, (n + 16,), dtype=torch.uint8, device=DEV, generator=g)
+    windows = [(0, 8192), (n // 2 - 4096, n // 2 + 4096),
+               ((1 << 32) - 5000, (1 << 32) + 3000), (n - 9000, n)]
+    for shift in (0, 1):              # co-aligned vector body / element path
+        s = s_full[shift:shift + n]
+        d = d0.clone()
+        lfa.write(9, 0, d, s, n)      # FI_BXOR, FI_INT8
+        torch.cuda.synchronize()
+        for lo, hi in windows:
+            _window_check(0, d, d0, s, 9, lo, hi)
+        lfa.write(9, 0, d, s, n)
+        torch.cuda.synchronize()
+        assert torch.equal(d, d0), f"x^y^y != x (shift {shift})"
+        del d
+    del d0, s_full
+    torch.cuda.empty_cache()
