@@ -626,7 +626,7 @@ struct lfa_coll_domain {
 struct pending {
 	hipEvent_t ev;
 	void *context;
-	int kind;               /* 0 collective, 1 join */
+	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
 	struct lfa_coll_mc *mc;
 };
 
@@ -709,6 +709,22 @@ int lfa_coll_domain_close(struct lfa_coll_domain *d)
 	return 0;
 }
 
+/* Frees whatever lfa_coll_ep_open managed to create (open's error path). */
+static void ep_release(struct lfa_coll_ep *ep)
+{
+	if (ep->barrier_dev)
+		hipFree(ep->barrier_dev);
+	if (ep->barrier_host)
+		hipHostFree(ep->barrier_host);
+	if (ep->copy_stream)
+		hipStreamDestroy(ep->copy_stream);
+	if (ep->stream)
+		hipStreamDestroy(ep->stream);
+	free(ep->q);
+	pthread_mutex_destroy(&ep->lock);
+	free(ep);
+}
+
 int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 {
 	struct lfa_coll_ep *ep;
@@ -727,7 +743,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
 	    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
 	    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess) {
-		free(ep);
+		ep_release(ep);
 		return -LFA_EIO;
 	}
 	ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
@@ -741,7 +757,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	ep->qcap = 256;
 	ep->q = calloc(ep->qcap, sizeof(*ep->q));
 	if (!ep->q) {
-		free(ep);
+		ep_release(ep);
 		return -LFA_ENOMEM;
 	}
 	*out = ep;
@@ -951,6 +967,8 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			ep->have_err = 1;
 		} else if (p->kind == 1) {
 			join_finish(ep, p->mc);
+		} else if (p->kind == 2) {
+			/* join of a handle closed before it completed */
 		} else {
 			struct lfa_cq_entry *c = &out[(*nout)++];
 
@@ -1598,6 +1616,19 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 	if (mc->is_world)
 		return -LFA_EINVAL;
 	lfa_coll_ep_flush(mc->ep);
+	/* a join still queued for this handle completes without it */
+	pthread_mutex_lock(&mc->ep->lock);
+	for (size_t i = 0; i < mc->ep->qlen; i++) {
+		struct pending *p = &mc->ep->q[(mc->ep->qhead + i) % mc->ep->qcap];
+
+		if (p->kind == 1 && p->mc == mc) {
+			p->kind = 2;
+			p->mc = NULL;
+		}
+	}
+	pthread_mutex_unlock(&mc->ep->lock);
+	if (mc->mask_host)
+		hipHostFree(mc->mask_host);
 	if (mc->owns_comm && mc->comm)
 		ncclCommDestroy(mc->comm);
 	if (mc->group_id < LFA_MAX_GROUP_ID)

@@ -211,6 +211,19 @@ def test_join_subset_via_comm_split(coll, ep):
     assert coll.lib().lfa_mc_close(mc) == 0
 
 
+def test_close_mc_with_join_in_flight(coll, ep):
+    """Closing a multicast handle before its join completed: the queued join
+    is dropped (no EQ event for the freed handle), later work is unaffected."""
+    mc, _ = ep.join([0])
+    assert coll.lib().lfa_mc_close(mc) == 0
+    assert ep.cq_read() == []
+    assert ep.eq_read() is None
+    x = torch.ones(256, device=DEV)
+    y = torch.zeros_like(x)
+    ep.wait(ep.allreduce(x, y, 256, 8, 2))
+    assert torch.equal(x, y)
+
+
 def test_errors_and_query(coll, ep):
     x = torch.ones(16, device=DEV)
     with pytest.raises(coll.CollError) as e:
