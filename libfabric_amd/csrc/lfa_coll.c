@@ -1251,7 +1251,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			    enum lfa_datatype dt, enum lfa_op op)
 {
 	size_t esz = lfa_datatype_size(dt);
-	size_t per = ep->chunk / esz, off = 0;
+	size_t per = ep->chunk / esz, off = 0, in_slot;
 	hipEvent_t h2d[2], done[2];
 	int ret = 0, slot = 0;
 
@@ -1259,7 +1259,9 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		per = 1;
 	if (per > count)
 		per = count;
-	if (grow_staging(ep, 2 * per * esz))
+	/* the output half starts 256-byte aligned (vector body of the kernels) */
+	in_slot = (per * esz + 255) & ~(size_t)255;
+	if (grow_staging(ep, in_slot + per * esz))
 		return -LFA_ENOMEM;
 	for (int i = 0; i < 2; i++) {
 		hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming);
@@ -1268,13 +1270,13 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	}
 	while (off < count && !ret) {
 		size_t n = count - off < per ? count - off : per;
-		char *din = ep->hs[slot], *dout = din + per * esz;
+		char *din = ep->hs[slot], *dout = din + in_slot;
 
 		/* slot reuse: wait until chunk c-2's D2H finished */
 		hipStreamWaitEvent(ep->copy_stream, done[slot], 0);
 		if (coll != LFA_BROADCAST || mc->rank == root)
 			hipMemcpyAsync(din, (const char *)buf + off * esz, n * esz,
-				       hipMemcpyHostToDevice, ep->copy_stream);
+				       hipMemcpyDefault, ep->copy_stream);
 		hipEventRecord(h2d[slot], ep->copy_stream);
 		hipStreamWaitEvent(ep->stream, h2d[slot], 0);
 		if (coll == LFA_BROADCAST)
@@ -1287,7 +1289,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		hipStreamWaitEvent(ep->copy_stream, h2d[slot], 0);
 		hipMemcpyAsync((char *)result + off * esz,
 			       coll == LFA_BROADCAST ? din : dout, n * esz,
-			       hipMemcpyDeviceToHost, ep->copy_stream);
+			       hipMemcpyDefault, ep->copy_stream);
 		hipEventRecord(done[slot], ep->copy_stream);
 		off += n;
 		slot ^= 1;
@@ -1301,7 +1303,9 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	return ret;
 }
 
-/* Host buffers for non-elementwise collectives: whole-buffer staging. */
+/* Host buffers for non-elementwise collectives: whole-buffer staging.
+ * (Staging copies use hipMemcpyDefault: one side may be device memory when
+ * the caller mixes a device buf with a host result.) */
 static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			  enum lfa_collective_op coll, const void *buf,
 			  size_t in_bytes, void *result, size_t out_bytes,
@@ -1316,10 +1320,10 @@ static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	din = ep->hs[0];
 	dout = din + ((in_bytes + 15) & ~(size_t)15);
 	if (buf && in_bytes)
-		hipMemcpyAsync(din, buf, in_bytes, hipMemcpyHostToDevice, ep->stream);
+		hipMemcpyAsync(din, buf, in_bytes, hipMemcpyDefault, ep->stream);
 	ret = run_device(ep, mc, coll, din, dout, count, root, dt, op, ep->stream);
 	if (!ret && result && out_bytes)
-		hipMemcpyAsync(result, dout, out_bytes, hipMemcpyDeviceToHost,
+		hipMemcpyAsync(result, dout, out_bytes, hipMemcpyDefault,
 			       ep->stream);
 	return ret;
 }

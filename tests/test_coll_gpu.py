@@ -138,6 +138,16 @@ def test_rccl_allreduce_device_and_host(coll, ep):
     ctx = ep.allreduce(hx, hy, count, 8, 2)
     ep.wait(ctx)
     assert np.array_equal(hx, hy)
+    # mixed: device buf, host result (and the reverse), both staging forms
+    hy[:] = 0
+    ep.wait(ep.allreduce(x, hy, count, 8, 2))
+    assert np.array_equal(x.cpu().numpy(), hy)
+    y.zero_()
+    ep.wait(ep.allreduce(hx, y, count, 8, 2))
+    assert np.array_equal(hx, y.cpu().numpy())
+    hy[:] = 0
+    ep.wait(ep.reduce_scatter(x, hy, count, 8, 2))
+    assert np.array_equal(x.cpu().numpy(), hy)
     ep.set_chunk(0)
 
 
