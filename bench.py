@@ -483,6 +483,58 @@ def tune_tree(args) -> None:
     print(json.dumps({"tune_tree": rows}))
 
 
+def tune_tree_layout(args) -> None:
+    """Where the N input blocks sit in HBM, for the product tree kernel
+    (float SUM, 8 x 32 MiB): separate allocations; one contiguous workspace
+    (the collective's layout: block k at ws + k*B); and the contiguous
+    workspace with block k skewed by k*skew bytes."""
+    import ctypes
+    from libfabric_amd import _native
+    L = _native.lib()
+    torch.cuda.set_device(0)
+    h = torch.cuda.current_stream().cuda_stream
+    nsrc, blk = 8, 32 * 1024 * 1024 // 4
+    layouts = {"separate": None}
+    for sk in (args.skews.split(",") if args.skews else
+               ["0", "256", "4096", "4352", "65536", "1048576"]):
+        layouts[f"skew_{int(sk)}"] = int(sk)
+    sets = {}
+    for name, skew in layouts.items():
+        per = []
+        for _ in range(2):
+            if skew is None:
+                srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
+                ptrs = [t.data_ptr() for t in srcs]
+                keep = srcs
+            else:
+                stride = blk * 4 + skew
+                ws = torch.rand((stride * nsrc) // 4 + 1024, device="cuda")
+                ptrs = [ws.data_ptr() + k * stride for k in range(nsrc)]
+                keep = ws
+            per.append((keep, torch.empty(blk, device="cuda"),
+                        (ctypes.c_void_p * nsrc)(*ptrs)))
+        sets[name] = per
+    times = {n: [] for n in layouts}
+    for _ in range(args.tune_rounds):
+        for name in layouts:
+            evs = [(torch.cuda.Event(enable_timing=True),
+                    torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+            for i, (a, b) in enumerate(evs):
+                _, out, arr = sets[name][i % 2]
+                a.record()
+                L.lfa__tune_tree_f32(-1, out.data_ptr(), arr, nsrc, blk, h)
+                b.record()
+            torch.cuda.synchronize()
+            times[name].extend(a.elapsed_time(b) for a, b in evs[2:])
+    rows = []
+    for name in layouts:
+        ms = statistics.median(times[name])
+        gbps = (nsrc + 1) * blk * 4 / (ms * 1e-3) / 1e9
+        rows.append({"layout": name, "median_us": round(ms * 1e3, 2),
+                     "gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)})
+    print(json.dumps({"tune_tree_layout": rows}))
+
+
 def sweep_ops(args) -> None:
     """Every (op, datatype) of the write table at 256 MiB: kernel time and
     fraction of the HBM roofline (3·S bytes per launch)."""
@@ -525,6 +577,8 @@ def main() -> None:
     ap.add_argument("--variants", default="", help="comma list for --tune")
     ap.add_argument("--tune-bytes", type=int, default=S_BYTES)
     ap.add_argument("--tune-tree", action="store_true")
+    ap.add_argument("--tune-tree-layout", action="store_true")
+    ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
@@ -534,6 +588,9 @@ def main() -> None:
 
     if args.tune:
         tune(args)
+        return
+    if args.tune_tree_layout:
+        tune_tree_layout(args)
         return
     if args.tune_tree:
         tune_tree(args)

@@ -85,6 +85,22 @@ def test_loopback_reduce_scatter_and_reduce(coll, algo, n, count):
     assert_parity(dt, rd[root].cpu().numpy(), want, "reduce root")
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3])
+def test_loopback_skewed_blocks(coll, algo):
+    """Blocks >= 1 MiB: TMP holds them 6 KiB-skewed; results
+    stay bit-exact with prov/coll (ragged count, so TREE_COLL falls back)."""
+    n, dt, op = 4, 9, 3
+    for count in (n * 300_001 + 3, n * 300_000):
+        sends = _inputs(dt, n, count, count, 0.9, 1.1)
+        want = oracle.allreduce(op, dt, sends)[0]
+        sd = [_dev(s) for s in sends]
+        rd = [torch.zeros_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, algo, n, -1, dt, op, count, sd, rd)
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert_parity(dt, rd[r].cpu().numpy(), want, f"count={count} r={r}")
+
+
 def test_loopback_moves(coll):
     n, count = 5, 12_345
     sends = _inputs(6, n, count, 5)

@@ -134,3 +134,33 @@ def test_block_split():
             assert [o for o, _ in offs] == list(np.cumsum([0] + [ln for _, ln in offs])[:-1])
             assert sum(ln for _, ln in offs) == count
             assert [(a, b - a) for a, b in oracle.slice_bounds(count, n)] == offs
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_tree_blocks_skewed_in_tmp(n):
+    """Blocks of >= 1 MiB sit round_up(B, 256) + 6 KiB apart in TMP (HBM
+    channel skew for the tree kernel's N concurrent streams); results stay
+    bit-exact with prov/coll for allreduce, reduce_scatter and reduce."""
+    dt, op, count = F64, PROD, n * 140_001 + 1
+    off, mlen = coll.block(count, n, 0)
+    stride = ((mlen * 8 + 255) // 256) * 256 + 6144
+    p = coll.plan(ALLREDUCE, coll.ALGO_TREE, 0, n, -1, count, 8)
+    assert p.tmp_bytes == n * stride
+    rng = np.random.default_rng(n)
+    sends = [rng.uniform(0.9, 1.1, count) for _ in range(n)]
+    want = oracle.allreduce(op, dt, sends)[0]
+    res = [np.zeros(count * 8, np.uint8) for _ in range(n)]
+    _plansim.run(ALLREDUCE, coll.ALGO_TREE, n, -1, dt, op, count,
+                 [s.view(np.uint8) for s in sends], res)
+    for r in range(n):
+        assert np.array_equal(res[r].view(np.float64), want)
+    res = [np.zeros(coll.block(count, n, r)[1] * 8, np.uint8) for r in range(n)]
+    _plansim.run(REDUCE_SCATTER, coll.ALGO_TREE, n, -1, dt, op, count,
+                 [s.view(np.uint8) for s in sends], res)
+    for r in range(n):
+        o, ln = coll.block(count, n, r)
+        assert np.array_equal(res[r].view(np.float64), want[o:o + ln])
+    res = [np.zeros(count * 8, np.uint8) for _ in range(n)]
+    _plansim.run(REDUCE, coll.ALGO_TREE, n, n - 1, dt, op, count,
+                 [s.view(np.uint8) for s in sends], res)
+    assert np.array_equal(res[n - 1].view(np.float64), want)
