@@ -408,6 +408,7 @@ def tune(args) -> None:
         if not torch.equal(a, want):
             raise SystemExit(f"tune variant {v} is WRONG")
     times = {v: [] for v in variants}
+    region = {v: [] for v in variants}
     for _ in range(3):
         for v in variants:
             for i in range(4):
@@ -425,12 +426,16 @@ def tune(args) -> None:
                 b.record(stream)
             torch.cuda.synchronize()
             times[v].extend(a.elapsed_time(b) for a, b in evs)
+            region[v].append(evs[0][0].elapsed_time(evs[-1][1]) / len(evs))
     rows = []
     for v in variants:
         ms = statistics.median(times[v])
         nb = args.tune_bytes
         rows.append({"variant": v, "bytes": nb, "median_us": round(ms * 1e3, 2),
                      "min_us": round(min(times[v]) * 1e3, 2),
+                     "region_us": round(statistics.median(region[v]) * 1e3, 2),
+                     "p10_p90_us": [round(x * 1e3, 2) for x in
+                                    statistics.quantiles(times[v], n=10)[::8]],
                      "tbps": round(3 * nb / (ms * 1e-3) / 1e12, 3),
                      "frac": round(3 * nb / (ms * 1e-3) / 1e9 / PEAK_GBPS, 4)})
     print(json.dumps({"tune": rows}))

@@ -164,8 +164,107 @@ __global__ __launch_bounds__(256) void sum_ldsdma_persist(u32x4 *__restrict__ ds
   }
 }
 
+// One wave's tile of U KiB per operand through LDS (the product body).
+template <int U, int UMAX, int AUX>
+__device__ __forceinline__ void ldsdma_tile(u32x4 *__restrict__ dst,
+                                            const u32x4 *__restrict__ src, size_t nvec,
+                                            size_t base, u32x4 (*lds)[UMAX][64],
+                                            unsigned l) {
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][u][0], 16, 0, AUX);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][u][0], 16, 0, AUX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<true>(dst + base + u * 64 + l, addf(lds[0][u][l], lds[1][u][l]));
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + u * 64 + l;
+      if (i < nvec) st<true>(dst + i, addf(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
+// Tapered grid: the first n4 workgroups take 4 KiB tiles per wave, the next
+// n2 take 2 KiB, the rest 1 KiB.  Workgroups dispatch roughly in blockIdx
+// order, so the last ones to start are the short ones and the drain at the
+// end of the launch (CUs going idle one by one) is shorter.
+template <int AUX>
+__global__ __launch_bounds__(256) void sum_taper(u32x4 *__restrict__ dst,
+                                                 const u32x4 *__restrict__ src,
+                                                 size_t nvec, unsigned n4, unsigned n2) {
+  __shared__ u32x4 lds[4][2][4][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64, b = blockIdx.x;
+  if (b < n4) {
+    ldsdma_tile<4, 4, AUX>(dst, src, nvec, (size_t)b * 1024 + w * 256, lds[w], l);
+  } else if (b < n4 + n2) {
+    ldsdma_tile<2, 4, AUX>(dst, src, nvec,
+                           (size_t)n4 * 1024 + (size_t)(b - n4) * 512 + w * 128, lds[w], l);
+  } else {
+    ldsdma_tile<1, 4, AUX>(dst, src, nvec,
+                           (size_t)n4 * 1024 + (size_t)n2 * 512 +
+                               (size_t)(b - n4 - n2) * 256 + w * 64,
+                           lds[w], l);
+  }
+}
+
+// LDS-DMA body with the stores issued as buffer stores carrying cache-policy
+// bits SAUX (gfx950 cpol: sc0=1, nt=2, sc1=16).  sc1 stores write through
+// the XCD L2 instead of leaving dirty lines for the end-of-kernel writeback.
+template <int U, int SAUX>
+__global__ __launch_bounds__(256) void sum_ldsdma_st(u32x4 *__restrict__ dst,
+                                                     const u32x4 *__restrict__ src,
+                                                     size_t nvec) {
+  __shared__ u32x4 lds[2][4][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (4 * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(addf(lds[0][w][u][l], lds[1][w][u][l]), r,
+                                             (u * 64 + l) * 16, 0, SAUX);
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + u * 64 + l;
+      if (i < nvec) st<true>(dst + i, addf(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
 static inline unsigned blocks(size_t nvec, size_t per) {
   return (unsigned)((nvec + per - 1) / per);
+}
+
+// Taper launch: the last s2 and s1 vectors (rounded) go to 2 KiB / 1 KiB tiles.
+template <int AUX>
+static void taper(u32x4 *d, const u32x4 *v, size_t nvec, size_t s2, size_t s1,
+                  hipStream_t s) {
+  size_t big = nvec > s2 + s1 ? nvec - s2 - s1 : 0;
+  unsigned n4 = (unsigned)(big / 1024);
+  size_t rest = nvec - (size_t)n4 * 1024;
+  size_t r2 = rest > s1 ? rest - s1 : 0;
+  unsigned n2 = (unsigned)(r2 / 512);
+  size_t r1 = rest - (size_t)n2 * 512;
+  unsigned n1 = blocks(r1, 256);
+  hipLaunchKernelGGL((sum_taper<AUX>), dim3(n4 + n2 + n1), dim3(256), 0, s, d, v, nvec,
+                     n4, n2);
 }
 
 }  // namespace lfa_tune
@@ -223,6 +322,27 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
                          d, v, nvec);
       break;
     case 23: RUN(256, 4, true, true, 1, true, true); break;
+    // tapered tails (last workgroups take shorter tiles)
+    case 40: taper<2>(d, v, nvec, 0, 1280 * 256, s); break;
+    case 41: taper<2>(d, v, nvec, 0, 2560 * 256, s); break;
+    case 42: taper<2>(d, v, nvec, 1280 * 512, 1280 * 256, s); break;
+    case 43: taper<2>(d, v, nvec, 2560 * 512, 1280 * 256, s); break;
+    case 47: taper<2>(d, v, nvec, 0, 640 * 256, s); break;
+    // cache-policy bits on the LDS-DMA loads (gfx950 cpol: sc0=1, nt=2, sc1=16)
+    case 44: LDSDMA(4, 4, 3, 0); break;
+    case 45: LDSDMA(4, 4, 18, 0); break;
+    case 46: LDSDMA(4, 4, 19, 0); break;
+#define LDSST(U, SAUX)                                                           \
+  hipLaunchKernelGGL((sum_ldsdma_st<U, SAUX>), dim3(blocks(nvec, 256 * U)), dim3(256), \
+                     0, s, d, v, nvec)
+    // store cache-policy bits (buffer stores)
+    case 50: LDSST(4, 2); break;   // nt (= product policy, buffer form)
+    case 51: LDSST(4, 16); break;  // sc1: write-through
+    case 52: LDSST(4, 18); break;  // sc1 nt
+    case 53: LDSST(4, 17); break;  // sc0 sc1
+    case 54: LDSST(4, 19); break;  // sc0 sc1 nt
+    case 55: LDSST(4, 0); break;   // plain
+#undef LDSST
     default: return -LFA_EINVAL;
   }
 #undef RUN
