@@ -319,58 +319,92 @@ def extra_e2e_staged(reps=3):
             "note": "pinned host dst/src, pipelined H2D / combine / D2H on two streams"}
 
 
+def _rs_sweep(ep, rank, world, algo):
+    """double PROD reduce_scatter, 4 KiB .. 256 MiB per rank (configs[4])."""
+    from libfabric_amd import coll
+    ep.set_algo(algo)
+    sweep = {}
+    for nbytes in [4096 * 4 ** k for k in range(9)]:   # 4 KiB .. 256 MiB
+        cnt = nbytes // 8
+        a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
+        off, ln = coll.block(cnt, world, rank)
+        b = torch.empty(max(ln, 1), device="cuda", dtype=torch.float64)
+        ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
+        barrier(world)
+        reps = 20 if nbytes < (16 << 20) else 5
+        t0 = time.perf_counter()
+        ctxs = [ep.reduce_scatter(a, b, cnt, 9, 3) for _ in range(reps)]
+        ep.wait(ctxs[-1])
+        t = max_over_ranks(time.perf_counter() - t0, world) / reps
+        sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
+                              "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+    return sweep
+
+
 def extra_collectives(rank, world, stream):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
-    (liblfa_coll.so) over RCCL.  algbw = S/t, busbw = 2(N-1)/N·S/t."""
+    (liblfa_coll.so).  algbw = S/t, busbw = 2(N-1)/N·S/t.  The exact
+    algorithms (TREE, TREE_COLL, P2P) must agree bit for bit; the line says
+    whether they did on this run."""
     from libfabric_amd import coll
     ep = coll.Endpoint.from_torch_dist()
     out = {}
     try:
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
+        ref = None
         for name, algo in (("allreduce_tree_exact", coll.ALGO_TREE),
                            ("allreduce_tree_exact_rccl_xfer", coll.ALGO_TREE_COLL),
+                           ("allreduce_p2p_exact", coll.ALGO_P2P),
                            ("allreduce_rccl", coll.ALGO_RCCL)):
-            ep.set_algo(algo)
-            ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
-            barrier(world)
-            reps = 10
-            t0 = time.perf_counter()
-            ctxs = [ep.allreduce(x, y, COUNT, 8, 2) for _ in range(reps)]
-            ep.wait(ctxs[-1])
-            t = max_over_ranks(time.perf_counter() - t0, world) / reps
-            out[name] = {"ms": round(t * 1e3, 3),
-                         "algbw_gbs": round(S_BYTES / t / 1e9, 1),
-                         "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)}
+            try:
+                ep.set_algo(algo)
+                y.zero_()
+                ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
+                row = {}
+                if algo != coll.ALGO_RCCL:
+                    if ref is None:
+                        ref = y.clone()
+                    else:
+                        row["bitwise_equal_tree"] = bool(torch.equal(y, ref))
+                barrier(world)
+                reps = 10
+                t0 = time.perf_counter()
+                ctxs = [ep.allreduce(x, y, COUNT, 8, 2) for _ in range(reps)]
+                ep.wait(ctxs[-1])
+                t = max_over_ranks(time.perf_counter() - t0, world) / reps
+                row.update({"ms": round(t * 1e3, 3),
+                            "algbw_gbs": round(S_BYTES / t / 1e9, 1),
+                            "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)})
+                out[name] = row
+            except Exception as e:  # noqa: BLE001 — one algorithm must not hide the rest
+                out[name] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        del ref
         ep.set_algo(coll.ALGO_TREE)
         out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
-        sweep = {}
-        for nbytes in [4096 * 4 ** k for k in range(9)]:   # 4 KiB .. 256 MiB
-            cnt = nbytes // 8
-            a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
-            off, ln = coll.block(cnt, world, rank)
-            b = torch.empty(max(ln, 1), device="cuda", dtype=torch.float64)
-            ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
-            barrier(world)
-            reps = 20 if nbytes < (16 << 20) else 5
-            t0 = time.perf_counter()
-            ctxs = [ep.reduce_scatter(a, b, cnt, 9, 3) for _ in range(reps)]
-            ep.wait(ctxs[-1])
-            t = max_over_ranks(time.perf_counter() - t0, world) / reps
-            sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
-                                  "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
-        out["reduce_scatter_double_prod_tree"] = sweep
+        out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE)
+        if world > 1:
+            try:
+                out["reduce_scatter_double_prod_p2p"] = _rs_sweep(ep, rank, world,
+                                                                  coll.ALGO_P2P)
+            except Exception as e:  # noqa: BLE001
+                out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
         a = torch.rand(1024, device="cuda")
         b = torch.empty_like(a)
-        ep.wait(ep.allreduce(a, b, 1024, 8, 2))
-        barrier(world)
-        t0 = time.perf_counter()
-        for _ in range(200):
+        for name, algo in (("allreduce_4kib_float_sum_us", coll.ALGO_TREE),
+                           ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P)):
+            if algo == coll.ALGO_P2P and world == 1:
+                continue
+            ep.set_algo(algo)
             ep.wait(ep.allreduce(a, b, 1024, 8, 2))
-        t = max_over_ranks(time.perf_counter() - t0, world) / 200
-        out["allreduce_4kib_float_sum_us"] = round(t * 1e6, 1)
+            barrier(world)
+            t0 = time.perf_counter()
+            for _ in range(200):
+                ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+            t = max_over_ranks(time.perf_counter() - t0, world) / 200
+            out[name] = round(t * 1e6, 1)
         if rank == 0:
             out["cpu_model_allreduce_256mib"] = cpu_model_allreduce(world)
     finally:

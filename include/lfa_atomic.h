@@ -25,6 +25,9 @@
  *   lfa_reduce_tree_async()      N-input fused combine in prov/coll's
  *                                  recursive-doubling association order
  *                                  (coll_coll.c:349-449), one pass over HBM
+ *   lfa_reduce_tree_put_async()  the same tree, result written to several
+ *                                  outputs, system-scope accesses (peer HBM
+ *                                  over xGMI; the LFA_ALGO_P2P kernel)
  *
  * Semantics are the shipping (HAVE_BUILTIN_MM_ATOMICS) table's, bit-exact:
  * dst-biased MIN/MAX, wrapping integer SUM/PROD, IEEE float/double with no
@@ -76,6 +79,19 @@ int lfa_atomic_write_async(enum lfa_op op, enum lfa_datatype datatype,
 int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype datatype,
 			  void *dst, const void *const *srcs, int nsrc,
 			  size_t cnt, void *stream);
+
+/*
+ * The same tree, its result written to each of dsts[0..ndst).  Inputs and
+ * outputs may be other GPUs' memory mapped over IPC (xGMI): every load and
+ * store is system scope (sc0 sc1), so a peer ordered after this kernel (e.g.
+ * by a stream-ordered barrier) reads the stored bytes.  `dsts`/`srcs` are
+ * HOST arrays of device pointers; outputs must not alias inputs.
+ * 1 <= nsrc <= LFA_TREE_MAX, 1 <= ndst <= LFA_PUT_MAX.
+ */
+#define LFA_PUT_MAX 32
+int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype datatype,
+			      void *const *dsts, int ndst, const void *const *srcs,
+			      int nsrc, size_t cnt, void *stream);
 
 /*
  * Fetch table — replaces ofi_atomic_readwrite_handlers (util_atomic.c:924-950):

@@ -70,6 +70,14 @@ enum lfa_coll_algo {
 	 * grouped ncclSend/ncclRecv (when count divides evenly over the
 	 * group; otherwise identical to LFA_ALGO_TREE).  Same bits. */
 	LFA_ALGO_TREE_COLL = 3,
+	/* direct xGMI peer access, same tree and bits as LFA_ALGO_TREE: each
+	 * rank stages its input in a symmetric workspace whose peers map it
+	 * over IPC (hipIpcOpenMemHandle); rank r's kernel reads block r of
+	 * every rank's input straight from peer HBM, reduces it and writes
+	 * (pushes) the result block into every rank's workspace in the same
+	 * pass; two stream-ordered barriers per operation.  No intermediate
+	 * transport copies, xGMI in and out directions busy at once. */
+	LFA_ALGO_P2P = 4,
 };
 
 /* ---- bootstrap (replaces fi_getinfo/fi_fabric/fi_domain/fi_endpoint
@@ -198,17 +206,27 @@ enum lfa_step_type {
 				  rank p, block q of dst comes from rank q    */
 	LFA_STEP_ALLGATHER = 7,/* count bytes: src (this rank's block) to
 				  block r of dst on every rank                */
+	LFA_STEP_BARRIER = 8,  /* every rank's earlier steps (its own stream)
+				  complete before any rank's later steps run  */
+	LFA_STEP_TREE_PUT = 9, /* TREE whose result also goes to `peer` more
+				  destinations: refs[first+nsrc ..
+				  first+nsrc+peer) (LFA_ALGO_P2P pushes)      */
 };
-enum lfa_buf_id { LFA_BUF_SEND = 0, LFA_BUF_RESULT = 1, LFA_BUF_TMP = 2 };
+/* SYM_IN / SYM_OUT: the symmetric workspace of group rank `ref.rank`, two
+ * regions of count·esz bytes each (input staging, gathered result), mapped
+ * into every member's address space; offsets mirror SEND / RESULT. */
+enum lfa_buf_id { LFA_BUF_SEND = 0, LFA_BUF_RESULT = 1, LFA_BUF_TMP = 2,
+		  LFA_BUF_SYM_IN = 3, LFA_BUF_SYM_OUT = 4 };
 
 struct lfa_ref {
 	int32_t buf;           /* enum lfa_buf_id */
-	uint32_t pad;
+	uint32_t rank;         /* SYM_IN/SYM_OUT: owning group rank */
 	uint64_t off;          /* byte offset */
 };
 struct lfa_step {
 	int32_t type;          /* enum lfa_step_type */
-	int32_t peer;          /* SEND/RECV: group rank */
+	int32_t peer;          /* SEND/RECV: group rank; TREE_PUT: extra
+				  destinations */
 	uint64_t count;        /* bytes (SEND/RECV/COPY) or elements */
 	struct lfa_ref dst;
 	struct lfa_ref src;

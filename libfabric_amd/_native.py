@@ -37,6 +37,10 @@ def _bind_lfa(L):
     L.lfa_reduce_tree_async.argtypes = [c_int, c_int, c_void_p,
                                         ctypes.POINTER(c_void_p), c_int,
                                         c_size_t, c_void_p]
+    L.lfa_reduce_tree_put_async.restype = c_int
+    L.lfa_reduce_tree_put_async.argtypes = [c_int, c_int, ctypes.POINTER(c_void_p), c_int,
+                                            ctypes.POINTER(c_void_p), c_int, c_size_t,
+                                            c_void_p]
     L.lfa_atomic_readwrite_async.restype = c_int
     L.lfa_atomic_readwrite_async.argtypes = [c_int, c_int, c_void_p, c_void_p,
                                              c_void_p, c_size_t, c_void_p]

@@ -135,3 +135,22 @@ def reduce_tree(op: int, dt: int, dst: torch.Tensor, srcs: list[torch.Tensor],
                                      len(srcs), cnt, _stream_handle(stream))
     if rc:
         raise LfaError(rc, f"lfa_reduce_tree_async({OP(op).name},{DT(dt).name})")
+
+
+def reduce_tree_put(op: int, dt: int, dsts: list[torch.Tensor], srcs: list[torch.Tensor],
+                    cnt: int | None = None, stream=None) -> None:
+    """Every dsts[j] = recursive-doubling tree of srcs, one pass, system-scope
+    accesses (lfa_reduce_tree_put_async, the LFA_ALGO_P2P kernel)."""
+    for i, t in enumerate(list(dsts) + list(srcs)):
+        _check_dev(t, f"operand {i}")
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dsts[0].nbytes // esz
+    if any(cnt * esz > t.nbytes for t in list(dsts) + list(srcs)):
+        raise ValueError("cnt exceeds buffer size")
+    sa = (ctypes.c_void_p * len(srcs))(*[t.data_ptr() for t in srcs])
+    da = (ctypes.c_void_p * len(dsts))(*[t.data_ptr() for t in dsts])
+    rc = lib().lfa_reduce_tree_put_async(int(op), int(dt), da, len(dsts), sa, len(srcs),
+                                         cnt, _stream_handle(stream))
+    if rc:
+        raise LfaError(rc, f"lfa_reduce_tree_put_async({OP(op).name},{DT(dt).name})")

@@ -28,9 +28,10 @@ c_int, c_size_t, c_void_p, c_uint64, c_uint32, c_int32 = (
     ctypes.c_uint32, ctypes.c_int32)
 c_ssize_t = ctypes.c_ssize_t
 
-ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL = 0, 1, 2, 3
-STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY = range(6)
-BUF_SEND, BUF_RESULT, BUF_TMP = 0, 1, 2
+ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL, ALGO_P2P = 0, 1, 2, 3, 4
+(STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY,
+ STEP_ALLTOALL, STEP_ALLGATHER, STEP_BARRIER, STEP_TREE_PUT) = range(10)
+BUF_SEND, BUF_RESULT, BUF_TMP, BUF_SYM_IN, BUF_SYM_OUT = 0, 1, 2, 3, 4
 ADDR_NOTAVAIL = (1 << 64) - 1
 EAGAIN, EIO = 11, 5
 JOIN_COMPLETE = 6
@@ -38,7 +39,7 @@ UNIQUE_ID_BYTES = 128
 
 
 class Ref(ctypes.Structure):
-    _fields_ = [("buf", c_int32), ("pad", c_uint32), ("off", c_uint64)]
+    _fields_ = [("buf", c_int32), ("rank", c_uint32), ("off", c_uint64)]
 
 
 class Step(ctypes.Structure):
@@ -182,12 +183,16 @@ def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
     _chk(L.lfa_coll_plan(coll, algo, rank, nranks, root, count, esz, steps,
                          ctypes.byref(ns), refs, ctypes.byref(nr),
                          ctypes.byref(tmp)), "lfa_coll_plan")
+    def tup(r):
+        # symmetric-workspace refs also name the owning group rank
+        return (r.buf, r.off, r.rank) if r.buf in (BUF_SYM_IN, BUF_SYM_OUT) else (r.buf, r.off)
+
     out = []
     for s in steps[:ns.value]:
         out.append({"type": s.type, "peer": s.peer, "count": s.count,
-                    "dst": (s.dst.buf, s.dst.off), "src": (s.src.buf, s.src.off),
+                    "dst": tup(s.dst), "src": tup(s.src),
                     "first": s.first, "nsrc": s.nsrc})
-    return Plan(out, [(r.buf, r.off) for r in refs[:nr.value]], tmp.value)
+    return Plan(out, [tup(r) for r in refs[:nr.value]], tmp.value)
 
 
 def block(count: int, nranks: int, r: int) -> tuple[int, int]:
@@ -397,4 +402,4 @@ def esz(dt: int) -> int:
 
 
 __all__ = ["plan", "block", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
-           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "esz"]
+           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz"]

@@ -17,6 +17,9 @@ extern "C" {
   int lfa__write_op##N(int, void *, const void *, size_t, void *);
 #define LFA_DECL_T(N)                                                          \
   int lfa__tree_op##N(int, void *, const void *const *, int, size_t, void *);
+#define LFA_DECL_TP(N)                                                         \
+  int lfa__treeput_op##N(int, void *const *, int, const void *const *, int,    \
+                         size_t, void *);
 #define LFA_DECL_RW(N)                                                         \
   int lfa__readwrite_op##N(int, void *, const void *, void *, size_t, void *);
 #define LFA_DECL_SW(N)                                                         \
@@ -27,6 +30,8 @@ LFA_DECL_W(5) LFA_DECL_W(6) LFA_DECL_W(7) LFA_DECL_W(8) LFA_DECL_W(9)
 LFA_DECL_W(11)
 LFA_DECL_T(0) LFA_DECL_T(1) LFA_DECL_T(2) LFA_DECL_T(3) LFA_DECL_T(4)
 LFA_DECL_T(5) LFA_DECL_T(6) LFA_DECL_T(7) LFA_DECL_T(8) LFA_DECL_T(9)
+LFA_DECL_TP(0) LFA_DECL_TP(1) LFA_DECL_TP(2) LFA_DECL_TP(3) LFA_DECL_TP(4)
+LFA_DECL_TP(5) LFA_DECL_TP(6) LFA_DECL_TP(7) LFA_DECL_TP(8) LFA_DECL_TP(9)
 LFA_DECL_RW(0) LFA_DECL_RW(1) LFA_DECL_RW(2) LFA_DECL_RW(3) LFA_DECL_RW(4)
 LFA_DECL_RW(5) LFA_DECL_RW(6) LFA_DECL_RW(7) LFA_DECL_RW(8) LFA_DECL_RW(9)
 LFA_DECL_RW(10) LFA_DECL_RW(11)
@@ -34,6 +39,7 @@ LFA_DECL_SW(12) LFA_DECL_SW(13) LFA_DECL_SW(14) LFA_DECL_SW(15)
 LFA_DECL_SW(16) LFA_DECL_SW(17) LFA_DECL_SW(18)
 #undef LFA_DECL_W
 #undef LFA_DECL_T
+#undef LFA_DECL_TP
 #undef LFA_DECL_RW
 #undef LFA_DECL_SW
 }
@@ -63,6 +69,13 @@ const swap_launch_t kSwap[LFA_SWAP_OP_CNT] = {
 const tree_launch_t kTree[LFA_BXOR + 1] = {
     lfa__tree_op0, lfa__tree_op1, lfa__tree_op2, lfa__tree_op3, lfa__tree_op4,
     lfa__tree_op5, lfa__tree_op6, lfa__tree_op7, lfa__tree_op8, lfa__tree_op9};
+
+typedef int (*treeput_launch_t)(int, void *const *, int, const void *const *, int,
+                                size_t, void *);
+const treeput_launch_t kTreePut[LFA_BXOR + 1] = {
+    lfa__treeput_op0, lfa__treeput_op1, lfa__treeput_op2, lfa__treeput_op3,
+    lfa__treeput_op4, lfa__treeput_op5, lfa__treeput_op6, lfa__treeput_op7,
+    lfa__treeput_op8, lfa__treeput_op9};
 
 // Table membership (util_atomic.c:907-922, HAVE_BUILTIN_MM_ATOMICS build with
 // 128-bit atomics): REALNO = int8..double + int128; ALL = REALNO + float
@@ -252,6 +265,22 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
   for (int k = 0; k < nsrc; k++)
     if (cnt && !srcs[k]) return -LFA_EINVAL;
   return kTree[op](dt, dst, srcs, nsrc, cnt, stream);
+}
+
+int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype dt,
+                              void *const *dsts, int ndst, const void *const *srcs,
+                              int nsrc, size_t cnt, void *stream) {
+  if ((unsigned)op > LFA_BXOR || (unsigned)dt >= LFA_DATATYPE_CNT ||
+      !in_table(op, dt))
+    return -LFA_EOPNOTSUPP;
+  if (nsrc < 1 || nsrc > LFA_TREE_MAX || !srcs || ndst < 1 || ndst > LFA_PUT_MAX ||
+      !dsts)
+    return -LFA_EINVAL;
+  for (int k = 0; k < nsrc; k++)
+    if (cnt && !srcs[k]) return -LFA_EINVAL;
+  for (int j = 0; j < ndst; j++)
+    if (cnt && !dsts[j]) return -LFA_EINVAL;
+  return kTreePut[op](dt, dsts, ndst, srcs, nsrc, cnt, stream);
 }
 
 }  // extern "C"

@@ -72,8 +72,17 @@ static struct lfa_ref ref(int buf, uint64_t off)
 	struct lfa_ref r;
 
 	r.buf = buf;
-	r.pad = 0;
+	r.rank = 0;
 	r.off = off;
+	return r;
+}
+
+/* A ref into group rank `rank`'s symmetric workspace (LFA_ALGO_P2P). */
+static struct lfa_ref sref(int buf, int rank, uint64_t off)
+{
+	struct lfa_ref r = ref(buf, off);
+
+	r.rank = (uint32_t)rank;
 	return r;
 }
 
@@ -179,6 +188,31 @@ static void p_tree_end(struct planner *p, uint32_t first, struct lfa_ref dst,
 		s->nsrc = (uint32_t)(p->nr - first);
 		s->count = count;
 	}
+}
+
+/* TREE_PUT: inputs pushed with p_tree_src() since `first`, then `nput`
+ * extra destinations pushed after them. */
+static void p_tree_put_end(struct planner *p, uint32_t first, uint32_t nsrc,
+			   struct lfa_ref dst, uint64_t count)
+{
+	struct lfa_step *s;
+
+	if (!count)
+		return;
+	s = push(p, LFA_STEP_TREE_PUT);
+	if (s) {
+		s->dst = dst;
+		s->first = first;
+		s->nsrc = nsrc;
+		s->peer = (int32_t)(p->nr - first - nsrc);
+		s->count = count;
+	}
+}
+
+static void p_barrier(struct planner *p)
+{
+	p_group_end(p);
+	push(p, LFA_STEP_BARRIER);
 }
 
 static void p_coll(struct planner *p, int type, struct lfa_ref dst,
@@ -355,6 +389,110 @@ static void plan_rd_allreduce(struct planner *p, uint64_t local, uint64_t n,
 	}
 }
 
+/*
+ * LFA_ALGO_P2P.  Every rank stages the blocks the others need in its own
+ * SYM_IN region (rank r's block is read in place from SEND), then, after a
+ * barrier, reduces block r of all inputs straight out of the peers' SYM_IN
+ * over xGMI and writes the result to `outs` (local result and/or peers'
+ * SYM_OUT).  A closing barrier guarantees no peer still reads or writes this
+ * rank's workspace once its operation completes (so the next operation may
+ * overwrite it, and close may free it).
+ */
+static void p2p_stage_input(struct planner *p, int r, int n, size_t count,
+			    size_t esz)
+{
+	size_t moff, mlen;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	p_copy(p, sref(LFA_BUF_SYM_IN, r, 0), ref(LFA_BUF_SEND, 0), moff * esz);
+	p_copy(p, sref(LFA_BUF_SYM_IN, r, (moff + mlen) * esz),
+	       ref(LFA_BUF_SEND, (moff + mlen) * esz), (count - moff - mlen) * esz);
+	p_barrier(p);
+}
+
+/* Tree of block r over all ranks' inputs; result to dst, and with push_all
+ * also into every peer's SYM_OUT at the block's offset. */
+static void p2p_tree_block(struct planner *p, int r, int n, size_t count,
+			   size_t esz, struct lfa_ref dst, int push_all)
+{
+	size_t moff, mlen;
+	uint32_t first;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	first = p_tree_begin(p);
+	for (int k = 0; k < n; k++)
+		p_tree_src(p, k == r ? ref(LFA_BUF_SEND, moff * esz) :
+			   sref(LFA_BUF_SYM_IN, k, moff * esz));
+	if (push_all) {
+		/* in the order r+1, r+2, …: each block's pushes start on a
+		 * different link */
+		for (int k = 1; k < n; k++)
+			p_tree_src(p, sref(LFA_BUF_SYM_OUT, (r + k) % n, moff * esz));
+	}
+	p_tree_put_end(p, first, (uint32_t)n, dst, mlen);
+}
+
+/* Copy the gathered blocks (all but block `skip`) from rank r's SYM_OUT. */
+static void p2p_unstage_output(struct planner *p, int r, int n, size_t count,
+			       size_t esz, int skip)
+{
+	size_t moff, mlen;
+
+	lfa_coll_block(count, n, skip, &moff, &mlen);
+	p_copy(p, ref(LFA_BUF_RESULT, 0), sref(LFA_BUF_SYM_OUT, r, 0), moff * esz);
+	p_copy(p, ref(LFA_BUF_RESULT, (moff + mlen) * esz),
+	       sref(LFA_BUF_SYM_OUT, r, (moff + mlen) * esz),
+	       (count - moff - mlen) * esz);
+}
+
+static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
+		    int n, int root, size_t count, size_t esz)
+{
+	size_t moff, mlen, bytes = count * esz;
+	uint32_t first;
+
+	lfa_coll_block(count, n, r, &moff, &mlen);
+	switch (coll) {
+	case LFA_ALLREDUCE:
+		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES) {
+			/* one phase: every rank reduces the whole vector */
+			p_copy(p, sref(LFA_BUF_SYM_IN, r, 0), ref(LFA_BUF_SEND, 0),
+			       bytes);
+			p_barrier(p);
+			first = p_tree_begin(p);
+			for (int k = 0; k < n; k++)
+				p_tree_src(p, k == r ? ref(LFA_BUF_SEND, 0) :
+					   sref(LFA_BUF_SYM_IN, k, 0));
+			p_tree_put_end(p, first, (uint32_t)n, ref(LFA_BUF_RESULT, 0),
+				       count);
+			p_barrier(p);
+			return 0;
+		}
+		p2p_stage_input(p, r, n, count, esz);
+		p2p_tree_block(p, r, n, count, esz, ref(LFA_BUF_RESULT, moff * esz),
+			       1);
+		p_barrier(p);
+		p2p_unstage_output(p, r, n, count, esz, r);
+		return 0;
+	case LFA_REDUCE_SCATTER:
+		p2p_stage_input(p, r, n, count, esz);
+		p2p_tree_block(p, r, n, count, esz, ref(LFA_BUF_RESULT, 0), 0);
+		p_barrier(p);
+		return 0;
+	case LFA_REDUCE:
+		p2p_stage_input(p, r, n, count, esz);
+		p2p_tree_block(p, r, n, count, esz,
+			       r == root ? ref(LFA_BUF_RESULT, moff * esz) :
+			       sref(LFA_BUF_SYM_OUT, root, moff * esz), 0);
+		p_barrier(p);
+		if (r == root)
+			p2p_unstage_output(p, r, n, count, esz, root);
+		return 0;
+	default:
+		return -LFA_ENOSYS;
+	}
+}
+
 int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		  int rank, int nranks, int root, size_t count, size_t esz,
 		  struct lfa_step *steps, size_t *nsteps, struct lfa_ref *refs,
@@ -379,6 +517,23 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 
 	if (algo == LFA_ALGO_RCCL)
 		algo = LFA_ALGO_TREE;   /* the RCCL algo is not a schedule */
+	if (algo == LFA_ALGO_P2P) {
+		/* reducing collectives over the symmetric workspace; the rest
+		 * (pure transport) keep the RCCL schedules */
+		if (n > 1 && (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER ||
+			      coll == LFA_REDUCE)) {
+			int ret = plan_p2p(&p, coll, r, n, root, count, esz);
+
+			if (ret)
+				return ret;
+			*nsteps = p.n;
+			*nrefs = p.nr;
+			if (!steps || !refs)
+				return 0;
+			return (p.n > p.cap || p.nr > p.rcap) ? -LFA_ETOOSMALL : 0;
+		}
+		algo = LFA_ALGO_TREE;
+	}
 	if (algo == LFA_ALGO_TREE_COLL) {
 		/* collective transport only for even blocks of the big path */
 		int even = count % (size_t)n == 0 &&
@@ -575,20 +730,33 @@ static int plan_make(struct plan *pl, enum lfa_collective_op coll,
 /* device helpers                                                          */
 /* ====================================================================== */
 
-static void *resolve(void *const base[3], struct lfa_ref r)
+/* Where a plan's refs point for one execution: the operation's buffers and,
+ * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
+ * (IN region at 0, OUT region at `region`). */
+struct xctx {
+	void *base[3];          /* SEND, RESULT, TMP */
+	char *const *sym;       /* [group rank] */
+	size_t region;
+};
+
+static void *resolve(const struct xctx *x, struct lfa_ref r)
 {
-	return (char *)base[r.buf] + r.off;
+	if (r.buf == LFA_BUF_SYM_IN)
+		return x->sym[r.rank] + r.off;
+	if (r.buf == LFA_BUF_SYM_OUT)
+		return x->sym[r.rank] + x->region + r.off;
+	return (char *)x->base[r.buf] + r.off;
 }
 
 /* Non-communication step on `stream`. */
 static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
-		     void *const base[3], enum lfa_op op,
+		     const struct xctx *x, enum lfa_op op,
 		     enum lfa_datatype dt, hipStream_t stream)
 {
 	switch (s->type) {
 	case LFA_STEP_REDUCE:
-		return lfa_atomic_write_async(op, dt, resolve(base, s->dst),
-					      resolve(base, s->src), s->count,
+		return lfa_atomic_write_async(op, dt, resolve(x, s->dst),
+					      resolve(x, s->src), s->count,
 					      stream);
 	case LFA_STEP_TREE: {
 		const void *srcs[LFA_TREE_MAX];
@@ -596,17 +764,46 @@ static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 		if (s->nsrc > LFA_TREE_MAX)
 			return -LFA_EINVAL;
 		for (uint32_t k = 0; k < s->nsrc; k++)
-			srcs[k] = resolve(base, refs[s->first + k]);
-		return lfa_reduce_tree_async(op, dt, resolve(base, s->dst), srcs,
+			srcs[k] = resolve(x, refs[s->first + k]);
+		return lfa_reduce_tree_async(op, dt, resolve(x, s->dst), srcs,
 					     (int)s->nsrc, s->count, stream);
 	}
+	case LFA_STEP_TREE_PUT: {
+		const void *srcs[LFA_TREE_MAX];
+		void *dsts[LFA_PUT_MAX];
+
+		if (s->nsrc > LFA_TREE_MAX || s->peer < 0 || s->peer + 1 > LFA_PUT_MAX)
+			return -LFA_EINVAL;
+		for (uint32_t k = 0; k < s->nsrc; k++)
+			srcs[k] = resolve(x, refs[s->first + k]);
+		dsts[0] = resolve(x, s->dst);
+		for (int j = 0; j < s->peer; j++)
+			dsts[1 + j] = resolve(x, refs[s->first + s->nsrc + (uint32_t)j]);
+		return lfa_reduce_tree_put_async(op, dt, dsts, 1 + s->peer, srcs,
+						 (int)s->nsrc, s->count, stream);
+	}
 	case LFA_STEP_COPY:
-		return hipMemcpyAsync(resolve(base, s->dst), resolve(base, s->src),
+		return hipMemcpyAsync(resolve(x, s->dst), resolve(x, s->src),
 				      s->count, hipMemcpyDeviceToDevice,
 				      stream) == hipSuccess ? 0 : -LFA_EIO;
 	default:
 		return -LFA_EINVAL;
 	}
+}
+
+/* Does the plan address the symmetric workspace? */
+static int plan_uses_sym(const struct lfa_step *st, size_t nsteps)
+{
+	for (size_t i = 0; i < nsteps; i++)
+		if (st[i].type == LFA_STEP_BARRIER || st[i].type == LFA_STEP_TREE_PUT)
+			return 1;
+	return 0;
+}
+
+/* Bytes of one symmetric-workspace region for `count` elements. */
+static size_t sym_region(size_t count, size_t esz)
+{
+	return (count * esz + 255) & ~(size_t)255;
 }
 
 static int is_device_ptr(const void *p)
@@ -637,6 +834,11 @@ struct lfa_coll_mc {
 	/* join in flight */
 	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
 	void *join_context;
+	/* LFA_ALGO_P2P symmetric workspace: `sym_local` (2 regions, hipMalloc,
+	 * IPC-exported) and every member's as mapped here (sym[rank] = local) */
+	char *sym_local;
+	char **sym;
+	size_t sym_region;
 };
 
 struct lfa_coll_domain {
@@ -681,6 +883,8 @@ struct lfa_coll_ep {
 	struct { uint32_t event; struct lfa_eq_entry entry; } eq[64];
 	size_t eqh, eqn;
 };
+
+static void p2p_release(struct lfa_coll_mc *mc);
 
 int lfa_coll_get_unique_id(void *id, size_t len)
 {
@@ -790,6 +994,8 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	if (!ep)
 		return -LFA_EINVAL;
 	lfa_coll_ep_flush(ep);
+	/* every P2P operation ended in a barrier: no peer touches it now */
+	p2p_release(&ep->world);
 	for (size_t i = 0; i < ep->qlen; i++)
 		hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
 	for (int i = 0; i < ep->nev; i++)
@@ -820,7 +1026,8 @@ void *lfa_coll_ep_stream(struct lfa_coll_ep *ep)
 int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo)
 {
 	if (!ep || (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
-		    algo != LFA_ALGO_RCCL && algo != LFA_ALGO_TREE_COLL))
+		    algo != LFA_ALGO_RCCL && algo != LFA_ALGO_TREE_COLL &&
+		    algo != LFA_ALGO_P2P))
 		return -LFA_EINVAL;
 	ep->algo = algo;
 	return 0;
@@ -1087,7 +1294,7 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 /* ---------------------------------------------------------------------- */
 
 static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
-		     void *const base[3], enum lfa_op op, enum lfa_datatype dt,
+		     const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
 		     hipStream_t s)
 {
 	int in_group = 0, ret = 0;
@@ -1104,11 +1311,11 @@ static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 				in_group = 1;
 			}
 			if (st->type == LFA_STEP_SEND)
-				ret = ncclSend(resolve(base, st->src), st->count, ncclUint8,
+				ret = ncclSend(resolve(x, st->src), st->count, ncclUint8,
 					       st->peer, mc->comm, s) == ncclSuccess ?
 				      0 : -LFA_EIO;
 			else
-				ret = ncclRecv(resolve(base, st->dst), st->count, ncclUint8,
+				ret = ncclRecv(resolve(x, st->dst), st->count, ncclUint8,
 					       st->peer, mc->comm, s) == ncclSuccess ?
 				      0 : -LFA_EIO;
 			break;
@@ -1118,22 +1325,139 @@ static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 			in_group = 0;
 			break;
 		case LFA_STEP_ALLTOALL:
-			ret = ncclAllToAll(resolve(base, st->src), resolve(base, st->dst),
+			ret = ncclAllToAll(resolve(x, st->src), resolve(x, st->dst),
 					   st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
 			      0 : -LFA_EIO;
 			break;
 		case LFA_STEP_ALLGATHER:
-			ret = ncclAllGather(resolve(base, st->src), resolve(base, st->dst),
+			ret = ncclAllGather(resolve(x, st->src), resolve(x, st->dst),
 					    st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
 			      0 : -LFA_EIO;
 			break;
+		case LFA_STEP_BARRIER: {
+			/* stream-ordered: a one-word allreduce completes on a rank
+			 * only after every member's stream has reached it */
+			uint64_t *w = (uint64_t *)mc->ep->barrier_dev + 2;
+
+			ret = ncclAllReduce(w, w, 1, ncclUint64, ncclSum, mc->comm, s) ==
+			      ncclSuccess ? 0 : -LFA_EIO;
+			break;
+		}
 		default:
-			ret = run_local(st, pl->refs, base, op, dt, s);
+			ret = run_local(st, pl->refs, x, op, dt, s);
 		}
 	}
 	if (in_group && ncclGroupEnd() != ncclSuccess && !ret)
 		ret = -LFA_EIO;
 	return ret;
+}
+
+/*
+ * The P2P symmetric workspace of `mc`, grown to `region` bytes per region.
+ * Collective: every member calls it at the same operation (the need depends
+ * only on the operation's shape).  The old workspace is released only after
+ * this rank's earlier operations have completed — each of which ends with a
+ * barrier, so no peer still touches it — and the members learn each other's
+ * new handle through one RCCL allgather of {ok, handle} records: a member
+ * that failed to allocate makes them all fail together instead of leaving
+ * the others waiting in a later barrier.
+ */
+struct sym_rec {
+	int32_t ok;
+	int32_t pad;
+	hipIpcMemHandle_t h;
+};
+
+static void p2p_release(struct lfa_coll_mc *mc)
+{
+	if (mc->sym) {
+		for (int k = 0; k < mc->size; k++)
+			if (k != mc->rank && mc->sym[k])
+				hipIpcCloseMemHandle(mc->sym[k]);
+		free(mc->sym);
+		mc->sym = NULL;
+	}
+	if (mc->sym_local)
+		hipFree(mc->sym_local);
+	mc->sym_local = NULL;
+	mc->sym_region = 0;
+}
+
+static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
+{
+	struct lfa_coll_ep *ep = mc->ep;
+	struct sym_rec *recs;
+	void *drec = NULL;
+	const size_t rb = sizeof(struct sym_rec);
+	int n = mc->size, ret = 0;
+
+	if (region <= mc->sym_region)
+		return 0;
+	if (region < 2 * mc->sym_region)
+		region = 2 * mc->sym_region;
+	if (region < (8u << 20))
+		region = 8u << 20;
+	region = (region + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+	if (hipStreamSynchronize(ep->stream) != hipSuccess)
+		return -LFA_EIO;
+	p2p_release(mc);
+	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
+	recs = calloc((size_t)n, rb);
+	/* host-side failures here are identical on every member only by
+	 * accident; they are out-of-memory conditions of the process */
+	if (!mc->sym || !recs || hipMalloc(&drec, (size_t)n * rb) != hipSuccess) {
+		free(recs);
+		p2p_release(mc);
+		return -LFA_ENOMEM;
+	}
+	recs[mc->rank].ok = hipMalloc((void **)&mc->sym_local, 2 * region) == hipSuccess;
+	if (!recs[mc->rank].ok)
+		mc->sym_local = NULL;
+	if (recs[mc->rank].ok && n > 1)
+		recs[mc->rank].ok = hipIpcGetMemHandle(&recs[mc->rank].h,
+						       mc->sym_local) == hipSuccess;
+	if (n > 1 &&
+	    (hipMemcpyAsync((char *)drec + (size_t)mc->rank * rb, &recs[mc->rank], rb,
+			    hipMemcpyHostToDevice, ep->stream) != hipSuccess ||
+	     ncclAllGather((char *)drec + (size_t)mc->rank * rb, drec, rb, ncclUint8,
+			   mc->comm, ep->stream) != ncclSuccess ||
+	     hipMemcpyAsync(recs, drec, (size_t)n * rb, hipMemcpyDeviceToHost,
+			    ep->stream) != hipSuccess ||
+	     hipStreamSynchronize(ep->stream) != hipSuccess))
+		ret = -LFA_EIO;
+	for (int k = 0; k < n && !ret; k++)
+		if (!recs[k].ok)
+			ret = -LFA_ENOMEM;
+	for (int k = 0; k < n && !ret; k++) {
+		if (k == mc->rank) {
+			mc->sym[k] = mc->sym_local;
+		} else if (hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
+					       hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+			mc->sym[k] = NULL;
+			ret = -LFA_EIO;
+		}
+	}
+	if (n > 1) {
+		/* agree that every member mapped every peer (MIN of the flags) */
+		int32_t ok = ret == 0;
+
+		if (hipMemcpyAsync(drec, &ok, sizeof(ok), hipMemcpyHostToDevice,
+				   ep->stream) != hipSuccess ||
+		    ncclAllReduce(drec, drec, 1, ncclInt32, ncclMin, mc->comm,
+				  ep->stream) != ncclSuccess ||
+		    hipMemcpyAsync(&ok, drec, sizeof(ok), hipMemcpyDeviceToHost,
+				   ep->stream) != hipSuccess ||
+		    hipStreamSynchronize(ep->stream) != hipSuccess || !ok)
+			ret = ret ? ret : -LFA_EIO;
+	}
+	hipFree(drec);
+	free(recs);
+	if (ret) {
+		p2p_release(mc);
+		return ret;
+	}
+	mc->sym_region = region;
+	return 0;
 }
 
 static int rccl_type(enum lfa_datatype dt, ncclDataType_t *t)
@@ -1240,7 +1564,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 {
 	const struct plan *pl;
 	size_t esz = lfa_datatype_size(dt);
-	void *base[3];
+	struct xctx x;
 	int ret;
 
 	if (ep->algo == LFA_ALGO_RCCL && mc->size > 1 &&
@@ -1250,12 +1574,20 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			  count, esz);
 	if (ret)
 		return ret;
+	memset(&x, 0, sizeof(x));
+	if (plan_uses_sym(pl->steps, pl->nsteps)) {
+		ret = p2p_ensure(mc, sym_region(count, esz));
+		if (ret)
+			return ret;
+		x.sym = mc->sym;
+		x.region = mc->sym_region;
+	}
 	ret = grow(&ep->ws, &ep->ws_size, pl->tmp, s);
 	if (!ret) {
-		base[LFA_BUF_SEND] = (void *)buf;
-		base[LFA_BUF_RESULT] = result;
-		base[LFA_BUF_TMP] = ep->ws;
-		ret = exec_plan(mc, pl, base, op, dt, s);
+		x.base[LFA_BUF_SEND] = (void *)buf;
+		x.base[LFA_BUF_RESULT] = result;
+		x.base[LFA_BUF_TMP] = ep->ws;
+		ret = exec_plan(mc, pl, &x, op, dt, s);
 	}
 	return ret;
 }
@@ -1654,6 +1986,7 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 	pthread_mutex_unlock(&mc->ep->lock);
 	if (mc->mask_host)
 		hipHostFree(mc->mask_host);
+	p2p_release(mc);
 	if (mc->owns_comm && mc->comm)
 		ncclCommDestroy(mc->comm);
 	if (mc->group_id < LFA_MAX_GROUP_ID)
@@ -1796,8 +2129,9 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 	hipStream_t s = (hipStream_t)stream;
 	size_t esz = lfa_datatype_size(dt);
 	struct plan *pl = NULL;
-	size_t *pc = NULL;
+	size_t *pc = NULL, *arrived = NULL, region = sym_region(count, esz);
 	void **tmp = NULL;
+	char **sym = NULL;
 	struct lb_msg **box = NULL;
 	int ret = 0, done, progressed;
 
@@ -1808,13 +2142,16 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		return ret;
 	if (algo == LFA_ALGO_RCCL)
 		algo = LFA_ALGO_TREE;
-	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD && algo != LFA_ALGO_TREE_COLL)
+	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
+	    algo != LFA_ALGO_TREE_COLL && algo != LFA_ALGO_P2P)
 		return -LFA_EINVAL;
 	pl = calloc((size_t)n, sizeof(*pl));
 	pc = calloc((size_t)n, sizeof(*pc));
+	arrived = calloc((size_t)n, sizeof(*arrived));
 	tmp = calloc((size_t)n, sizeof(*tmp));
+	sym = calloc((size_t)n, sizeof(*sym));
 	box = calloc((size_t)n * (size_t)n, sizeof(*box));
-	if (!pl || !pc || !tmp || !box) {
+	if (!pl || !pc || !arrived || !tmp || !sym || !box) {
 		ret = -LFA_ENOMEM;
 		goto out;
 	}
@@ -1829,6 +2166,10 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		if (!ret && pl[r].tmp &&
 		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)
 			ret = -LFA_ENOMEM;
+		/* P2P: every rank's symmetric workspace, plain pointers here */
+		if (!ret && plan_uses_sym(pl[r].steps, pl[r].nsteps) &&
+		    hipMallocAsync((void **)&sym[r], 2 * region, s) != hipSuccess)
+			ret = -LFA_ENOMEM;
 	}
 	/*
 	 * Lockstep: a rank runs local steps freely; at a comm group it posts
@@ -1839,16 +2180,35 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		done = 1;
 		progressed = 0;
 		for (int r = 0; r < n && !ret; r++) {
-			void *base[3] = {send[r], result[r], tmp[r]};
+			struct xctx xc = {{send[r], result[r], tmp[r]}, sym, region};
 
 			if (coll == LFA_BROADCAST)
-				base[LFA_BUF_SEND] = result[r];
+				xc.base[LFA_BUF_SEND] = result[r];
 			while (pc[r] < pl[r].nsteps && !ret) {
 				struct lfa_step *st = &pl[r].steps[pc[r]];
 
+				if (st->type == LFA_STEP_BARRIER) {
+					/* one stream: a rank passes barrier b once every
+					 * rank has enqueued everything before its b-th */
+					int all = 1;
+
+					if (!(arrived[r] & 1)) {
+						arrived[r] += 3;   /* count in bits 1.., flag 1 */
+						progressed = 1;
+					}
+					for (int q = 0; q < n; q++)
+						if ((arrived[q] >> 1) < (arrived[r] >> 1))
+							all = 0;
+					if (!all)
+						break;
+					arrived[r] &= ~(size_t)1;
+					pc[r]++;
+					progressed = 1;
+					continue;
+				}
 				if (st->type != LFA_STEP_SEND && st->type != LFA_STEP_RECV &&
 				    st->type != LFA_STEP_GROUP_END) {
-					ret = run_local(st, pl[r].refs, base, op, dt, s);
+					ret = run_local(st, pl[r].refs, &xc, op, dt, s);
 					pc[r]++;
 					progressed = 1;
 					continue;
@@ -1874,7 +2234,7 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 						break;
 					}
 					m->bytes = x->count;
-					hipMemcpyAsync(m->data, resolve(base, x->src), x->count,
+					hipMemcpyAsync(m->data, resolve(&xc, x->src), x->count,
 						       hipMemcpyDeviceToDevice, s);
 					t = &box[(size_t)r * n + x->peer];
 					while (*t)
@@ -1915,7 +2275,7 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 					box[(size_t)x->peer * n + r] = m->next;
 					if (m->bytes != x->count)
 						ret = -LFA_EIO;
-					hipMemcpyAsync(resolve(base, x->dst), m->data, x->count,
+					hipMemcpyAsync(resolve(&xc, x->dst), m->data, x->count,
 						       hipMemcpyDeviceToDevice, s);
 					hipFreeAsync(m->data, s);
 					free(m);
@@ -1944,12 +2304,18 @@ out:
 		for (int r = 0; r < n; r++)
 			if (tmp[r])
 				hipFreeAsync(tmp[r], s);
+	if (sym)
+		for (int r = 0; r < n; r++)
+			if (sym[r])
+				hipFreeAsync(sym[r], s);
 	if (pl)
 		for (int r = 0; r < n; r++)
 			plan_free(&pl[r]);
 	free(pl);
 	free(pc);
+	free(arrived);
 	free(tmp);
+	free(sym);
 	free(box);
 	return ret;
 }

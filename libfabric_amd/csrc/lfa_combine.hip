@@ -17,6 +17,9 @@
 //                  recursive-doubling association order (coll_coll.c:349-449):
 //                  replaces log2(N) pairwise REDUCE+COPY items, traffic
 //                  (N+1)·S instead of ~3·log2(N)·S.
+//   reduce_tree_put the same tree with its result written to several
+//                  outputs, every access system scope: the LFA_ALGO_P2P kernel
+//                  that reads peers' HBM and pushes into it over xGMI.
 //   fetch_vec/elem the fetch (readwrite) and compare-swap tables
 //                  (util_atomic.c:924-980): res = old dst, then the update.
 //
@@ -356,6 +359,119 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
 }
 
 // ---------------------------------------------------------------------------
+// N-input tree with fan-out, across GPUs (LFA_ALGO_P2P)
+// ---------------------------------------------------------------------------
+// Inputs and outputs may be other GPUs' HBM mapped into this process over
+// IPC (xGMI).  Every access is system scope (sc0 sc1): such loads miss in any
+// cache that is not coherent with the owning GPU's memory, and such stores
+// write through instead of leaving dirty lines in this XCD's L2, so a peer
+// that orders itself after this kernel (a stream-ordered barrier) reads the
+// bytes, and the next operation here reads the peer's fresh input.
+constexpr int kSysAux = 17;  // cpol sc0 | sc1
+constexpr int kMaxPut = 32;
+
+struct PutArgs {
+  TreeArgs t;
+  void *out[kMaxPut];
+  int nout;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void *base,
+                                                            unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes,
+                                           0x00020000);
+}
+
+// Vector body: wave w of workgroup b owns U KiB (64·U vectors) of every
+// input; its loads and stores go through buffer descriptors sized to the
+// wave's tile, so the last, partial tile needs no guards (out-of-range lanes
+// load 0 and their stores are dropped by the hardware).
+template <int OP, typename T, int NLEAF, int U>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0,
+                     kSysAux));
+    });
+  }
+  for (int j = 0; j < a.nout; j++) {  // wave-uniform
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0,
+                                             kSysAux);
+  }
+}
+
+// One element at system scope (relaxed atomics of the element's width; a
+// 16-byte element as two 8-byte halves — the halves of one element are
+// written by one lane, so no reader sees a torn value after the barrier).
+template <typename T>
+__device__ __forceinline__ T sys_load(const T *p) {
+  T v;
+  if constexpr (sizeof(T) == 16) {
+    uint64_t h[2];
+    h[0] = __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    h[1] = __hip_atomic_load((const uint64_t *)p + 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_memcpy(&v, h, 16);
+  } else {
+    typedef typename std::conditional<
+        sizeof(T) == 1, uint8_t,
+        typename std::conditional<
+            sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type U;
+    U x = __hip_atomic_load((const U *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_memcpy(&v, &x, sizeof(T));
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void sys_store(T *p, T v) {
+  if constexpr (sizeof(T) == 16) {
+    uint64_t h[2];
+    __builtin_memcpy(h, &v, 16);
+    __hip_atomic_store((uint64_t *)p, h[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((uint64_t *)p + 1, h[1], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    typedef typename std::conditional<
+        sizeof(T) == 1, uint8_t,
+        typename std::conditional<
+            sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type U;
+    U x;
+    __builtin_memcpy(&x, &v, sizeof(T));
+    __hip_atomic_store((U *)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t n0,
+                                                               size_t off1, size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    T v = tree_eval_with<OP, T, T, NLEAF>(
+        a.t, [&](int s) { return sys_load<T>((const T *)a.t.in[s] + k); });
+    for (int j = 0; j < a.nout; j++) sys_store<T>((T *)a.out[j] + k, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // fetch (readwrite) and compare-swap tables
 // ---------------------------------------------------------------------------
 // One launch shape for both: a functor F carries the operand pointers and
@@ -572,6 +688,26 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
   }
 }
 
+// Leaf pairing of prov/coll's tree for nsrc ranks (see TreeArgs); returns
+// the number of leaves (largest power of two <= nsrc).
+static int tree_leaves(TreeArgs &a, const void *const *srcs, int nsrc) {
+  int pof2 = 1;
+  while (pof2 * 2 <= nsrc) pof2 *= 2;
+  const int rem = nsrc - pof2;
+  memset(&a, 0, sizeof(a));
+  for (int k = 0; k < nsrc; k++) a.in[k] = srcs[k];
+  for (int k = 0; k < pof2; k++) {
+    if (k < rem) {
+      a.hi[k] = (signed char)(2 * k + 1);
+      a.lo[k] = (signed char)(2 * k);
+    } else {
+      a.hi[k] = (signed char)(k + rem);
+      a.lo[k] = -1;
+    }
+  }
+  return pof2;
+}
+
 template <int OP, typename T, int NLEAF>
 static int launch_tree_n(const TreeArgs &a, int nsrc, void *dst, size_t cnt,
                          bool vec, size_t head, size_t nvec, hipStream_t s,
@@ -608,27 +744,14 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
       return hipMemcpyAsync(dst, srcs[0], cnt * E, hipMemcpyDeviceToDevice,
                             s) == hipSuccess ? 0 : -LFA_EIO;
     }
-    int pof2 = 1;
-    while (pof2 * 2 <= nsrc) pof2 *= 2;
-    int rem = nsrc - pof2;
     TreeArgs a;
-    memset(&a, 0, sizeof(a));
+    const int pof2 = tree_leaves(a, srcs, nsrc);
     uintptr_t mis = (uintptr_t)dst % 16, anyelem = (uintptr_t)dst % E;
     for (int k = 0; k < nsrc; k++) {
-      a.in[k] = srcs[k];
       mis |= ((uintptr_t)srcs[k] % 16) ^ ((uintptr_t)dst % 16);
       anyelem |= (uintptr_t)srcs[k] % E;
     }
     if (anyelem) return -LFA_EINVAL;  // element-misaligned inputs: unsupported
-    for (int k = 0; k < pof2; k++) {
-      if (k < rem) {
-        a.hi[k] = (signed char)(2 * k + 1);
-        a.lo[k] = (signed char)(2 * k);
-      } else {
-        a.hi[k] = (signed char)(k + rem);
-        a.lo[k] = -1;
-      }
-    }
     bool vec = (mis == 0) && E <= 16;
     size_t head = vec ? ((16 - (uintptr_t)dst % 16) % 16) / E : 0;
     if (head > cnt) head = cnt;
@@ -639,6 +762,71 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
       case 8: return launch_tree_n<OP, T, 8>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
       case 16: return launch_tree_n<OP, T, 16>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
       case 32: return launch_tree_n<OP, T, 32>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      default: return -LFA_EINVAL;
+    }
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
+                             hipStream_t s) {
+  constexpr size_t E = sizeof(T);
+  constexpr int U = 2;
+  size_t nvec = vec ? (cnt - head) * E / 16 : 0;
+  if (nvec) {
+    PutArgs b = a;
+    for (int k = 0; k < kMaxLeaf; k++)
+      if (b.t.in[k]) b.t.in[k] = (const char *)b.t.in[k] + head * E;
+    for (int j = 0; j < b.nout; j++) b.out[j] = (char *)b.out[j] + head * E;
+    hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, U>),
+                       dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, nvec);
+  }
+  size_t body = nvec * 16 / E;
+  size_t n0 = vec ? head : cnt;
+  size_t tail = vec ? cnt - head - body : 0;
+  if (n0 + tail)
+    hipLaunchKernelGGL((reduce_tree_put_elem<OP, T, NLEAF>),
+                       dim3(grid_for(n0 + tail, kBlock, kElemGridCap)), dim3(kBlock),
+                       0, s, a, n0, head + body, tail);
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T>
+static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
+                           int nsrc, size_t cnt, hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    if (nsrc < 1 || nsrc > kMaxLeaf || ndst < 1 || ndst > kMaxPut) return -LFA_EINVAL;
+    if (cnt == 0) return 0;
+    PutArgs a;
+    const int pof2 = tree_leaves(a.t, srcs, nsrc);
+    memset(a.out, 0, sizeof(a.out));
+    a.nout = ndst;
+    const uintptr_t p0 = (uintptr_t)dsts[0];
+    uintptr_t mis = 0, anyelem = 0;
+    for (int k = 0; k < nsrc; k++) {
+      mis |= ((uintptr_t)srcs[k] ^ p0) % 16;
+      anyelem |= (uintptr_t)srcs[k] % E;
+    }
+    for (int j = 0; j < ndst; j++) {
+      a.out[j] = dsts[j];
+      mis |= ((uintptr_t)dsts[j] ^ p0) % 16;
+      anyelem |= (uintptr_t)dsts[j] % E;
+    }
+    if (anyelem) return -LFA_EINVAL;
+    const bool vec = mis == 0 && E <= 16;
+    size_t head = vec ? ((16 - p0 % 16) % 16) / E : 0;
+    if (head > cnt) head = cnt;
+    switch (pof2) {
+      case 1: return launch_tree_put_n<OP, T, 1>(a, cnt, vec, head, s);
+      case 2: return launch_tree_put_n<OP, T, 2>(a, cnt, vec, head, s);
+      case 4: return launch_tree_put_n<OP, T, 4>(a, cnt, vec, head, s);
+      case 8: return launch_tree_put_n<OP, T, 8>(a, cnt, vec, head, s);
+      case 16: return launch_tree_put_n<OP, T, 16>(a, cnt, vec, head, s);
+      case 32: return launch_tree_put_n<OP, T, 32>(a, cnt, vec, head, s);
       default: return -LFA_EINVAL;
     }
   }
@@ -776,6 +964,16 @@ extern "C" int LFA_CAT(lfa__tree_op, LFA_OP)(int dt, void *dst,
     typedef typename std::remove_pointer<decltype(tag)>::type T;
     return lfa::launch_tree<LFA_OP, T>(dst, srcs, nsrc, cnt,
                                        (hipStream_t)stream);
+  });
+}
+
+extern "C" int LFA_CAT(lfa__treeput_op, LFA_OP)(int dt, void *const *dsts, int ndst,
+                                                const void *const *srcs, int nsrc,
+                                                size_t cnt, void *stream) {
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_tree_put<LFA_OP, T>(dsts, ndst, srcs, nsrc, cnt,
+                                           (hipStream_t)stream);
   });
 }
 #endif

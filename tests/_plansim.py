@@ -11,7 +11,8 @@ import numpy as np
 import oracle
 from libfabric_amd import coll
 
-SEND, RECV, GEND, REDUCE, TREE, COPY, ALLTOALL, ALLGATHER = range(8)
+SEND, RECV, GEND, REDUCE, TREE, COPY, ALLTOALL, ALLGATHER, BARRIER, TREE_PUT = range(10)
+SYM_IN, SYM_OUT = 3, 4
 
 
 def lower(steps, r, n):
@@ -44,6 +45,14 @@ def lower(steps, r, n):
 
 
 def _view(bufs, ref, nbytes):
+    """ref = (buf, off) into this rank's buffers, or (SYM_IN|SYM_OUT, off,
+    owner) into group rank `owner`'s symmetric workspace (bufs["sym"])."""
+    if len(ref) == 3:
+        b, off, k = ref
+        sym, region = bufs["sym"]
+        if b == SYM_OUT:
+            off += region
+        return sym[k][off:off + nbytes]
     b, off = ref
     return bufs[b][off:off + nbytes]
 
@@ -55,12 +64,17 @@ def run(coll_op, algo, n, root, dt, op, count, sends, results):
     plans = [coll.plan(coll_op, algo, r, n, root, count, esz) for r in range(n)]
     for r in range(n):
         plans[r].steps = lower(plans[r].steps, r, n)
+    region = (count * esz + 255) // 256 * 256
+    # symmetric workspaces (LFA_ALGO_P2P), poisoned so stale reads show
+    sym = [np.full(2 * region, 0xA5, np.uint8) for _ in range(n)]
     bufs = []
     for r in range(n):
         tmp = np.zeros(plans[r].tmp_bytes, np.uint8)
         send = sends[r] if coll_op != 1 else results[r]   # broadcast: in/out
-        bufs.append({0: send, 1: results[r], 2: tmp})
+        bufs.append({0: send, 1: results[r], 2: tmp, "sym": (sym, region)})
     pc = [0] * n
+    arrived = [0] * n          # barriers reached
+    waiting = [False] * n
     box = {}
     posted = [set() for _ in range(n)]
     while True:
@@ -69,6 +83,17 @@ def run(coll_op, algo, n, root, dt, op, count, sends, results):
             st = plans[r].steps
             while pc[r] < len(st):
                 s = st[pc[r]]
+                if s["type"] == BARRIER:
+                    if not waiting[r]:
+                        waiting[r] = True
+                        arrived[r] += 1
+                        progressed = True
+                    if min(arrived) < arrived[r]:
+                        break
+                    waiting[r] = False
+                    pc[r] += 1
+                    progressed = True
+                    continue
                 if s["type"] not in (SEND, RECV, GEND):
                     if s["type"] == REDUCE:
                         d = _view(bufs[r], s["dst"], s["count"] * esz).view(nd)
@@ -78,11 +103,17 @@ def run(coll_op, algo, n, root, dt, op, count, sends, results):
                         src = _view(bufs[r], s["src"], s["count"]).copy()
                         _view(bufs[r], s["dst"], s["count"])[:] = src
                     else:
-                        ins = [_view(bufs[r], plans[r].refs[s["first"] + k],
-                                     s["count"] * esz).view(nd).copy()
+                        nb = s["count"] * esz
+                        refs = plans[r].refs
+                        ins = [_view(bufs[r], refs[s["first"] + k], nb).view(nd).copy()
                                for k in range(s["nsrc"])]
-                        out = oracle.allreduce(op, dt, ins)[0]
-                        _view(bufs[r], s["dst"], s["count"] * esz)[:] = out.view(np.uint8)
+                        out = oracle.allreduce(op, dt, ins)[0].view(np.uint8)
+                        dsts = [s["dst"]]
+                        if s["type"] == TREE_PUT:
+                            base = s["first"] + s["nsrc"]
+                            dsts += [refs[base + j] for j in range(s["peer"])]
+                        for d in dsts:
+                            _view(bufs[r], d, nb)[:] = out
                     pc[r] += 1
                     progressed = True
                     continue

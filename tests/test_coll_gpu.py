@@ -45,7 +45,7 @@ def _dev(a):
 CASES = [(8, 2), (9, 3), (6, 0), (6, 6), (1, 7), (4, 9), (8, 1)]
 
 
-@pytest.mark.parametrize("algo", [0, 1, 3])
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 def test_loopback_allreduce(coll, algo, n):
     for dt, op in CASES:
@@ -61,7 +61,7 @@ def test_loopback_allreduce(coll, algo, n):
                 assert_parity(dt, rd[r].cpu().numpy(), want, f"n={n} dt={dt} op={op} r={r}")
 
 
-@pytest.mark.parametrize("algo", [0, 1, 3])
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
 @pytest.mark.parametrize("n", [2, 3, 8])
 @pytest.mark.parametrize("count", [50_001, 48_000])
 def test_loopback_reduce_scatter_and_reduce(coll, algo, n, count):
@@ -85,7 +85,7 @@ def test_loopback_reduce_scatter_and_reduce(coll, algo, n, count):
     assert_parity(dt, rd[root].cpu().numpy(), want, "reduce root")
 
 
-@pytest.mark.parametrize("algo", [0, 1, 3])
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
 def test_loopback_skewed_blocks(coll, algo):
     """Blocks >= 1 MiB: TMP holds them 6 KiB-skewed; results
     stay bit-exact with prov/coll (ragged count, so TREE_COLL falls back)."""
@@ -270,3 +270,55 @@ def test_errors_and_query(coll, ep):
     assert ep.query(8, 2, 8)[0] == -38              # GATHER
     assert ep.query(0, 256, 256)[0] == 0            # BARRIER
     assert ep.query(5, 2, 8)[0] == 0                # REDUCE_SCATTER (new here)
+
+
+def test_p2p_kernel_on_ipc_mapped_memory(coll):
+    """LFA_ALGO_P2P's data path across processes: a child process maps this
+    process's hipMalloc'd buffer with hipIpcOpenMemHandle and runs the P2P
+    kernel on it — N inputs read from and N-1 outputs written into the
+    mapping (on one GPU the mapping is same-device; on the 8-GPU node the
+    provider maps peers over xGMI the same way).  Outputs == prov/coll's
+    tree, bit-exact."""
+    import ctypes
+    import os
+    import subprocess
+    import sys
+    from libfabric_amd import _native
+    L = _native.lib()
+    nsrc, ndst, count, dt, op = 8, 7, 300_007, 8, 2
+    stride = (count * 4 + 4095) // 4096 * 4096
+    out_off = nsrc * stride
+    total = out_off + ndst * stride
+    sends = _inputs(dt, nsrc, count, 4242)
+    want = oracle.allreduce(op, dt, sends)[0]
+
+    class IpcHandle(ctypes.Structure):
+        _fields_ = [("reserved", ctypes.c_char * 64)]
+
+    base = ctypes.c_void_p()
+    assert L.hipMalloc(ctypes.byref(base), ctypes.c_size_t(total)) == 0
+    try:
+        L.hipMemset(base, 0, ctypes.c_size_t(total))
+        for k, x in enumerate(sends):
+            assert L.hipMemcpy(ctypes.c_void_p(base.value + k * stride),
+                               x.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.c_size_t(count * 4), 1) == 0   # H2D
+        assert L.hipDeviceSynchronize() == 0
+        h = IpcHandle()
+        L.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(IpcHandle), ctypes.c_void_p]
+        assert L.hipIpcGetMemHandle(ctypes.byref(h), base) == 0
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        r = subprocess.run([sys.executable, os.path.join(root, "tests", "_ipc_child.py"),
+                            bytes(h).hex(), str(nsrc), str(ndst), str(count), str(dt),
+                            str(op), str(stride), str(out_off)],
+                           cwd=root, capture_output=True, text=True, timeout=180,
+                           env=dict(os.environ, PYTHONPATH=root))
+        assert r.returncode == 0, r.stdout + r.stderr
+        out = np.zeros(count, np.float32)
+        for j in range(ndst):
+            assert L.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.c_void_p(base.value + out_off + j * stride),
+                               ctypes.c_size_t(count * 4), 2) == 0   # D2H
+            assert_parity(dt, out, want, f"ipc out{j}")
+    finally:
+        L.hipFree(base)

@@ -31,7 +31,10 @@ NS = [1, 2, 3, 4, 5, 7, 8]
 COUNTS = [0, 1, 5, 1000, 70_001]
 
 
-@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL])
+ALGOS = [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL, coll.ALGO_P2P]
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("n", NS)
 @pytest.mark.parametrize("count", COUNTS + [8 * 9000])
 def test_allreduce_schedule(algo, n, count):
@@ -45,7 +48,7 @@ def test_allreduce_schedule(algo, n, count):
             assert res[r].tobytes() == want.view(np.uint8).tobytes(), (r, dt)
 
 
-@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL])
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("n", NS)
 @pytest.mark.parametrize("count", COUNTS + [8 * 9000])
 def test_reduce_scatter_schedule(algo, n, count):
@@ -63,7 +66,7 @@ def test_reduce_scatter_schedule(algo, n, count):
         assert res[r].tobytes() == full[off:off + ln].tobytes()
 
 
-@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD])
+@pytest.mark.parametrize("algo", [coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_P2P])
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
 def test_reduce_schedule(algo, n):
     dt, op, count = U8, BAND, 4099
@@ -115,6 +118,48 @@ def test_tree_coll_uses_rccl_collectives_when_even():
     assert kinds == [6, 4, 7]          # ALLTOALL, TREE, ALLGATHER
     p = coll.plan(ALLREDUCE, coll.ALGO_TREE_COLL, 2, 8, -1, 8 * 1_000_000 + 1, 4)
     assert 6 not in [s["type"] for s in p.steps]   # ragged: grouped p2p
+
+
+def test_p2p_schedule_shape():
+    """LFA_ALGO_P2P allreduce, big path: stage the N-1 foreign blocks,
+    barrier, ONE tree over every rank's SYM_IN pushing its result into all
+    N-1 peers' SYM_OUT, barrier, copy the gathered blocks out.  Bytes staged
+    in and out are (N-1)/N·S each; no RCCL data transfers at all."""
+    n, count, esz, r = 8, 8 * 1_000_000, 4, 3
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, r, n, -1, count, esz)
+    kinds = [s["type"] for s in p.steps]
+    assert kinds == [coll.STEP_COPY, coll.STEP_COPY, coll.STEP_BARRIER,
+                     coll.STEP_TREE_PUT, coll.STEP_BARRIER,
+                     coll.STEP_COPY, coll.STEP_COPY]
+    assert p.tmp_bytes == 0
+    copies = [s for s in p.steps if s["type"] == coll.STEP_COPY]
+    assert sum(c["count"] for c in copies[:2]) == (n - 1) * count * esz // n
+    assert sum(c["count"] for c in copies[2:]) == (n - 1) * count * esz // n
+    t = p.steps[3]
+    assert t["nsrc"] == n and t["peer"] == n - 1
+    off, ln = coll.block(count, n, r)
+    ins = p.refs[t["first"]:t["first"] + n]
+    outs = p.refs[t["first"] + n:t["first"] + n + n - 1]
+    assert ins[r] == (coll.BUF_SEND, off * esz)            # own block in place
+    assert all(ins[k] == (coll.BUF_SYM_IN, off * esz, k) for k in range(n) if k != r)
+    assert sorted(o[2] for o in outs) == [k for k in range(n) if k != r]
+    assert all(o[:2] == (coll.BUF_SYM_OUT, off * esz) for o in outs)
+    assert t["dst"] == (coll.BUF_RESULT, off * esz)
+    # reduce_scatter: one tree into the result, closing barrier, no pushes
+    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, r, n, -1, count, esz)
+    assert [s["type"] for s in p.steps][-2:] == [coll.STEP_TREE_PUT, coll.STEP_BARRIER]
+    assert p.steps[-2]["peer"] == 0
+    # transport-only collectives keep the RCCL schedules
+    p = coll.plan(ALLGATHER, coll.ALGO_P2P, r, n, -1, 100, 8)
+    assert coll.STEP_BARRIER not in [s["type"] for s in p.steps]
+
+
+def test_p2p_small_allreduce_is_one_phase():
+    n, count = 4, 1000
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 1, n, -1, count, 4)
+    assert [s["type"] for s in p.steps] == [coll.STEP_COPY, coll.STEP_BARRIER,
+                                            coll.STEP_TREE_PUT, coll.STEP_BARRIER]
+    assert p.steps[2]["count"] == count and p.steps[2]["peer"] == 0
 
 
 def test_plan_errors():

@@ -209,6 +209,64 @@ def test_tree_misaligned_and_minmax_zero_sign(lfa):
     assert_parity(dt, out.cpu().numpy()[1:], want, "tree min zeros")
 
 
+def test_tree_put_fixtures_every_output(lfa, manifest, golden_dir):
+    """The LFA_ALGO_P2P kernel (system-scope loads/stores, fan-out): every
+    output == prov/coll's recursive-doubling result, all fixture ops."""
+    for case in manifest["allreduce"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        srcs = [torch.from_numpy(x.copy()).to(DEV) for x in z["sends"]]
+        outs = [torch.full_like(srcs[0], 7) for _ in range(3)]
+        lfa.reduce_tree_put(case["op"], case["dt"], outs, srcs)
+        torch.cuda.synchronize()
+        for j, o in enumerate(outs):
+            assert_parity(case["dt"], o.cpu().numpy(), z["out"], f"{case['file']} out{j}")
+
+
+@pytest.mark.parametrize("nsrc,ndst", [(1, 1), (2, 1), (3, 2), (5, 4), (8, 7), (8, 1),
+                                       (9, 8), (16, 15), (32, 32)])
+@pytest.mark.parametrize("dt", [8, 6, 9, 10, 14, 1])
+def test_tree_put_vs_oracle(lfa, nsrc, ndst, dt):
+    """Ragged count (partial last tile: the buffer-descriptor bounds drop the
+    out-of-range lanes), misaligned head, every datatype width 1..16 B."""
+    op = 3 if dt in (8, 9, 10) else 2
+    esz = oracle.datatype_size(dt)
+    n = 5_003
+    sends = [np.random.default_rng(nsrc * 31 + k).integers(0, 256, (n + 2) * esz,
+                                                           dtype=np.uint8)
+             for k in range(nsrc)]
+    if dt in (8, 9, 10):  # keep PROD finite and meaningful
+        nd = oracle.DT_NP[dt]
+        sends = [np.random.default_rng(k).uniform(0.9, 1.1, (n + 2) * esz // nd.itemsize)
+                 .astype(nd).view(np.uint8) for k in range(nsrc)]
+    want = oracle.allreduce(op, dt, [s[esz:(n + 1) * esz].view(oracle.DT_NP[dt]).copy()
+                                     for s in sends])[0]
+    srcs = [torch.from_numpy(s).to(DEV) for s in sends]
+    outs = [torch.zeros((n + 2) * esz, dtype=torch.uint8, device=DEV) for _ in range(ndst)]
+    import ctypes
+    from libfabric_amd import _native
+    sa = (ctypes.c_void_p * nsrc)(*[t.data_ptr() + esz for t in srcs])
+    da = (ctypes.c_void_p * ndst)(*[t.data_ptr() + esz for t in outs])
+    assert _native.lib().lfa_reduce_tree_put_async(op, dt, da, ndst, sa, nsrc, n, None) == 0
+    torch.cuda.synchronize()
+    for j, o in enumerate(outs):
+        o = o.cpu().numpy()
+        assert_parity(dt, o[esz:(n + 1) * esz], want, f"out{j}")
+        assert not o[:esz].any() and not o[(n + 1) * esz:].any(), "wrote outside [0, n)"
+
+
+def test_tree_put_errors(lfa):
+    import ctypes
+    from libfabric_amd import _native
+    L = _native.lib()
+    x = torch.zeros(64, dtype=torch.float32, device=DEV)
+    one = (ctypes.c_void_p * 1)(x.data_ptr())
+    assert L.lfa_reduce_tree_put_async(6, 8, one, 1, one, 1, 16, None) == -95  # BOR float
+    assert L.lfa_reduce_tree_put_async(2, 8, one, 0, one, 1, 16, None) == -22  # no outputs
+    assert L.lfa_reduce_tree_put_async(2, 8, one, 33, one, 1, 16, None) == -22
+    odd = (ctypes.c_void_p * 1)(x.data_ptr() + 2)
+    assert L.lfa_reduce_tree_put_async(2, 8, odd, 1, one, 1, 4, None) == -22  # element-misaligned
+
+
 # ----------------------------------------------- fetch / compare tables ----
 
 def test_readwrite_fixtures(lfa, manifest, golden_dir):
