@@ -227,6 +227,34 @@ def extra_tree(dev, stream, nsrc=8):
             "achieved_gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
 
 
+def extra_tree_put(dev, stream, nsrc=8):
+    """The LFA_ALGO_P2P kernel on local HBM: 8 x 32 MiB float blocks -> 1
+    and -> 8 outputs, system-scope (sc0 sc1) loads and stores.  Traffic
+    (nsrc + ndst)·B per launch.  On the 8-GPU node 7 of the inputs and 7 of
+    the outputs are peers' HBM over xGMI instead."""
+    from libfabric_amd import atomic
+    blk = 32 * 1024 * 1024 // 4
+    out = {}
+    for ndst in (1, 8):
+        sets = []
+        for k in range(2):
+            srcs = [torch.rand(blk, device=dev) for _ in range(nsrc)]
+            sets.append((srcs, [torch.empty(blk, device=dev) for _ in range(ndst)]))
+
+        def fn(i):
+            srcs, dsts = sets[i % 2]
+            atomic.reduce_tree_put(2, 8, dsts, srcs, blk, stream)
+        for i in range(4):
+            fn(i)
+        ms = _kernel_events(fn, 20, stream)
+        gbps = (nsrc + ndst) * blk * 4 / (ms * 1e-3) / 1e9
+        out[f"{nsrc}to{ndst}"] = {"kernel_us": round(ms * 1e3, 2),
+                                  "achieved_gbs": round(gbps, 1),
+                                  "frac": round(gbps / PEAK_GBPS, 4)}
+        del sets
+    return out
+
+
 def extra_e2e_host(dev, stream, reps=5):
     """The same 256 MiB float SUM combine when the buffers start and end in
     pinned host memory (what a libfabric caller hands over): H2D dst and src,
@@ -619,6 +647,7 @@ def main() -> None:
     ap.add_argument("--tune-tree-layout", action="store_true")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
+    ap.add_argument("--only-extra", default="", help="run one extra (dev): tree_put")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
@@ -636,6 +665,11 @@ def main() -> None:
         return
     if args.sweep_ops:
         sweep_ops(args)
+        return
+    if args.only_extra == "tree_put":
+        torch.cuda.set_device(0)
+        print(json.dumps({"tree_put": extra_tree_put(torch.device("cuda", 0),
+                                                     torch.cuda.current_stream())}))
         return
 
     rank, world, local = init_dist(args.gpus)
@@ -754,6 +788,7 @@ def main() -> None:
             if world == 1:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
+                ex["tree8_put_p2p_kernel_local"] = extra_tree_put(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
                 ex["e2e_host_staged_float_sum_256mib"] = extra_e2e_staged()
             if world > 1 or not args.no_extras_coll:

@@ -25,9 +25,25 @@ def _free_port():
     return p
 
 
-def _exec_plan(pl, bufs, op, dt, esz, nd, seq):
+def _view(bufs, ref, nbytes):
+    """(buf, off) into this rank's buffers, or (SYM_IN|SYM_OUT, off, owner)
+    into group rank `owner`'s symmetric workspace — a shared-memory mapping
+    here, as the provider maps peers' HBM over IPC."""
+    if len(ref) == 3:
+        b, off, k = ref
+        sym, region = bufs["sym"]
+        off += region if b == 4 else 0
+        return sym[k][off:off + nbytes]
+    b, off = ref
+    return bufs[b][off:off + nbytes]
+
+
+def _exec_plan(pl, bufs, op, dt, esz, nd, seq, jitter=None):
     """seq: per-(direction, peer) message counters — messages between a pair
-    match FIFO, as RCCL's do, whatever group structure each rank has."""
+    match FIFO, as RCCL's do, whatever group structure each rank has.
+    BARRIER = dist.barrier(); `jitter` (rng) delays this rank at random
+    points, so a missing barrier shows up as a data race."""
+    import time
     import oracle
     from tests._plansim import lower
     st = lower(pl.steps, dist.get_rank(), dist.get_world_size())
@@ -56,23 +72,28 @@ def _exec_plan(pl, bufs, op, dt, esz, nd, seq):
                 bufs[b][off:off + n] = t.numpy()
             i += 1  # GROUP_END
             continue
-        if s["type"] == 3:
+        if jitter is not None and jitter.random() < 0.3:
+            time.sleep(jitter.random() * 0.02)
+        if s["type"] == 8:
+            dist.barrier()
+        elif s["type"] == 3:
             b, off = s["dst"]
             d = bufs[b][off:off + s["count"] * esz].view(nd)
             sb, so = s["src"]
             oracle.write(op, dt, d, bufs[sb][so:so + s["count"] * esz].copy().view(nd))
         elif s["type"] == 5:
-            sb, so = s["src"]
-            b, off = s["dst"]
-            bufs[b][off:off + s["count"]] = bufs[sb][so:so + s["count"]].copy()
-        elif s["type"] == 4:
-            ins = []
-            for k in range(s["nsrc"]):
-                rb, ro = pl.refs[s["first"] + k]
-                ins.append(bufs[rb][ro:ro + s["count"] * esz].copy().view(nd))
-            out = oracle.allreduce(op, dt, ins)[0]
-            b, off = s["dst"]
-            bufs[b][off:off + s["count"] * esz] = out.view(np.uint8)
+            _view(bufs, s["dst"], s["count"])[:] = _view(bufs, s["src"], s["count"]).copy()
+        elif s["type"] in (4, 9):
+            nb = s["count"] * esz
+            ins = [_view(bufs, pl.refs[s["first"] + k], nb).copy().view(nd)
+                   for k in range(s["nsrc"])]
+            out = oracle.allreduce(op, dt, ins)[0].view(np.uint8)
+            dsts = [s["dst"]]
+            if s["type"] == 9:
+                base = s["first"] + s["nsrc"]
+                dsts += [pl.refs[base + j] for j in range(s["peer"])]
+            for d in dsts:
+                _view(bufs, d, nb)[:] = out
         i += 1
 
 
@@ -136,6 +157,82 @@ def test_schedules_across_gloo_processes(world):
     results = {}
     for _ in range(world):
         r, msg = q.get(timeout=150)
+        results[r] = msg
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert results[r] == "ok", results[r]
+
+
+SYM_BYTES = 4 << 20
+
+
+def _p2p_worker(rank, world, port, q, shm):
+    """LFA_ALGO_P2P schedules across processes: every rank's symmetric
+    workspace is a shared-memory file all ranks map; BARRIER is a gloo
+    barrier; ranks are delayed at random points and run many operations
+    back to back, so a schedule whose barriers did not fence the workspace
+    (a rank restaging while a peer still reads) would corrupt results."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from libfabric_amd import coll
+        sym = [np.memmap(f"{shm}.{k}", dtype=np.uint8, mode="r+", shape=(SYM_BYTES,))
+               for k in range(world)]
+        jitter = np.random.default_rng(rank + 17)
+        seq = {}
+        for rep in range(3):
+            for dt, op, count in ((8, 2, 70_001), (8, 2, 1000), (6, 0, 5), (1, 7, 3),
+                                  (9, 3, 4099), (8, 2, 6 * 20_000), (6, 6, 100_000)):
+                nd = oracle.DT_NP[dt]
+                esz = nd.itemsize
+                region = (count * esz + 255) // 256 * 256
+                assert 2 * region <= SYM_BYTES
+                for coll_op, root in ((3, -1), (5, -1), (6, (rep + count) % world)):
+                    # fresh inputs per operation: a rank restaging early
+                    # would change bytes a peer is still reading
+                    rng = np.random.default_rng(1234 + rep * 7 + count + coll_op)
+                    allsends = [(rng.uniform(0.9, 1.1, count) if nd.kind == "f" else
+                                 rng.integers(0, 255, count)).astype(nd)
+                                for _ in range(world)]
+                    want = oracle.allreduce(op, dt, allsends)[0]
+                    off, ln = coll.block(count, world, rank)
+                    pl = coll.plan(coll_op, coll.ALGO_P2P, rank, world, root, count, esz)
+                    nres = ln if coll_op == 5 else count
+                    bufs = {0: allsends[rank].view(np.uint8).copy(),
+                            1: np.zeros(nres * esz, np.uint8),
+                            2: np.zeros(pl.tmp_bytes, np.uint8), "sym": (sym, region)}
+                    _exec_plan(pl, bufs, op, dt, esz, nd, seq, jitter)
+                    if coll_op == 3 or (coll_op == 6 and rank == root):
+                        assert bufs[1].tobytes() == want.view(np.uint8).tobytes(), \
+                            f"p2p coll={coll_op} dt={dt} count={count} rep={rep}"
+                    elif coll_op == 5:
+                        assert bufs[1].tobytes() == want[off:off + ln].view(np.uint8).tobytes()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_schedules_across_gloo_processes(world, tmp_path):
+    shm = str(tmp_path / "sym")
+    for k in range(world):
+        with open(f"{shm}.{k}", "wb") as f:
+            f.truncate(SYM_BYTES)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, world, port, q, shm))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, msg = q.get(timeout=240)
         results[r] = msg
     for p in procs:
         p.join(timeout=60)
