@@ -1021,7 +1021,7 @@ static int olfa_ep_setopt(fid_t fid, int level, int optname, const void *optval,
 			if (ret)
 				return ret;
 		} else if (*(const int *)optval < LFA_ALGO_TREE ||
-			   *(const int *)optval > LFA_ALGO_TREE_COLL) {
+			   *(const int *)optval > LFA_ALGO_P2P) {
 			return -FI_EINVAL;
 		}
 		ep->algo = *(const int *)optval;
