@@ -13,7 +13,7 @@ N > 1  : one process per GPU, each rank combines its own 256 MiB buckets (the
          bucket reduction shards with no data-path exchange): weak scaling.
 
 Extra objects on the JSON line:
-  roofline      dominant kernel (combine_vec<SUM,float>): algorithmic bytes per
+  roofline      dominant kernel (combine_lds<SUM,float>): algorithmic bytes per
                 launch (3·S) ÷ its average duration from HIP events on the
                 launch stream; peak 8.0 TB/s (MI355X HBM3E spec); ``traffic``
                 from the committed rocprofv3 PMC pass (profiles/) when present.
@@ -169,15 +169,17 @@ def cpu_baseline(sample_reps: int = 5):
 # ------------------------------------------------------------------ extras --
 
 def _kernel_events(fn, reps, stream):
-    """Mean per-launch duration (ms) of fn(i) from HIP events on `stream`."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(reps)]
-    for i, (a, b) in enumerate(evs):
-        a.record(stream)
-        fn(i)
-        b.record(stream)
+    """Mean per-launch duration (ms) of fn(i): one HIP event pair on `stream`
+    around `reps` back-to-back launches, as for the headline (an event pair
+    per launch adds its own gap: +2.5 us on a 31 us kernel)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    return statistics.mean(a.elapsed_time(b) for a, b in evs)
+    a.record(stream)
+    for i in range(reps):
+        fn(i)
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
 
 
 def extra_config3(dev, stream):
@@ -752,13 +754,15 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "combine_lds<FI_SUM,float,U=4> (LDS-DMA staged, nt)",
+            "kernel": "combine_lds<FI_SUM,float,U=4,nt> (LDS-DMA staged, nt stores at "
+                      ">= 192 MiB)",
             "kernel_us": round(kern_ms * 1e3, 2),
             "kernel_us_isolated_median": round(kern_med * 1e3, 2),
             "timing": "HIP event pair around the timed region on the launch stream, "
                       "divided by steps (includes inter-kernel dispatch gaps); "
                       "isolated per-launch event median beside it; rocprofv3 "
-                      "kernel-trace mean 122.5 us for the same kernel",
+                      "kernel-trace mean 121.2 us for the same kernel "
+                      "(profiles/r01_rocprof_headline_kernel_stats.csv)",
             "algorithmic_bytes_per_launch": 3 * S_BYTES,
             "traffic_source": traffic_src,
         },

@@ -110,7 +110,15 @@ __global__ __launch_bounds__(kBlock) void combine_vec(
 typedef __attribute__((address_space(3))) void lds_void;
 constexpr int kLdsWaves = 4;
 
-template <int OP, typename T, int U>
+// Store cache policy of the body (gfx950 cpol bits): nt keeps the line in
+// the XCD's L2 for the end-of-kernel writeback; sc1 writes through.  sc1 is
+// 1.6-6.7 % faster per launch from 16 to 128 MiB per operand and level at
+// 256 MiB (rocprofv3 kernel durations, profiles/r01_rocprof_store_policy.csv),
+// so launches below kSc1Bytes write through.
+constexpr int kStoreNt = 2, kStoreSc1 = 16;
+constexpr size_t kSc1Bytes = (size_t)192 << 20;
+
+template <int OP, typename T, int U, int SAUX>
 __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
     u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
   __shared__ u32x4 lds[2][kLdsWaves][U][64];
@@ -130,13 +138,20 @@ __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
       __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
                                        (lds_void *)&lds[1][w][u][0], 16, 0, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // sc1: the wave's tile through one buffer descriptor whose stores carry
+    // the bits; nt: plain global stores (0.5 % faster than the buffer form
+    // at 256 MiB in rocprofv3)
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      if constexpr (OP == OP_WRITE)
-        st<true>(dst + base + u * 64 + l, lds[1][w][u][l]);
+      u32x4 v;
+      if constexpr (OP == OP_WRITE) v = lds[1][w][u][l];
+      else v = apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == kStoreNt)
+        st<true>(dst + base + u * 64 + l, v);
       else
-        st<true>(dst + base + u * 64 + l,
-                 apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]));
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
     }
   } else {
     for (int u = 0; u < U; u++) {
@@ -617,10 +632,13 @@ static int launch_write(void *dst, const void *src, size_t cnt,
       if (nvec) {
         u32x4 *d = (u32x4 *)((char *)dst + head * E);
         const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
-        hipLaunchKernelGGL((combine_lds<OP, T, kUnroll>),
-                           dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll,
-                                         0x7fffffffu)),
-                           dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+        const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll, 0x7fffffffu));
+        if (nvec * 16 < kSc1Bytes)
+          hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreSc1>), grid,
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+        else
+          hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreNt>), grid,
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec);
       }
       if (head + tail)
         hipLaunchKernelGGL((combine_elem<OP, T>),
