@@ -520,7 +520,7 @@ def tune_tree(args) -> None:
             srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
             sets.append((srcs, torch.empty(blk, device="cuda"),
                          (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs])))
-        variants = [0, 1, 2, 3, 4, 5, 6, 7, 8, -1]
+        variants = [int(x) for x in args.variants.split(",")] if args.variants else [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, -1]
         ref = None
         for v in variants:  # correctness: every form equals the product's bits
             srcs, out, arr = sets[0]

@@ -291,7 +291,8 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_vec(TreeArgs a,
 
 // Chunked register form: workgroup b owns [b·kBlock·U, (b+1)·kBlock·U),
 // every input read with nt loads (U·nsrc 16-B loads in flight per lane).
-template <int OP, typename T, int NLEAF, int U>
+// SAUX = kStoreSc1: the result is written through (buffer stores, sc1).
+template <int OP, typename T, int NLEAF, int U, int SAUX = kStoreNt>
 __global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
                                                             u32x4 *dst,
                                                             size_t nvec) {
@@ -299,10 +300,18 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
 #pragma unroll
   for (int u = 0; u < U; u++) {
     size_t i = base + (size_t)u * kBlock;
-    if (i < nvec)
-      st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
-                 return ld<true>((const u32x4 *)a.in[k] + i);
-               }));
+    if (i < nvec) {
+      u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(
+          a, [&](int k) { return ld<true>((const u32x4 *)a.in[k] + i); });
+      if constexpr (SAUX == kStoreNt) {
+        st<true>(dst + i, v);
+      } else {
+        const size_t wb = i - threadIdx.x % 64;  // the wave's first vector
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, __builtin_amdgcn_make_buffer_rsrc(dst + wb, 0, 64 * 16, 0x00020000),
+            (threadIdx.x % 64) * 16, 0, SAUX);
+      }
+    }
   }
 }
 
@@ -669,7 +678,18 @@ static void launch_tree_lds(const TreeArgs &b, int nsrc, u32x4 *dst,
 template <int OP, typename T, int NLEAF>
 static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                              size_t nvec, hipStream_t s, int variant = -1) {
+  // Product choice (bench.py --tune-tree, profiles/r01_tune_tree_sc1.log):
+  // below kSc1Bytes of output the U=2 chunk form with write-through stores
+  // wins at every fan-in (2..16 inputs: 58.9/53.4/52.1/51.7 us against
+  // 63.2/58.2/53.9/51.7 for the nt-store forms, 256 MiB of inputs).
+  if (variant < 0 && nvec * 16 < kSc1Bytes) variant = 11;
   if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
+  if (variant == 11) {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+    return;
+  }
   if constexpr (OP == OP_SUM && __is_same(T, float)) {
     // tuning-only forms (bench.py --tune-tree), float SUM only
     switch (variant) {
@@ -684,6 +704,16 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
       case 8:
         hipLaunchKernelGGL((reduce_tree_wave<OP, T, NLEAF, 4>),
                            dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 9:
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 10:
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
                            dim3(kBlock), 0, s, b, dst, nvec);
         return;
       default: break;
