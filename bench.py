@@ -282,10 +282,10 @@ def extra_e2e_host(dev, stream, reps=5):
             "note": "pinned host buffers; 2x256 MiB H2D + combine + 256 MiB D2H, serial"}
 
 
-def extra_host_allreduce(ep, world, reps=3):
+def extra_host_allreduce(ep, world, reps=3, sweep=False):
     """fi_allreduce on HOST buffers (what a libfabric caller hands over):
-    the provider streams 64 MiB chunks H2D -> collective -> D2H on two HIP
-    streams.  Rate = buffer bytes / wall time, PCIe-inclusive."""
+    the provider streams 32 MiB chunks H2D -> collective -> D2H on three HIP
+    streams (both PCIe directions busy at once).  Rate = buffer bytes / wall time, PCIe-inclusive."""
     hx = torch.rand(COUNT).pin_memory()
     hy = torch.empty(COUNT).pin_memory()
     ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
@@ -296,9 +296,58 @@ def extra_host_allreduce(ep, world, reps=3):
         ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
         ts.append(max_over_ranks(time.perf_counter() - t0, world))
     t = statistics.median(ts)
-    return {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
-            "note": "pinned host in/out, 64 MiB chunks, H2D/D2H overlapped with the "
-                    "collective"}
+    by_chunk = {}
+    if sweep:
+        for mib in (8, 16, 32, 64, 128):
+            ep.set_chunk(mib << 20)
+            ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+            tc = []
+            for _ in range(reps):
+                barrier(world)
+                t0 = time.perf_counter()
+                ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+                tc.append(max_over_ranks(time.perf_counter() - t0, world))
+            by_chunk[str(mib)] = round(statistics.median(tc) * 1e3, 2)
+        ep.set_chunk(0)
+    row = {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
+           "note": "pinned host in/out, default chunks; H2D, collective and D2H on "
+                   "three streams"}
+    if by_chunk:
+        row["ms_by_chunk_mib"] = by_chunk
+    return row
+
+
+def extra_host_reduce_scatter(ep, rank, world, reps=3):
+    """fi_reduce_scatter on HOST buffers, double PROD, 256 MiB per rank: the
+    provider streams 32 MiB chunks (one 2-D H2D gathers chunk j of every
+    rank's block) through the device reduce_scatter, H2D/D2H overlapped.
+    Checked bitwise against the device-buffer result; the one-chunk
+    (serial-staging) time beside it."""
+    from libfabric_amd import coll
+    cnt = S_BYTES // 8
+    cnt -= cnt % world
+    off, ln = coll.block(cnt, world, rank)
+    g = torch.Generator().manual_seed(200 + rank)
+    hx = (torch.rand(cnt, generator=g, dtype=torch.float64) * 0.2 + 0.9).pin_memory()
+    hy = torch.zeros(ln, dtype=torch.float64).pin_memory()
+    dx = hx.to("cuda")
+    dy = torch.empty(ln, device="cuda", dtype=torch.float64)
+    ep.wait(ep.reduce_scatter(dx, dy, cnt, 9, 3))
+    ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
+    row = {"bitwise_equal_device": bool(torch.equal(hy, dy.cpu()))}
+    for name, chunk in (("ms", 0), ("one_chunk_ms", 1 << 40)):
+        ep.set_chunk(chunk)
+        ts = []
+        for _ in range(reps):
+            barrier(world)
+            t0 = time.perf_counter()
+            ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
+            ts.append(max_over_ranks(time.perf_counter() - t0, world))
+        row[name] = round(statistics.median(ts) * 1e3, 2)
+    ep.set_chunk(0)
+    row["buffer_gib_s"] = round(S_BYTES / (row["ms"] * 1e-3) / 2**30, 2)
+    row["note"] = "pinned host in/out; default 32 MiB chunks vs one chunk (serial staging)"
+    return row
 
 
 def cpu_model_allreduce(world: int):
@@ -413,6 +462,11 @@ def extra_collectives(rank, world, stream):
         del ref
         ep.set_algo(coll.ALGO_TREE)
         out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
+        try:
+            out["reduce_scatter_host_buffers_256mib"] = extra_host_reduce_scatter(
+                ep, rank, world)
+        except Exception as e:  # noqa: BLE001
+            out["reduce_scatter_host_buffers_256mib"] = {"error": f"{e}"[:200]}
         out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE)
         if world > 1:
             try:
@@ -649,7 +703,7 @@ def main() -> None:
     ap.add_argument("--tune-tree-layout", action="store_true")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
-    ap.add_argument("--only-extra", default="", help="run one extra (dev): tree_put")
+    ap.add_argument("--only-extra", default="", help="run one extra (dev): tree_put, host_rs")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
@@ -667,6 +721,16 @@ def main() -> None:
         return
     if args.sweep_ops:
         sweep_ops(args)
+        return
+    if args.only_extra == "host_rs":
+        from libfabric_amd import coll
+        torch.cuda.set_device(0)
+        ep = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+        try:
+            print(json.dumps({"host_rs": extra_host_reduce_scatter(ep, 0, 1),
+                              "host_allreduce": extra_host_allreduce(ep, 1, sweep=True)}))
+        finally:
+            ep.close()
         return
     if args.only_extra == "tree_put":
         torch.cuda.set_device(0)
@@ -802,6 +866,11 @@ def main() -> None:
         wd.cancel()
     _emit()
     if world > 1:
+        # The line is out; a peer stuck in a collective must not hold this
+        # rank in teardown past the driver's clock.
+        bye = threading.Timer(60.0, lambda: os._exit(0))
+        bye.daemon = True
+        bye.start()
         dist.destroy_process_group()
 
 

@@ -98,7 +98,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep);
 /* The endpoint's HIP stream (hipStream_t), for callers that order work. */
 void *lfa_coll_ep_stream(struct lfa_coll_ep *ep);
 int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo);
-/* Host-staging chunk size in bytes (0 = default 64 MiB). */
+/* Host-staging chunk size in bytes (0 = default 32 MiB). */
 int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
 
 /* ---- groups (fi_join_collective) -------------------------------------- */

@@ -43,7 +43,9 @@
 
 #define LFA_MAX_GROUP_ID 256            /* OFI_MAX_GROUP_ID, ofi_coll.h:44 */
 #define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
-#define LFA_DEFAULT_CHUNK (64u << 20)
+/* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
+ * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
+#define LFA_DEFAULT_CHUNK (32u << 20)
 #define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
 
 /* ====================================================================== */
@@ -857,7 +859,9 @@ struct lfa_coll_ep {
 	struct lfa_coll_domain *dom;
 	pthread_mutex_t lock;
 	hipStream_t stream;         /* executor stream (RCCL + kernels) */
-	hipStream_t copy_stream;    /* host staging copies */
+	hipStream_t copy_stream;    /* host staging copies, H2D */
+	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
+				     * PCIe direction runs concurrently) */
 	enum lfa_coll_algo algo;
 	size_t chunk;
 	void *ws;                   /* device workspace */
@@ -943,6 +947,8 @@ static void ep_release(struct lfa_coll_ep *ep)
 		hipHostFree(ep->barrier_host);
 	if (ep->copy_stream)
 		hipStreamDestroy(ep->copy_stream);
+	if (ep->d2h_stream)
+		hipStreamDestroy(ep->d2h_stream);
 	if (ep->stream)
 		hipStreamDestroy(ep->stream);
 	free(ep->q);
@@ -966,6 +972,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	ep->chunk = LFA_DEFAULT_CHUNK;
 	if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
 	    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipStreamCreateWithFlags(&ep->d2h_stream, hipStreamNonBlocking) != hipSuccess ||
 	    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
 	    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess) {
 		ep_release(ep);
@@ -1013,6 +1020,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	hipHostFree(ep->barrier_host);
 	hipStreamDestroy(ep->stream);
 	hipStreamDestroy(ep->copy_stream);
+	hipStreamDestroy(ep->d2h_stream);
 	pthread_mutex_destroy(&ep->lock);
 	free(ep);
 	return 0;
@@ -1286,7 +1294,8 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 	if (!ep)
 		return -LFA_EINVAL;
 	return hipStreamSynchronize(ep->stream) == hipSuccess &&
-	       hipStreamSynchronize(ep->copy_stream) == hipSuccess ? 0 : -LFA_EIO;
+	       hipStreamSynchronize(ep->copy_stream) == hipSuccess &&
+	       hipStreamSynchronize(ep->d2h_stream) == hipSuccess ? 0 : -LFA_EIO;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -1593,10 +1602,16 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 }
 
 /*
- * Host buffers: stream chunks through HBM.  Chunk c's H2D (copy stream)
- * overlaps chunk c-1's collective (executor stream) and its D2H; two staging
- * slots, ordered with events.  Valid for the element-wise collectives
- * (allreduce, broadcast), where chunks are independent.
+ * Host buffers: stream chunks through HBM on three streams: chunk c+1's H2D
+ * (copy stream), chunk c's collective (executor stream) and chunk c-1's D2H
+ * (d2h stream) run together, so both PCIe directions are busy at once; two
+ * staging slots, ordered with events.  Valid for the element-wise collectives
+ * (allreduce, reduce, broadcast), where chunks are independent, and for
+ * reduce_scatter with equal blocks (count % N == 0): chunk c holds elements
+ * [j, j+n) of EVERY rank's block (one 2-D H2D, height N), so the device
+ * reduce_scatter of those N·n elements hands rank r elements [j, j+n) of its
+ * own block.  Every element meets the same schedule as unchunked, so the
+ * result is bit-identical to the whole-buffer form.
  */
 static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			    enum lfa_collective_op coll, const void *buf,
@@ -1604,30 +1619,40 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			    enum lfa_datatype dt, enum lfa_op op)
 {
 	size_t esz = lfa_datatype_size(dt);
-	size_t per = ep->chunk / esz, off = 0, in_slot;
-	hipEvent_t h2d[2], done[2];
+	const int rs = coll == LFA_REDUCE_SCATTER;
+	const size_t nb = rs ? (size_t)mc->size : 1;  /* blocks per chunk */
+	const size_t span = count / nb;               /* elements per block */
+	size_t per = ep->chunk / esz / nb, off = 0, in_slot;
+	hipEvent_t h2d[2], comp[2], done[2];
 	int ret = 0, slot = 0;
+	const int out = coll != LFA_REDUCE || mc->rank == root;
 
 	if (!per)
 		per = 1;
-	if (per > count)
-		per = count;
+	if (per > span)
+		per = span;
 	/* the output half starts 256-byte aligned (vector body of the kernels) */
-	in_slot = (per * esz + 255) & ~(size_t)255;
+	in_slot = (nb * per * esz + 255) & ~(size_t)255;
 	if (grow_staging(ep, in_slot + per * esz))
 		return -LFA_ENOMEM;
 	for (int i = 0; i < 2; i++) {
 		hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming);
+		hipEventCreateWithFlags(&comp[i], hipEventDisableTiming);
 		hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
 		hipEventRecord(done[i], ep->stream);
 	}
-	while (off < count && !ret) {
-		size_t n = count - off < per ? count - off : per;
+	while (off < span && !ret) {
+		size_t n = span - off < per ? span - off : per;
 		char *din = ep->hs[slot], *dout = din + in_slot;
 
 		/* slot reuse: wait until chunk c-2's D2H finished */
 		hipStreamWaitEvent(ep->copy_stream, done[slot], 0);
-		if (coll != LFA_BROADCAST || mc->rank == root)
+		if (rs)
+			hipMemcpy2DAsync(din, n * esz,
+					 (const char *)buf + off * esz,
+					 span * esz, n * esz, nb,
+					 hipMemcpyDefault, ep->copy_stream);
+		else if (coll != LFA_BROADCAST || mc->rank == root)
 			hipMemcpyAsync(din, (const char *)buf + off * esz, n * esz,
 				       hipMemcpyDefault, ep->copy_stream);
 		hipEventRecord(h2d[slot], ep->copy_stream);
@@ -1636,14 +1661,16 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			ret = run_device(ep, mc, coll, din, din, n, root, dt, op,
 					 ep->stream);
 		else
-			ret = run_device(ep, mc, coll, din, dout, n, root, dt, op,
-					 ep->stream);
-		hipEventRecord(h2d[slot], ep->stream);
-		hipStreamWaitEvent(ep->copy_stream, h2d[slot], 0);
-		hipMemcpyAsync((char *)result + off * esz,
-			       coll == LFA_BROADCAST ? din : dout, n * esz,
-			       hipMemcpyDefault, ep->copy_stream);
-		hipEventRecord(done[slot], ep->copy_stream);
+			ret = run_device(ep, mc, coll, din, dout, nb * n, root,
+					 dt, op, ep->stream);
+		hipEventRecord(comp[slot], ep->stream);
+		hipStreamWaitEvent(ep->d2h_stream, comp[slot], 0);
+		if (out)
+			hipMemcpyAsync((char *)result + off * esz,
+				       coll == LFA_BROADCAST ? din : dout,
+				       n * esz, hipMemcpyDefault,
+				       ep->d2h_stream);
+		hipEventRecord(done[slot], ep->d2h_stream);
 		off += n;
 		slot ^= 1;
 	}
@@ -1651,6 +1678,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	hipStreamWaitEvent(ep->stream, done[slot ^ 1], 0);
 	for (int i = 0; i < 2; i++) {
 		hipEventDestroy(h2d[i]);
+		hipEventDestroy(comp[i]);
 		hipEventDestroy(done[i]);
 	}
 	return ret;
@@ -1737,7 +1765,9 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	} else if (!host) {
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
 				 ep->stream);
-	} else if (coll == LFA_ALLREDUCE || coll == LFA_BROADCAST) {
+	} else if (coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
+		   coll == LFA_REDUCE ||
+		   (coll == LFA_REDUCE_SCATTER && !(count % mc->size))) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op);
 	} else {

@@ -167,6 +167,30 @@ def test_rccl_allreduce_device_and_host(coll, ep):
     ep.set_chunk(0)
 
 
+def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
+    """reduce and reduce_scatter on host buffers go through the chunked
+    H2D / collective / D2H pipeline (reduce_scatter: one 2-D H2D per chunk);
+    ragged last chunks, an odd chunk size and mixed host/device operands."""
+    count = (1 << 20) + 37
+    rng = np.random.default_rng(7)
+    hx = rng.uniform(0.9, 1.1, count)
+    for chunk in (1 << 16, 3 * 8 * 1000 + 8, 0):
+        ep.set_chunk(chunk)
+        ho = np.zeros_like(hx)
+        ep.wait(ep.reduce_scatter(hx, ho, count, 9, 3))
+        assert np.array_equal(ho, hx)
+        ho[:] = 0
+        ep.wait(ep.reduce(hx, ho, count, 0, 9, 3))
+        assert np.array_equal(ho, hx)
+        d = torch.zeros(count, device=DEV, dtype=torch.float64)
+        ep.wait(ep.reduce_scatter(hx, d, count, 9, 3))
+        assert np.array_equal(d.cpu().numpy(), hx)
+        ho[:] = 0
+        ep.wait(ep.reduce_scatter(torch.from_numpy(hx).to(DEV), ho, count, 9, 3))
+        assert np.array_equal(ho, hx)
+    ep.set_chunk(0)
+
+
 def test_rccl_other_collectives(coll, ep):
     count = 10_000
     x = torch.arange(count, dtype=torch.int64, device=DEV)
