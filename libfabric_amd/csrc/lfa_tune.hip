@@ -130,6 +130,46 @@ __global__ __launch_bounds__(W * 64) void sum_ldsdma(u32x4 *__restrict__ dst,
 
 // Persistent LDS-DMA form: a grid sized to the resident capacity walks the
 // chunks in a grid-stride loop (fewer workgroup launches, one tail).
+// Workgroup-interleaved tiles: load u of wave w covers vectors
+// wg_base + (u·W + w)·64 + l, so the W waves' u-th loads are one contiguous
+// W KiB span (the product gives each wave U contiguous KiB instead).
+template <int W, int U, int SAUX>
+__global__ __launch_bounds__(W * 64) void sum_ldsdma_il(u32x4 *__restrict__ dst,
+                                                        const u32x4 *__restrict__ src,
+                                                        size_t nvec) {
+  __shared__ u32x4 lds[2][W][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t wg = (size_t)blockIdx.x * (W * 64 * U);
+  if (wg + W * 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + wg + (u * W + w) * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + wg + (u * W + w) * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u32x4 v = addf(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == 2) {
+        st<true>(dst + wg + (u * W + w) * 64 + l, v);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, __builtin_amdgcn_make_buffer_rsrc(dst + wg + (u * W + w) * 64, 0, 64 * 16,
+                                                 0x00020000),
+            l * 16, 0, SAUX);
+      }
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = wg + (size_t)(u * W + w) * 64 + l;
+      if (i < nvec) st<true>(dst + i, addf(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void sum_ldsdma_persist(u32x4 *__restrict__ dst,
                                                           const u32x4 *__restrict__ src,
@@ -343,6 +383,15 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
     case 54: LDSST(4, 19); break;  // sc0 sc1 nt
     case 55: LDSST(4, 0); break;   // plain
 #undef LDSST
+#define LDSIL(W, U, SAUX)                                                        \
+  hipLaunchKernelGGL((sum_ldsdma_il<W, U, SAUX>), dim3(blocks(nvec, W * 64 * U)),    \
+                     dim3(W * 64), 0, s, d, v, nvec)
+    // workgroup-interleaved tiles
+    case 60: LDSIL(4, 4, 2); break;
+    case 61: LDSIL(4, 4, 16); break;
+    case 62: LDSIL(8, 2, 2); break;
+    case 63: LDSIL(4, 2, 2); break;
+#undef LDSIL
     default: return -LFA_EINVAL;
   }
 #undef RUN
