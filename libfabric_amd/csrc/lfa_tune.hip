@@ -382,6 +382,10 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
     case 53: LDSST(4, 17); break;  // sc0 sc1
     case 54: LDSST(4, 19); break;  // sc0 sc1 nt
     case 55: LDSST(4, 0); break;   // plain
+    case 56: LDSST(4, 1); break;   // sc0
+    case 57: LDSST(4, 3); break;   // sc0 nt
+    case 58: LDSDMA(4, 4, 16, 0); break;  // loads sc1 only, nt global stores
+    case 59: LDSDMA(4, 4, 1, 0); break;   // loads sc0 only
 #undef LDSST
 #define LDSIL(W, U, SAUX)                                                        \
   hipLaunchKernelGGL((sum_ldsdma_il<W, U, SAUX>), dim3(blocks(nvec, W * 64 * U)),    \
