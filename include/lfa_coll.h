@@ -252,6 +252,24 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 void lfa_coll_block(size_t count, int nranks, int r, size_t *off, size_t *len);
 
 /*
+ * Host-buffer staging plan: chunk `idx` of a collective of `count` elements
+ * of `esz` bytes over `nranks`, staged `chunk_bytes` at a time (the geometry
+ * lfa_allreduce & co. use for host memory).  Chunk idx copies `height` rows
+ * of `width` bytes, `src_pitch` apart, from buf + src_off into a dense
+ * staging area, runs the device collective on `dev_count` elements of it and
+ * copies `width` bytes back to result + dst_off.  Returns 1 and fills *c for
+ * an existing chunk, 0 past the last one, -LFA_EINVAL for a collective the
+ * pipeline does not chunk (ragged reduce_scatter, allgather, scatter).
+ * Host-only, no GPU needed.
+ */
+struct lfa_host_chunk {
+	size_t src_off, src_pitch, width, height, dev_count, dst_off;
+};
+int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
+			size_t esz, size_t chunk_bytes, size_t idx,
+			struct lfa_host_chunk *c);
+
+/*
  * Single-GPU multi-rank execution of the schedules: runs the plans of all
  * `nranks` ranks on this device, matching every SEND with its RECV by a
  * device-to-device copy, with the real combine kernels.  send[r]/result[r]

@@ -4,6 +4,7 @@ The provider is C; this module only marshals arguments:
 
   plan(...)        lfa_coll_plan — a rank's schedule as data (host only)
   block(...)       lfa_coll_block — reduce_scatter block bounds
+  host_chunks(...) lfa_coll_host_chunk — host-buffer staging geometry
   loopback(...)    lfa_coll_loopback — all ranks' schedules on ONE GPU
   Endpoint         domain + endpoint over RCCL; fi_ops_collective calls
                    (allreduce, reduce_scatter, reduce, allgather, broadcast,
@@ -85,6 +86,9 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_plan.argtypes = [c_int, c_int, c_int, c_int, c_int, c_size_t,
                                 c_size_t, P(Step), P(c_size_t), P(Ref),
                                 P(c_size_t), P(c_size_t)]
+    L.lfa_coll_host_chunk.restype = c_int
+    L.lfa_coll_host_chunk.argtypes = [c_int, c_size_t, c_int, c_size_t, c_size_t,
+                                      c_size_t, P(HostChunk)]
     L.lfa_coll_block.restype = None
     L.lfa_coll_block.argtypes = [c_size_t, c_int, c_int, P(c_size_t), P(c_size_t)]
     L.lfa_coll_loopback.restype = c_int
@@ -150,6 +154,11 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+class HostChunk(ctypes.Structure):
+    _fields_ = [("src_off", c_size_t), ("src_pitch", c_size_t), ("width", c_size_t),
+                ("height", c_size_t), ("dev_count", c_size_t), ("dst_off", c_size_t)]
+
+
 class CollError(RuntimeError):
     def __init__(self, rc: int, what: str):
         super().__init__(f"{what} -> {rc}")
@@ -193,6 +202,23 @@ def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
                     "dst": tup(s.dst), "src": tup(s.src),
                     "first": s.first, "nsrc": s.nsrc})
     return Plan(out, [tup(r) for r in refs[:nr.value]], tmp.value)
+
+
+def host_chunks(coll: int, count: int, nranks: int, esz: int,
+                chunk_bytes: int) -> list[HostChunk]:
+    """lfa_coll_host_chunk for every chunk: the staging geometry the provider
+    uses for host-memory buffers."""
+    out, idx = [], 0
+    while True:
+        c = HostChunk()
+        rc = lib().lfa_coll_host_chunk(coll, count, nranks, esz, chunk_bytes, idx,
+                                       ctypes.byref(c))
+        if rc < 0:
+            raise CollError(rc, "lfa_coll_host_chunk")
+        if rc == 0:
+            return out
+        out.append(c)
+        idx += 1
 
 
 def block(count: int, nranks: int, r: int) -> tuple[int, int]:
@@ -401,5 +427,5 @@ def esz(dt: int) -> int:
     return SIZES[DT(dt)]
 
 
-__all__ = ["plan", "block", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
+__all__ = ["plan", "block", "host_chunks", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
            "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz"]

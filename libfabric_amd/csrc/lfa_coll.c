@@ -1601,6 +1601,37 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	return ret;
 }
 
+int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
+			size_t esz, size_t chunk_bytes, size_t idx,
+			struct lfa_host_chunk *c)
+{
+	const int rs = coll == LFA_REDUCE_SCATTER;
+	size_t nb, span, per, off;
+
+	if (!c || !esz || nranks < 1 ||
+	    !(coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
+	      coll == LFA_REDUCE || rs) ||
+	    (rs && count % (size_t)nranks))
+		return -LFA_EINVAL;
+	nb = rs ? (size_t)nranks : 1;       /* blocks gathered per chunk */
+	span = count / nb;                  /* elements per block */
+	per = chunk_bytes / esz / nb;
+	if (!per)
+		per = 1;
+	if (per > span)
+		per = span;
+	if (!per || idx >= (span + per - 1) / per)
+		return 0;
+	off = idx * per;
+	c->src_off = off * esz;
+	c->src_pitch = span * esz;
+	c->width = (span - off < per ? span - off : per) * esz;
+	c->height = nb;
+	c->dev_count = nb * (c->width / esz);
+	c->dst_off = off * esz;
+	return 1;
+}
+
 /*
  * Host buffers: stream chunks through HBM on three streams: chunk c+1's H2D
  * (copy stream), chunk c's collective (executor stream) and chunk c-1's D2H
@@ -1618,60 +1649,53 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			    void *result, size_t count, int root,
 			    enum lfa_datatype dt, enum lfa_op op)
 {
-	size_t esz = lfa_datatype_size(dt);
-	const int rs = coll == LFA_REDUCE_SCATTER;
-	const size_t nb = rs ? (size_t)mc->size : 1;  /* blocks per chunk */
-	const size_t span = count / nb;               /* elements per block */
-	size_t per = ep->chunk / esz / nb, off = 0, in_slot;
+	size_t esz = lfa_datatype_size(dt), in_slot, idx;
+	struct lfa_host_chunk c0, c;
 	hipEvent_t h2d[2], comp[2], done[2];
-	int ret = 0, slot = 0;
+	int ret, slot = 0;
 	const int out = coll != LFA_REDUCE || mc->rank == root;
 
-	if (!per)
-		per = 1;
-	if (per > span)
-		per = span;
-	/* the output half starts 256-byte aligned (vector body of the kernels) */
-	in_slot = (nb * per * esz + 255) & ~(size_t)255;
-	if (grow_staging(ep, in_slot + per * esz))
+	ret = lfa_coll_host_chunk(coll, count, mc->size, esz, ep->chunk, 0, &c0);
+	if (ret <= 0)
+		return ret < 0 ? ret : 0;
+	/* chunk 0 is the widest; the output half starts 256-byte aligned
+	 * (vector body of the kernels) */
+	in_slot = (c0.height * c0.width + 255) & ~(size_t)255;
+	if (grow_staging(ep, in_slot + c0.width))
 		return -LFA_ENOMEM;
+	ret = 0;
 	for (int i = 0; i < 2; i++) {
 		hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming);
 		hipEventCreateWithFlags(&comp[i], hipEventDisableTiming);
 		hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
 		hipEventRecord(done[i], ep->stream);
 	}
-	while (off < span && !ret) {
-		size_t n = span - off < per ? span - off : per;
+	for (idx = 0; !ret &&
+	     lfa_coll_host_chunk(coll, count, mc->size, esz, ep->chunk, idx, &c) == 1;
+	     idx++) {
 		char *din = ep->hs[slot], *dout = din + in_slot;
 
 		/* slot reuse: wait until chunk c-2's D2H finished */
 		hipStreamWaitEvent(ep->copy_stream, done[slot], 0);
-		if (rs)
-			hipMemcpy2DAsync(din, n * esz,
-					 (const char *)buf + off * esz,
-					 span * esz, n * esz, nb,
+		if (c.height > 1)
+			hipMemcpy2DAsync(din, c.width, (const char *)buf + c.src_off,
+					 c.src_pitch, c.width, c.height,
 					 hipMemcpyDefault, ep->copy_stream);
 		else if (coll != LFA_BROADCAST || mc->rank == root)
-			hipMemcpyAsync(din, (const char *)buf + off * esz, n * esz,
+			hipMemcpyAsync(din, (const char *)buf + c.src_off, c.width,
 				       hipMemcpyDefault, ep->copy_stream);
 		hipEventRecord(h2d[slot], ep->copy_stream);
 		hipStreamWaitEvent(ep->stream, h2d[slot], 0);
-		if (coll == LFA_BROADCAST)
-			ret = run_device(ep, mc, coll, din, din, n, root, dt, op,
-					 ep->stream);
-		else
-			ret = run_device(ep, mc, coll, din, dout, nb * n, root,
-					 dt, op, ep->stream);
+		ret = run_device(ep, mc, coll, din,
+				 coll == LFA_BROADCAST ? din : dout, c.dev_count,
+				 root, dt, op, ep->stream);
 		hipEventRecord(comp[slot], ep->stream);
 		hipStreamWaitEvent(ep->d2h_stream, comp[slot], 0);
 		if (out)
-			hipMemcpyAsync((char *)result + off * esz,
+			hipMemcpyAsync((char *)result + c.dst_off,
 				       coll == LFA_BROADCAST ? din : dout,
-				       n * esz, hipMemcpyDefault,
-				       ep->d2h_stream);
+				       c.width, hipMemcpyDefault, ep->d2h_stream);
 		hipEventRecord(done[slot], ep->d2h_stream);
-		off += n;
 		slot ^= 1;
 	}
 	/* the operation completes when the last D2H lands */

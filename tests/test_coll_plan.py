@@ -209,3 +209,76 @@ def test_tree_blocks_skewed_in_tmp(n):
     _plansim.run(REDUCE, coll.ALGO_TREE, n, n - 1, dt, op, count,
                  [s.view(np.uint8) for s in sends], res)
     assert np.array_equal(res[n - 1].view(np.float64), want)
+
+
+# ---- host-buffer staging geometry (lfa_coll_host_chunk) -------------------
+
+def _stage_and_run(kind, bufs, count, n, esz, chunk, root=0):
+    """Replay the provider's host pipeline on numpy: per chunk, the 2-D H2D
+    gather, the device collective on dev_count elements (integer SUM, so
+    order-free) and the D2H; returns every rank's result."""
+    chunks = coll.host_chunks(kind, count, n, esz, chunk)
+    res = [np.zeros(count // n if kind == REDUCE_SCATTER else count, np.int64)
+           for _ in range(n)]
+    covered = 0
+    for c in chunks:
+        w = c.width // esz
+        assert c.dev_count == c.height * w
+        staged = []
+        for b in bufs:
+            rows = [b[(c.src_off + h * c.src_pitch) // esz:][:w] for h in range(c.height)]
+            staged.append(np.concatenate(rows))
+        total = np.sum(staged, axis=0)
+        for r in range(n):
+            if kind == REDUCE_SCATTER:
+                off, ln = coll.block(c.dev_count, n, r)
+                assert ln == w
+                part = total[off:off + ln]
+            else:
+                part = total
+            if kind != REDUCE or r == root:
+                res[r][c.dst_off // esz:][:w] = part
+        covered += w
+    return res, covered
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("count_per", [1, 7, 1000, 4097])
+@pytest.mark.parametrize("chunk", [8, 24, 1000, 4096, 1 << 20])
+def test_host_chunked_reduce_scatter_geometry(n, count_per, chunk):
+    """Chunked host reduce_scatter hands rank r exactly block r of the sum:
+    every chunk gathers elements [j, j+w) of all N blocks with one 2-D copy."""
+    esz, count = 8, n * count_per
+    rng = np.random.default_rng(count + n)
+    bufs = [rng.integers(-2**40, 2**40, count) for _ in range(n)]
+    res, covered = _stage_and_run(REDUCE_SCATTER, bufs, count, n, esz, chunk)
+    assert covered == count_per
+    total = np.sum(bufs, axis=0)
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        assert np.array_equal(res[r], total[off:off + ln])
+
+
+@pytest.mark.parametrize("kind", [ALLREDUCE, REDUCE])
+@pytest.mark.parametrize("count", [1, 5, 1000, 70_001])
+@pytest.mark.parametrize("chunk", [8, 24, 4096, 1 << 20])
+def test_host_chunked_elementwise_geometry(kind, count, chunk):
+    n, esz = 3, 8
+    rng = np.random.default_rng(count)
+    bufs = [rng.integers(-2**40, 2**40, count) for _ in range(n)]
+    res, covered = _stage_and_run(kind, bufs, count, n, esz, chunk, root=1)
+    assert covered == count
+    total = np.sum(bufs, axis=0)
+    for r in range(n):
+        if kind == ALLREDUCE or r == 1:
+            assert np.array_equal(res[r], total)
+        else:
+            assert not res[r].any()
+
+
+def test_host_chunk_rejects_unchunked_collectives():
+    with pytest.raises(coll.CollError):
+        coll.host_chunks(REDUCE_SCATTER, 10, 3, 8, 1 << 20)   # ragged blocks
+    with pytest.raises(coll.CollError):
+        coll.host_chunks(ALLGATHER, 10, 2, 8, 1 << 20)
+    assert coll.host_chunks(ALLREDUCE, 0, 2, 8, 1 << 20) == []
