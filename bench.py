@@ -7,10 +7,17 @@ step   : one pass of the hot path — ofi_atomic_write_handler(FI_SUM, FI_FLOAT,
          256 MiB (dst, src) pair already resident in HBM, launched through the
          C ABI (lfa_atomic_write_async, liblfa.so).
 value  : whole-job traffic rate, 3·S bytes per step (read dst, read src,
-         write dst) × steps × ranks ÷ the max-over-ranks wall time, in GiB/s.
+         write dst) × steps ÷ the max-over-ranks wall time, in GiB/s.
          The buffer rate S/t is reported beside it.
-N > 1  : one process per GPU, each rank combines its own 256 MiB buckets (the
-         bucket reduction shards with no data-path exchange): weak scaling.
+N > 1  : one process per GPU.  The headline is STRONG-scaled (SURVEY §8(e),
+         BASELINE configs[3]): the one 256 MiB buffer pair is partitioned into
+         N contiguous 4 KiB-aligned shards and GPU g combines shard g with no
+         exchange, so a step is still one 256 MiB combine, done by N GPUs.  The
+         weak-scaled figure (every rank its own 256 MiB pair) sits beside it in
+         extras.  `python bench.py --gpus N` without RANK in the environment
+         starts the N rank processes itself (before any GPU call); under
+         torch.distributed.run it is one of them.  A world size that differs
+         from --gpus is an error (exit 2).
 
 Extra objects on the JSON line:
   roofline      dominant kernel (combine_lds<SUM,float>): algorithmic bytes per
@@ -49,17 +56,82 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, cmd: list[str], timeout_s: float | None = None) -> int:
+    """Start `cmd` as N rank processes (one per GPU) with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run
+    would, and return the worst exit code.  Runs before anything in this
+    process touches the GPU (children are started with Popen, never exec).
+    If a rank fails, the others are stopped by PID so none is left waiting in
+    a collective."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen(cmd, env=env))
+    t0 = time.time()
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in pending:       # a failed rank: stop its peers
+                    q.kill()
+        if timeout_s is not None and time.time() - t0 > timeout_s:
+            for q in pending:
+                q.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def check_world(expected: int, world: int) -> None:
+    if world != expected:
+        log(f"bench.py: --gpus {expected} but the job has WORLD_SIZE={world}")
+        sys.exit(2)
+
+
 def init_dist(n_gpus: int):
     if n_gpus > 1 or "RANK" in os.environ:
         rank = int(os.environ.get("RANK", 0))
         world = int(os.environ.get("WORLD_SIZE", 1))
         local = int(os.environ.get("LOCAL_RANK", rank))
+        check_world(n_gpus, world)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
+        check_world(n_gpus, dist.get_world_size())
         return rank, world, local
     torch.cuda.set_device(0)
     return 0, 1, 0
+
+
+def shard_of(count: int, world: int, rank: int, align_elems: int = 1024):
+    """Rank `rank`'s contiguous shard [off, off + len) of a `count`-element
+    buffer split over `world` GPUs, shard starts 4 KiB-aligned (1024 float)."""
+    per = -(-count // world)
+    per = -(-per // align_elems) * align_elems
+    off = min(rank * per, count)
+    return off, min(per, count - off)
 
 
 def barrier(world: int) -> None:
@@ -75,14 +147,36 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def make_buffers(dev, seed: int):
+ROTATE_BYTES = 1 << 30                 # >= 1 GiB of operands per GPU rotated
+
+
+def n_sets(count: int) -> int:
+    """Buffer pairs to rotate so the 256 MiB MALL cannot serve repeats."""
+    return max(BUFFER_SETS, -(-ROTATE_BYTES // max(1, 2 * 4 * count)))
+
+
+def make_buffers(dev, seed: int, count: int = COUNT, nsets: int | None = None):
     g = torch.Generator(device=dev).manual_seed(seed)
     sets = []
-    for _ in range(BUFFER_SETS):
-        src = torch.rand(COUNT, device=dev, generator=g) * 2 - 1
-        dst = torch.rand(COUNT, device=dev, generator=g) * 2 - 1
+    for _ in range(nsets or n_sets(count)):
+        src = torch.rand(count, device=dev, generator=g) * 2 - 1
+        dst = torch.rand(count, device=dev, generator=g) * 2 - 1
         sets.append((dst, src))
     return sets
+
+
+def prewarm(step, min_s: float) -> int:
+    """Untimed launches of the step until `min_s` seconds have passed, so the
+    timed region starts at steady-state GPU clocks (a short run otherwise
+    measures the ramp: 129 us/launch after 10 launches vs 121 us at steady
+    state).  Returns the number of launches."""
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min_s:
+        for _ in range(20):
+            step(n)
+            n += 1
+        torch.cuda.synchronize()
+    return n
 
 
 def read_traffic():
@@ -165,6 +259,68 @@ def cpu_baseline(sample_reps: int = 5):
     return out
 
 
+def splitmix64(seed: int, n: int):
+    """SURVEY §8(d) config 3 data: full-range splitmix64 stream."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+             + np.uint64(seed))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z.view(np.int64)
+
+
+def config3_data(seed: int, n: int):
+    """splitmix64 int64 lanes with ~1 % forced to INT64_MIN/MAX/0/-1."""
+    import numpy as np
+    x = splitmix64(seed, n)
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(n, n // 100, replace=False)
+    x[idx] = rng.choice(np.array([np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1],
+                                 dtype=np.int64), idx.size)
+    return x
+
+
+def cpu_baseline_config3(sample_reps: int = 5):
+    """BASELINE configs[2] on ONE pinned host core: int64 FI_BOR (`lock or`,
+    util_atomic.c:78-79) and FI_MIN (CAS-if-smaller, util_atomic.c:71,
+    291-316), 64 MiB, the SURVEY §8(d) data distribution; shipping atomic
+    handler restated in oracle/ ("port") and the plain loop beside it.
+    GiB/s of traffic (3 x 64 MiB per combine)."""
+    import oracle
+    n = 64 * 1024 * 1024 // 8
+    src, dst0 = config3_data(4, n), config3_data(3, n)
+    dst = dst0.copy()
+    try:
+        prev = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {sorted(prev)[-1]})
+    except (AttributeError, OSError):
+        prev = None
+    out = {}
+    try:
+        for name, op in (("bor", 6), ("min", 0)):
+            row = {}
+            for var, vname in ((oracle.CAS, "atomic"), (oracle.PLAIN, "plain")):
+                ts = []
+                for _ in range(sample_reps):
+                    dst[:] = dst0
+                    t0 = time.perf_counter()
+                    oracle.write(op, 6, dst, src, var)
+                    ts.append(time.perf_counter() - t0)
+                t = statistics.median(ts)
+                row[vname] = {"ms": round(t * 1e3, 2),
+                              "gib_s": round(3 * n * 8 / t / 2**30, 3)}
+            out[name] = row
+    finally:
+        if prev is not None:
+            os.sched_setaffinity(0, prev)
+    out.update({"cores": 1, "kind": "port",
+                "sample": f"64 MiB int64 (8,388,608 lanes) splitmix64 seeds 3/4 with 1 % "
+                          f"INT64_MIN/MAX/0/-1 lanes, median of {sample_reps}, 1 pinned core"})
+    return out
+
+
 
 # ------------------------------------------------------------------ extras --
 
@@ -205,6 +361,36 @@ def extra_config3(dev, stream):
         out[name] = {"kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
                      "frac": round(gbps / PEAK_GBPS, 4),
                      "gib_s": round(3 * n * 8 / (ms * 1e-3) / 2**30, 1)}
+    return out
+
+
+def extra_config1_loopback(dev, stream, reps=1000, warm=100):
+    """BASELINE configs[0] at its stated shape on ONE GPU: a 2-rank float
+    FI_SUM allreduce of 4 KiB per rank, both ranks' schedules executed by the
+    C executor with the real kernels and a device-copy loopback transport
+    (lfa_coll_loopback).  Median wall time per collective (launch + sync) of
+    `reps` after `warm`; the result is checked against r1 + r0 bitwise.  The
+    reference's own figure for this shape is the known answer of
+    fabtests/multinode/src/core_coll.c:230-277 over tcp;ofi_rxm."""
+    from libfabric_amd import coll
+    g = torch.Generator(device=dev).manual_seed(0x5EED)
+    sends = [torch.rand(1024, device=dev, generator=g) * 2 - 1 for _ in range(2)]
+    results = [torch.empty(1024, device=dev) for _ in range(2)]
+    want = sends[1] + sends[0]
+    out = {}
+    for name, algo in (("tree_us", coll.ALGO_TREE), ("rd_us", coll.ALGO_RD)):
+        ts = []
+        for i in range(warm + reps):
+            t0 = time.perf_counter()
+            coll.loopback(3, algo, 2, -1, 8, 2, 1024, sends, results, stream)
+            torch.cuda.synchronize()
+            if i >= warm:
+                ts.append(time.perf_counter() - t0)
+        ok = all(torch.equal(r, want) for r in results)
+        out[name] = round(statistics.median(ts) * 1e6, 1)
+        out[name.replace("_us", "_bitwise_ok")] = bool(ok)
+    out["note"] = ("2 ranks on one GPU, loopback transport; median of 1000 after 100 "
+                   "warm-up; wall time incl. hipStreamSynchronize")
     return out
 
 
@@ -708,6 +894,8 @@ def main() -> None:
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
     ap.add_argument("--extras-timeout", type=float, default=300.0)
+    ap.add_argument("--prewarm-s", type=float, default=0.25,
+                    help="untimed clock-ramp launches before the W warmup steps (s)")
     args = ap.parse_args()
 
     if args.tune:
@@ -738,56 +926,24 @@ def main() -> None:
                                                      torch.cuda.current_stream())}))
         return
 
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # Self-launch: one process per GPU, before this process touches one.
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__),
+                                          *sys.argv[1:]]))
     rank, world, local = init_dist(args.gpus)
-    from libfabric_amd import atomic, lib
+    from libfabric_amd import lib
     lib()  # no fallback: raises if liblfa.so is missing
     dev = torch.device("cuda", local)
-    sets = make_buffers(dev, 1000 + rank)
     stream = torch.cuda.current_stream()
 
-    def step(i):
-        d, s = sets[i % BUFFER_SETS]
-        atomic.write(FI_SUM, FI_FLOAT, d, s, COUNT, stream)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-
-    # Timed region: K back-to-back launches, nothing else in the queue but
-    # one HIP event pair around the whole region (on the launch stream), so
-    # the wall clock measures the kernels, not event markers.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0, world)
-    # roofline: average launch duration = region GPU time / K.  This keeps
-    # the ~1-2 us dispatch gap between consecutive kernels in, so it is a
-    # slightly conservative figure for the kernel itself.
-    kern_ms = max_over_ranks(ev0.elapsed_time(ev1) / args.steps, world)
-    # Diagnostic only (not timed): per-launch event pairs, median; tracks
-    # rocprofv3's kernel-trace mean (profiles/r01_rocprof_kernel_stats.csv).
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(min(args.steps, 30))]
-    for i, (a, b) in enumerate(evs):
-        a.record(stream)
-        step(i)
-        b.record(stream)
-    torch.cuda.synchronize()
-    durs = [a.elapsed_time(b) for a, b in evs][3:] or [kern_ms]
-    kern_med = statistics.median(durs)
-
-    total_bytes = 3 * S_BYTES * args.steps * world
-    value = total_bytes / elapsed / 2**30
-    achieved = 3 * S_BYTES / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = read_traffic()
+    # Headline: ONE 256 MiB buffer pair, sharded over the N GPUs (strong).
+    off, cnt = shard_of(COUNT, world, rank)
+    r = timed_combine(dev, stream, cnt, 1000 + rank, args, world)
+    elapsed, kern_ms, kern_med = r["elapsed"], r["kern_ms"], r["kern_med"]
+    shard_bytes = cnt * 4
+    value = 3 * S_BYTES * args.steps / elapsed / 2**30
+    achieved = 3 * shard_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = read_traffic() if world == 1 else (None, None)
 
     line = {
         "metric": "device-resident GiB/s, float32 FI_SUM reduce, 256 MiB buffers",
@@ -798,18 +954,22 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (uniform[-1,1) float32, torch.Generator seeds 1000+rank)",
         "config": {
-            "workload": "float32 FI_SUM local combine, 256 MiB device-resident per GPU "
-                        "(BASELINE.json configs[1]); dst += src through "
-                        "lfa_atomic_write_async",
-            "count": COUNT, "buffer_bytes": S_BYTES, "buffer_sets": BUFFER_SETS,
-            "bytes_per_step_per_gpu": 3 * S_BYTES,
-            "buffer_rate_gib_s": round(S_BYTES * args.steps * world / elapsed / 2**30, 2),
-            "parallelism": f"shard{world} (independent buckets per GPU, no exchange)",
+            "workload": "float32 FI_SUM local combine of one 256 MiB device-resident "
+                        "buffer pair per step (BASELINE.json configs[1]), dst += src "
+                        "through lfa_atomic_write_async; at N>1 split into N contiguous "
+                        "4 KiB-aligned shards, GPU g combines shard g (SURVEY §8(e))",
+            "count": COUNT, "buffer_bytes": S_BYTES,
+            "shard_bytes_per_gpu": shard_bytes,
+            "buffer_sets": r["nsets"],
+            "bytes_per_step": 3 * S_BYTES,
+            "buffer_rate_gib_s": round(S_BYTES * args.steps / elapsed / 2**30, 2),
+            "prewarm_launches": r["prewarm"],
+            "parallelism": f"shard{world} (contiguous shards of one buffer, no exchange)",
         },
         "roofline": {
             "bound": "hbm",
@@ -818,21 +978,21 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "combine_lds<FI_SUM,float,U=4,nt> (LDS-DMA staged, nt stores at "
-                      ">= 192 MiB)",
+            "kernel": "combine_lds<FI_SUM,float,U=4> (LDS-DMA staged; nt stores at "
+                      ">= 192 MiB per operand, sc1 write-through below)",
             "kernel_us": round(kern_ms * 1e3, 2),
             "kernel_us_isolated_median": round(kern_med * 1e3, 2),
             "timing": "HIP event pair around the timed region on the launch stream, "
-                      "divided by steps (includes inter-kernel dispatch gaps); "
-                      "isolated per-launch event median beside it; rocprofv3 "
-                      "kernel-trace mean 121.2 us for the same kernel "
-                      "(profiles/r01_rocprof_headline_kernel_stats.csv)",
-            "algorithmic_bytes_per_launch": 3 * S_BYTES,
+                      "divided by steps (includes inter-kernel dispatch gaps), max over "
+                      "ranks; isolated per-launch event median beside it; rocprofv3 "
+                      "kernel-trace summary in profiles/",
+            "algorithmic_bytes_per_launch": 3 * shard_bytes,
             "traffic_source": traffic_src,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
+        line["cpu_baseline"]["config3_int64_64mib"] = cpu_baseline_config3(args.cpu_reps)
 
     # Extras (never the headline).  A watchdog prints the line collected so
     # far and exits if an extra stalls, so the metric is always reported.
@@ -845,7 +1005,6 @@ def main() -> None:
             print(json.dumps(line), flush=True)
 
     if not args.no_extras:
-        del sets
         torch.cuda.empty_cache()
         wd = threading.Timer(args.extras_timeout, lambda: (_emit("extras timed out"),
                                                            os._exit(0)))
@@ -853,8 +1012,19 @@ def main() -> None:
         wd.start()
         ex = line.setdefault("extras", {})
         try:
+            if world > 1:
+                # weak scaling beside the strong headline: every rank its own
+                # full 256 MiB pair per step
+                w = timed_combine(dev, stream, COUNT, 2000 + rank, args, world)
+                ex["weak_scaling_256mib_per_gpu"] = {
+                    "value": round(3 * S_BYTES * args.steps * world / w["elapsed"] / 2**30, 2),
+                    "unit": "GiB/s", "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
+                    "kernel_us": round(w["kern_ms"] * 1e3, 2),
+                    "frac": round(3 * S_BYTES / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4)}
+                torch.cuda.empty_cache()
             if world == 1:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
+                ex["config1_2rank_4kib_loopback"] = extra_config1_loopback(dev, stream)
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
                 ex["tree8_put_p2p_kernel_local"] = extra_tree_put(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
@@ -872,6 +1042,55 @@ def main() -> None:
         bye.daemon = True
         bye.start()
         dist.destroy_process_group()
+
+
+def timed_combine(dev, stream, count: int, seed: int, args, world: int) -> dict:
+    """The bench step on this rank: float FI_SUM combine of `count` elements,
+    rotating over enough buffer pairs to defeat the MALL.  W warmup launches
+    (after a short time-based clock prewarm), then EXACTLY K timed launches
+    between a barrier + synchronize on both sides; wall time and the launch
+    stream's event time are maxed over ranks."""
+    from libfabric_amd import atomic
+    sets = make_buffers(dev, seed, count)
+    nsets = len(sets)
+
+    def step(i):
+        d, s = sets[i % nsets]
+        atomic.write(FI_SUM, FI_FLOAT, d, s, count, stream)
+
+    npre = prewarm(step, args.prewarm_s) if args.prewarm_s > 0 else 0
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    # Timed region: K back-to-back launches, nothing else in the queue but
+    # one HIP event pair around the whole region (on the launch stream).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    elapsed = max_over_ranks(t1 - t0, world)
+    # roofline: average launch duration = region GPU time / K (keeps the
+    # ~1 us dispatch gap between consecutive kernels in: conservative).
+    kern_ms = max_over_ranks(ev0.elapsed_time(ev1) / args.steps, world)
+    # Diagnostic only (not timed): per-launch event pairs, median.
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(min(args.steps, 30))]
+    for i, (a, b) in enumerate(evs):
+        a.record(stream)
+        step(i)
+        b.record(stream)
+    torch.cuda.synchronize()
+    durs = [a.elapsed_time(b) for a, b in evs][3:] or [kern_ms]
+    del sets
+    return {"elapsed": elapsed, "kern_ms": kern_ms, "kern_med": statistics.median(durs),
+            "nsets": nsets, "prewarm": npre}
 
 
 if __name__ == "__main__":

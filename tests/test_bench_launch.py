@@ -1,0 +1,102 @@
+"""bench.py's N-rank launch and sharding, on CPU (no GPU call is made).
+
+`python bench.py --gpus N` without RANK in the environment must start N rank
+processes itself (the driver may invoke it that way), each with the
+torch.distributed.run environment, and a job whose world size differs from
+--gpus must fail instead of reporting n_gpus = 1.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+_STUB = (
+    "import json, os, sys\n"
+    "keys = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT',\n"
+    "        'HSA_ENABLE_IPC_MODE_LEGACY']\n"
+    "d = {k: os.environ.get(k) for k in keys}\n"
+    "open(os.path.join(sys.argv[1], 'rank%s.json' % d['RANK']), 'w').write(json.dumps(d))\n"
+)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_launch_starts_n_ranks(tmp_path, n):
+    rc = bench.launch_ranks(n, [sys.executable, "-c", _STUB, str(tmp_path)], timeout_s=60)
+    assert rc == 0
+    seen = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(n)]
+    assert [int(d["RANK"]) for d in seen] == list(range(n))
+    assert [int(d["LOCAL_RANK"]) for d in seen] == list(range(n))
+    assert {d["WORLD_SIZE"] for d in seen} == {str(n)}
+    assert {d["MASTER_ADDR"] for d in seen} == {"127.0.0.1"}
+    assert len({d["MASTER_PORT"] for d in seen}) == 1
+    assert {d["HSA_ENABLE_IPC_MODE_LEGACY"] for d in seen} == {"0"}
+
+
+def test_launch_failed_rank_stops_peers():
+    # rank 1 fails at once; rank 0 would sleep a minute and must be stopped
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(60)\n")
+    t0 = time.time()
+    rc = bench.launch_ranks(2, [sys.executable, "-c", code], timeout_s=120)
+    assert rc == 3
+    assert time.time() - t0 < 30
+
+
+def test_world_size_mismatch_fails_before_gpu():
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "0"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "WORLD_SIZE=1" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_check_world():
+    bench.check_world(4, 4)
+    with pytest.raises(SystemExit):
+        bench.check_world(8, 1)
+
+
+@pytest.mark.parametrize("world", range(1, 9))
+def test_shards_partition_the_buffer(world):
+    """Contiguous, 4 KiB-aligned shards that cover [0, COUNT) exactly."""
+    pos = 0
+    for r in range(world):
+        off, ln = bench.shard_of(bench.COUNT, world, r)
+        assert off == pos
+        assert off * 4 % 4096 == 0
+        pos += ln
+    assert pos == bench.COUNT
+    # ragged sizes too
+    for count in (1, 1023, 1025, 10_000_019):
+        pos = 0
+        for r in range(world):
+            off, ln = bench.shard_of(count, world, r)
+            assert off == pos or ln == 0
+            pos += ln
+        assert pos == count
+
+
+def test_rotation_defeats_mall():
+    for world in range(1, 9):
+        _, ln = bench.shard_of(bench.COUNT, world, 0)
+        assert bench.n_sets(ln) * 2 * ln * 4 >= (1 << 30)
+
+
+def test_config3_data_distribution():
+    import numpy as np
+    x = bench.config3_data(3, 1 << 16)
+    special = np.isin(x, [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]).sum()
+    assert 0.009 < special / x.size < 0.011
+    assert x.min() < -(1 << 60) and x.max() > (1 << 60)   # full range
