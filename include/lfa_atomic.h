@@ -134,6 +134,22 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype datatype,
 			    void *dst, const void *src, size_t cnt,
 			    size_t chunk_bytes);
 
+/*
+ * Host-memory forms (no GPU involved): the same element semantics as the
+ * kernels — one functor source, lfa_ops.hpp — for operands that live in host
+ * memory: the synchronous table's small host buckets and endpoints opened with
+ * lfa_coll_domain_open_host.  Device pointers must not be passed here.
+ * lfa_host_write:       dst[i] = dst[i] OP src[i]  (ofi_atomic_write_handler
+ *                       argument order, util_atomic.c:907-922)
+ * lfa_host_reduce_tree: dst = prov/coll's recursive-doubling tree of srcs
+ *                       (coll_coll.c:349-449), 1 <= nsrc <= LFA_TREE_MAX
+ * Return 0, -LFA_EOPNOTSUPP or -LFA_EINVAL.
+ */
+int lfa_host_write(enum lfa_op op, enum lfa_datatype datatype, void *dst,
+		   const void *src, size_t cnt);
+int lfa_host_reduce_tree(enum lfa_op op, enum lfa_datatype datatype, void *dst,
+			 const void *const *srcs, int nsrc, size_t cnt);
+
 /* Version string of the kernel library (build id, target arch). */
 const char *lfa_version(void);
 

@@ -51,6 +51,11 @@ def _bind_lfa(L):
     L.lfa_atomic_write_staged.argtypes = [c_int, c_int, c_void_p, c_void_p, c_size_t,
                                           c_size_t]
     L.lfa_version.restype = ctypes.c_char_p
+    L.lfa_host_write.restype = c_int
+    L.lfa_host_write.argtypes = [c_int, c_int, c_void_p, c_void_p, c_size_t]
+    L.lfa_host_reduce_tree.restype = c_int
+    L.lfa_host_reduce_tree.argtypes = [c_int, c_int, c_void_p, ctypes.POINTER(c_void_p),
+                                       c_int, c_size_t]
     L.lfa__tune_tree_f32.restype = c_int
     L.lfa__tune_tree_f32.argtypes = [c_int, c_void_p, ctypes.POINTER(c_void_p),
                                      c_int, c_size_t, c_void_p]

@@ -154,3 +154,35 @@ def reduce_tree_put(op: int, dt: int, dsts: list[torch.Tensor], srcs: list[torch
                                          cnt, _stream_handle(stream))
     if rc:
         raise LfaError(rc, f"lfa_reduce_tree_put_async({OP(op).name},{DT(dt).name})")
+
+
+# ------------------------------------------------------- host-memory forms --
+
+def _host_ptr(a) -> int:
+    if isinstance(a, torch.Tensor):
+        if a.is_cuda:
+            raise ValueError("host form called with a device tensor")
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def host_write(op: int, dt: int, dst, src, cnt: int | None = None) -> None:
+    """dst[i] = dst[i] OP src[i] for HOST buffers (numpy arrays or CPU
+    tensors), lfa_host_write: the kernels' functors run on the host."""
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    rc = lib().lfa_host_write(int(op), int(dt), _host_ptr(dst), _host_ptr(src), cnt)
+    if rc:
+        raise LfaError(rc, f"lfa_host_write({op},{dt})")
+
+
+def host_reduce_tree(op: int, dt: int, dst, srcs, cnt: int | None = None) -> None:
+    """dst = prov/coll's recursive-doubling tree of HOST buffers srcs."""
+    esz = datatype_size(dt)
+    if cnt is None:
+        cnt = dst.nbytes // esz
+    arr = (ctypes.c_void_p * len(srcs))(*[_host_ptr(s) for s in srcs])
+    rc = lib().lfa_host_reduce_tree(int(op), int(dt), _host_ptr(dst), arr, len(srcs), cnt)
+    if rc:
+        raise LfaError(rc, f"lfa_host_reduce_tree({op},{dt})")

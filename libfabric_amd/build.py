@@ -72,6 +72,14 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
         steps.append(["g++", "-O2", "-fPIC", "-std=c++17", "-Wall",
                       "-D__HIP_PLATFORM_AMD__", "-I" + INC,
                       "-I" + os.path.join(ROCM, "include"), "-c", capi, "-o", o])
+    host = os.path.join(CSRC, "lfa_host.cpp")
+    o = os.path.join(BUILD, "lfa_host.o")
+    objs.append(o)
+    if _newer(o, [host] + hdrs):
+        # the host-memory combine: the kernels' functors compiled by g++,
+        # no FMA contraction (as the reference's x86-64 build)
+        steps.append(["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-ffp-contract=off",
+                      "-I" + INC, "-c", host, "-o", o])
     if steps:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             for f in [ex.submit(_run, s) for s in steps]:

@@ -14,10 +14,19 @@
 //
 // Everything is compiled with -ffp-contract=off: a contracted FMA would change
 // PROD/SUM chains and the complex product away from the reference's rounding.
+//
+// One source for both sides: hipcc compiles these functors for gfx950 (the
+// kernels) and, through LFA_HD, for the host as well; g++ compiles them as
+// plain inline host code for the product's host-memory loop (lfa_host.cpp).
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define LFA_HD __host__ __device__ __forceinline__
+#else
+#define LFA_HD inline __attribute__((always_inline))
+#endif
 
 namespace lfa {
 
@@ -51,21 +60,21 @@ template <> struct IsFloat<float> { static constexpr bool value = true; };
 template <> struct IsFloat<double> { static constexpr bool value = true; };
 
 template <typename T>
-__device__ __forceinline__ bool truth(T v) { return v != T(0); }
+LFA_HD bool truth(T v) { return v != T(0); }
 template <>
-__device__ __forceinline__ bool truth<cf32>(cf32 v) {
+LFA_HD bool truth<cf32>(cf32 v) {
   return v.re != 0.0f || v.im != 0.0f;
 }
 
 template <typename T>
-__device__ __forceinline__ T from_bool(bool b) { return b ? T(1) : T(0); }
+LFA_HD T from_bool(bool b) { return b ? T(1) : T(0); }
 template <>
-__device__ __forceinline__ cf32 from_bool<cf32>(bool b) {
+LFA_HD cf32 from_bool<cf32>(bool b) {
   return cf32{b ? 1.0f : 0.0f, 0.0f};
 }
 
 template <typename T>
-__device__ __forceinline__ T add(T a, T b) {
+LFA_HD T add(T a, T b) {
   if constexpr (IsFloat<T>::value) {
     return a + b;
   } else {
@@ -75,7 +84,7 @@ __device__ __forceinline__ T add(T a, T b) {
 }
 
 template <typename T>
-__device__ __forceinline__ T mul(T a, T b) {
+LFA_HD T mul(T a, T b) {
   if constexpr (IsFloat<T>::value) {
     return a * b;
   } else {
@@ -85,11 +94,11 @@ __device__ __forceinline__ T mul(T a, T b) {
 }
 
 template <>
-__device__ __forceinline__ cf32 add<cf32>(cf32 a, cf32 b) {
+LFA_HD cf32 add<cf32>(cf32 a, cf32 b) {
   return cf32{a.re + b.re, a.im + b.im};
 }
 
-__device__ __forceinline__ float copysign0(float mag, float sgn) {
+LFA_HD float copysign0(float mag, float sgn) {
   return __builtin_copysignf(mag, sgn);
 }
 
@@ -97,8 +106,10 @@ __device__ __forceinline__ float copysign0(float mag, float sgn) {
 // formula with every product rounded, and the C11 Annex G recovery when both
 // parts are NaN (libgcc __mulsc3).
 template <>
-__device__ __forceinline__ cf32 mul<cf32>(cf32 x, cf32 y) {
+LFA_HD cf32 mul<cf32>(cf32 x, cf32 y) {
+#ifdef __clang__
 #pragma clang fp contract(off)
+#endif
   float a = x.re, b = x.im, c = y.re, d = y.im;
   float ac = a * c, bd = b * d, ad = a * d, bc = b * c;
   float re = ac - bd, im = ad + bc;
@@ -136,7 +147,7 @@ __device__ __forceinline__ cf32 mul<cf32>(cf32 x, cf32 y) {
 
 // d OP s for one element.  OP is an enum fi_op value.
 template <int OP, typename T>
-__device__ __forceinline__ T apply(T d, T s) {
+LFA_HD T apply(T d, T s) {
   if constexpr (OP == OP_MIN) {
     return (d > s) ? s : d;
   } else if constexpr (OP == OP_MAX) {
@@ -204,7 +215,7 @@ template <> struct Bits<16> { typedef u128 type; };
 // __atomic_compare_exchange compares object representations, not values:
 // the shipping CSWAP swaps on identical BITS (-0.0 != +0.0, NaN == same NaN).
 template <typename T>
-__device__ __forceinline__ bool bits_eq(T a, T b) {
+LFA_HD bool bits_eq(T a, T b) {
   typename Bits<sizeof(T)>::type x, y;
   __builtin_memcpy(&x, &a, sizeof(T));
   __builtin_memcpy(&y, &b, sizeof(T));
@@ -212,15 +223,15 @@ __device__ __forceinline__ bool bits_eq(T a, T b) {
 }
 
 template <typename T>
-__device__ __forceinline__ bool val_ne(T c, T d) { return c != d; }
+LFA_HD bool val_ne(T c, T d) { return c != d; }
 template <>
-__device__ __forceinline__ bool val_ne<cf32>(cf32 c, cf32 d) {
+LFA_HD bool val_ne<cf32>(cf32 c, cf32 d) {
   return !(c.re == d.re && c.im == d.im);
 }
 
 // new dst for the swap row OP given dst a, src b, compare c
 template <int OP, typename T>
-__device__ __forceinline__ T swap_apply(T a, T b, T c) {
+LFA_HD T swap_apply(T a, T b, T c) {
   if constexpr (OP == OP_CSWAP) {
     return bits_eq(a, c) ? b : a;
   } else if constexpr (OP == OP_CSWAP_NE) {
