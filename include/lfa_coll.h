@@ -89,6 +89,38 @@ int lfa_coll_get_unique_id(void *id, size_t len);
 
 int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
 			 size_t id_len, struct lfa_coll_domain **domain);
+
+/*
+ * Peer transfer: a domain whose buffers are HOST memory and whose transport
+ * is the owner provider's tagged messaging — prov/coll's own configuration,
+ * where SEND/RECV work items become fi_tsendmsg / fi_trecvmsg(FI_PEER_TRANSFER)
+ * on the host provider's endpoint (coll_coll.c:770-814) and completions come
+ * back through peer_ops->complete (coll_coll.c:1218-1241).
+ *
+ * send / recv post one transfer of `bytes` to / from domain rank `peer` with
+ * prov/coll's tag (coll_form_tag, coll_coll.c:37-45: the operation's cid
+ * (group_id << 16 | seq) | the SENDING group rank << 32) and store a handle
+ * in *req; messages between one pair with one tag match in posting order.
+ * test returns 1 once the transfer behind `req` has completed (the handle is
+ * then released), 0 while pending, or a negative LFA_E* code.
+ *
+ * Endpoints of such a domain run each collective's schedule on the host:
+ * transfers through these callbacks, REDUCE / TREE items through
+ * lfa_host_write / lfa_host_reduce_tree (include/lfa_atomic.h), progressed by
+ * lfa_cq_read as prov/coll progresses in fi_cq_read.  LFA_ALGO_P2P and
+ * LFA_ALGO_RCCL run as LFA_ALGO_TREE; LFA_ALGO_TREE_COLL's collective items
+ * become grouped sends/receives.
+ */
+struct lfa_peer_xfer_ops {
+	int (*send)(void *ctx, int peer, const void *buf, size_t bytes,
+		    uint64_t tag, void **req);
+	int (*recv)(void *ctx, int peer, void *buf, size_t bytes, uint64_t tag,
+		    void **req);
+	int (*test)(void *ctx, void *req);
+};
+int lfa_coll_domain_open_host(int rank, int nranks,
+			      const struct lfa_peer_xfer_ops *ops, void *ctx,
+			      struct lfa_coll_domain **domain);
 int lfa_coll_domain_close(struct lfa_coll_domain *domain);
 
 /* An endpoint owns one HIP stream (its progress context), a work-item
@@ -115,6 +147,9 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			const int *ranks, size_t nmembers, uint64_t flags,
 			struct lfa_coll_mc **mc, void *context);
 lfa_addr_t lfa_mc_addr(struct lfa_coll_mc *mc);
+/* The group id the join agreed on (util_coll_mc.group_id, ofi_util.h:849-856;
+ * the world group is 0), or -LFA_EAGAIN before the join completed. */
+int lfa_mc_group_id(struct lfa_coll_mc *mc);
 int lfa_mc_close(struct lfa_coll_mc *mc);
 /* The world group, usable without a join (the reference's av_set coll_mc). */
 lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep);

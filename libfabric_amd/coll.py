@@ -99,6 +99,11 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_domain_open.restype = c_int
     L.lfa_coll_domain_open.argtypes = [c_int, c_int, c_int, c_void_p, c_size_t,
                                        P(c_void_p)]
+    L.lfa_coll_domain_open_host.restype = c_int
+    L.lfa_coll_domain_open_host.argtypes = [c_int, c_int, P(PeerXferOps), c_void_p,
+                                            P(c_void_p)]
+    L.lfa_mc_group_id.restype = c_int
+    L.lfa_mc_group_id.argtypes = [c_void_p]
     L.lfa_coll_domain_close.restype = c_int
     L.lfa_coll_domain_close.argtypes = [c_void_p]
     L.lfa_coll_ep_open.restype = c_int
@@ -152,6 +157,16 @@ def lib() -> ctypes.CDLL:
     L.lfa_eq_read.argtypes = [c_void_p, P(c_uint32), P(EqEntry)]
     _bound = True
     return L
+
+
+XferPost = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_size_t, c_uint64,
+                            ctypes.POINTER(c_void_p))
+XferTest = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p)
+
+
+class PeerXferOps(ctypes.Structure):
+    """struct lfa_peer_xfer_ops: the owner's tagged transport (FI_PEER_TRANSFER)."""
+    _fields_ = [("send", XferPost), ("recv", XferPost), ("test", XferTest)]
 
 
 class HostChunk(ctypes.Structure):
@@ -283,6 +298,9 @@ class Endpoint:
         dist.broadcast_object_list(obj, src=0)
         return cls(rank, world, torch.cuda.current_device() if device is None
                    else device, obj[0])
+
+    def group_id(self, mc: int) -> int:
+        return lib().lfa_mc_group_id(mc)
 
     def close(self) -> None:
         L = lib()
@@ -423,9 +441,52 @@ class Endpoint:
                 raise TimeoutError("join did not complete")
 
 
+class HostEndpoint(Endpoint):
+    """An endpoint of a peer-transfer domain (lfa_coll_domain_open_host):
+    host-memory buffers, transfers through `transport` — an object with
+    send(peer, ptr, nbytes, tag) -> handle, recv(peer, ptr, nbytes, tag) ->
+    handle and test(handle) -> 1 done / 0 pending / <0 error — the way
+    prov/coll rides on the owner provider's tagged messages."""
+
+    def __init__(self, rank: int, nranks: int, transport):
+        L = lib()
+        self.rank, self.nranks, self.device = rank, nranks, -1
+        self.transport = transport
+
+        def _send(ctx, peer, buf, nbytes, tag, req):
+            try:
+                req[0] = transport.send(peer, buf, nbytes, tag)
+                return 0
+            except Exception:  # noqa: BLE001 — an exception must not cross C
+                return -EIO
+
+        def _recv(ctx, peer, buf, nbytes, tag, req):
+            try:
+                req[0] = transport.recv(peer, buf, nbytes, tag)
+                return 0
+            except Exception:  # noqa: BLE001
+                return -EIO
+
+        def _test(ctx, req):
+            try:
+                return int(transport.test(req))
+            except Exception:  # noqa: BLE001
+                return -EIO
+
+        # keep the trampolines alive as long as the endpoint
+        self._ops = PeerXferOps(XferPost(_send), XferPost(_recv), XferTest(_test))
+        self.dom, self.ep = c_void_p(), c_void_p()
+        _chk(L.lfa_coll_domain_open_host(rank, nranks, ctypes.byref(self._ops), None,
+                                         ctypes.byref(self.dom)), "domain_open_host")
+        _chk(L.lfa_coll_ep_open(self.dom, ctypes.byref(self.ep)), "ep_open")
+        self.world = L.lfa_coll_world_addr(self.ep)
+        self._ctx = 0
+
+
 def esz(dt: int) -> int:
     return SIZES[DT(dt)]
 
 
 __all__ = ["plan", "block", "host_chunks", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
-           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz"]
+           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz",
+           "HostEndpoint", "PeerXferOps"]

@@ -30,6 +30,7 @@
 #define _GNU_SOURCE
 #include <errno.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -67,6 +68,8 @@ struct planner {
 	struct lfa_ref *refs;
 	size_t rcap, nr;
 	int pending_comm;       /* SEND/RECV since the last GROUP_END */
+	uint64_t tmp_base;      /* TMP bytes the schedule itself uses */
+	uint64_t tmp_extra;     /* + partials of split trees (p_tree_any) */
 };
 
 static struct lfa_ref ref(int buf, uint64_t off)
@@ -233,6 +236,15 @@ static void p_coll(struct planner *p, int type, struct lfa_ref dst,
 	}
 }
 
+static uint64_t pof2_floor(uint64_t v)
+{
+	uint64_t q = 1;
+
+	while (q * 2 <= v)
+		q *= 2;
+	return q;
+}
+
 /*
  * Tree algorithm, phase 1: rank r collects block r of every rank's input.
  * TMP slot p (block-r sized) receives rank p's block; rank r's own block is
@@ -277,18 +289,86 @@ static void plan_gather_blocks(struct planner *p, int r, int n, size_t count,
 	p_group_end(p);
 }
 
+/*
+ * A tree over n inputs of any size.  Up to LFA_TREE_MAX inputs it is ONE
+ * TREE item (one fused kernel).  Above that it is split into whole subtrees
+ * of prov/coll's recursive-doubling tree, so the bits do not change:
+ * virtual rank v < pof2 is the leaf pair (in[2v+1] OP in[2v]) for v < rem
+ * and in[v + rem] otherwise (coll_coll.c:366-389); aligned runs of 16
+ * virtual ranks are subtrees of at most 32 inputs, each reduced into a TMP
+ * partial, and the pof2/16 partials are combined by the same rule
+ * (recursively, for groups above 512 ranks).  A run with k < 16 pairs is
+ * the kernel's own tree for 16 + k inputs (pairs first, as in the kernel); a
+ * run of 16 pairs is its plain 32-input tree, whose first level is exactly
+ * the pairs.
+ */
+struct tree_in {
+	int kind;               /* 0: rank order, `own` in place, the rest TMP
+				   slots k*stride; 1: TMP run at base + k*stride */
+	int own;
+	struct lfa_ref own_ref;
+	uint64_t base, stride;
+};
+
+static struct lfa_ref tree_in_ref(const struct tree_in *t, int k)
+{
+	if (t->kind == 0 && k == t->own)
+		return t->own_ref;
+	return ref(LFA_BUF_TMP, t->base + (uint64_t)k * t->stride);
+}
+
+#define LFA_TREE_GROUP 16       /* virtual ranks per split subtree */
+
+static void p_tree_any(struct planner *p, const struct tree_in *in, int lo,
+		       int n, struct lfa_ref dst, uint64_t count, size_t esz)
+{
+	uint64_t pof2 = pof2_floor((uint64_t)n), rem = (uint64_t)n - pof2;
+	uint64_t ngrp, pstride, pbase;
+	struct tree_in parts;
+	uint32_t first;
+
+	if (n <= LFA_TREE_MAX) {
+		first = p_tree_begin(p);
+		for (int k = 0; k < n; k++)
+			p_tree_src(p, tree_in_ref(in, lo + k));
+		p_tree_end(p, first, dst, count);
+		return;
+	}
+	ngrp = pof2 / LFA_TREE_GROUP;
+	pstride = ((uint64_t)count * esz + 255) & ~(uint64_t)255;
+	pbase = (p->tmp_base + p->tmp_extra + 255) & ~(uint64_t)255;
+	p->tmp_extra = pbase + ngrp * pstride - p->tmp_base;
+	for (uint64_t g = 0; g < ngrp; g++) {
+		uint64_t v0 = g * LFA_TREE_GROUP, v1 = v0 + LFA_TREE_GROUP;
+		uint64_t s0 = v0 < rem ? 2 * v0 : v0 + rem;
+		uint64_t s1 = v1 < rem ? 2 * v1 : v1 + rem;
+
+		first = p_tree_begin(p);
+		for (uint64_t k = s0; k < s1; k++)
+			p_tree_src(p, tree_in_ref(in, lo + (int)k));
+		p_tree_end(p, first, ref(LFA_BUF_TMP, pbase + g * pstride), count);
+	}
+	parts.kind = 1;
+	parts.own = -1;
+	parts.base = pbase;
+	parts.stride = pstride;
+	p_tree_any(p, &parts, 0, (int)ngrp, dst, count, esz);
+}
+
 static void plan_tree_block(struct planner *p, int r, int n, size_t count,
 			    size_t esz, struct lfa_ref dst)
 {
 	size_t moff, mlen;
-	uint32_t first;
+	struct tree_in in;
 
 	lfa_coll_block(count, n, r, &moff, &mlen);
-	first = p_tree_begin(p);
-	for (int k = 0; k < n; k++)
-		p_tree_src(p, k == r ? ref(LFA_BUF_SEND, moff * esz) :
-			   ref(LFA_BUF_TMP, (uint64_t)k * blk_stride(mlen, esz)));
-	p_tree_end(p, first, dst, mlen);
+	in.kind = 0;
+	in.own = r;
+	in.own_ref = ref(LFA_BUF_SEND, moff * esz);
+	in.base = 0;
+	in.stride = blk_stride(mlen, esz);
+	p->tmp_base = n > 1 ? (uint64_t)n * blk_stride(mlen, esz) : 0;
+	p_tree_any(p, &in, 0, n, dst, mlen, esz);
 }
 
 static void plan_allgather_blocks(struct planner *p, int r, int n,
@@ -314,7 +394,7 @@ static void plan_allgather_blocks(struct planner *p, int r, int n,
 static void plan_allreduce_small(struct planner *p, int r, int n, size_t count,
 				 size_t esz, struct lfa_ref dst)
 {
-	uint32_t first;
+	struct tree_in in;
 
 	for (int k = 1; k < n; k++) {
 		int to = (r + k) % n, from = (r - k + n) % n;
@@ -324,20 +404,13 @@ static void plan_allreduce_small(struct planner *p, int r, int n, size_t count,
 		       ref(LFA_BUF_TMP, (uint64_t)from * count * esz), count * esz);
 	}
 	p_group_end(p);
-	first = p_tree_begin(p);
-	for (int k = 0; k < n; k++)
-		p_tree_src(p, k == r ? ref(LFA_BUF_SEND, 0) :
-			   ref(LFA_BUF_TMP, (uint64_t)k * count * esz));
-	p_tree_end(p, first, dst, count);
-}
-
-static uint64_t pof2_floor(uint64_t v)
-{
-	uint64_t q = 1;
-
-	while (q * 2 <= v)
-		q *= 2;
-	return q;
+	in.kind = 0;
+	in.own = r;
+	in.own_ref = ref(LFA_BUF_SEND, 0);
+	in.base = 0;
+	in.stride = (uint64_t)count * esz;
+	p->tmp_base = (uint64_t)n * count * esz;
+	p_tree_any(p, &in, 0, n, dst, count, esz);
 }
 
 /*
@@ -522,8 +595,9 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 	if (algo == LFA_ALGO_P2P) {
 		/* reducing collectives over the symmetric workspace; the rest
 		 * (pure transport) keep the RCCL schedules */
-		if (n > 1 && (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER ||
-			      coll == LFA_REDUCE)) {
+		if (n > 1 && n <= LFA_TREE_MAX && n <= LFA_PUT_MAX &&
+		    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER ||
+		     coll == LFA_REDUCE)) {
 			int ret = plan_p2p(&p, coll, r, n, root, count, esz);
 
 			if (ret)
@@ -538,7 +612,7 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 	}
 	if (algo == LFA_ALGO_TREE_COLL) {
 		/* collective transport only for even blocks of the big path */
-		int even = count % (size_t)n == 0 &&
+		int even = count % (size_t)n == 0 && n <= LFA_TREE_MAX &&
 			   !(coll == LFA_ALLREDUCE &&
 			     bytes * (size_t)n <= LFA_SMALL_AG_BYTES);
 
@@ -677,6 +751,7 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		return -LFA_ENOSYS;
 	}
 	p_group_end(&p);
+	*tmp_bytes += p.tmp_extra;      /* partials of trees over > 32 ranks */
 
 	*nsteps = p.n;
 	*nrefs = p.nr;
@@ -727,6 +802,8 @@ static int plan_make(struct plan *pl, enum lfa_collective_op coll,
 		plan_free(pl);
 	return ret;
 }
+
+static int lower_plan(const struct plan *in, int r, int n, struct plan *out);
 
 /* ====================================================================== */
 /* device helpers                                                          */
@@ -833,6 +910,9 @@ struct lfa_coll_mc {
 	uint16_t group_id;
 	uint16_t seq;
 	int is_world;
+	/* host (peer-transfer) domains: group rank -> domain rank, NULL for
+	 * the world group (prov/coll's av_set fi_addr_array) */
+	int *members;
 	/* join in flight */
 	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
 	void *join_context;
@@ -846,10 +926,16 @@ struct lfa_coll_mc {
 struct lfa_coll_domain {
 	int device, rank, nranks;
 	ncclComm_t comm;
+	int host;                       /* peer-transfer domain (host memory) */
+	struct lfa_peer_xfer_ops xops;
+	void *xctx;
 };
 
+struct hop;
+
 struct pending {
-	hipEvent_t ev;
+	hipEvent_t ev;          /* device domains */
+	struct hop *hop;        /* host domains: the operation's state */
 	void *context;
 	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
 	struct lfa_coll_mc *mc;
@@ -857,7 +943,9 @@ struct pending {
 
 struct lfa_coll_ep {
 	struct lfa_coll_domain *dom;
-	pthread_mutex_t lock;
+	pthread_mutex_t lock;       /* queue, CQ/EQ, stream enqueue order */
+	pthread_mutex_t comm_lock;  /* communicator management (split/destroy,
+				     * P2P workspace exchange), in call order */
 	hipStream_t stream;         /* executor stream (RCCL + kernels) */
 	hipStream_t copy_stream;    /* host staging copies, H2D */
 	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
@@ -870,6 +958,8 @@ struct lfa_coll_ep {
 	size_t hs_size;
 	uint64_t *barrier_host;     /* pinned ~rank for barrier */
 	void *barrier_dev;          /* 2 x uint64 */
+	void *ctl_dev;              /* P2P handle exchange, nranks records */
+	void *ctl_host;
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
 	hipEvent_t evpool[64];      /* recycled completion events */
@@ -929,11 +1019,34 @@ int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
 	return 0;
 }
 
+int lfa_coll_domain_open_host(int rank, int nranks,
+			      const struct lfa_peer_xfer_ops *ops, void *ctx,
+			      struct lfa_coll_domain **domain)
+{
+	struct lfa_coll_domain *d;
+
+	if (!domain || !ops || !ops->send || !ops->recv || !ops->test ||
+	    nranks < 1 || rank < 0 || rank >= nranks)
+		return -LFA_EINVAL;
+	d = calloc(1, sizeof(*d));
+	if (!d)
+		return -LFA_ENOMEM;
+	d->device = -1;
+	d->rank = rank;
+	d->nranks = nranks;
+	d->host = 1;
+	d->xops = *ops;
+	d->xctx = ctx;
+	*domain = d;
+	return 0;
+}
+
 int lfa_coll_domain_close(struct lfa_coll_domain *d)
 {
 	if (!d)
 		return -LFA_EINVAL;
-	ncclCommDestroy(d->comm);
+	if (!d->host)
+		ncclCommDestroy(d->comm);
 	free(d);
 	return 0;
 }
@@ -943,6 +1056,8 @@ static void ep_release(struct lfa_coll_ep *ep)
 {
 	if (ep->barrier_dev)
 		hipFree(ep->barrier_dev);
+	if (ep->ctl_dev)
+		hipFree(ep->ctl_dev);
 	if (ep->barrier_host)
 		hipHostFree(ep->barrier_host);
 	if (ep->copy_stream)
@@ -951,34 +1066,48 @@ static void ep_release(struct lfa_coll_ep *ep)
 		hipStreamDestroy(ep->d2h_stream);
 	if (ep->stream)
 		hipStreamDestroy(ep->stream);
+	free(ep->ctl_host);
 	free(ep->q);
 	pthread_mutex_destroy(&ep->lock);
+	pthread_mutex_destroy(&ep->comm_lock);
 	free(ep);
 }
+
+/* Bytes of one P2P handle-exchange record (struct sym_rec, below). */
+#define LFA_SYM_REC_BYTES 80
 
 int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 {
 	struct lfa_coll_ep *ep;
+	size_t ctl;
 
 	if (!d || !out)
 		return -LFA_EINVAL;
-	hipSetDevice(d->device);
 	ep = calloc(1, sizeof(*ep));
 	if (!ep)
 		return -LFA_ENOMEM;
 	ep->dom = d;
 	pthread_mutex_init(&ep->lock, NULL);
+	pthread_mutex_init(&ep->comm_lock, NULL);
 	ep->algo = LFA_ALGO_TREE;
 	ep->chunk = LFA_DEFAULT_CHUNK;
-	if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipStreamCreateWithFlags(&ep->d2h_stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
-	    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess) {
-		ep_release(ep);
-		return -LFA_EIO;
+	/* the P2P workspace exchange needs these on every member even when a
+	 * local allocation fails later, so they exist up front */
+	ctl = (size_t)d->nranks * LFA_SYM_REC_BYTES;
+	if (!d->host) {
+		hipSetDevice(d->device);
+		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipStreamCreateWithFlags(&ep->d2h_stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
+		    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess ||
+		    hipMalloc(&ep->ctl_dev, ctl) != hipSuccess ||
+		    !(ep->ctl_host = calloc(1, ctl))) {
+			ep_release(ep);
+			return -LFA_EIO;
+		}
+		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	}
-	ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	memset(ep->cid_mask, 0xff, sizeof(ep->cid_mask));
 	ep->cid_mask[0] &= (uint8_t)~1u;            /* world group id 0 taken */
 	ep->world.ep = ep;
@@ -996,11 +1125,22 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	return 0;
 }
 
+static void hop_free(struct hop *h);
+
 int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 {
 	if (!ep)
 		return -LFA_EINVAL;
 	lfa_coll_ep_flush(ep);
+	if (ep->dom->host) {
+		for (size_t i = 0; i < ep->qlen; i++)
+			hop_free(ep->q[(ep->qhead + i) % ep->qcap].hop);
+		free(ep->q);
+		pthread_mutex_destroy(&ep->lock);
+		pthread_mutex_destroy(&ep->comm_lock);
+		free(ep);
+		return 0;
+	}
 	/* every P2P operation ended in a barrier: no peer touches it now */
 	p2p_release(&ep->world);
 	for (size_t i = 0; i < ep->qlen; i++)
@@ -1017,11 +1157,14 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		if (ep->hs[i])
 			hipFree(ep->hs[i]);
 	hipFree(ep->barrier_dev);
+	hipFree(ep->ctl_dev);
+	free(ep->ctl_host);
 	hipHostFree(ep->barrier_host);
 	hipStreamDestroy(ep->stream);
 	hipStreamDestroy(ep->copy_stream);
 	hipStreamDestroy(ep->d2h_stream);
 	pthread_mutex_destroy(&ep->lock);
+	pthread_mutex_destroy(&ep->comm_lock);
 	free(ep);
 	return 0;
 }
@@ -1057,6 +1200,13 @@ lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep)
 lfa_addr_t lfa_mc_addr(struct lfa_coll_mc *mc)
 {
 	return (lfa_addr_t)(uintptr_t)mc;
+}
+
+int lfa_mc_group_id(struct lfa_coll_mc *mc)
+{
+	if (!mc)
+		return -LFA_EINVAL;
+	return mc->group_id < LFA_MAX_GROUP_ID ? (int)mc->group_id : -LFA_EAGAIN;
 }
 
 static struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a)
@@ -1119,16 +1269,14 @@ static void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
 		hipEventDestroy(ev);
 }
 
-static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
-			      void *context, int kind, struct lfa_coll_mc *mc)
+/* A free slot at the tail of the FIFO of in-flight operations. */
+static struct pending *queue_slot(struct lfa_coll_ep *ep)
 {
-	struct pending *p;
-
 	if (ep->qlen == ep->qcap) {
 		struct pending *nq = calloc(ep->qcap * 2, sizeof(*nq));
 
 		if (!nq)
-			return -LFA_ENOMEM;
+			return NULL;
 		for (size_t i = 0; i < ep->qlen; i++)
 			nq[i] = ep->q[(ep->qhead + i) % ep->qcap];
 		free(ep->q);
@@ -1136,7 +1284,17 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 		ep->qhead = 0;
 		ep->qcap *= 2;
 	}
-	p = &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
+	return &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
+}
+
+static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
+			      void *context, int kind, struct lfa_coll_mc *mc)
+{
+	struct pending *p = queue_slot(ep);
+
+	if (!p)
+		return -LFA_ENOMEM;
+	memset(p, 0, sizeof(*p));
 	if (ep->nev)
 		p->ev = ep->evpool[--ep->nev];
 	else if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess)
@@ -1150,6 +1308,193 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 	p->mc = mc;
 	ep->qlen++;
 	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* host (peer-transfer) executor                                          */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * One collective on a host domain: prov/coll's util_coll_operation and its
+ * work queue (ofi_coll.h:146-163), as a schedule and a program counter.
+ * A SEND/RECV group is posted once through the owner's transport and the
+ * operation resumes past its GROUP_END only when every transfer of the group
+ * has completed (prov/coll's fence, coll_coll.c:196-201); REDUCE / TREE / COPY
+ * items run inline with the host combine.
+ */
+struct hop {
+	struct plan pl;
+	struct xctx x;
+	void *tmp;
+	struct lfa_coll_mc *mc;
+	enum lfa_op op;
+	enum lfa_datatype dt;
+	uint64_t cid;           /* group_id << 16 | seq (coll_get_next_id) */
+	size_t pc;
+	void **reqs;            /* the current group's transfers; NULL = done */
+	size_t nreq, creq;
+	int posted, done, err;
+	uint64_t scratch[2];    /* barrier word and its result */
+};
+
+static void hop_free(struct hop *h)
+{
+	if (!h)
+		return;
+	plan_free(&h->pl);
+	free(h->tmp);
+	free(h->reqs);
+	free(h);
+}
+
+static int world_rank(const struct lfa_coll_mc *mc, int grank)
+{
+	return mc->members ? mc->members[grank] : grank;
+}
+
+static int host_local(struct hop *h, const struct lfa_step *st)
+{
+	switch (st->type) {
+	case LFA_STEP_REDUCE:
+		return lfa_host_write(h->op, h->dt, resolve(&h->x, st->dst),
+				      resolve(&h->x, st->src), st->count);
+	case LFA_STEP_TREE: {
+		const void *srcs[LFA_TREE_MAX];
+
+		if (st->nsrc > LFA_TREE_MAX)
+			return -LFA_EINVAL;
+		for (uint32_t k = 0; k < st->nsrc; k++)
+			srcs[k] = resolve(&h->x, h->pl.refs[st->first + k]);
+		return lfa_host_reduce_tree(h->op, h->dt, resolve(&h->x, st->dst),
+					    srcs, (int)st->nsrc, st->count);
+	}
+	case LFA_STEP_COPY:
+		memmove(resolve(&h->x, st->dst), resolve(&h->x, st->src), st->count);
+		return 0;
+	default:
+		return -LFA_EINVAL;     /* BARRIER / TREE_PUT / collectives: not planned here */
+	}
+}
+
+/* Run the operation as far as it goes: 1 done, 0 waiting on transfers, <0. */
+static int host_advance(struct lfa_coll_ep *ep, struct hop *h)
+{
+	const struct lfa_peer_xfer_ops *xo = &ep->dom->xops;
+	void *xc = ep->dom->xctx;
+
+	while (h->pc < h->pl.nsteps) {
+		const struct lfa_step *st = &h->pl.steps[h->pc];
+		size_t end;
+		int ret, pending = 0;
+
+		if (st->type == LFA_STEP_GROUP_END) {
+			h->pc++;
+			continue;
+		}
+		if (st->type != LFA_STEP_SEND && st->type != LFA_STEP_RECV) {
+			ret = host_local(h, st);
+			if (ret)
+				return ret;
+			h->pc++;
+			continue;
+		}
+		for (end = h->pc; end < h->pl.nsteps &&
+		     h->pl.steps[end].type != LFA_STEP_GROUP_END; end++)
+			;
+		if (!h->posted) {
+			size_t need = end - h->pc;
+
+			if (need > h->creq) {
+				void **nr = realloc(h->reqs, need * sizeof(*nr));
+
+				if (!nr)
+					return -LFA_ENOMEM;
+				h->reqs = nr;
+				h->creq = need;
+			}
+			h->nreq = 0;
+			for (size_t i = h->pc; i < end; i++) {
+				const struct lfa_step *x = &h->pl.steps[i];
+				void **rq = &h->reqs[h->nreq];
+
+				*rq = NULL;
+				if (x->type == LFA_STEP_SEND)
+					ret = xo->send(xc, world_rank(h->mc, x->peer),
+						       resolve(&h->x, x->src), x->count,
+						       h->cid | (uint64_t)h->mc->rank << 32, rq);
+				else
+					ret = xo->recv(xc, world_rank(h->mc, x->peer),
+						       resolve(&h->x, x->dst), x->count,
+						       h->cid | (uint64_t)x->peer << 32, rq);
+				h->nreq++;
+				if (ret)
+					return ret;
+			}
+			h->posted = 1;
+		}
+		for (size_t i = 0; i < h->nreq; i++) {
+			if (!h->reqs[i])
+				continue;
+			ret = xo->test(xc, h->reqs[i]);
+			if (ret < 0)
+				return ret;
+			if (ret)
+				h->reqs[i] = NULL;
+			else
+				pending = 1;
+		}
+		if (pending)
+			return 0;
+		h->posted = 0;
+		h->pc = end < h->pl.nsteps ? end + 1 : end;
+	}
+	return 1;
+}
+
+/* Advance every in-flight host operation (ep->lock held). */
+static void host_progress_all(struct lfa_coll_ep *ep)
+{
+	for (size_t i = 0; i < ep->qlen; i++) {
+		struct hop *h = ep->q[(ep->qhead + i) % ep->qcap].hop;
+		int ret;
+
+		if (!h || h->done || h->err)
+			continue;
+		ret = host_advance(ep, h);
+		if (ret < 0)
+			h->err = ret;
+		else if (ret)
+			h->done = 1;
+	}
+}
+
+static int enqueue_host(struct lfa_coll_ep *ep, struct hop *h, void *context,
+			int kind, struct lfa_coll_mc *mc)
+{
+	struct pending *p = queue_slot(ep);
+
+	if (!p)
+		return -LFA_ENOMEM;
+	memset(p, 0, sizeof(*p));
+	p->hop = h;
+	p->context = context;
+	p->kind = kind;
+	p->mc = mc;
+	ep->qlen++;
+	/* kick: run up to the first transfer now (coll_progress_work) */
+	host_progress_all(ep);
+	return 0;
+}
+
+static void free_mask(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
+{
+	if (!mc->mask_host)
+		return;
+	if (ep->dom->host)
+		free(mc->mask_host);
+	else
+		hipHostFree(mc->mask_host);
+	mc->mask_host = NULL;
 }
 
 static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
@@ -1169,8 +1514,7 @@ static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
 		ep->cid_mask[gid / 8] &= (uint8_t)~(1u << (gid % 8));
 	}
 	mc->seq = 0;
-	hipHostFree(mc->mask_host);
-	mc->mask_host = NULL;
+	free_mask(ep, mc);
 	if (ep->eqn < 64) {
 		size_t i = (ep->eqh + ep->eqn) % 64;
 
@@ -1182,24 +1526,57 @@ static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
 	}
 }
 
+/* Completion state of a queued operation: 0 done, 1 pending, <0 / hip error
+ * code (>0 in *perr) failed. */
+static int pending_state(const struct pending *p, int *perr)
+{
+	if (p->hop) {
+		if (p->hop->err) {
+			*perr = -p->hop->err;
+			return -1;
+		}
+		return p->hop->done ? 0 : 1;
+	}
+	hipError_t e = hipEventQuery(p->ev);
+
+	if (e == hipErrorNotReady)
+		return 1;
+	if (e != hipSuccess) {
+		*perr = (int)e;
+		return -1;
+	}
+	return 0;
+}
+
+static void pending_release(struct lfa_coll_ep *ep, struct pending *p)
+{
+	if (p->hop)
+		hop_free(p->hop);
+	else
+		release_event(ep, p->ev);
+	p->hop = NULL;
+}
+
 /* Reap completed operations in issue order. */
 static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 		     size_t count, size_t *nout)
 {
 	*nout = 0;
+	if (ep->dom->host)
+		host_progress_all(ep);
 	while (ep->qlen && !ep->have_err) {
 		struct pending *p = &ep->q[ep->qhead];
-		hipError_t e = hipEventQuery(p->ev);
+		int perr = 0, st = pending_state(p, &perr);
 
-		if (e == hipErrorNotReady)
+		if (st > 0)
 			break;
-		if (p->kind == 0 && e == hipSuccess && *nout >= count)
+		if (p->kind == 0 && st == 0 && *nout >= count)
 			break;
-		if (e != hipSuccess) {
+		if (st < 0) {
 			ep->err.op_context = p->context;
 			ep->err.flags = LFA_COLLECTIVE;
-			ep->err.err = LFA_EIO;
-			ep->err.prov_errno = (int)e;
+			ep->err.err = p->hop ? perr : LFA_EIO;
+			ep->err.prov_errno = perr;
 			ep->have_err = 1;
 		} else if (p->kind == 1) {
 			join_finish(ep, p->mc);
@@ -1212,7 +1589,7 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			c->op_context = p->context;
 			c->flags = LFA_COLLECTIVE;
 		}
-		release_event(ep, p->ev);
+		pending_release(ep, p);
 		ep->qhead = (ep->qhead + 1) % ep->qcap;
 		ep->qlen--;
 	}
@@ -1229,7 +1606,7 @@ ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
 		return -LFA_EINVAL;
 	pthread_mutex_lock(&ep->lock);
 	progress(ep, buf, count, &n);
-	if (!n && !ep->have_err &&
+	if (!n && !ep->have_err && !ep->dom->host &&
 	    ncclCommGetAsyncError(ep->dom->comm, &async) == ncclSuccess &&
 	    async != ncclSuccess && async != ncclInProgress) {
 		ep->err.op_context = ep->qlen ? ep->q[ep->qhead].context : NULL;
@@ -1273,11 +1650,15 @@ ssize_t lfa_eq_read(struct lfa_coll_ep *ep, uint32_t *event,
 	pthread_mutex_lock(&ep->lock);
 	/* progress joins only up to the first collective completion */
 	while (ep->qlen && ep->q[ep->qhead].kind == 1 && !ep->have_err) {
+		int perr;
+
 		progress(ep, tmp, 0, &n);
 		if (ep->qlen && ep->q[ep->qhead].kind == 1 &&
-		    hipEventQuery(ep->q[ep->qhead].ev) == hipErrorNotReady)
+		    pending_state(&ep->q[ep->qhead], &perr) > 0)
 			break;
 	}
+	if (ep->dom->host && !(ep->qlen && ep->q[ep->qhead].kind == 1))
+		host_progress_all(ep);
 	if (ep->eqn) {
 		*event = ep->eq[ep->eqh].event;
 		*entry = ep->eq[ep->eqh].entry;
@@ -1293,6 +1674,29 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 {
 	if (!ep)
 		return -LFA_EINVAL;
+	if (ep->dom->host) {
+		/* drive the transfers until every queued operation finished */
+		for (;;) {
+			int busy = 0, err = 0;
+
+			pthread_mutex_lock(&ep->lock);
+			host_progress_all(ep);
+			for (size_t i = 0; i < ep->qlen; i++) {
+				struct hop *h = ep->q[(ep->qhead + i) % ep->qcap].hop;
+
+				if (h && h->err)
+					err = h->err;
+				else if (h && !h->done)
+					busy = 1;
+			}
+			pthread_mutex_unlock(&ep->lock);
+			if (err)
+				return err;
+			if (!busy)
+				return 0;
+			sched_yield();
+		}
+	}
 	return hipStreamSynchronize(ep->stream) == hipSuccess &&
 	       hipStreamSynchronize(ep->copy_stream) == hipSuccess &&
 	       hipStreamSynchronize(ep->d2h_stream) == hipSuccess ? 0 : -LFA_EIO;
@@ -1392,13 +1796,15 @@ static void p2p_release(struct lfa_coll_mc *mc)
 	mc->sym_region = 0;
 }
 
+_Static_assert(sizeof(struct sym_rec) <= LFA_SYM_REC_BYTES, "sym_rec");
+
 static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 {
 	struct lfa_coll_ep *ep = mc->ep;
-	struct sym_rec *recs;
-	void *drec = NULL;
+	struct sym_rec *recs = ep->ctl_host;    /* nranks records, from ep open */
+	void *drec = ep->ctl_dev;
 	const size_t rb = sizeof(struct sym_rec);
-	int n = mc->size, ret = 0;
+	int n = mc->size, ret = 0, ok;
 
 	if (region <= mc->sym_region)
 		return 0;
@@ -1407,24 +1813,24 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 	if (region < (8u << 20))
 		region = 8u << 20;
 	region = (region + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-	if (hipStreamSynchronize(ep->stream) != hipSuccess)
-		return -LFA_EIO;
+	/*
+	 * A local failure (the old workspace still busy, no memory for the
+	 * new one or its peer table, no IPC handle) is not returned before the
+	 * collective steps below: this rank still takes part in them with
+	 * ok = 0, so every member fails together instead of leaving its peers
+	 * waiting in the allgather.
+	 */
+	ok = hipStreamSynchronize(ep->stream) == hipSuccess;
 	p2p_release(mc);
+	memset(recs, 0, (size_t)n * rb);
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
-	recs = calloc((size_t)n, rb);
-	/* host-side failures here are identical on every member only by
-	 * accident; they are out-of-memory conditions of the process */
-	if (!mc->sym || !recs || hipMalloc(&drec, (size_t)n * rb) != hipSuccess) {
-		free(recs);
-		p2p_release(mc);
-		return -LFA_ENOMEM;
-	}
-	recs[mc->rank].ok = hipMalloc((void **)&mc->sym_local, 2 * region) == hipSuccess;
-	if (!recs[mc->rank].ok)
+	ok = ok && mc->sym;
+	ok = ok && hipMalloc((void **)&mc->sym_local, 2 * region) == hipSuccess;
+	if (!ok)
 		mc->sym_local = NULL;
-	if (recs[mc->rank].ok && n > 1)
-		recs[mc->rank].ok = hipIpcGetMemHandle(&recs[mc->rank].h,
-						       mc->sym_local) == hipSuccess;
+	if (ok && n > 1)
+		ok = hipIpcGetMemHandle(&recs[mc->rank].h, mc->sym_local) == hipSuccess;
+	recs[mc->rank].ok = ok;
 	if (n > 1 &&
 	    (hipMemcpyAsync((char *)drec + (size_t)mc->rank * rb, &recs[mc->rank], rb,
 			    hipMemcpyHostToDevice, ep->stream) != hipSuccess ||
@@ -1448,19 +1854,17 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 	}
 	if (n > 1) {
 		/* agree that every member mapped every peer (MIN of the flags) */
-		int32_t ok = ret == 0;
+		int32_t all = ret == 0;
 
-		if (hipMemcpyAsync(drec, &ok, sizeof(ok), hipMemcpyHostToDevice,
+		if (hipMemcpyAsync(drec, &all, sizeof(all), hipMemcpyHostToDevice,
 				   ep->stream) != hipSuccess ||
 		    ncclAllReduce(drec, drec, 1, ncclInt32, ncclMin, mc->comm,
 				  ep->stream) != ncclSuccess ||
-		    hipMemcpyAsync(&ok, drec, sizeof(ok), hipMemcpyDeviceToHost,
+		    hipMemcpyAsync(&all, drec, sizeof(all), hipMemcpyDeviceToHost,
 				   ep->stream) != hipSuccess ||
-		    hipStreamSynchronize(ep->stream) != hipSuccess || !ok)
+		    hipStreamSynchronize(ep->stream) != hipSuccess || !all)
 			ret = ret ? ret : -LFA_EIO;
 	}
-	hipFree(drec);
-	free(recs);
 	if (ret) {
 		p2p_release(mc);
 		return ret;
@@ -1505,6 +1909,12 @@ static int try_rccl(struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 	ncclResult_t r;
 
 	if (!rccl_type(dt, &t) || !rccl_op(op, &o))
+		return 0;
+	/* float MIN/MAX: RCCL's NaN and signed-zero rules are its own, not
+	 * libfabric's dst-biased compare (util_atomic.c:291-316); the tree
+	 * keeps the reference's bits */
+	if ((op == LFA_MIN || op == LFA_MAX) &&
+	    (dt == LFA_FLOAT || dt == LFA_DOUBLE))
 		return 0;
 	switch (coll) {
 	case LFA_ALLREDUCE:
@@ -1618,7 +2028,12 @@ int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
 	per = chunk_bytes / esz / nb;
 	if (!per)
 		per = 1;
-	if (per > span)
+	/* N > 1: one chunk, the whole buffer.  Every member then issues the
+	 * same device schedule as for device buffers, whatever its memory type
+	 * or chunk setting — chunking is a local choice the peers cannot see
+	 * (mixed host/device ranks would issue different RCCL
+	 * schedules and hang). */
+	if (per > span || nranks > 1)
 		per = span;
 	if (!per || idx >= (span + per - 1) / per)
 		return 0;
@@ -1751,6 +2166,66 @@ static int group_rank(struct lfa_coll_mc *mc, lfa_addr_t a)
 	return (int)a;
 }
 
+/* Can this rank issue collectives on the group? */
+static int mc_member(const struct lfa_coll_mc *mc)
+{
+	return mc->rank >= 0 && (mc->ep->dom->host || mc->comm);
+}
+
+/* Schedule `h` for one collective on a host domain: the algorithm's plan
+ * (P2P / RCCL run as TREE; TREE_COLL's collective items lowered to grouped
+ * sends/receives) and its own TMP, so operations may overlap. */
+static int host_start(struct lfa_coll_ep *ep, struct hop *h,
+		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
+		      const void *buf, void *result, size_t count, int root,
+		      enum lfa_datatype dt, enum lfa_op op)
+{
+	enum lfa_coll_algo algo = ep->algo;
+	size_t esz = lfa_datatype_size(dt);
+	struct plan raw;
+	int ret;
+
+	if (algo == LFA_ALGO_P2P || algo == LFA_ALGO_RCCL)
+		algo = LFA_ALGO_TREE;
+	ret = plan_make(&raw, coll, algo, mc->rank, mc->size, root, count, esz);
+	if (ret)
+		return ret;
+	ret = lower_plan(&raw, mc->rank, mc->size, &h->pl);
+	plan_free(&raw);
+	if (ret)
+		return ret;
+	if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp)))
+		return -LFA_ENOMEM;
+	h->mc = mc;
+	h->op = op;
+	h->dt = dt;
+	h->cid = (uint64_t)mc->group_id << 16 | (uint16_t)(mc->seq - 1);
+	h->x.base[LFA_BUF_SEND] = coll == LFA_BROADCAST ? result : (void *)buf;
+	h->x.base[LFA_BUF_RESULT] = result;
+	h->x.base[LFA_BUF_TMP] = h->tmp;
+	return 0;
+}
+
+static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+		       enum lfa_collective_op coll, const void *buf,
+		       void *result, size_t count, int root,
+		       enum lfa_datatype dt, enum lfa_op op, void *context,
+		       int kind, struct lfa_coll_mc *jmc)
+{
+	struct hop *h = calloc(1, sizeof(*h));
+	int ret;
+
+	if (!h)
+		return -LFA_ENOMEM;
+	mc->seq++;                              /* coll_get_next_id :48-52 */
+	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op);
+	if (!ret)
+		ret = enqueue_host(ep, h, context, kind, jmc);
+	if (ret)
+		hop_free(h);
+	return ret;
+}
+
 static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		      const void *buf, size_t count, void *result,
 		      lfa_addr_t coll_addr, lfa_addr_t root_addr,
@@ -1763,7 +2238,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	if (!ep)
 		return -LFA_EINVAL;
 	mc = mc_of(ep, coll_addr);
-	if (!mc || !mc->comm || mc->rank < 0)
+	if (!mc || !mc_member(mc))
 		return -LFA_EINVAL;   /* not a member of this group */
 	esz = lfa_datatype_size(dt);
 	if (!esz)
@@ -1780,6 +2255,12 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 			return ret;
 	}
 	pthread_mutex_lock(&ep->lock);
+	if (ep->dom->host) {
+		ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
+				  context, 0, NULL);
+		pthread_mutex_unlock(&ep->lock);
+		return ret;
+	}
 	hipSetDevice(ep->dom->device);
 	mc->seq++;                              /* coll_get_next_id :48-52 */
 	host = (buf && count && !is_device_ptr(buf)) ||
@@ -1789,9 +2270,13 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	} else if (!host) {
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
 				 ep->stream);
-	} else if (coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
-		   coll == LFA_REDUCE ||
-		   (coll == LFA_REDUCE_SCATTER && !(count % mc->size))) {
+	} else if ((coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
+		    coll == LFA_REDUCE ||
+		    (coll == LFA_REDUCE_SCATTER && !(count % mc->size)))) {
+		/* chunked at N = 1 only (lfa_coll_host_chunk): at N > 1 the one
+		 * chunk is the whole buffer, so the device schedule is the same
+		 * as for device buffers whatever memory type or chunk size the
+		 * other members use */
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op);
 	} else {
@@ -1900,9 +2385,26 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	if (!ep)
 		return -LFA_EINVAL;
 	mc = mc_of(ep, coll_addr);
-	if (!mc->comm || mc->rank < 0)
+	if (!mc_member(mc))
 		return -LFA_EINVAL;
 	pthread_mutex_lock(&ep->lock);
+	if (ep->dom->host) {
+		struct hop *h = calloc(1, sizeof(*h));
+
+		ret = h ? 0 : -LFA_ENOMEM;
+		if (!ret) {
+			h->scratch[0] = ~(uint64_t)mc->rank;
+			mc->seq++;
+			ret = host_start(ep, h, mc, LFA_ALLREDUCE, &h->scratch[0],
+					 &h->scratch[1], 1, -1, LFA_UINT64, LFA_BAND);
+			if (!ret)
+				ret = enqueue_host(ep, h, context, 0, NULL);
+			if (ret)
+				hop_free(h);
+		}
+		pthread_mutex_unlock(&ep->lock);
+		return ret;
+	}
 	hipSetDevice(ep->dom->device);
 	ep->barrier_host[0] = ~(uint64_t)mc->rank;
 	ret = hipMemcpyAsync(ep->barrier_dev, ep->barrier_host, sizeof(uint64_t),
@@ -1927,14 +2429,17 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			struct lfa_coll_mc **mcp, void *context)
 {
 	struct lfa_coll_mc *parent, *mc;
-	int member = 0, pos = -1, ret;
+	int member = 0, pos = -1, ret = 0, host;
 	void *dmask;
 
 	if (!ep || !mcp)
 		return -LFA_EINVAL;
 	if (flags & ~LFA_COLLECTIVE)
 		return -LFA_EBADFLAGS;
+	host = ep->dom->host;
 	parent = mc_of(ep, coll_addr);
+	if (!mc_member(parent))
+		return -LFA_EINVAL;
 	if (ranks) {
 		for (size_t i = 0; i < nmembers; i++) {
 			if (ranks[i] < 0 || ranks[i] >= parent->size ||
@@ -1955,24 +2460,47 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		return -LFA_ENOMEM;
 	mc->ep = ep;
 	mc->join_context = context;
-	pthread_mutex_lock(&ep->lock);
-	hipSetDevice(ep->dom->device);
+	mc->group_id = LFA_MAX_GROUP_ID;        /* none until the join completes */
 	if (!ranks) {
 		mc->comm = parent->comm;
 		mc->rank = parent->rank;
 		mc->size = parent->size;
+		if (host && parent->members) {
+			mc->members = malloc(nmembers * sizeof(*mc->members));
+			if (!mc->members)
+				ret = -LFA_ENOMEM;
+			else
+				memcpy(mc->members, parent->members,
+				       nmembers * sizeof(*mc->members));
+		}
+	} else if (host) {
+		/* prov/coll's av_set: group rank -> the owner's address (here
+		 * the domain rank) */
+		mc->rank = pos;
+		mc->size = (int)nmembers;
+		mc->members = malloc(nmembers * sizeof(*mc->members));
+		if (!mc->members)
+			ret = -LFA_ENOMEM;
+		for (size_t i = 0; !ret && i < nmembers; i++)
+			mc->members[i] = world_rank(parent, ranks[i]);
 	} else {
-		/* every parent rank takes part in the split (non-members with
-		 * NCCL_SPLIT_NOCOLOR) */
+		/*
+		 * Every parent rank takes part in the split (non-members with
+		 * NCCL_SPLIT_NOCOLOR).  The split is a blocking rendezvous of the
+		 * parent's members; it is issued under comm_lock, in this rank's
+		 * call order, and NOT under ep->lock, so completions keep being
+		 * reaped (lfa_cq_read, e.g. from off_lfa's progress thread)
+		 * while the members meet (DESIGN.md §6 "ordering").
+		 */
 		ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
 
+		pthread_mutex_lock(&ep->comm_lock);
+		hipSetDevice(ep->dom->device);
 		if (ncclCommSplit(parent->comm, member ? 0 : NCCL_SPLIT_NOCOLOR,
-				  parent->rank, &mc->comm, &cfg) != ncclSuccess) {
-			pthread_mutex_unlock(&ep->lock);
-			free(mc);
-			return -LFA_EIO;
-		}
-		mc->owns_comm = 1;
+				  parent->rank, &mc->comm, &cfg) != ncclSuccess)
+			ret = -LFA_EIO;
+		pthread_mutex_unlock(&ep->comm_lock);
+		mc->owns_comm = !ret;
 		mc->rank = pos;
 		mc->size = (int)nmembers;
 	}
@@ -1987,32 +2515,51 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		mc->rank = -1;
 		mc->size = (int)nmembers;
 	}
+	pthread_mutex_lock(&ep->lock);
 	/* agree on the group id: BAND of the free-id masks over the PARENT
 	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 */
-	ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) == hipSuccess ?
-	      0 : -LFA_ENOMEM;
-	if (!ret && grow_staging(ep, 4 * LFA_CID_BYTES))
-		ret = -LFA_ENOMEM;
-	if (!ret) {
-		dmask = ep->hs[0];
-		memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
-		hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
-			       hipMemcpyHostToDevice, ep->stream);
-		ret = run_device(ep, parent, LFA_ALLREDUCE, dmask,
-				 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
-				 LFA_UINT8, LFA_BAND, ep->stream);
+	if (!ret && host) {
+		mc->mask_host = malloc(2 * LFA_CID_BYTES);
+		if (!mc->mask_host)
+			ret = -LFA_ENOMEM;
+		if (!ret) {
+			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
+			ret = host_submit(ep, parent, LFA_ALLREDUCE,
+					  mc->mask_host + LFA_CID_BYTES, mc->mask_host,
+					  LFA_CID_BYTES, -1, LFA_UINT8, LFA_BAND,
+					  context, 1, mc);
+		}
+	} else if (!ret) {
+		hipSetDevice(ep->dom->device);
+		ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) ==
+		      hipSuccess ? 0 : -LFA_ENOMEM;
+		if (!ret && grow_staging(ep, 4 * LFA_CID_BYTES))
+			ret = -LFA_ENOMEM;
+		if (!ret) {
+			dmask = ep->hs[0];
+			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
+			hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
+				       hipMemcpyHostToDevice, ep->stream);
+			ret = run_device(ep, parent, LFA_ALLREDUCE, dmask,
+					 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
+					 LFA_UINT8, LFA_BAND, ep->stream);
+			if (!ret)
+				hipMemcpyAsync(mc->mask_host, (char *)dmask + LFA_CID_BYTES,
+					       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
+		}
 		if (!ret)
-			hipMemcpyAsync(mc->mask_host, (char *)dmask + LFA_CID_BYTES,
-				       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
+			ret = enqueue_completion(ep, ep->stream, context, 1, mc);
 	}
-	if (!ret)
-		ret = enqueue_completion(ep, ep->stream, context, 1, mc);
+	if (ret)
+		free_mask(ep, mc);
 	pthread_mutex_unlock(&ep->lock);
 	if (ret) {
-		if (mc->owns_comm && mc->comm)
+		if (mc->owns_comm && mc->comm) {
+			pthread_mutex_lock(&ep->comm_lock);
 			ncclCommDestroy(mc->comm);
-		if (mc->mask_host)
-			hipHostFree(mc->mask_host);
+			pthread_mutex_unlock(&ep->comm_lock);
+		}
+		free(mc->members);
 		free(mc);
 		return ret;
 	}
@@ -2022,29 +2569,38 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 
 int lfa_mc_close(struct lfa_coll_mc *mc)
 {
+	struct lfa_coll_ep *ep;
+
 	if (!mc)
 		return -LFA_EINVAL;
 	if (mc->is_world)
 		return -LFA_EINVAL;
-	lfa_coll_ep_flush(mc->ep);
+	ep = mc->ep;
+	lfa_coll_ep_flush(ep);
 	/* a join still queued for this handle completes without it */
-	pthread_mutex_lock(&mc->ep->lock);
-	for (size_t i = 0; i < mc->ep->qlen; i++) {
-		struct pending *p = &mc->ep->q[(mc->ep->qhead + i) % mc->ep->qcap];
+	pthread_mutex_lock(&ep->lock);
+	for (size_t i = 0; i < ep->qlen; i++) {
+		struct pending *p = &ep->q[(ep->qhead + i) % ep->qcap];
 
 		if (p->kind == 1 && p->mc == mc) {
 			p->kind = 2;
 			p->mc = NULL;
 		}
 	}
-	pthread_mutex_unlock(&mc->ep->lock);
-	if (mc->mask_host)
-		hipHostFree(mc->mask_host);
-	p2p_release(mc);
-	if (mc->owns_comm && mc->comm)
-		ncclCommDestroy(mc->comm);
+	free_mask(ep, mc);
+	/* release the group id only if the join assigned one (a
+	 * never-completed join must not free the world's reserved id 0) */
 	if (mc->group_id < LFA_MAX_GROUP_ID)
-		mc->ep->cid_mask[mc->group_id / 8] |= (uint8_t)(1u << (mc->group_id % 8));
+		ep->cid_mask[mc->group_id / 8] |= (uint8_t)(1u << (mc->group_id % 8));
+	pthread_mutex_unlock(&ep->lock);
+	if (!ep->dom->host) {
+		pthread_mutex_lock(&ep->comm_lock);
+		p2p_release(mc);
+		if (mc->owns_comm && mc->comm)
+			ncclCommDestroy(mc->comm);
+		pthread_mutex_unlock(&ep->comm_lock);
+	}
+	free(mc->members);
 	free(mc);
 	return 0;
 }

@@ -1,0 +1,257 @@
+"""The C executor and the C join at N > 1, on CPU: 1, 2 and 3 processes.
+
+Every process opens a peer-transfer domain (lfa_coll_domain_open_host): the
+collective provider (liblfa_coll.so) builds its schedules, posts their
+SEND/RECV items through the transport callbacks — here torch.distributed
+gloo isend/irecv, standing in for the owner provider's FI_PEER_TRANSFER
+tagged messages (coll_coll.c:770-814) — and runs REDUCE / TREE items with the
+product's host combine (lfa_host_write / lfa_host_reduce_tree).  Progress is
+lfa_cq_read, as in prov/coll.  Results must match the oracle bit for bit.
+The oracle is only the checker here.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class GlooXfer:
+    """The owner's tagged transport, over gloo.  prov/coll's tag
+    (cid | sender << 32) is folded into gloo's 31-bit tag space."""
+
+    def __init__(self):
+        self.reqs, self.next = {}, 1
+        self.sent = self.received = 0
+
+    @staticmethod
+    def _tag(tag):
+        return ((tag >> 32) & 0x7F) << 24 | (tag & 0xFFFFFF)
+
+    def _put(self, v):
+        h = self.next
+        self.next += 1
+        self.reqs[h] = v
+        return h
+
+    def send(self, peer, ptr, nbytes, tag):
+        t = torch.frombuffer(bytearray(ctypes.string_at(ptr, nbytes)), dtype=torch.uint8)
+        self.sent += nbytes
+        return self._put((dist.isend(t, peer, tag=self._tag(tag)), t, None, 0))
+
+    def recv(self, peer, ptr, nbytes, tag):
+        t = torch.empty(nbytes, dtype=torch.uint8)
+        return self._put((dist.irecv(t, peer, tag=self._tag(tag)), t, ptr, nbytes))
+
+    def test(self, h):
+        # gloo's send/recv Work objects only report completion through
+        # wait(); every transfer of a group is posted before the executor
+        # tests any, so waiting here cannot deadlock the schedule
+        w, t, ptr, n = self.reqs[h]
+        w.wait()
+        if ptr:
+            ctypes.memmove(ptr, t.data_ptr(), n)
+            self.received += n
+        del self.reqs[h]
+        return 1
+
+
+def _inputs(oracle, dt, count, world, seed):
+    nd = oracle.DT_NP[dt]
+    rng = np.random.default_rng(seed)
+    if nd.kind == "f":
+        return [rng.uniform(0.9, 1.1, count).astype(nd) for _ in range(world)]
+    return [rng.integers(0, 255, count).astype(nd) for _ in range(world)]
+
+
+def _collectives(ep, rank, world, oracle, coll):
+    """Every fi_ops_collective slot, every algorithm, ragged counts."""
+    for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL, coll.ALGO_P2P,
+                 coll.ALGO_RCCL):
+        ep.set_algo(algo)
+        for dt, op, count in ((8, 2, 70_001), (8, 2, 1000), (6, 0, 5), (1, 7, 3),
+                              (9, 3, 4099), (6, 6, 6 * 1000), (10, 3, 33)):
+            sends = _inputs(oracle, dt, count, world, 1234 + count + algo)
+            want = oracle.allreduce(op, dt, sends)[0]
+            nd = sends[0].dtype
+            # allreduce
+            res = np.zeros(count, nd)
+            ep.wait(ep.allreduce(sends[rank], res, count, dt, op))
+            assert res.tobytes() == want.tobytes(), f"allreduce algo={algo} dt={dt} n={count}"
+            # reduce_scatter (block r of the allreduce)
+            off, ln = coll.block(count, world, rank)
+            res = np.zeros(max(ln, 1), nd)
+            ep.wait(ep.reduce_scatter(sends[rank], res, count, dt, op))
+            assert res[:ln].tobytes() == want[off:off + ln].tobytes(), "reduce_scatter"
+            # reduce to every root
+            for root in range(world):
+                res = np.zeros(count, nd)
+                ep.wait(ep.reduce(sends[rank], res, count, root, dt, op))
+                if rank == root:
+                    assert res.tobytes() == want.tobytes(), f"reduce root={root}"
+        # data movement
+        x = np.arange(10, dtype=np.int32) + 100 * rank
+        res = np.zeros(10 * world, np.int32)
+        ep.wait(ep.allgather(x, res, 10, 4))
+        assert np.array_equal(res, np.concatenate([np.arange(10) + 100 * k
+                                                   for k in range(world)]))
+        for root in range(world):
+            b = np.arange(7, dtype=np.float64) * (root + 1) if rank == root else np.zeros(7)
+            ep.wait(ep.broadcast(b, 7, root, 9))
+            assert np.array_equal(b, np.arange(7) * (root + 1))
+            src = (np.arange(5 * world, dtype=np.int64) if rank == root
+                   else np.zeros(5 * world, np.int64))
+            res = np.zeros(5, np.int64)
+            ep.wait(ep.scatter(src, res, 5, root, 6))
+            assert np.array_equal(res, np.arange(5) + 5 * rank)
+        ep.wait(ep.barrier())
+    ep.set_algo(coll.ALGO_TREE)
+
+
+def _overlap(ep, rank, world, oracle):
+    """Several operations in flight at once: each progresses on its own tag
+    (cid = group_id << 16 | seq) and completes in issue order."""
+    outs, wants, ctxs = [], [], []
+    for k in range(5):
+        sends = _inputs(oracle, 8, 3000 + k, world, 77 + k)
+        want = oracle.allreduce(2, 8, sends)[0]
+        res = np.zeros_like(want)
+        ctxs.append(ep.allreduce(sends[rank], res, res.size, 8, 2))
+        outs.append((res, sends))
+        wants.append(want)
+    done = []
+    while len(done) < len(ctxs):
+        done += ep.cq_read()
+    assert done == ctxs, "completion order"
+    for (res, _), want in zip(outs, wants):
+        assert res.tobytes() == want.tobytes()
+
+
+def _joins(ep, rank, world, oracle):
+    """fi_join_collective: the cid-mask BAND allreduce over the parent, the
+    lowest common free id, subset membership (coll_coll.c:912-995)."""
+    assert ep.group_id(ep.world) == 0
+    # world join
+    mc, ctx = ep.join()
+    ev = ep.wait_join()
+    assert ev[0] == 6 and ev[2] == ctx
+    gid_world = ep.group_id(mc)
+    assert gid_world == 1            # id 0 is the world group
+    # subset: the first and the last rank
+    members = sorted({0, world - 1})
+    sub, ctx2 = ep.join(members)
+    ev = ep.wait_join()
+    assert ev[2] == ctx2
+    assert ep.group_id(sub) == 2
+    addr = ep.mc_addr(sub)
+    if rank in members:
+        pos = members.index(rank)
+        sends = _inputs(oracle, 9, 2001, world, 5)
+        mine = [sends[m] for m in members]
+        want = oracle.allreduce(3, 9, mine)[0]
+        res = np.zeros(2001)
+        ep.wait(ep.allreduce(mine[pos], res, 2001, 9, 3, coll_addr=addr))
+        assert res.tobytes() == want.tobytes()
+        # reduce to the last group rank of the subset
+        root = len(members) - 1
+        res = np.zeros(2001)
+        ep.wait(ep.reduce(mine[pos], res, 2001, root, 9, 3, coll_addr=addr))
+        if pos == root:
+            assert res.tobytes() == want.tobytes()
+        ep.wait(ep.barrier(coll_addr=addr))
+    else:
+        from libfabric_amd.coll import CollError
+        with pytest.raises(CollError):
+            ep.allreduce(np.zeros(4), np.zeros(4), 4, 9, 2, coll_addr=addr)
+    # a join on the subgroup (parent = subset): members only
+    if rank in members:
+        sub2, _ = ep.join(None, coll_addr=addr)
+        ep.wait_join()
+        assert ep.group_id(sub2) == 3
+        x = np.array([rank + 1], np.uint64)
+        res = np.zeros(1, np.uint64)
+        ep.wait(ep.allreduce(x, res, 1, 7, 2, coll_addr=ep.mc_addr(sub2)))
+        assert int(res[0]) == sum(m + 1 for m in members)
+        from libfabric_amd import coll
+        coll.lib().lfa_mc_close(sub2)
+    # closing frees the id: the next world join reuses 1
+    from libfabric_amd import coll
+    assert coll.lib().lfa_mc_close(mc) == 0
+    mc3, _ = ep.join()
+    ep.wait_join()
+    assert ep.group_id(mc3) == 1
+    coll.lib().lfa_mc_close(mc3)
+    coll.lib().lfa_mc_close(sub)
+    # the known answer of fabtests/multinode/src/core_coll.c:230-277
+    x = np.array([1234 + rank], np.uint64)
+    res = np.zeros(1, np.uint64)
+    ep.wait(ep.allreduce(x, res, 1, 7, 2))
+    assert int(res[0]) == sum(1234 + k for k in range(world))
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from libfabric_amd import coll
+        xfer = GlooXfer()
+        ep = coll.HostEndpoint(rank, world, xfer)
+        try:
+            _collectives(ep, rank, world, oracle, coll)
+            _overlap(ep, rank, world, oracle)
+            _joins(ep, rank, world, oracle)
+            if world > 1:
+                assert xfer.sent > 0 and xfer.received > 0
+            assert not xfer.reqs, "transfers left behind"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_c_executor_across_processes(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=150)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
+
+
+def test_host_domain_errors():
+    from libfabric_amd import coll
+    L = coll.lib()
+    d = ctypes.c_void_p()
+    ops = coll.PeerXferOps()
+    assert L.lfa_coll_domain_open_host(0, 1, None, None, ctypes.byref(d)) == -22
+    assert L.lfa_coll_domain_open_host(2, 2, ctypes.byref(ops), None, ctypes.byref(d)) == -22

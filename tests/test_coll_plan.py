@@ -282,3 +282,84 @@ def test_host_chunk_rejects_unchunked_collectives():
     with pytest.raises(coll.CollError):
         coll.host_chunks(ALLGATHER, 10, 2, 8, 1 << 20)
     assert coll.host_chunks(ALLREDUCE, 0, 2, 8, 1 << 20) == []
+
+
+# ------------------------------------------------ groups above 32 ranks --
+# (one TREE item per group capped groups at LFA_TREE_MAX = 32.)
+
+def _rd_tree(xs):
+    """prov/coll's recursive-doubling association as a nested tuple: leaf
+    pairs (x[2v+1], x[2v]) for v < rem, then hi-over-lo merges."""
+    n = len(xs)
+    if n == 1:
+        return xs[0]
+    pof2 = 1
+    while pof2 * 2 <= n:
+        pof2 *= 2
+    rem = n - pof2
+    level = [(xs[2 * v + 1], xs[2 * v]) if v < rem else xs[v + rem] for v in range(pof2)]
+    while len(level) > 1:
+        level = [(level[i + 1], level[i]) for i in range(0, len(level), 2)]
+    return level[0]
+
+
+def _symbolic_tree_result(n, r, count=3):
+    """Execute rank r's TREE items of the allreduce schedule symbolically:
+    TMP slot k (block exchange) holds x_k, SEND holds x_r; TREE items are
+    _rd_tree of their inputs.  Returns the expression left in RESULT."""
+    pl = coll.plan(ALLREDUCE, coll.ALGO_TREE, r, n, -1, count * 1000, 4)
+    moff, mlen = coll.block(count * 1000, n, r)
+    stride = mlen * 4          # < 1 MiB blocks: dense slots
+    mem = {("S", moff * 4): f"x{r}"}
+    for k in range(n):
+        if k != r:
+            mem[("T", k * stride)] = f"x{k}"
+    out = None
+    for s in pl.steps:
+        if s["type"] != _plansim.TREE:
+            continue
+        ins = []
+        for k in range(s["nsrc"]):
+            b, off = pl.refs[s["first"] + k][:2]
+            ins.append(mem[("S" if b == 0 else "T", off)])
+        e = _rd_tree(ins)
+        b, off = s["dst"][:2]
+        if b == 2:
+            mem[("T", off)] = e
+        else:
+            out = e
+    assert pl.tmp_bytes >= max(off for (b, off) in mem if b == "T") + mlen * 4
+    return out
+
+
+@pytest.mark.parametrize("n", [32, 33, 47, 48, 64, 100, 511, 512, 513, 1024, 1100])
+def test_large_group_tree_is_the_reference_tree(n):
+    want = _rd_tree([f"x{k}" for k in range(n)])
+    for r in sorted({0, n // 2, n - 1}):
+        assert _symbolic_tree_result(n, r) == want, (n, r)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("n", [33, 40, 64])
+def test_large_group_schedules_execute(algo, n):
+    """> 32 ranks, every algorithm (P2P / TREE_COLL fall back to TREE):
+    executed across all ranks, bit-exact with the oracle."""
+    count = 3 * n + 5
+    for dt, op in ((F32, SUM), (I64, BXOR_ := 9)):
+        sends = _inputs(dt, n, count, n + 99)
+        want = oracle.allreduce(op, dt, sends)[0]
+        res = [np.zeros(count * sends[0].itemsize, np.uint8) for _ in range(n)]
+        _plansim.run(ALLREDUCE, algo, n, -1, dt, op, count,
+                     [s.view(np.uint8) for s in sends], res)
+        for r in range(n):
+            assert res[r].tobytes() == want.view(np.uint8).tobytes(), (r, dt)
+    # reduce_scatter and reduce at n > 32 too
+    dt, op = F64, PROD
+    sends = _inputs(dt, n, count, 5)
+    full = oracle.allreduce(op, dt, sends)[0]
+    res = [np.zeros(coll.block(count, n, r)[1] * 8, np.uint8) for r in range(n)]
+    _plansim.run(REDUCE_SCATTER, algo, n, -1, dt, op, count,
+                 [s.view(np.uint8) for s in sends], res)
+    for r in range(n):
+        off, ln = coll.block(count, n, r)
+        assert res[r].tobytes() == full[off:off + ln].tobytes()
