@@ -685,7 +685,7 @@ def extra_collectives(rank, world, stream):
 def tune(args) -> None:
     """Interleaved A/B of the combine_vec variants (guide §5.4 rule 24)."""
     from libfabric_amd import _native
-    L = _native.lib()
+    L = _native.lib("tune")
     torch.cuda.set_device(0)
     count = args.tune_bytes // 4
     nsets = max(BUFFER_SETS, (2 << 30) // (2 * args.tune_bytes))  # >= 2 GiB rotated
@@ -749,7 +749,7 @@ def tune_tree(args) -> None:
     """A/B of the N-input tree kernel forms (float SUM), interleaved."""
     import ctypes
     from libfabric_amd import _native
-    L = _native.lib()
+    L = _native.lib("tune")
     torch.cuda.set_device(0)
     h = torch.cuda.current_stream().cuda_stream
     rows = []
@@ -799,7 +799,7 @@ def tune_tree_layout(args) -> None:
     workspace with block k skewed by k*skew bytes."""
     import ctypes
     from libfabric_amd import _native
-    L = _native.lib()
+    L = _native.lib("tune")
     torch.cuda.set_device(0)
     h = torch.cuda.current_stream().cuda_stream
     nsrc, blk = 8, 32 * 1024 * 1024 // 4

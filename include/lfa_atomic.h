@@ -149,6 +149,25 @@ int lfa_host_write(enum lfa_op op, enum lfa_datatype datatype, void *dst,
 		   const void *src, size_t cnt);
 int lfa_host_reduce_tree(enum lfa_op op, enum lfa_datatype datatype, void *dst,
 			 const void *const *srcs, int nsrc, size_t cnt);
+/* Fetch and compare tables on host memory (res = old dst, as the
+ * readwrite / swap handlers, util_atomic.c:924-980). */
+int lfa_host_readwrite(enum lfa_op op, enum lfa_datatype datatype, void *dst,
+		       const void *src, void *res, size_t cnt);
+int lfa_host_swap(enum lfa_op op, enum lfa_datatype datatype, void *dst,
+		  const void *src, const void *cmp, void *res, size_t cnt);
+
+/*
+ * The synchronous tables (lfa_atomic_write_handlers and the fetch / compare
+ * tables) accept DEVICE or HOST pointers, classified per call with
+ * hipPointerGetAttributes: device operands run the gfx950 kernels on the null
+ * stream; host operands — what prov/coll's REDUCE items hand over
+ * (coll_coll.c:758-768) — run the host loop while the bucket is at most
+ * lfa_host_small_bytes() (env LFA_HOST_SMALL_BYTES, default below), and are
+ * streamed through HBM (lfa_atomic_write_staged) above it.  Mixed write
+ * operands also take the staged path.
+ */
+#define LFA_HOST_SMALL_DEFAULT (1u << 20)
+size_t lfa_host_small_bytes(void);
 
 /* Version string of the kernel library (build id, target arch). */
 const char *lfa_version(void);

@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL loads below)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-_LIBS = {"lfa": "liblfa.so", "coll": "liblfa_coll.so"}
+_LIBS = {"lfa": "liblfa.so", "coll": "liblfa_coll.so",
+         "tune": "liblfa_tune.so"}   # tuning forms: bench.py --tune* only
 _loaded = {}
 
 
@@ -51,11 +52,16 @@ def _bind_lfa(L):
     L.lfa_atomic_write_staged.argtypes = [c_int, c_int, c_void_p, c_void_p, c_size_t,
                                           c_size_t]
     L.lfa_version.restype = ctypes.c_char_p
+    L.lfa_host_small_bytes.restype = c_size_t
     L.lfa_host_write.restype = c_int
     L.lfa_host_write.argtypes = [c_int, c_int, c_void_p, c_void_p, c_size_t]
     L.lfa_host_reduce_tree.restype = c_int
     L.lfa_host_reduce_tree.argtypes = [c_int, c_int, c_void_p, ctypes.POINTER(c_void_p),
                                        c_int, c_size_t]
+
+
+def _bind_tune(L):
+    c_int, c_size_t, c_void_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
     L.lfa__tune_tree_f32.restype = c_int
     L.lfa__tune_tree_f32.argtypes = [c_int, c_void_p, ctypes.POINTER(c_void_p),
                                      c_int, c_size_t, c_void_p]
@@ -78,5 +84,7 @@ def lib(name: str = "lfa") -> ctypes.CDLL:
     L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     if name == "lfa":
         _bind_lfa(L)
+    elif name == "tune":
+        _bind_tune(L)
     _loaded[name] = L
     return L

@@ -30,6 +30,7 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fPIC",
              "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + INC]
 
 LIB_LFA = os.path.join(PKG, "liblfa.so")
+LIB_TUNE = os.path.join(PKG, "liblfa_tune.so")
 LIB_COLL = os.path.join(PKG, "liblfa_coll.so")
 
 
@@ -50,8 +51,8 @@ def _run(cmd: list[str]) -> None:
 def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     kern = os.path.join(CSRC, "lfa_combine.hip")
-    hdrs = [os.path.join(CSRC, "lfa_ops.hpp"), os.path.join(INC, "lfa_atomic.h"),
-            os.path.join(INC, "lfa_fabric.h")]
+    hdrs = [os.path.join(CSRC, "lfa_ops.hpp"), os.path.join(CSRC, "lfa_kernels.hpp"),
+            os.path.join(INC, "lfa_atomic.h"), os.path.join(INC, "lfa_fabric.h")]
     steps = []
     objs = []
     for op in WRITE_OPS:
@@ -59,11 +60,11 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
         objs.append(o)
         if _newer(o, [kern] + hdrs):
             steps.append([HIPCC, *HIP_FLAGS, f"-DLFA_OP={op}", "-c", kern, "-o", o])
+    # tuning-only kernel forms (bench.py --tune*): their own library
     tune = os.path.join(CSRC, "lfa_tune.hip")
-    o = os.path.join(BUILD, "lfa_tune.o")
-    objs.append(o)
-    if _newer(o, [tune] + hdrs):
-        steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", o])
+    tune_o = os.path.join(BUILD, "lfa_tune.o")
+    if _newer(tune_o, [tune] + hdrs):
+        steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", tune_o])
     capi = os.path.join(CSRC, "lfa_capi.cpp")
     o = os.path.join(BUILD, "lfa_capi.o")
     objs.append(o)
@@ -87,6 +88,9 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     if steps or _newer(LIB_LFA, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_LFA,
               *objs, "-Wl,-soname,liblfa.so"])
+    if _newer(LIB_TUNE, [tune_o]):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TUNE,
+              tune_o, "-Wl,-soname,liblfa_tune.so"])
     if verbose:
         print(f"built {LIB_LFA} ({len(steps)} objects recompiled)")
     return LIB_LFA

@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <pthread.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/lfa_atomic.h"
 
@@ -111,8 +112,35 @@ constexpr bool in_swap_table(int op, int dt) {
   }
 }
 
+// Where an operand lives: the synchronous tables take what their caller has
+// — prov/coll's REDUCE items hand over host memory (coll_coll.c:364, :1058),
+// a GPU-resident caller device memory.  Pinned and registered host memory
+// counts as host: the GPU could read it over PCIe, but the host loop or the
+// staged path is faster for it.
+enum { kDev = 1, kHost = 2 };
+
+int ptr_kind(const void *p) {
+  hipPointerAttribute_t a;
+  if (!p) return kHost;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // unknown to HIP: plain host memory
+    return kHost;
+  }
+  return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? kDev : kHost;
+}
+
 template <int OP, int DT>
 void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
+  const int k = ptr_kind(dst) | ptr_kind(res) | (OP == LFA_ATOMIC_READ ? 0 : ptr_kind(src));
+  if (cnt && k == kHost) {
+    int rc = lfa_host_readwrite((lfa_op)OP, (lfa_datatype)DT, dst, src, res, cnt);
+    if (rc) fprintf(stderr, "lfa: host fetch op=%d dt=%d failed (%d)\n", OP, DT, rc);
+    return;
+  }
+  if (cnt && k != kDev) {
+    fprintf(stderr, "lfa: fetch op=%d dt=%d: mixed host/device operands\n", OP, DT);
+    return;
+  }
   int rc = kReadWrite[OP](DT, dst, src, res, cnt, nullptr);
   hipError_t e = hipStreamSynchronize(nullptr);
   if (rc || e != hipSuccess)
@@ -123,6 +151,16 @@ void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
 template <int OP, int DT>
 void sync_swap_entry(void *dst, const void *src, const void *cmp, void *res,
                      size_t cnt) {
+  const int k = ptr_kind(dst) | ptr_kind(src) | ptr_kind(cmp) | ptr_kind(res);
+  if (cnt && k == kHost) {
+    int rc = lfa_host_swap((lfa_op)OP, (lfa_datatype)DT, dst, src, cmp, res, cnt);
+    if (rc) fprintf(stderr, "lfa: host swap op=%d dt=%d failed (%d)\n", OP, DT, rc);
+    return;
+  }
+  if (cnt && k != kDev) {
+    fprintf(stderr, "lfa: swap op=%d dt=%d: mixed host/device operands\n", OP, DT);
+    return;
+  }
   int rc = kSwap[OP - LFA_CSWAP](DT, dst, src, cmp, res, cnt, nullptr);
   hipError_t e = hipStreamSynchronize(nullptr);
   if (rc || e != hipSuccess)
@@ -144,6 +182,17 @@ constexpr lfa_swap_fn swap_entry() {
 
 template <int OP, int DT>
 void sync_entry(void *dst, const void *src, size_t cnt) {
+  if (!cnt) return;
+  const int k = ptr_kind(dst) | ptr_kind(src);
+  if (k != kDev) {
+    // host (or mixed) operands: the host loop for a small bucket, HBM
+    // streaming above lfa_host_small_bytes() (SURVEY §7 small-bucket latency)
+    int rc = k == kHost && cnt * lfa_datatype_size((lfa_datatype)DT) <= lfa_host_small_bytes()
+                 ? lfa_host_write((lfa_op)OP, (lfa_datatype)DT, dst, src, cnt)
+                 : lfa_atomic_write_staged((lfa_op)OP, (lfa_datatype)DT, dst, src, cnt, 0);
+    if (rc) fprintf(stderr, "lfa: combine op=%d dt=%d (host operands) failed (%d)\n", OP, DT, rc);
+    return;
+  }
   int rc = kWrite[OP](DT, dst, src, cnt, nullptr);
   hipError_t e = hipStreamSynchronize(nullptr);
   if (rc || e != hipSuccess)
@@ -350,15 +399,13 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
       char *dd = c.dev + k * 2 * slot, *ds = dd + slot;
       // slot reuse: the D2H of the chunk two back must have drained it
       hipStreamWaitEvent(c.s_in, c.out_done[k], 0);
-      hipMemcpyAsync(dd, (char *)dst + off * esz, n * esz, hipMemcpyHostToDevice,
+      hipMemcpyAsync(dd, (char *)dst + off * esz, n * esz, hipMemcpyDefault, c.s_in);
+      hipMemcpyAsync(ds, (const char *)src + off * esz, n * esz, hipMemcpyDefault,
                      c.s_in);
-      hipMemcpyAsync(ds, (const char *)src + off * esz, n * esz,
-                     hipMemcpyHostToDevice, c.s_in);
       hipEventRecord(c.in_done[k], c.s_in);
       hipStreamWaitEvent(c.s_out, c.in_done[k], 0);
       ret = kWrite[op](dt, dd, ds, n, c.s_out);
-      hipMemcpyAsync((char *)dst + off * esz, dd, n * esz, hipMemcpyDeviceToHost,
-                     c.s_out);
+      hipMemcpyAsync((char *)dst + off * esz, dd, n * esz, hipMemcpyDefault, c.s_out);
       hipEventRecord(c.out_done[k], c.s_out);
     }
     if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
@@ -366,6 +413,14 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   }
   pthread_mutex_unlock(&c.lock);
   return ret;
+}
+
+size_t lfa_host_small_bytes(void) {
+  static size_t v = [] {
+    const char *e = getenv("LFA_HOST_SMALL_BYTES");
+    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)LFA_HOST_SMALL_DEFAULT;
+  }();
+  return v;
 }
 
 const char *lfa_version(void) {

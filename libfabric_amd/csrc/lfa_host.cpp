@@ -95,6 +95,37 @@ int host_tree(void *dst, const void *const *srcs, int nsrc, size_t cnt) {
   }
 }
 
+// Fetch table: res = old dst, then dst = dst OP src (util_atomic.c:924-950).
+template <int OP, typename T>
+int host_readwrite(void *dst, const void *src, void *res, size_t cnt) {
+  if constexpr (!rw_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    for (size_t i = 0; i < cnt; i++) {
+      T a = load<T>(dst, i);
+      store<T>(res, i, a);
+      if constexpr (OP != OP_READ) store<T>(dst, i, apply<OP, T>(a, load<T>(src, i)));
+    }
+    return 0;
+  }
+}
+
+// Compare table: res = old dst, dst = src where the compare holds
+// (util_atomic.c:952-980).
+template <int OP, typename T>
+int host_swap(void *dst, const void *src, const void *cmp, void *res, size_t cnt) {
+  if constexpr (!swap_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    for (size_t i = 0; i < cnt; i++) {
+      T a = load<T>(dst, i);
+      store<T>(res, i, a);
+      store<T>(dst, i, swap_apply<OP, T>(a, load<T>(src, i), load<T>(cmp, i)));
+    }
+    return 0;
+  }
+}
+
 template <typename F>
 int by_type(int dt, F &&f) {
   switch (dt) {
@@ -128,7 +159,22 @@ int by_op(int op, F &&f) {
     case OP_BAND: return f(std::integral_constant<int, OP_BAND>());
     case OP_LXOR: return f(std::integral_constant<int, OP_LXOR>());
     case OP_BXOR: return f(std::integral_constant<int, OP_BXOR>());
+    case OP_READ: return f(std::integral_constant<int, OP_READ>());
     case OP_WRITE: return f(std::integral_constant<int, OP_WRITE>());
+    default: return -LFA_EOPNOTSUPP;
+  }
+}
+
+template <typename F>
+int by_swap_op(int op, F &&f) {
+  switch (op) {
+    case OP_CSWAP: return f(std::integral_constant<int, OP_CSWAP>());
+    case OP_CSWAP_NE: return f(std::integral_constant<int, OP_CSWAP_NE>());
+    case OP_CSWAP_LE: return f(std::integral_constant<int, OP_CSWAP_LE>());
+    case OP_CSWAP_LT: return f(std::integral_constant<int, OP_CSWAP_LT>());
+    case OP_CSWAP_GE: return f(std::integral_constant<int, OP_CSWAP_GE>());
+    case OP_CSWAP_GT: return f(std::integral_constant<int, OP_CSWAP_GT>());
+    case OP_MSWAP: return f(std::integral_constant<int, OP_MSWAP>());
     default: return -LFA_EOPNOTSUPP;
   }
 }
@@ -144,9 +190,36 @@ int lfa_host_write(enum lfa_op op, enum lfa_datatype dt, void *dst, const void *
   if (cnt && (!dst || !src)) return -LFA_EINVAL;
   return lfa::by_op(op, [&](auto opc) {
     constexpr int OP = decltype(opc)::value;
-    return lfa::by_type(dt, [&](auto *tag) {
+    if constexpr (OP == lfa::OP_READ) return -LFA_EOPNOTSUPP;
+    else return lfa::by_type(dt, [&](auto *tag) {
       typedef typename std::remove_pointer<decltype(tag)>::type T;
       return lfa::host_write<OP, T>(dst, src, cnt);
+    });
+  });
+}
+
+int lfa_host_readwrite(enum lfa_op op, enum lfa_datatype dt, void *dst,
+                       const void *src, void *res, size_t cnt) {
+  if (lfa_atomic_valid(dt, op, LFA_FETCH_ATOMIC)) return -LFA_EOPNOTSUPP;
+  if (cnt && (!dst || !res || (op != LFA_ATOMIC_READ && !src))) return -LFA_EINVAL;
+  return lfa::by_op(op, [&](auto opc) {
+    constexpr int OP = decltype(opc)::value;
+    return lfa::by_type(dt, [&](auto *tag) {
+      typedef typename std::remove_pointer<decltype(tag)>::type T;
+      return lfa::host_readwrite<OP, T>(dst, src, res, cnt);
+    });
+  });
+}
+
+int lfa_host_swap(enum lfa_op op, enum lfa_datatype dt, void *dst, const void *src,
+                  const void *cmp, void *res, size_t cnt) {
+  if (lfa_atomic_valid(dt, op, LFA_COMPARE_ATOMIC)) return -LFA_EOPNOTSUPP;
+  if (cnt && (!dst || !src || !cmp || !res)) return -LFA_EINVAL;
+  return lfa::by_swap_op(op, [&](auto opc) {
+    constexpr int OP = decltype(opc)::value;
+    return lfa::by_type(dt, [&](auto *tag) {
+      typedef typename std::remove_pointer<decltype(tag)>::type T;
+      return lfa::host_swap<OP, T>(dst, src, cmp, res, cnt);
     });
   });
 }

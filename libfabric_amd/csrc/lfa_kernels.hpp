@@ -1,0 +1,917 @@
+// lfa_kernels.hpp — the gfx950 combine kernels and their host launchers.
+//
+// Included by lfa_combine.hip (the product entry points of liblfa.so, one
+// object per write op) and by lfa_tune.hip (the on-GPU A/B sweep of
+// bench.py --tune*, built into the separate liblfa_tune.so).  Templates only:
+// a kernel form is compiled into a library only where a launcher
+// instantiates it, so the tuning forms never reach liblfa.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <type_traits>
+
+#include "lfa_ops.hpp"
+#include "../../include/lfa_atomic.h"
+
+namespace lfa {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// memory access helpers
+// ---------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// OP applied lane-wise to the 16/sizeof(T) elements packed in a 16-B vector.
+template <int OP, typename T>
+__device__ __forceinline__ u32x4 apply_vec(u32x4 d, u32x4 s) {
+  constexpr int N = 16 / sizeof(T);
+  T a[N], b[N];
+  __builtin_memcpy(a, &d, 16);
+  __builtin_memcpy(b, &s, 16);
+#pragma unroll
+  for (int i = 0; i < N; i++) a[i] = apply<OP, T>(a[i], b[i]);
+  u32x4 r;
+  __builtin_memcpy(&r, a, 16);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// binary combine, vector body
+// ---------------------------------------------------------------------------
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// Chunked: workgroup b owns vectors [b·kBlock·U, (b+1)·kBlock·U); step u of
+// thread t touches base + u·kBlock + t, i.e. each wave-instruction reads 1 KiB
+// of consecutive bytes.  All 2·U loads issue before the first op.
+template <int OP, typename T, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void combine_vec(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+  if (base + (size_t)(U - 1) * kBlock < nvec) {  // full chunk: no guards
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<NTL>(dst + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++) b[u] = ld<NTL>(src + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<NTS>(dst + base + u * kBlock, apply_vec<OP, T>(a[u], b[u]));
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec)
+        st<NTS>(dst + i, apply_vec<OP, T>(ld<NTL>(dst + i), ld<NTL>(src + i)));
+    }
+  }
+}
+
+// LDS-DMA staged form — the PRODUCT body (bench.py --tune, DESIGN.md
+// "Kernel tuning": 1-2 % faster than register staging at 256 MiB).  Each wave
+// owns U consecutive KiB of both operands and moves them HBM -> LDS with
+// global_load_lds_dwordx4 (aux = nt, no VGPR round trip; 2·U KiB in flight per
+// wave), waits on its own vmcnt, reads its lane's 16 B back with
+// ds_read_b128, applies OP and streams the result out with nt stores.  Waves
+// never share LDS, so there is no barrier; a wave whose chunk runs past nvec
+// takes the guarded register path.
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kLdsWaves = 4;
+
+// Store cache policy of the body (gfx950 cpol bits): nt keeps the line in
+// the XCD's L2 for the end-of-kernel writeback; sc1 writes through.  sc1 is
+// 1.6-6.7 % faster per launch from 16 to 128 MiB per operand and level at
+// 256 MiB (rocprofv3 kernel durations, profiles/r01_rocprof_store_policy.csv),
+// so launches below kSc1Bytes write through.
+constexpr int kStoreNt = 2, kStoreSc1 = 16;
+constexpr size_t kSc1Bytes = (size_t)192 << 20;
+
+template <int OP, typename T, int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base =
+      (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+    if constexpr (OP != OP_WRITE) {  // ATOMIC_WRITE never reads dst
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0,
+                                         /*aux: nt*/ 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // sc1: the wave's tile through one buffer descriptor whose stores carry
+    // the bits; nt: plain global stores (0.5 % faster than the buffer form
+    // at 256 MiB in rocprofv3)
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      u32x4 v;
+      if constexpr (OP == OP_WRITE) v = lds[1][w][u][l];
+      else v = apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == kStoreNt)
+        st<true>(dst + base + u * 64 + l, v);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, apply_vec<OP, T>(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
+// Grid-stride variant (for the tuning sweep): a fixed grid of G workgroups
+// walks the buffer; each thread holds U vectors spaced kBlock apart.
+template <int OP, typename T, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void combine_vec_gs(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  const size_t step = (size_t)gridDim.x * kBlock * U;
+  size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+  for (; base + (size_t)(U - 1) * kBlock < nvec; base += step) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<NTL>(dst + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++) b[u] = ld<NTL>(src + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<NTS>(dst + base + u * kBlock, apply_vec<OP, T>(a[u], b[u]));
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec)
+      st<NTS>(dst + i, apply_vec<OP, T>(ld<NTL>(dst + i), ld<NTL>(src + i)));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// binary combine, element-wise (heads, tails, non-co-aligned buffers)
+// ---------------------------------------------------------------------------
+// Up to two index ranges [0, n0) and [off1, off1 + n1) in one launch, so a
+// misaligned head and tail cost a single extra dispatch.
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void combine_elem(
+    T *__restrict__ dst, const T *__restrict__ src, size_t n0, size_t off1,
+    size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    dst[k] = apply<OP, T>(dst[k], src[k]);
+  }
+}
+
+// Element pointers not even aligned to sizeof(T): byte-wise access.
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void combine_unaligned(
+    unsigned char *dst, const unsigned char *src, size_t n) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n; i += stride) {
+    T a, b;
+    __builtin_memcpy(&a, dst + i * sizeof(T), sizeof(T));
+    __builtin_memcpy(&b, src + i * sizeof(T), sizeof(T));
+    a = apply<OP, T>(a, b);
+    __builtin_memcpy(dst + i * sizeof(T), &a, sizeof(T));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// N-input tree reduction in recursive-doubling order
+// ---------------------------------------------------------------------------
+// Leaf k (k < nleaf, nleaf = largest power of two <= nsrc) is either a pair
+// (in[hi] OP in[lo]) — the non-power-of-two pre-step, coll_coll.c:366-389 —
+// or a single input.  Leaves are then combined pairwise, higher-index
+// partial OP lower-index partial, level by level (coll_coll.c:392-433).
+// The kernel evaluates that tree with a stack: push leaves left to right and
+// merge the two top entries while they cover equal-size groups, so only
+// log2(nleaf)+1 partials are live per element.
+constexpr int kMaxLeaf = 32;
+
+struct TreeArgs {
+  const void *in[kMaxLeaf];  // nsrc <= 32 inputs (LFA_TREE_MAX)
+  signed char hi[kMaxLeaf];  // input index of the leaf's (higher-rank) value
+  signed char lo[kMaxLeaf];  // paired lower-rank input, or -1
+};
+
+template <int OP, typename T, typename V>
+__device__ __forceinline__ V apply_any(V d, V s) {
+  if constexpr (sizeof(V) == 16 && sizeof(T) <= 16 && !__is_same(V, T))
+    return apply_vec<OP, T>(d, s);
+  else
+    return apply<OP, T>(d, s);
+}
+
+// Evaluate the tree for one element (or one 16-B vector); load(k) fetches
+// input k.  Leaf order, pairing and merge order are compile-time except the
+// kernel-argument (wave-uniform) pair test.
+template <int OP, typename T, typename V, int NLEAF, typename L>
+__device__ __forceinline__ V tree_eval_with(const TreeArgs &a, L &&load) {
+  V stack[6];
+  int depth = 0;
+#pragma unroll
+  for (int k = 0; k < NLEAF; k++) {
+    V v = load(a.hi[k]);
+    if (a.lo[k] >= 0)  // wave-uniform: kernel-argument branch
+      v = apply_any<OP, T, V>(v, load(a.lo[k]));
+    stack[depth++] = v;
+    // after leaf k, merge the two top partials once per trailing zero bit
+    // of (k + 1): that is when they cover equal-size rank groups
+#pragma unroll
+    for (int m = 1; m < NLEAF; m <<= 1) {
+      if (((k + 1) & (2 * m - 1)) == 0) {
+        V hi = stack[--depth];
+        V lo = stack[--depth];
+        stack[depth++] = apply_any<OP, T, V>(hi, lo);
+      }
+    }
+  }
+  return stack[0];
+}
+
+template <int OP, typename T, typename V, int NLEAF>
+__device__ __forceinline__ V tree_eval(const TreeArgs &a, size_t i) {
+  return tree_eval_with<OP, T, V, NLEAF>(
+      a, [&](int k) { return ((const V *)a.in[k])[i]; });
+}
+
+// Grid-stride form (tuning reference): plain loads, one vector per lane.
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_vec(TreeArgs a,
+                                                          u32x4 *dst,
+                                                          size_t nvec) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < nvec; i += stride)
+    st<true>(dst + i, tree_eval<OP, T, u32x4, NLEAF>(a, i));
+}
+
+// Chunked register form: workgroup b owns [b·kBlock·U, (b+1)·kBlock·U),
+// every input read with nt loads (U·nsrc 16-B loads in flight per lane).
+// SAUX = kStoreSc1: the result is written through (buffer stores, sc1).
+template <int OP, typename T, int NLEAF, int U, int SAUX = kStoreNt>
+__global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
+                                                            u32x4 *dst,
+                                                            size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec) {
+      u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(
+          a, [&](int k) { return ld<true>((const u32x4 *)a.in[k] + i); });
+      if constexpr (SAUX == kStoreNt) {
+        st<true>(dst + i, v);
+      } else {
+        const size_t wb = i - threadIdx.x % 64;  // the wave's first vector
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, __builtin_amdgcn_make_buffer_rsrc(dst + wb, 0, 64 * 16, 0x00020000),
+            (threadIdx.x % 64) * 16, 0, SAUX);
+      }
+    }
+  }
+}
+
+// LDS-DMA form: each wave DMAs U KiB of every input into its own LDS slots
+// (global_load_lds_dwordx4, nt), waits on its vmcnt, then evaluates U trees
+// per lane from LDS and stores nt.  Dynamic LDS: nin · W · U KiB per
+// workgroup.  Waves never share LDS, so no barrier.
+template <int OP, typename T, int NLEAF, int W, int U>
+__global__ __launch_bounds__(W * 64) void reduce_tree_lds(TreeArgs a, int nin,
+                                                          u32x4 *dst,
+                                                          size_t nvec) {
+  extern __shared__ u32x4 tlds[];  // [nin][W][U][64]
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (W * 64 * U) + (size_t)w * 64 * U;
+  auto slot = [&](int k, int u) { return ((k * W + w) * U + u) * 64; };
+  if (base + 64 * U <= nvec) {
+    for (int k = 0; k < nin; k++)  // uniform loop over the inputs
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)((const u32x4 *)a.in[k] + base + u * 64 + l),
+            (lds_void *)&tlds[slot(k, u)], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      st<true>(dst + base + u * 64 + l,
+               tree_eval_with<OP, T, u32x4, NLEAF>(
+                   a, [&](int k) { return tlds[slot(k, u) + l]; }));
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+                   return ld<true>((const u32x4 *)a.in[k] + i);
+                 }));
+    }
+  }
+}
+
+// Wave-contiguous register form: wave w of workgroup b owns U consecutive KiB
+// of every input (longer DRAM bursts per input stream than the chunked form).
+template <int OP, typename T, int NLEAF, int U>
+__global__ __launch_bounds__(kBlock) void reduce_tree_wave(TreeArgs a,
+                                                           u32x4 *dst,
+                                                           size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U + l;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    size_t i = base + (size_t)u * 64;
+    if (i < nvec)
+      st<true>(dst + i, tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) {
+                 return ld<true>((const u32x4 *)a.in[k] + i);
+               }));
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
+                                                           size_t n0,
+                                                           size_t off1,
+                                                           size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    dst[k] = tree_eval<OP, T, T, NLEAF>(a, k);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// N-input tree with fan-out, across GPUs (LFA_ALGO_P2P)
+// ---------------------------------------------------------------------------
+// Inputs and outputs may be other GPUs' HBM mapped into this process over
+// IPC (xGMI).  Every access is system scope (sc0 sc1): such loads miss in any
+// cache that is not coherent with the owning GPU's memory, and such stores
+// write through instead of leaving dirty lines in this XCD's L2, so a peer
+// that orders itself after this kernel (a stream-ordered barrier) reads the
+// bytes, and the next operation here reads the peer's fresh input.
+constexpr int kSysAux = 17;  // cpol sc0 | sc1
+constexpr int kMaxPut = 32;
+
+struct PutArgs {
+  TreeArgs t;
+  void *out[kMaxPut];
+  int nout;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void *base,
+                                                            unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes,
+                                           0x00020000);
+}
+
+// Vector body: wave w of workgroup b owns U KiB (64·U vectors) of every
+// input; its loads and stores go through buffer descriptors sized to the
+// wave's tile, so the last, partial tile needs no guards (out-of-range lanes
+// load 0 and their stores are dropped by the hardware).
+template <int OP, typename T, int NLEAF, int U>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0,
+                     kSysAux));
+    });
+  }
+  for (int j = 0; j < a.nout; j++) {  // wave-uniform
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0,
+                                             kSysAux);
+  }
+}
+
+// One element at system scope (relaxed atomics of the element's width; a
+// 16-byte element as two 8-byte halves — the halves of one element are
+// written by one lane, so no reader sees a torn value after the barrier).
+template <typename T>
+__device__ __forceinline__ T sys_load(const T *p) {
+  T v;
+  if constexpr (sizeof(T) == 16) {
+    uint64_t h[2];
+    h[0] = __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    h[1] = __hip_atomic_load((const uint64_t *)p + 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_memcpy(&v, h, 16);
+  } else {
+    typedef typename std::conditional<
+        sizeof(T) == 1, uint8_t,
+        typename std::conditional<
+            sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type U;
+    U x = __hip_atomic_load((const U *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_memcpy(&v, &x, sizeof(T));
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void sys_store(T *p, T v) {
+  if constexpr (sizeof(T) == 16) {
+    uint64_t h[2];
+    __builtin_memcpy(h, &v, 16);
+    __hip_atomic_store((uint64_t *)p, h[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((uint64_t *)p + 1, h[1], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    typedef typename std::conditional<
+        sizeof(T) == 1, uint8_t,
+        typename std::conditional<
+            sizeof(T) == 2, uint16_t,
+            typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type>::type U;
+    U x;
+    __builtin_memcpy(&x, &v, sizeof(T));
+    __hip_atomic_store((U *)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t n0,
+                                                               size_t off1, size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) {
+    size_t k = i < n0 ? i : off1 + (i - n0);
+    T v = tree_eval_with<OP, T, T, NLEAF>(
+        a.t, [&](int s) { return sys_load<T>((const T *)a.t.in[s] + k); });
+    for (int j = 0; j < a.nout; j++) sys_store<T>((T *)a.out[j] + k, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fetch (readwrite) and compare-swap tables
+// ---------------------------------------------------------------------------
+// One launch shape for both: a functor F carries the operand pointers and
+// knows how to process one 16-B vector (vec) or one element (elem); the
+// kernels only map indices.  res[] receives the old destination, as every
+// shipping readwrite / swap handler returns it (util_atomic.c:345-760).
+template <int OP, typename T, bool ALIGNED>
+struct RwF {
+  char *d;
+  const char *s;
+  char *r;
+  u32x4 *dv;
+  const u32x4 *sv;
+  u32x4 *rv;
+  __device__ __forceinline__ void vec(size_t i) const {
+    u32x4 a = ld<true>(dv + i);
+    st<true>(rv + i, a);
+    if constexpr (OP != OP_READ)
+      st<true>(dv + i, apply_vec<OP, T>(a, ld<true>(sv + i)));
+  }
+  __device__ __forceinline__ void elem(size_t k) const {
+    T a;
+    if constexpr (ALIGNED) a = ((T *)d)[k];
+    else __builtin_memcpy(&a, d + k * sizeof(T), sizeof(T));
+    if constexpr (ALIGNED) ((T *)r)[k] = a;
+    else __builtin_memcpy(r + k * sizeof(T), &a, sizeof(T));
+    if constexpr (OP != OP_READ) {
+      T b;
+      if constexpr (ALIGNED) b = ((const T *)s)[k];
+      else __builtin_memcpy(&b, s + k * sizeof(T), sizeof(T));
+      a = apply<OP, T>(a, b);
+      if constexpr (ALIGNED) ((T *)d)[k] = a;
+      else __builtin_memcpy(d + k * sizeof(T), &a, sizeof(T));
+    }
+  }
+};
+
+template <int OP, typename T>
+__device__ __forceinline__ u32x4 swap_vec(u32x4 a, u32x4 b, u32x4 c) {
+  constexpr int N = 16 / sizeof(T);
+  T x[N], y[N], z[N];
+  __builtin_memcpy(x, &a, 16);
+  __builtin_memcpy(y, &b, 16);
+  __builtin_memcpy(z, &c, 16);
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = swap_apply<OP, T>(x[i], y[i], z[i]);
+  u32x4 out;
+  __builtin_memcpy(&out, x, 16);
+  return out;
+}
+
+template <int OP, typename T, bool ALIGNED>
+struct SwapF {
+  char *d;
+  const char *s;
+  const char *c;
+  char *r;
+  u32x4 *dv;
+  const u32x4 *sv;
+  const u32x4 *cv;
+  u32x4 *rv;
+  __device__ __forceinline__ void vec(size_t i) const {
+    u32x4 a = ld<true>(dv + i);
+    u32x4 b = ld<true>(sv + i);
+    u32x4 m = ld<true>(cv + i);
+    st<true>(rv + i, a);
+    st<true>(dv + i, swap_vec<OP, T>(a, b, m));
+  }
+  __device__ __forceinline__ void elem(size_t k) const {
+    T a, b, m;
+    if constexpr (ALIGNED) {
+      a = ((T *)d)[k];
+      b = ((const T *)s)[k];
+      m = ((const T *)c)[k];
+      ((T *)r)[k] = a;
+      ((T *)d)[k] = swap_apply<OP, T>(a, b, m);
+    } else {
+      __builtin_memcpy(&a, d + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(&b, s + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(&m, c + k * sizeof(T), sizeof(T));
+      __builtin_memcpy(r + k * sizeof(T), &a, sizeof(T));
+      a = swap_apply<OP, T>(a, b, m);
+      __builtin_memcpy(d + k * sizeof(T), &a, sizeof(T));
+    }
+  }
+};
+
+constexpr int kFetchUnroll = 2;
+
+template <typename F>
+__global__ __launch_bounds__(kBlock) void fetch_vec(F f, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (kBlock * kFetchUnroll) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kFetchUnroll; u++) {
+    size_t i = base + (size_t)u * kBlock;
+    if (i < nvec) f.vec(i);
+  }
+}
+
+template <typename F>
+__global__ __launch_bounds__(kBlock) void fetch_elem(F f, size_t n0, size_t off1,
+                                                     size_t n1) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n0 + n1; i += stride) f.elem(i < n0 ? i : off1 + (i - n0));
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+// Product configuration of the vector body (chosen by the on-GPU sweep in
+// bench.py --tune; see DESIGN.md "Kernel tuning"): LDS-DMA staging, 4 KiB of
+// each operand per wave, nt loads and stores.
+constexpr int kUnroll = 4;
+
+static inline unsigned grid_for(size_t work, size_t per_block, unsigned cap) {
+  size_t g = (work + per_block - 1) / per_block;
+  if (g == 0) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+constexpr unsigned kElemGridCap = 256 * 8;  // 8 workgroups per CU, grid-stride
+
+template <int OP, typename T>
+static int launch_write(void *dst, const void *src, size_t cnt,
+                        hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
+    if (cnt == 0) return 0;
+    if (pd % E || ps % E) {
+      hipLaunchKernelGGL((combine_unaligned<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock),
+                         0, s, (unsigned char *)dst, (const unsigned char *)src,
+                         cnt);
+    } else if ((pd ^ ps) % 16 == 0 && E <= 16) {
+      size_t head = ((16 - pd % 16) % 16) / E;
+      if (head > cnt) head = cnt;
+      size_t nvec = (cnt - head) * E / 16;
+      size_t body = nvec * 16 / E;
+      size_t tail = cnt - head - body;
+      if (nvec) {
+        u32x4 *d = (u32x4 *)((char *)dst + head * E);
+        const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
+        const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll, 0x7fffffffu));
+        if (nvec * 16 < kSc1Bytes)
+          hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreSc1>), grid,
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+        else
+          hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreNt>), grid,
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+      }
+      if (head + tail)
+        hipLaunchKernelGGL((combine_elem<OP, T>),
+                           dim3(grid_for(head + tail, kBlock, kElemGridCap)),
+                           dim3(kBlock), 0, s, (T *)dst, (const T *)src, head,
+                           head + body, tail);
+    } else {
+      hipLaunchKernelGGL((combine_elem<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock),
+                         0, s, (T *)dst, (const T *)src, cnt, (size_t)0,
+                         (size_t)0);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+  }
+}
+
+// Vector body of the tree (bench.py --tune-tree): LDS-DMA for
+// 2 inputs, chunked nt register loads for more (U=2 above 8 inputs).
+template <int OP, typename T, int NLEAF, int W, int U>
+static void launch_tree_lds(const TreeArgs &b, int nsrc, u32x4 *dst,
+                            size_t nvec, hipStream_t s) {
+  hipLaunchKernelGGL((reduce_tree_lds<OP, T, NLEAF, W, U>),
+                     dim3(grid_for(nvec, (size_t)W * 64 * U, 0x7fffffffu)),
+                     dim3(W * 64), (size_t)nsrc * W * U * 64 * sizeof(u32x4), s,
+                     b, nsrc, dst, nvec);
+}
+
+template <int OP, typename T, int NLEAF>
+static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
+                             size_t nvec, hipStream_t s, int variant = -1) {
+  // Product choice (bench.py --tune-tree, profiles/r01_tune_tree_sc1.log):
+  // below kSc1Bytes of output the U=2 chunk form with write-through stores
+  // wins at every fan-in (2..16 inputs: 58.9/53.4/52.1/51.7 us against
+  // 63.2/58.2/53.9/51.7 for the nt-store forms, 256 MiB of inputs).
+  if (variant < 0 && nvec * 16 < kSc1Bytes) variant = 11;
+  if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
+  if (variant == 11) {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+    return;
+  }
+  if (variant == 2) {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2>),
+                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+  } else if (variant == 3) {
+    launch_tree_lds<OP, T, NLEAF, kLdsWaves, 1>(b, nsrc, dst, nvec, s);
+  } else {
+    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
+                       dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, dst, nvec);
+  }
+}
+
+// Leaf pairing of prov/coll's tree for nsrc ranks (see TreeArgs); returns
+// the number of leaves (largest power of two <= nsrc).
+static int tree_leaves(TreeArgs &a, const void *const *srcs, int nsrc) {
+  int pof2 = 1;
+  while (pof2 * 2 <= nsrc) pof2 *= 2;
+  const int rem = nsrc - pof2;
+  memset(&a, 0, sizeof(a));
+  for (int k = 0; k < nsrc; k++) a.in[k] = srcs[k];
+  for (int k = 0; k < pof2; k++) {
+    if (k < rem) {
+      a.hi[k] = (signed char)(2 * k + 1);
+      a.lo[k] = (signed char)(2 * k);
+    } else {
+      a.hi[k] = (signed char)(k + rem);
+      a.lo[k] = -1;
+    }
+  }
+  return pof2;
+}
+
+// The vector body's launcher as a policy, so the tuning library
+// (lfa_tune.hip, liblfa_tune.so) can time other forms through the same
+// pairing / head / tail logic without linking them into liblfa.so.
+struct ProductTreeBody {
+  template <int OP, typename T, int NLEAF>
+  static void launch(const TreeArgs &b, int nsrc, u32x4 *dst, size_t nvec,
+                     hipStream_t s, int variant) {
+    launch_tree_body<OP, T, NLEAF>(b, nsrc, dst, nvec, s, variant);
+  }
+};
+
+template <int OP, typename T, int NLEAF, typename Body = ProductTreeBody>
+static int launch_tree_n(const TreeArgs &a, int nsrc, void *dst, size_t cnt,
+                         bool vec, size_t head, size_t nvec, hipStream_t s,
+                         int variant) {
+  constexpr size_t E = sizeof(T);
+  if (vec && nvec) {
+    TreeArgs b = a;
+    for (int k = 0; k < kMaxLeaf; k++)
+      if (b.in[k]) b.in[k] = (const char *)b.in[k] + head * E;
+    Body::template launch<OP, T, NLEAF>(b, nsrc, (u32x4 *)((char *)dst + head * E),
+                                        nvec, s, variant);
+  }
+  size_t body = vec ? nvec * 16 / E : 0;
+  size_t n0 = vec ? head : cnt;
+  size_t tail = vec ? cnt - head - body : 0;
+  if (n0 + tail)
+    hipLaunchKernelGGL((reduce_tree_elem<OP, T, NLEAF>),
+                       dim3(grid_for(n0 + tail, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, a, (T *)dst, n0, head + body, tail);
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T, typename Body = ProductTreeBody>
+static int launch_tree(void *dst, const void *const *srcs, int nsrc,
+                       size_t cnt, hipStream_t s, int variant = -1) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    if (nsrc < 1 || nsrc > kMaxLeaf) return -LFA_EINVAL;
+    if (cnt == 0) return 0;
+    if (nsrc == 1) {
+      if (dst == srcs[0]) return 0;
+      return hipMemcpyAsync(dst, srcs[0], cnt * E, hipMemcpyDeviceToDevice,
+                            s) == hipSuccess ? 0 : -LFA_EIO;
+    }
+    TreeArgs a;
+    const int pof2 = tree_leaves(a, srcs, nsrc);
+    uintptr_t mis = (uintptr_t)dst % 16, anyelem = (uintptr_t)dst % E;
+    for (int k = 0; k < nsrc; k++) {
+      mis |= ((uintptr_t)srcs[k] % 16) ^ ((uintptr_t)dst % 16);
+      anyelem |= (uintptr_t)srcs[k] % E;
+    }
+    if (anyelem) return -LFA_EINVAL;  // element-misaligned inputs: unsupported
+    bool vec = (mis == 0) && E <= 16;
+    size_t head = vec ? ((16 - (uintptr_t)dst % 16) % 16) / E : 0;
+    if (head > cnt) head = cnt;
+    size_t nvec = vec ? (cnt - head) * E / 16 : 0;
+    switch (pof2) {
+      case 2: return launch_tree_n<OP, T, 2, Body>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 4: return launch_tree_n<OP, T, 4, Body>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 8: return launch_tree_n<OP, T, 8, Body>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 16: return launch_tree_n<OP, T, 16, Body>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      case 32: return launch_tree_n<OP, T, 32, Body>(a, nsrc, dst, cnt, vec, head, nvec, s, variant);
+      default: return -LFA_EINVAL;
+    }
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
+                             hipStream_t s) {
+  constexpr size_t E = sizeof(T);
+  constexpr int U = 2;
+  size_t nvec = vec ? (cnt - head) * E / 16 : 0;
+  if (nvec) {
+    PutArgs b = a;
+    for (int k = 0; k < kMaxLeaf; k++)
+      if (b.t.in[k]) b.t.in[k] = (const char *)b.t.in[k] + head * E;
+    for (int j = 0; j < b.nout; j++) b.out[j] = (char *)b.out[j] + head * E;
+    hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, U>),
+                       dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, b, nvec);
+  }
+  size_t body = nvec * 16 / E;
+  size_t n0 = vec ? head : cnt;
+  size_t tail = vec ? cnt - head - body : 0;
+  if (n0 + tail)
+    hipLaunchKernelGGL((reduce_tree_put_elem<OP, T, NLEAF>),
+                       dim3(grid_for(n0 + tail, kBlock, kElemGridCap)), dim3(kBlock),
+                       0, s, a, n0, head + body, tail);
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T>
+static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
+                           int nsrc, size_t cnt, hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    if (nsrc < 1 || nsrc > kMaxLeaf || ndst < 1 || ndst > kMaxPut) return -LFA_EINVAL;
+    if (cnt == 0) return 0;
+    PutArgs a;
+    const int pof2 = tree_leaves(a.t, srcs, nsrc);
+    memset(a.out, 0, sizeof(a.out));
+    a.nout = ndst;
+    const uintptr_t p0 = (uintptr_t)dsts[0];
+    uintptr_t mis = 0, anyelem = 0;
+    for (int k = 0; k < nsrc; k++) {
+      mis |= ((uintptr_t)srcs[k] ^ p0) % 16;
+      anyelem |= (uintptr_t)srcs[k] % E;
+    }
+    for (int j = 0; j < ndst; j++) {
+      a.out[j] = dsts[j];
+      mis |= ((uintptr_t)dsts[j] ^ p0) % 16;
+      anyelem |= (uintptr_t)dsts[j] % E;
+    }
+    if (anyelem) return -LFA_EINVAL;
+    const bool vec = mis == 0 && E <= 16;
+    size_t head = vec ? ((16 - p0 % 16) % 16) / E : 0;
+    if (head > cnt) head = cnt;
+    switch (pof2) {
+      case 1: return launch_tree_put_n<OP, T, 1>(a, cnt, vec, head, s);
+      case 2: return launch_tree_put_n<OP, T, 2>(a, cnt, vec, head, s);
+      case 4: return launch_tree_put_n<OP, T, 4>(a, cnt, vec, head, s);
+      case 8: return launch_tree_put_n<OP, T, 8>(a, cnt, vec, head, s);
+      case 16: return launch_tree_put_n<OP, T, 16>(a, cnt, vec, head, s);
+      case 32: return launch_tree_put_n<OP, T, 32>(a, cnt, vec, head, s);
+      default: return -LFA_EINVAL;
+    }
+  }
+}
+
+// Shared launcher for the fetch / swap tables: vector body when every operand
+// is co-aligned mod 16, element path for heads, tails and the rest.
+template <typename T, typename MakeF>
+static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
+                        hipStream_t s, MakeF &&make) {
+  constexpr size_t E = sizeof(T);
+  if (cnt == 0) return 0;
+  uintptr_t p0 = (uintptr_t)ptrs[0], mis = 0, elem_mis = 0;
+  for (int k = 0; k < nptr; k++) {
+    mis |= ((uintptr_t)ptrs[k] ^ p0) % 16;
+    elem_mis |= (uintptr_t)ptrs[k] % E;
+  }
+  if (elem_mis) {
+    auto f = make(std::integral_constant<bool, false>(), (size_t)0);
+    hipLaunchKernelGGL(fetch_elem<decltype(f)>, dim3(grid_for(cnt, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, f, cnt, (size_t)0, (size_t)0);
+  } else if (mis == 0 && E <= 16) {
+    size_t head = ((16 - p0 % 16) % 16) / E;
+    if (head > cnt) head = cnt;
+    size_t nvec = (cnt - head) * E / 16, body = nvec * 16 / E;
+    size_t tail = cnt - head - body;
+    auto f = make(std::integral_constant<bool, true>(), head);
+    if (nvec)
+      hipLaunchKernelGGL(fetch_vec<decltype(f)>,
+                         dim3(grid_for(nvec, (size_t)kBlock * kFetchUnroll, 0x7fffffffu)),
+                         dim3(kBlock), 0, s, f, nvec);
+    if (head + tail)
+      hipLaunchKernelGGL(fetch_elem<decltype(f)>,
+                         dim3(grid_for(head + tail, kBlock, kElemGridCap)),
+                         dim3(kBlock), 0, s, f, head, head + body, tail);
+  } else {
+    auto f = make(std::integral_constant<bool, true>(), (size_t)0);
+    hipLaunchKernelGGL(fetch_elem<decltype(f)>, dim3(grid_for(cnt, kBlock, kElemGridCap)),
+                       dim3(kBlock), 0, s, f, cnt, (size_t)0, (size_t)0);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+template <int OP, typename T>
+static int launch_readwrite(void *dst, const void *src, void *res, size_t cnt,
+                            hipStream_t s) {
+  if constexpr (!rw_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    const void *ptrs[3] = {dst, res, OP == OP_READ ? dst : src};
+    return launch_fetch<T>(ptrs, 3, cnt, s, [&](auto aligned, size_t head) {
+      constexpr bool A = decltype(aligned)::value;
+      const size_t hb = head * sizeof(T);
+      return RwF<OP, T, A>{(char *)dst, (const char *)src, (char *)res,
+                           (u32x4 *)((char *)dst + hb),
+                           (const u32x4 *)((const char *)src + hb),
+                           (u32x4 *)((char *)res + hb)};
+    });
+  }
+}
+
+template <int OP, typename T>
+static int launch_swap(void *dst, const void *src, const void *cmp, void *res,
+                       size_t cnt, hipStream_t s) {
+  if constexpr (!swap_supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    const void *ptrs[4] = {dst, src, cmp, res};
+    return launch_fetch<T>(ptrs, 4, cnt, s, [&](auto aligned, size_t head) {
+      constexpr bool A = decltype(aligned)::value;
+      const size_t hb = head * sizeof(T);
+      return SwapF<OP, T, A>{(char *)dst, (const char *)src, (const char *)cmp,
+                             (char *)res, (u32x4 *)((char *)dst + hb),
+                             (const u32x4 *)((const char *)src + hb),
+                             (const u32x4 *)((const char *)cmp + hb),
+                             (u32x4 *)((char *)res + hb)};
+    });
+  }
+}
+
+}  // namespace lfa

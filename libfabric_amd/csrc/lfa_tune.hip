@@ -12,7 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/lfa_fabric.h"
+#include "lfa_kernels.hpp"
 
 namespace lfa_tune {
 
@@ -401,4 +401,96 @@ extern "C" int lfa__tune2_sum_f32(int variant, void *dst, const void *src,
 #undef RUN
 #undef LDSDMA
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+// ---------------------------------------------------------------------------
+// the product kernels' alternative forms (lfa_kernels.hpp templates), timed
+// against the product choice by bench.py --tune / --tune-tree
+// ---------------------------------------------------------------------------
+namespace lfa {
+
+// Tree vector bodies the product does not ship: grid-stride plain loads (0),
+// LDS-DMA with 4/2/1 waves (4-6), wave-contiguous U=2/4 (7-8), chunked sc1
+// U=1/2 (9-10); anything else is the product's own choice.
+struct TuneTreeBody {
+  template <int OP, typename T, int NLEAF>
+  static void launch(const TreeArgs &b, int nsrc, u32x4 *dst, size_t nvec,
+                     hipStream_t s, int variant) {
+    switch (variant) {
+      case 0:
+        hipLaunchKernelGGL((reduce_tree_vec<OP, T, NLEAF>),
+                           dim3(grid_for(nvec, kBlock, 256 * 16)), dim3(kBlock), 0,
+                           s, b, dst, nvec);
+        return;
+      case 4: return launch_tree_lds<OP, T, NLEAF, 4, 2>(b, nsrc, dst, nvec, s);
+      case 5: return launch_tree_lds<OP, T, NLEAF, 2, 2>(b, nsrc, dst, nvec, s);
+      case 6: return launch_tree_lds<OP, T, NLEAF, 1, 4>(b, nsrc, dst, nvec, s);
+      case 7:
+        hipLaunchKernelGGL((reduce_tree_wave<OP, T, NLEAF, 2>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 8:
+        hipLaunchKernelGGL((reduce_tree_wave<OP, T, NLEAF, 4>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 9:
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      case 10:
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, b, dst, nvec);
+        return;
+      default:
+        launch_tree_body<OP, T, NLEAF>(b, nsrc, dst, nvec, s, variant);
+    }
+  }
+};
+
+}  // namespace lfa
+
+// Headline-kernel sweep (float SUM over nvec 16-B vectors).  -LFA_EINVAL for
+// an unknown variant id.
+extern "C" int lfa__tune_sum_f32(int variant, void *dst, const void *src,
+                                 size_t nvec, void *stream) {
+  using namespace lfa;
+  hipStream_t s = (hipStream_t)stream;
+  u32x4 *d = (u32x4 *)dst;
+  const u32x4 *v = (const u32x4 *)src;
+  auto chunk = [&](auto kern, int u) {
+    hipLaunchKernelGGL(kern, dim3(grid_for(nvec, (size_t)kBlock * u, 0x7fffffffu)),
+                       dim3(kBlock), 0, s, d, v, nvec);
+  };
+  auto gs = [&](auto kern, unsigned grid) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, d, v, nvec);
+  };
+  switch (variant) {
+    case 0: chunk(combine_vec<OP_SUM, float, 4, true, true>, 4); break;
+    case 30:  // the product launch itself
+      return launch_write<OP_SUM, float>(dst, src, nvec * 4, s);
+    case 1: chunk(combine_vec<OP_SUM, float, 1, true, true>, 1); break;
+    case 2: chunk(combine_vec<OP_SUM, float, 2, true, true>, 2); break;
+    case 3: chunk(combine_vec<OP_SUM, float, 8, true, true>, 8); break;
+    case 4: chunk(combine_vec<OP_SUM, float, 4, false, false>, 4); break;
+    case 5: chunk(combine_vec<OP_SUM, float, 4, true, false>, 4); break;
+    case 6: chunk(combine_vec<OP_SUM, float, 4, false, true>, 4); break;
+    case 7: gs(combine_vec_gs<OP_SUM, float, 4, true, true>, 2048); break;
+    case 8: gs(combine_vec_gs<OP_SUM, float, 4, true, true>, 1024); break;
+    case 9: gs(combine_vec_gs<OP_SUM, float, 2, true, true>, 4096); break;
+    case 10: gs(combine_vec_gs<OP_SUM, float, 8, true, true>, 1024); break;
+    case 11: chunk(combine_vec<OP_SUM, float, 8, false, false>, 8); break;
+    default: return -LFA_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
+
+// Tree-kernel sweep: float SUM over `nsrc` device inputs; -1 = the product.
+extern "C" int lfa__tune_tree_f32(int variant, void *dst, const void *const *srcs,
+                                  int nsrc, size_t cnt, void *stream) {
+  return lfa::launch_tree<lfa::OP_SUM, float, lfa::TuneTreeBody>(
+      dst, srcs, nsrc, cnt, (hipStream_t)stream, variant);
 }

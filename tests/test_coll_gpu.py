@@ -346,3 +346,52 @@ def test_p2p_kernel_on_ipc_mapped_memory(coll):
             assert_parity(dt, out, want, f"ipc out{j}")
     finally:
         L.hipFree(base)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+@pytest.mark.parametrize("n", [33, 64])
+def test_loopback_groups_above_32_ranks(coll, algo, n):
+    """Groups larger than one tree kernel's 32 inputs: the TREE is split into
+    whole subtrees of the reference tree (TMP partials), P2P / TREE_COLL run
+    as TREE; the bits stay prov/coll's (ADVICE r1)."""
+    for dt, op, count in ((8, 2, 1000), (5, 9, 4 * n + 3), (9, 3, 20_001)):
+        sends = _inputs(dt, n, count, n + op, *((0.9, 1.1) if op == 3 else (-1, 1)))
+        want = oracle.allreduce(op, dt, sends)[0]
+        sd = [_dev(s) for s in sends]
+        rd = [torch.zeros_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, algo, n, -1, dt, op, count, sd, rd)
+        torch.cuda.synchronize()
+        for r in (0, n // 2, n - 1):
+            assert_parity(dt, rd[r].cpu().numpy(), want, f"n={n} algo={algo} r={r}")
+
+
+def test_progress_continues_during_subset_join(coll, ep):
+    """The subset join's communicator split runs outside ep->lock: a thread
+    polling the CQ (off_lfa's progress thread does this) is never held up
+    behind it (VERDICT r1 weak #10)."""
+    import threading
+    import time
+    stamps, stop = [], threading.Event()
+
+    def poll():
+        while not stop.is_set():
+            ep.cq_read()
+            stamps.append(time.perf_counter())
+            time.sleep(0.001)
+
+    t = threading.Thread(target=poll)
+    t.start()
+    try:
+        time.sleep(0.05)
+        t0 = time.perf_counter()
+        mc, _ = ep.join([0])
+        ev = ep.wait_join()
+        t1 = time.perf_counter()
+    finally:
+        stop.set()
+        t.join(timeout=30)
+    assert ev[1] == mc
+    inside = [s for s in stamps if t0 <= s <= t1]
+    gaps = np.diff([t0] + inside + [t1])
+    assert gaps.max() < 0.5, f"poller stalled {gaps.max():.3f} s during the join"
+    assert coll.lib().lfa_mc_close(mc) == 0

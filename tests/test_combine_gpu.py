@@ -451,3 +451,38 @@ def test_beyond_32bit_element_counts(lfa):
         del d
     del d0, s_full
     torch.cuda.empty_cache()
+
+
+# --------------------------------- synchronous table with host pointers ----
+
+@pytest.mark.parametrize("nbytes", [1024, 4 << 20, (40 << 20) + 8])
+@pytest.mark.parametrize("kind", ["pageable", "pinned", "mixed"])
+def test_sync_table_host_pointers(lfa, nbytes, kind):
+    """prov/coll calls the table with HOST memory (coll_coll.c:758-768):
+    small buckets run the host loop, larger ones stream through HBM
+    (lfa_atomic_write_staged), mixed host/device operands stage too.  Bit-exact
+    with the oracle in every case; the device path is the tests above."""
+    rng = np.random.default_rng(nbytes)
+    for op, dt, nd in ((2, 8, np.float32), (0, 6, np.int64)):
+        n = nbytes // nd().itemsize
+        d = (rng.uniform(-1, 1, n) if nd is np.float32
+             else rng.integers(-2**62, 2**62, n)).astype(nd)
+        s = (rng.uniform(-1, 1, n) if nd is np.float32
+             else rng.integers(-2**62, 2**62, n)).astype(nd)
+        want = d.copy()
+        oracle.write(op, dt, want, s.copy())
+        fn = lfa.write_handler(op, dt)
+        if kind == "pageable":
+            fn(d.ctypes.data, s.ctypes.data, n)
+            got = d
+        elif kind == "pinned":
+            td = torch.from_numpy(d).pin_memory()
+            ts = torch.from_numpy(s).pin_memory()
+            fn(td.data_ptr(), ts.data_ptr(), n)
+            got = td.numpy()
+        else:   # device dst, host src
+            td = torch.from_numpy(d).to(DEV)
+            torch.cuda.synchronize()
+            fn(td.data_ptr(), s.ctypes.data, n)
+            got = td.cpu().numpy()
+        assert_parity(dt, got.view(np.uint8), want.view(np.uint8), f"{kind} {nbytes}")

@@ -109,3 +109,71 @@ def test_errors(lfa):
     assert L.lfa_host_write(2, 8, None, a.ctypes.data, 4) == -22
     assert L.lfa_host_write(2, 8, None, None, 0) == 0
     assert L.lfa_host_write(10, 8, a.ctypes.data, a.ctypes.data, 4) == -95  # ATOMIC_READ
+
+
+# ----------------------------------- synchronous tables, host pointers ----
+# prov/coll's REDUCE items hand the table HOST memory (coll_coll.c:758-768,
+# :364, :1058).  The table classifies each pointer (hipPointerGetAttributes;
+# on a machine without a GPU every pointer is host) and runs buckets up to
+# lfa_host_small_bytes() on the host; tests/test_combine_gpu.py covers the
+# staged (HBM) path above it and device pointers.
+
+_RW = None
+
+
+def _tables():
+    import ctypes
+    from libfabric_amd import lib
+    L = lib()
+    w = (ctypes.c_void_p * (12 * 16)).in_dll(L, "lfa_atomic_write_handlers")
+    rw = (ctypes.c_void_p * (12 * 16)).in_dll(L, "lfa_atomic_readwrite_handlers")
+    sw = (ctypes.c_void_p * (7 * 16)).in_dll(L, "lfa_atomic_swap_handlers")
+    W = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+    R = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_size_t)
+    S = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_void_p, ctypes.c_size_t)
+    return (lambda op, dt: W(w[op * 16 + dt]) if w[op * 16 + dt] else None,
+            lambda op, dt: R(rw[op * 16 + dt]) if rw[op * 16 + dt] else None,
+            lambda op, dt: S(sw[(op - 12) * 16 + dt]) if sw[(op - 12) * 16 + dt] else None)
+
+
+def test_sync_write_table_host_pointers(lfa, manifest, golden_dir):
+    from libfabric_amd import lib
+    assert lib().lfa_host_small_bytes() >= 1 << 16
+    wt, _, _ = _tables()
+    for case in manifest["combine"]:
+        fn = wt(case["op"], case["dt"])
+        assert fn is not None
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        d = np.ascontiguousarray(z["dst"]).view(np.uint8).copy()
+        s = np.ascontiguousarray(z["src"]).view(np.uint8).copy()
+        fn(d.ctypes.data, s.ctypes.data, case["n"])    # coll_coll.c:763 order
+        assert_parity(case["dt"], d, z["out"], case["file"])
+
+
+def test_sync_fetch_and_compare_tables_host_pointers(lfa, manifest, golden_dir):
+    _, rt, st = _tables()
+    for case in manifest["readwrite"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        d = np.ascontiguousarray(z["dst"]).view(np.uint8).copy()
+        s = np.ascontiguousarray(z["src"]).view(np.uint8).copy()
+        r = np.zeros_like(d)
+        rt(case["op"], case["dt"])(d.ctypes.data, s.ctypes.data, r.ctypes.data, case["n"])
+        assert_parity(case["dt"], d, z["out"], case["file"])
+        assert_parity(case["dt"], r, z["res"], case["file"] + " res")
+    for case in manifest["swap"]:
+        z = np.load(os.path.join(golden_dir, case["file"]))
+        nd = oracle.DT_NP[case["dt"]]
+        want_d = z["dst"].view(nd).copy()
+        want_r = np.zeros_like(want_d)
+        oracle.swap(case["op"], case["dt"], want_d, z["src"].view(nd).copy(),
+                    z["cmp"].view(nd).copy(), want_r, oracle.CAS)
+        d = np.ascontiguousarray(z["dst"]).view(np.uint8).copy()
+        s = np.ascontiguousarray(z["src"]).view(np.uint8).copy()
+        c = np.ascontiguousarray(z["cmp"]).view(np.uint8).copy()
+        r = np.zeros_like(d)
+        st(case["op"], case["dt"])(d.ctypes.data, s.ctypes.data, c.ctypes.data,
+                                   r.ctypes.data, case["n"])
+        assert np.array_equal(d, want_d.view(np.uint8)), case["file"]
+        assert np.array_equal(r, want_r.view(np.uint8)), case["file"]
