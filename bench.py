@@ -364,6 +364,30 @@ def extra_config3(dev, stream):
     return out
 
 
+def extra_sizes(dev, stream):
+    """The product float SUM combine vs size per operand (the shard sizes of
+    the strong-scaled headline: 256 MiB / N): average launch duration from an
+    event pair around 100 back-to-back launches over >= 1 GiB of rotated
+    operands, after a clock prewarm."""
+    from libfabric_amd import atomic
+    out = {}
+    for mib in (8, 16, 32, 64, 128, 256):
+        n = mib * 1024 * 1024 // 4
+        sets = make_buffers(dev, 5, n)
+
+        def fn(i, sets=sets, n=n):
+            d, s = sets[i % len(sets)]
+            atomic.write(FI_SUM, FI_FLOAT, d, s, n, stream)
+        prewarm(fn, 0.1)
+        ms = _kernel_events(fn, 100, stream)
+        gbps = 3 * n * 4 / (ms * 1e-3) / 1e9
+        out[str(mib)] = {"kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
+                         "frac": round(gbps / PEAK_GBPS, 4)}
+        del sets
+        torch.cuda.empty_cache()
+    return out
+
+
 def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     """BASELINE configs[0] at its stated shape on ONE GPU: a 2-rank float
     FI_SUM allreduce of 4 KiB per rank, both ranks' schedules executed by the
@@ -919,6 +943,16 @@ def main() -> None:
                               "host_allreduce": extra_host_allreduce(ep, 1, sweep=True)}))
         finally:
             ep.close()
+        return
+    if args.only_extra == "config3":
+        torch.cuda.set_device(0)
+        print(json.dumps({"config3": extra_config3(torch.device("cuda", 0),
+                                                   torch.cuda.current_stream())}))
+        return
+    if args.only_extra == "sizes":
+        torch.cuda.set_device(0)
+        print(json.dumps({"sizes": extra_sizes(torch.device("cuda", 0),
+                                               torch.cuda.current_stream())}))
         return
     if args.only_extra == "tree_put":
         torch.cuda.set_device(0)
