@@ -816,6 +816,57 @@ def tune_tree(args) -> None:
     print(json.dumps({"tune_tree": rows}))
 
 
+def tune_treeput(args) -> None:
+    """A/B of reduce_tree_put forms on LOCAL memory (float SUM, 8 x 32 MiB
+    inputs -> 1 and 8 outputs): the product vs variants without system-scope
+    bits or with other tiling (lfa__tune_treeput_f32, liblfa_tune.so)."""
+    import ctypes
+    from libfabric_amd import _native
+    L = _native.lib("tune")
+    torch.cuda.set_device(0)
+    h = torch.cuda.current_stream().cuda_stream
+    nsrc, blk = 8, 32 * 1024 * 1024 // 4
+    variants = ([int(x) for x in args.variants.split(",")] if args.variants
+                else [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+    rows = []
+    for ndst in (1, 8):
+        sets = []
+        for _ in range(2):
+            srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
+            dsts = [torch.empty(blk, device="cuda") for _ in range(ndst)]
+            sets.append((srcs, dsts, (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs]),
+                         (ctypes.c_void_p * ndst)(*[t.data_ptr() for t in dsts])))
+        ref = None
+        for v in variants:
+            srcs, dsts, sa, da = sets[0]
+            assert L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h) == 0
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = dsts[0].clone()
+            elif not all(torch.equal(ref, d) for d in dsts):
+                raise SystemExit(f"treeput variant {v} ndst={ndst} WRONG")
+        times = {v: [] for v in variants}
+        for _ in range(args.tune_rounds):
+            for v in variants:
+                evs = [(torch.cuda.Event(enable_timing=True),
+                        torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+                for i, (a, b) in enumerate(evs):
+                    srcs, dsts, sa, da = sets[i % 2]
+                    a.record()
+                    L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h)
+                    b.record()
+                torch.cuda.synchronize()
+                times[v].extend(a.elapsed_time(b) for a, b in evs[2:])
+        for v in variants:
+            ms = statistics.median(times[v])
+            gbps = (nsrc + ndst) * blk * 4 / (ms * 1e-3) / 1e9
+            rows.append({"ndst": ndst, "variant": v, "median_us": round(ms * 1e3, 2),
+                         "gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)})
+        del sets
+        torch.cuda.empty_cache()
+    print(json.dumps({"tune_treeput": rows}))
+
+
 def tune_tree_layout(args) -> None:
     """Where the N input blocks sit in HBM, for the product tree kernel
     (float SUM, 8 x 32 MiB): separate allocations; one contiguous workspace
@@ -911,6 +962,7 @@ def main() -> None:
     ap.add_argument("--tune-bytes", type=int, default=S_BYTES)
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--tune-tree-layout", action="store_true")
+    ap.add_argument("--tune-treeput", action="store_true")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
     ap.add_argument("--only-extra", default="", help="run one extra (dev): tree_put, host_rs")
@@ -927,6 +979,9 @@ def main() -> None:
         return
     if args.tune_tree_layout:
         tune_tree_layout(args)
+        return
+    if args.tune_treeput:
+        tune_treeput(args)
         return
     if args.tune_tree:
         tune_tree(args)

@@ -65,6 +65,9 @@ def _bind_tune(L):
     L.lfa__tune_tree_f32.restype = c_int
     L.lfa__tune_tree_f32.argtypes = [c_int, c_void_p, ctypes.POINTER(c_void_p),
                                      c_int, c_size_t, c_void_p]
+    L.lfa__tune_treeput_f32.restype = c_int
+    L.lfa__tune_treeput_f32.argtypes = [c_int, ctypes.POINTER(c_void_p), c_int,
+                                        ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]
     for fn in (L.lfa__tune_sum_f32, L.lfa__tune2_sum_f32):
         fn.restype = c_int
         fn.argtypes = [c_int, c_void_p, c_void_p, c_size_t, c_void_p]

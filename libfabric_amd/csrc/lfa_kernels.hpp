@@ -372,7 +372,12 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
 // write through instead of leaving dirty lines in this XCD's L2, so a peer
 // that orders itself after this kernel (a stream-ordered barrier) reads the
 // bytes, and the next operation here reads the peer's fresh input.
-constexpr int kSysAux = 17;  // cpol sc0 | sc1
+constexpr int kSysAux = 17;      // cpol sc0 | sc1: system scope (stores)
+constexpr int kSysLoadAux = 19;  // sc0 | sc1 | nt: system scope + streaming
+// The nt hint on the loads is worth 63 % -> 73 % of HBM peak on local memory
+// (8 -> 1, 8 x 32 MiB), U = 4 a further 2 points; the scope bits themselves
+// cost nothing (default-policy loads: 62.6 %).  bench.py --tune-treeput,
+// profiles/r02_tune_treeput*.log.
 constexpr int kMaxPut = 32;
 
 struct PutArgs {
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec
       return __builtin_bit_cast(
           u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                      tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0,
-                     kSysAux));
+                     kSysLoadAux));
     });
   }
   for (int j = 0; j < a.nout; j++) {  // wave-uniform
@@ -778,7 +783,7 @@ template <int OP, typename T, int NLEAF>
 static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
                              hipStream_t s) {
   constexpr size_t E = sizeof(T);
-  constexpr int U = 2;
+  constexpr int U = 4;  // 4 KiB of every input per wave (tune variant 14)
   size_t nvec = vec ? (cnt - head) * E / 16 : 0;
   if (nvec) {
     PutArgs b = a;

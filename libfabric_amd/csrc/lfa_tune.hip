@@ -494,3 +494,124 @@ extern "C" int lfa__tune_tree_f32(int variant, void *dst, const void *const *src
   return lfa::launch_tree<lfa::OP_SUM, float, lfa::TuneTreeBody>(
       dst, srcs, nsrc, cnt, (hipStream_t)stream, variant);
 }
+
+// ---------------------------------------------------------------------------
+// reduce_tree_put (LFA_ALGO_P2P kernel) forms, float SUM, vector body only:
+// the product's loads/stores carry sc0 sc1 (system scope) for peer HBM over
+// xGMI; these variants separate the cost of the scope bits from the tiling
+// on LOCAL memory (bench.py --tune-treeput).  Not correct across GPUs unless
+// they keep the product's scope bits.
+// ---------------------------------------------------------------------------
+namespace lfa {
+
+template <int NLEAF, int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void tp_tune(PutArgs a, size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, NLEAF>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, LAUX));
+    });
+  }
+  for (int j = 0; j < a.nout; j++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
+// All loads of a wave's tile issued before any tree step (8 inputs, no
+// leaf pairs: leaf k = input k, compile-time indices so the tiles stay in
+// registers); the product evaluates input by input instead.
+template <int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void tp_tune_pre(PutArgs a, size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 x[8][U];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x[k][u] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(u * 64 + l) * 16, 0,
+                                                       LAUX));
+  }
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    auto f = [](u32x4 hi, u32x4 lo) { return apply_vec<OP_SUM, float>(hi, lo); };
+    v[u] = f(f(f(x[7][u], x[6][u]), f(x[5][u], x[4][u])),
+             f(f(x[3][u], x[2][u]), f(x[1][u], x[0][u])));
+  }
+  for (int j = 0; j < a.nout; j++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
+}  // namespace lfa
+
+extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
+                                     const void *const *srcs, int nsrc, size_t cnt,
+                                     void *stream) {
+  using namespace lfa;
+  hipStream_t s = (hipStream_t)stream;
+  if (variant == 0)
+    return launch_tree_put<OP_SUM, float>(dsts, ndst, srcs, nsrc, cnt, s);
+  if (nsrc != 8 || ndst < 1 || ndst > kMaxPut || cnt % 4) return -LFA_EINVAL;
+  PutArgs a;
+  tree_leaves(a.t, srcs, nsrc);
+  memset(a.out, 0, sizeof(a.out));
+  a.nout = ndst;
+  for (int j = 0; j < ndst; j++) a.out[j] = dsts[j];
+  const size_t nvec = cnt / 4;
+#define TP(U, L, S)                                                               \
+  hipLaunchKernelGGL((tp_tune<8, U, L, S>), dim3(grid_for(nvec, (size_t)kBlock * U, \
+                                                          0x7fffffffu)),           \
+                     dim3(kBlock), 0, s, a, nvec)
+#define TPP(U, L, S)                                                              \
+  hipLaunchKernelGGL((tp_tune_pre<U, L, S>),                                       \
+                     dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)),         \
+                     dim3(kBlock), 0, s, a, nvec)
+  switch (variant) {
+    case 1: TP(2, 17, 17); break;   // the product body, through this harness
+    case 2: TP(2, 2, 16); break;    // local policy: nt loads, sc1 stores
+    case 3: TP(2, 16, 17); break;   // sc1 loads
+    case 4: TP(4, 17, 17); break;
+    case 5: TP(1, 17, 17); break;
+    case 6: TP(2, 17, 16); break;   // sc1-only stores
+    case 7: TP(4, 2, 16); break;
+    case 8: TPP(2, 17, 17); break;  // every load before the tree
+    case 9: TPP(1, 17, 17); break;
+    case 10: TPP(2, 2, 16); break;
+    case 11: TP(2, 0, 0); break;    // default policy both ways
+    // system scope kept (sc0 sc1) + the nt streaming hint on loads / stores
+    case 12: TP(2, 19, 17); break;
+    case 13: TPP(2, 19, 17); break;
+    case 14: TP(4, 19, 17); break;
+    case 15: TP(2, 19, 19); break;
+    case 16: TPP(2, 19, 19); break;
+    case 17: TP(1, 19, 17); break;
+    default: return -LFA_EINVAL;
+  }
+#undef TP
+#undef TPP
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
