@@ -1315,25 +1315,203 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 /* ---------------------------------------------------------------------- */
 
 /*
- * One collective on a host domain: prov/coll's util_coll_operation and its
- * work queue (ofi_coll.h:146-163), as a schedule and a program counter.
- * A SEND/RECV group is posted once through the owner's transport and the
- * operation resumes past its GROUP_END only when every transfer of the group
- * has completed (prov/coll's fence, coll_coll.c:196-201); REDUCE / TREE / COPY
- * items run inline with the host combine.
+ * The executor.  A schedule (struct plan) runs through ONE loop,
+ * xrun_advance, whatever carries its transfers; a transport table (xport)
+ * supplies the transfers and the local items:
+ *   xport_rccl  device buffers: SEND/RECV groups are RCCL grouped
+ *               ncclSend/ncclRecv, ALLTOALL/ALLGATHER/BARRIER RCCL
+ *               collectives, REDUCE/TREE/TREE_PUT/COPY gfx950 kernels — all
+ *               enqueued on the endpoint's stream, so a group "completes" as
+ *               soon as it is posted and one call runs the whole schedule;
+ *   xport_peer  host buffers of a peer-transfer domain: SEND/RECV are the
+ *               owner's tagged transfers (lfa_peer_xfer_ops), REDUCE/TREE the
+ *               host combine; a group is waited on with test() and the run
+ *               resumes there on the next progress call (prov/coll's fenced
+ *               work queue, coll_coll.c:153-227, 816-890).
+ * The multi-process CPU tests (tests/test_coll_host.py) therefore run this
+ * same loop, planner and tag scheme that the GPU endpoints run.
  */
-struct hop {
-	struct plan pl;
+struct xrun;
+struct xport {
+	int (*group_start)(struct xrun *r);
+	int (*post)(struct xrun *r, const struct lfa_step *st, void **req);
+	int (*group_end)(struct xrun *r);
+	int (*test)(struct xrun *r, void *req);       /* NULL: stream-ordered */
+	int (*local)(struct xrun *r, const struct lfa_step *st);
+	int (*coll)(struct xrun *r, const struct lfa_step *st);
+};
+
+struct xrun {
+	const struct xport *xp;
+	const struct plan *pl;
 	struct xctx x;
-	void *tmp;
 	struct lfa_coll_mc *mc;
 	enum lfa_op op;
 	enum lfa_datatype dt;
-	uint64_t cid;           /* group_id << 16 | seq (coll_get_next_id) */
+	hipStream_t stream;     /* xport_rccl */
+	uint64_t cid;           /* xport_peer tags: group_id << 16 | seq */
 	size_t pc;
 	void **reqs;            /* the current group's transfers; NULL = done */
 	size_t nreq, creq;
-	int posted, done, err;
+	int posted;
+};
+
+/* Run the schedule as far as it goes: 1 done, 0 waiting on transfers, <0. */
+static int xrun_advance(struct xrun *r)
+{
+	const struct plan *pl = r->pl;
+	int ret;
+
+	while (r->pc < pl->nsteps) {
+		const struct lfa_step *st = &pl->steps[r->pc];
+		size_t end;
+		int pending = 0;
+
+		switch (st->type) {
+		case LFA_STEP_GROUP_END:
+			r->pc++;
+			continue;
+		case LFA_STEP_SEND:
+		case LFA_STEP_RECV:
+			break;
+		case LFA_STEP_ALLTOALL:
+		case LFA_STEP_ALLGATHER:
+		case LFA_STEP_BARRIER:
+			ret = r->xp->coll(r, st);
+			if (ret)
+				return ret;
+			r->pc++;
+			continue;
+		default:
+			ret = r->xp->local(r, st);
+			if (ret)
+				return ret;
+			r->pc++;
+			continue;
+		}
+		for (end = r->pc; end < pl->nsteps &&
+		     pl->steps[end].type != LFA_STEP_GROUP_END; end++)
+			;
+		if (!r->posted) {
+			size_t need = end - r->pc;
+
+			if (r->xp->test && need > r->creq) {
+				void **nr = realloc(r->reqs, need * sizeof(*nr));
+
+				if (!nr)
+					return -LFA_ENOMEM;
+				r->reqs = nr;
+				r->creq = need;
+			}
+			r->nreq = 0;
+			ret = r->xp->group_start(r);
+			for (size_t i = r->pc; i < end && !ret; i++) {
+				void *req = NULL;
+
+				ret = r->xp->post(r, &pl->steps[i], &req);
+				if (r->xp->test)
+					r->reqs[r->nreq++] = req;
+			}
+			if (r->xp->group_end(r) && !ret)
+				ret = -LFA_EIO;
+			if (ret)
+				return ret;
+			r->posted = 1;
+		}
+		for (size_t i = 0; i < r->nreq; i++) {
+			if (!r->reqs[i])
+				continue;
+			ret = r->xp->test(r, r->reqs[i]);
+			if (ret < 0)
+				return ret;
+			if (ret)
+				r->reqs[i] = NULL;
+			else
+				pending = 1;
+		}
+		if (pending)
+			return 0;
+		r->posted = 0;
+		r->pc = end < pl->nsteps ? end + 1 : end;
+	}
+	return 1;
+}
+
+/* ---- xport_peer: the owner's tagged transfers + the host combine ------ */
+
+static int world_rank(const struct lfa_coll_mc *mc, int grank)
+{
+	return mc->members ? mc->members[grank] : grank;
+}
+
+static int peer_nop(struct xrun *r)
+{
+	return 0;
+}
+
+static int peer_post(struct xrun *r, const struct lfa_step *st, void **req)
+{
+	const struct lfa_coll_domain *d = r->mc->ep->dom;
+
+	/* coll_form_tag (coll_coll.c:37-45): cid | the SENDING rank << 32 */
+	if (st->type == LFA_STEP_SEND)
+		return d->xops.send(d->xctx, world_rank(r->mc, st->peer),
+				    resolve(&r->x, st->src), st->count,
+				    r->cid | (uint64_t)r->mc->rank << 32, req);
+	return d->xops.recv(d->xctx, world_rank(r->mc, st->peer),
+			    resolve(&r->x, st->dst), st->count,
+			    r->cid | (uint64_t)st->peer << 32, req);
+}
+
+static int peer_test(struct xrun *r, void *req)
+{
+	const struct lfa_coll_domain *d = r->mc->ep->dom;
+
+	return d->xops.test(d->xctx, req);
+}
+
+static int peer_local(struct xrun *r, const struct lfa_step *st)
+{
+	switch (st->type) {
+	case LFA_STEP_REDUCE:
+		return lfa_host_write(r->op, r->dt, resolve(&r->x, st->dst),
+				      resolve(&r->x, st->src), st->count);
+	case LFA_STEP_TREE: {
+		const void *srcs[LFA_TREE_MAX];
+
+		if (st->nsrc > LFA_TREE_MAX)
+			return -LFA_EINVAL;
+		for (uint32_t k = 0; k < st->nsrc; k++)
+			srcs[k] = resolve(&r->x, r->pl->refs[st->first + k]);
+		return lfa_host_reduce_tree(r->op, r->dt, resolve(&r->x, st->dst),
+					    srcs, (int)st->nsrc, st->count);
+	}
+	case LFA_STEP_COPY:
+		memmove(resolve(&r->x, st->dst), resolve(&r->x, st->src), st->count);
+		return 0;
+	default:
+		return -LFA_EINVAL;     /* TREE_PUT: P2P plans are not used here */
+	}
+}
+
+static int peer_coll(struct xrun *r, const struct lfa_step *st)
+{
+	return -LFA_EINVAL;             /* lowered to SEND/RECV by host_start */
+}
+
+static const struct xport xport_peer = {
+	peer_nop, peer_post, peer_nop, peer_test, peer_local, peer_coll,
+};
+
+/*
+ * One collective on a host domain: prov/coll's util_coll_operation and its
+ * work queue (ofi_coll.h:146-163) — the schedule, its own TMP, and the run.
+ */
+struct hop {
+	struct xrun r;
+	struct plan pl;
+	void *tmp;
+	int done, err;
 	uint64_t scratch[2];    /* barrier word and its result */
 };
 
@@ -1343,112 +1521,8 @@ static void hop_free(struct hop *h)
 		return;
 	plan_free(&h->pl);
 	free(h->tmp);
-	free(h->reqs);
+	free(h->r.reqs);
 	free(h);
-}
-
-static int world_rank(const struct lfa_coll_mc *mc, int grank)
-{
-	return mc->members ? mc->members[grank] : grank;
-}
-
-static int host_local(struct hop *h, const struct lfa_step *st)
-{
-	switch (st->type) {
-	case LFA_STEP_REDUCE:
-		return lfa_host_write(h->op, h->dt, resolve(&h->x, st->dst),
-				      resolve(&h->x, st->src), st->count);
-	case LFA_STEP_TREE: {
-		const void *srcs[LFA_TREE_MAX];
-
-		if (st->nsrc > LFA_TREE_MAX)
-			return -LFA_EINVAL;
-		for (uint32_t k = 0; k < st->nsrc; k++)
-			srcs[k] = resolve(&h->x, h->pl.refs[st->first + k]);
-		return lfa_host_reduce_tree(h->op, h->dt, resolve(&h->x, st->dst),
-					    srcs, (int)st->nsrc, st->count);
-	}
-	case LFA_STEP_COPY:
-		memmove(resolve(&h->x, st->dst), resolve(&h->x, st->src), st->count);
-		return 0;
-	default:
-		return -LFA_EINVAL;     /* BARRIER / TREE_PUT / collectives: not planned here */
-	}
-}
-
-/* Run the operation as far as it goes: 1 done, 0 waiting on transfers, <0. */
-static int host_advance(struct lfa_coll_ep *ep, struct hop *h)
-{
-	const struct lfa_peer_xfer_ops *xo = &ep->dom->xops;
-	void *xc = ep->dom->xctx;
-
-	while (h->pc < h->pl.nsteps) {
-		const struct lfa_step *st = &h->pl.steps[h->pc];
-		size_t end;
-		int ret, pending = 0;
-
-		if (st->type == LFA_STEP_GROUP_END) {
-			h->pc++;
-			continue;
-		}
-		if (st->type != LFA_STEP_SEND && st->type != LFA_STEP_RECV) {
-			ret = host_local(h, st);
-			if (ret)
-				return ret;
-			h->pc++;
-			continue;
-		}
-		for (end = h->pc; end < h->pl.nsteps &&
-		     h->pl.steps[end].type != LFA_STEP_GROUP_END; end++)
-			;
-		if (!h->posted) {
-			size_t need = end - h->pc;
-
-			if (need > h->creq) {
-				void **nr = realloc(h->reqs, need * sizeof(*nr));
-
-				if (!nr)
-					return -LFA_ENOMEM;
-				h->reqs = nr;
-				h->creq = need;
-			}
-			h->nreq = 0;
-			for (size_t i = h->pc; i < end; i++) {
-				const struct lfa_step *x = &h->pl.steps[i];
-				void **rq = &h->reqs[h->nreq];
-
-				*rq = NULL;
-				if (x->type == LFA_STEP_SEND)
-					ret = xo->send(xc, world_rank(h->mc, x->peer),
-						       resolve(&h->x, x->src), x->count,
-						       h->cid | (uint64_t)h->mc->rank << 32, rq);
-				else
-					ret = xo->recv(xc, world_rank(h->mc, x->peer),
-						       resolve(&h->x, x->dst), x->count,
-						       h->cid | (uint64_t)x->peer << 32, rq);
-				h->nreq++;
-				if (ret)
-					return ret;
-			}
-			h->posted = 1;
-		}
-		for (size_t i = 0; i < h->nreq; i++) {
-			if (!h->reqs[i])
-				continue;
-			ret = xo->test(xc, h->reqs[i]);
-			if (ret < 0)
-				return ret;
-			if (ret)
-				h->reqs[i] = NULL;
-			else
-				pending = 1;
-		}
-		if (pending)
-			return 0;
-		h->posted = 0;
-		h->pc = end < h->pl.nsteps ? end + 1 : end;
-	}
-	return 1;
 }
 
 /* Advance every in-flight host operation (ep->lock held). */
@@ -1460,7 +1534,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 
 		if (!h || h->done || h->err)
 			continue;
-		ret = host_advance(ep, h);
+		ret = xrun_advance(&h->r);
 		if (ret < 0)
 			h->err = ret;
 		else if (ret)
@@ -1706,63 +1780,83 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 /* executor: schedule -> RCCL + kernels on the endpoint stream             */
 /* ---------------------------------------------------------------------- */
 
+/* ---- xport_rccl: RCCL over xGMI + the gfx950 kernels, stream-ordered -- */
+
+static int rccl_group_start(struct xrun *r)
+{
+	return ncclGroupStart() == ncclSuccess ? 0 : -LFA_EIO;
+}
+
+static int rccl_group_end(struct xrun *r)
+{
+	return ncclGroupEnd() == ncclSuccess ? 0 : -LFA_EIO;
+}
+
+static int rccl_post(struct xrun *r, const struct lfa_step *st, void **req)
+{
+	ncclResult_t e;
+
+	if (st->type == LFA_STEP_SEND)
+		e = ncclSend(resolve(&r->x, st->src), st->count, ncclUint8, st->peer,
+			     r->mc->comm, r->stream);
+	else
+		e = ncclRecv(resolve(&r->x, st->dst), st->count, ncclUint8, st->peer,
+			     r->mc->comm, r->stream);
+	return e == ncclSuccess ? 0 : -LFA_EIO;
+}
+
+static int rccl_local(struct xrun *r, const struct lfa_step *st)
+{
+	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
+}
+
+static int rccl_coll(struct xrun *r, const struct lfa_step *st)
+{
+	ncclComm_t c = r->mc->comm;
+	ncclResult_t e;
+
+	switch (st->type) {
+	case LFA_STEP_ALLTOALL:
+		e = ncclAllToAll(resolve(&r->x, st->src), resolve(&r->x, st->dst),
+				 st->count, ncclUint8, c, r->stream);
+		break;
+	case LFA_STEP_ALLGATHER:
+		e = ncclAllGather(resolve(&r->x, st->src), resolve(&r->x, st->dst),
+				  st->count, ncclUint8, c, r->stream);
+		break;
+	default: {
+		/* BARRIER, stream-ordered: a one-word allreduce completes on a
+		 * rank only after every member's stream has reached it */
+		uint64_t *w = (uint64_t *)r->mc->ep->barrier_dev + 2;
+
+		e = ncclAllReduce(w, w, 1, ncclUint64, ncclSum, c, r->stream);
+	}
+	}
+	return e == ncclSuccess ? 0 : -LFA_EIO;
+}
+
+static const struct xport xport_rccl = {
+	rccl_group_start, rccl_post, rccl_group_end, NULL, rccl_local, rccl_coll,
+};
+
+/* Enqueue a whole schedule on `s` (one xrun_advance pass runs it all). */
 static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 		     const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
 		     hipStream_t s)
 {
-	int in_group = 0, ret = 0;
+	struct xrun r;
+	int ret;
 
-	for (size_t i = 0; i < pl->nsteps && !ret; i++) {
-		const struct lfa_step *st = &pl->steps[i];
-
-		switch (st->type) {
-		case LFA_STEP_SEND:
-		case LFA_STEP_RECV:
-			if (!in_group) {
-				if (ncclGroupStart() != ncclSuccess)
-					return -LFA_EIO;
-				in_group = 1;
-			}
-			if (st->type == LFA_STEP_SEND)
-				ret = ncclSend(resolve(x, st->src), st->count, ncclUint8,
-					       st->peer, mc->comm, s) == ncclSuccess ?
-				      0 : -LFA_EIO;
-			else
-				ret = ncclRecv(resolve(x, st->dst), st->count, ncclUint8,
-					       st->peer, mc->comm, s) == ncclSuccess ?
-				      0 : -LFA_EIO;
-			break;
-		case LFA_STEP_GROUP_END:
-			if (in_group && ncclGroupEnd() != ncclSuccess)
-				return -LFA_EIO;
-			in_group = 0;
-			break;
-		case LFA_STEP_ALLTOALL:
-			ret = ncclAllToAll(resolve(x, st->src), resolve(x, st->dst),
-					   st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
-			      0 : -LFA_EIO;
-			break;
-		case LFA_STEP_ALLGATHER:
-			ret = ncclAllGather(resolve(x, st->src), resolve(x, st->dst),
-					    st->count, ncclUint8, mc->comm, s) == ncclSuccess ?
-			      0 : -LFA_EIO;
-			break;
-		case LFA_STEP_BARRIER: {
-			/* stream-ordered: a one-word allreduce completes on a rank
-			 * only after every member's stream has reached it */
-			uint64_t *w = (uint64_t *)mc->ep->barrier_dev + 2;
-
-			ret = ncclAllReduce(w, w, 1, ncclUint64, ncclSum, mc->comm, s) ==
-			      ncclSuccess ? 0 : -LFA_EIO;
-			break;
-		}
-		default:
-			ret = run_local(st, pl->refs, x, op, dt, s);
-		}
-	}
-	if (in_group && ncclGroupEnd() != ncclSuccess && !ret)
-		ret = -LFA_EIO;
-	return ret;
+	memset(&r, 0, sizeof(r));
+	r.xp = &xport_rccl;
+	r.pl = pl;
+	r.x = *x;
+	r.mc = mc;
+	r.op = op;
+	r.dt = dt;
+	r.stream = s;
+	ret = xrun_advance(&r);
+	return ret == 1 ? 0 : ret ? ret : -LFA_EIO;
 }
 
 /*
@@ -2196,13 +2290,15 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		return ret;
 	if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp)))
 		return -LFA_ENOMEM;
-	h->mc = mc;
-	h->op = op;
-	h->dt = dt;
-	h->cid = (uint64_t)mc->group_id << 16 | (uint16_t)(mc->seq - 1);
-	h->x.base[LFA_BUF_SEND] = coll == LFA_BROADCAST ? result : (void *)buf;
-	h->x.base[LFA_BUF_RESULT] = result;
-	h->x.base[LFA_BUF_TMP] = h->tmp;
+	h->r.xp = &xport_peer;
+	h->r.pl = &h->pl;
+	h->r.mc = mc;
+	h->r.op = op;
+	h->r.dt = dt;
+	h->r.cid = (uint64_t)mc->group_id << 16 | (uint16_t)(mc->seq - 1);
+	h->r.x.base[LFA_BUF_SEND] = coll == LFA_BROADCAST ? result : (void *)buf;
+	h->r.x.base[LFA_BUF_RESULT] = result;
+	h->r.x.base[LFA_BUF_TMP] = h->tmp;
 	return 0;
 }
 

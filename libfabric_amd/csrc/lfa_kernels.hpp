@@ -783,7 +783,11 @@ template <int OP, typename T, int NLEAF>
 static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
                              hipStream_t s) {
   constexpr size_t E = sizeof(T);
-  constexpr int U = 4;  // 4 KiB of every input per wave (tune variant 14)
+  // 4 KiB of every input per wave (tune variant 14: +2 points over 2 KiB at
+  // 8 inputs) where the registers allow it: up to 8 leaves of 4-16 B
+  // elements.  Wider fan-in or byte/short lanes keep 2 KiB (U = 4 there
+  // needs > 256 VGPRs and gave wrong uint8 results at 16 leaves).
+  constexpr int U = (NLEAF <= 8 && E >= 4) ? 4 : 2;
   size_t nvec = vec ? (cnt - head) * E / 16 : 0;
   if (nvec) {
     PutArgs b = a;
