@@ -1,0 +1,757 @@
+/*
+ * off_lfa_peer — N processes drive liboff_lfa-fi.so with the provider's
+ * PEER transport: every transfer of a collective goes through the owner
+ * endpoint's tagged messaging (fi_tsendmsg / fi_trecvmsg with
+ * FI_PEER_TRANSFER), the way prov/coll's do through rxm
+ * (prov/coll/src/coll_coll.c:770-814), and the owner reports each finished
+ * transfer back through the peer_ops->complete the provider installed
+ * (rxm_cq.c:846-872, 1532-1546).
+ *
+ *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual]
+ *
+ * The owner here is a minimal stand-in for rxm over a socket provider: one
+ * AF_UNIX socket pair per rank pair (made before fork), non-blocking,
+ * messages framed as {tag, length, payload}, matched per (source, tag) in
+ * arrival order; sends complete once written, receives once matched.  Each
+ * rank joins the world group over an av_set of every rank, runs allreduce /
+ * reduce_scatter / reduce / allgather / broadcast / barrier and a subset
+ * join, and writes every input and output under <outdir> (r<rank>_<case>_in /
+ * _out .bin) for tests/test_off_lfa.py to check against the oracle; the
+ * known answer of fabtests/multinode/src/core_coll.c:230-277 is checked
+ * here.  CPU only: no HIP call is made.  Prints "OK peer" and exits 0 when
+ * every rank passed.
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <rdma/fabric.h>
+#include <rdma/fi_cm.h>
+#include <rdma/fi_collective.h>
+#include <rdma/fi_domain.h>
+#include <rdma/fi_endpoint.h>
+#include <rdma/fi_eq.h>
+#include <rdma/fi_errno.h>
+#include <rdma/fi_tagged.h>
+#include <rdma/providers/fi_peer.h>
+#include <rdma/providers/fi_prov.h>
+
+#include "off_lfa.h"
+
+#define MAXR 16
+static int failures, me, nranks;
+#define CHECK(cond, ...)                                                        \
+	do {                                                                    \
+		if (!(cond)) {                                                  \
+			fprintf(stderr, "rank %d FAIL %s:%d: ", me, __FILE__, __LINE__); \
+			fprintf(stderr, __VA_ARGS__);                           \
+			fprintf(stderr, "\n");                                  \
+			failures++;                                             \
+		}                                                               \
+	} while (0)
+
+/* ------------------------------------------ the owner's tagged transport -- */
+
+struct msg {
+	struct msg *next;
+	uint64_t tag;
+	size_t len, off;
+	unsigned char *data;         /* owned copy (sends, unexpected receives) */
+	void *user;                  /* posted receive buffer */
+	void *context;               /* provider's fi_msg_tagged.context */
+};
+
+struct link {
+	int fd;
+	struct msg *sendq, **send_tail;
+	struct msg *posted, *unexp;  /* receives: posted / arrived unmatched */
+	unsigned char hdr[16];
+	size_t hdr_got;
+	struct msg *in;              /* message being read */
+};
+
+static struct owner {
+	struct fid_ep ep;
+	struct fi_ops ep_fi_ops;
+	struct fi_ops_cm cm;
+	struct fi_ops_tagged tagged;
+	struct fid_domain domain;
+	struct fid_peer_av peer_av;
+	struct fi_ops_av_owner av_ops;
+	struct fid_peer_cq peer_cq;
+	struct fi_ops_cq_owner cq_ops;
+	struct fid_eq eq;
+	struct fi_ops_eq eq_ops;
+	struct fid_ep *offload;              /* the off_lfa endpoint */
+	struct fi_ops_transfer_peer *xfer;   /* its peer_ops */
+	struct link link[MAXR];
+	pthread_mutex_t lock;                /* the provider's progress thread
+					      * posts while we progress */
+	void *comp[256];
+	int ncomp;
+	struct fi_eq_entry eve[8];
+	uint32_t ev[8];
+	int nev;
+	uint64_t bytes_sent, bytes_recv;
+} own;
+
+static void complete_xfer(void *context, uint64_t flags, size_t len, uint64_t tag)
+{
+	struct fi_cq_tagged_entry e;
+
+	memset(&e, 0, sizeof(e));
+	e.op_context = context;
+	e.flags = flags | FI_TAGGED;
+	e.len = len;
+	e.tag = tag;
+	CHECK(own.xfer->complete(own.offload, &e, FI_ADDR_NOTAVAIL) == 0, "peer complete");
+}
+
+static ssize_t owner_tsendmsg(struct fid_ep *ep, const struct fi_msg_tagged *m,
+			      uint64_t flags)
+{
+	struct link *l;
+	struct msg *x;
+	size_t len = 0;
+
+	if (!(flags & FI_PEER_TRANSFER) || m->addr >= (fi_addr_t)nranks ||
+	    (int)m->addr == me)
+		return -FI_EINVAL;
+	for (size_t i = 0; i < m->iov_count; i++)
+		len += m->msg_iov[i].iov_len;
+	x = calloc(1, sizeof(*x));
+	x->data = malloc(16 + len);
+	memcpy(x->data, &m->tag, 8);
+	memcpy(x->data + 8, &len, 8);
+	for (size_t i = 0, o = 16; i < m->iov_count; o += m->msg_iov[i].iov_len, i++)
+		memcpy(x->data + o, m->msg_iov[i].iov_base, m->msg_iov[i].iov_len);
+	x->len = 16 + len;
+	x->tag = m->tag;
+	x->context = m->context;
+	l = &own.link[m->addr];
+	pthread_mutex_lock(&own.lock);
+	*l->send_tail = x;
+	l->send_tail = &x->next;
+	pthread_mutex_unlock(&own.lock);
+	return 0;
+}
+
+static ssize_t owner_trecvmsg(struct fid_ep *ep, const struct fi_msg_tagged *m,
+			      uint64_t flags)
+{
+	struct link *l;
+	struct msg **pp, *x;
+
+	if (!(flags & FI_PEER_TRANSFER) || m->iov_count != 1 ||
+	    m->addr >= (fi_addr_t)nranks || (int)m->addr == me)
+		return -FI_EINVAL;
+	l = &own.link[m->addr];
+	pthread_mutex_lock(&own.lock);
+	for (pp = &l->unexp; *pp && (*pp)->tag != m->tag; pp = &(*pp)->next)
+		;
+	if ((x = *pp)) {             /* arrived before it was posted */
+		*pp = x->next;
+		pthread_mutex_unlock(&own.lock);
+		CHECK(x->len == m->msg_iov[0].iov_len, "length %zu vs %zu", x->len,
+		      m->msg_iov[0].iov_len);
+		memcpy(m->msg_iov[0].iov_base, x->data, x->len);
+		own.bytes_recv += x->len;
+		complete_xfer(m->context, FI_RECV, x->len, x->tag);
+		free(x->data);
+		free(x);
+		return 0;
+	}
+	x = calloc(1, sizeof(*x));
+	x->tag = m->tag;
+	x->len = m->msg_iov[0].iov_len;
+	x->user = m->msg_iov[0].iov_base;
+	x->context = m->context;
+	for (pp = &l->posted; *pp; pp = &(*pp)->next)
+		;
+	*pp = x;
+	pthread_mutex_unlock(&own.lock);
+	return 0;
+}
+
+/* A message arrived whole: the first posted receive with its tag takes it,
+ * else it waits in the unexpected list (rxm's eager path). */
+static void deliver(struct link *l, struct msg *in)
+{
+	struct msg **pp, *r;
+
+	for (pp = &l->posted; *pp && (*pp)->tag != in->tag; pp = &(*pp)->next)
+		;
+	if (!(r = *pp)) {
+		struct msg **t = &l->unexp;
+
+		while (*t)
+			t = &(*t)->next;
+		*t = in;
+		return;
+	}
+	*pp = r->next;
+	CHECK(r->len == in->len, "length %zu vs %zu", r->len, in->len);
+	memcpy(r->user, in->data, in->len);
+	own.bytes_recv += in->len;
+	complete_xfer(r->context, FI_RECV, in->len, in->tag);
+	free(in->data);
+	free(in);
+	free(r);
+}
+
+/* The owner's progress (rxm's, driven by fi_cq_read): move bytes both ways. */
+static void owner_progress(void)
+{
+	pthread_mutex_lock(&own.lock);
+	for (int p = 0; p < nranks; p++) {
+		struct link *l = &own.link[p];
+		ssize_t n;
+
+		if (p == me)
+			continue;
+		while (l->sendq) {
+			struct msg *x = l->sendq;
+
+			n = write(l->fd, x->data + x->off, x->len - x->off);
+			if (n <= 0)
+				break;
+			x->off += (size_t)n;
+			if (x->off < x->len)
+				break;
+			l->sendq = x->next;
+			if (!l->sendq)
+				l->send_tail = &l->sendq;
+			own.bytes_sent += x->len - 16;
+			complete_xfer(x->context, FI_SEND, x->len - 16, x->tag);
+			free(x->data);
+			free(x);
+		}
+		for (;;) {
+			if (!l->in) {
+				n = read(l->fd, l->hdr + l->hdr_got, 16 - l->hdr_got);
+				if (n <= 0)
+					break;
+				l->hdr_got += (size_t)n;
+				if (l->hdr_got < 16)
+					continue;
+				l->in = calloc(1, sizeof(*l->in));
+				memcpy(&l->in->tag, l->hdr, 8);
+				memcpy(&l->in->len, l->hdr + 8, 8);
+				l->in->data = malloc(l->in->len ? l->in->len : 1);
+				l->hdr_got = 0;
+			}
+			if (l->in->off < l->in->len) {
+				n = read(l->fd, l->in->data + l->in->off, l->in->len - l->in->off);
+				if (n <= 0)
+					break;
+				l->in->off += (size_t)n;
+			}
+			if (l->in->off == l->in->len) {
+				struct msg *in = l->in;
+
+				l->in = NULL;
+				deliver(l, in);
+			}
+		}
+	}
+	pthread_mutex_unlock(&own.lock);
+}
+
+static int owner_av_query(struct fid_peer_av *av, struct fi_av_attr *attr)
+{
+	memset(attr, 0, sizeof(*attr));
+	attr->count = nranks;
+	return 0;
+}
+
+static fi_addr_t owner_ep_addr(struct fid_peer_av *av, struct fid_ep *ep)
+{
+	return ep == &own.ep ? (fi_addr_t)me : FI_ADDR_NOTAVAIL;
+}
+
+static ssize_t owner_cq_write(struct fid_peer_cq *cq, void *context, uint64_t flags,
+			      size_t len, void *buf, uint64_t data, uint64_t tag,
+			      fi_addr_t src)
+{
+	CHECK(flags & FI_COLLECTIVE, "cq flags");
+	__atomic_store_n(&own.comp[__atomic_fetch_add(&own.ncomp, 1, __ATOMIC_ACQ_REL) & 255],
+			 context, __ATOMIC_RELEASE);
+	return 0;
+}
+
+static ssize_t owner_cq_writeerr(struct fid_peer_cq *cq, const struct fi_cq_err_entry *e)
+{
+	CHECK(0, "collective error %d", e->err);
+	return 0;
+}
+
+static ssize_t owner_eq_write(struct fid_eq *eq, uint32_t event, const void *buf,
+			      size_t len, uint64_t flags)
+{
+	int i = own.nev;
+
+	if (i >= 8 || len != sizeof(struct fi_eq_entry))
+		return -FI_EINVAL;
+	own.ev[i] = event;
+	memcpy(&own.eve[i], buf, len);
+	__atomic_store_n(&own.nev, i + 1, __ATOMIC_RELEASE);
+	return (ssize_t)len;
+}
+
+static int owner_getname(fid_t fid, void *addr, size_t *addrlen)
+{
+	if (*addrlen < sizeof(uint64_t)) {
+		*addrlen = sizeof(uint64_t);
+		return -FI_ETOOSMALL;
+	}
+	*(uint64_t *)addr = 0x4c4641ull + (uint64_t)me;
+	*addrlen = sizeof(uint64_t);
+	return 0;
+}
+
+static void owner_init(void)
+{
+	own.cm.size = sizeof(own.cm);
+	own.cm.getname = owner_getname;
+	own.tagged.size = sizeof(own.tagged);
+	own.tagged.sendmsg = owner_tsendmsg;
+	own.tagged.recvmsg = owner_trecvmsg;
+	own.ep_fi_ops.size = sizeof(own.ep_fi_ops);
+	own.ep.fid.fclass = FI_CLASS_EP;
+	own.ep.fid.ops = &own.ep_fi_ops;
+	own.ep.cm = &own.cm;
+	own.ep.tagged = &own.tagged;
+	own.domain.fid.fclass = FI_CLASS_DOMAIN;
+	own.av_ops.size = sizeof(own.av_ops);
+	own.av_ops.query = owner_av_query;
+	own.av_ops.ep_addr = owner_ep_addr;
+	own.peer_av.fid.fclass = FI_CLASS_PEER_AV;
+	own.peer_av.owner_ops = &own.av_ops;
+	own.cq_ops.size = sizeof(own.cq_ops);
+	own.cq_ops.write = owner_cq_write;
+	own.cq_ops.writeerr = owner_cq_writeerr;
+	own.peer_cq.fid.fclass = FI_CLASS_PEER_CQ;
+	own.peer_cq.owner_ops = &own.cq_ops;
+	own.eq_ops.size = sizeof(own.eq_ops);
+	own.eq_ops.write = owner_eq_write;
+	own.eq.fid.fclass = FI_CLASS_EQ;
+	own.eq.ops = &own.eq_ops;
+	pthread_mutex_init(&own.lock, NULL);
+	for (int p = 0; p < nranks; p++)
+		own.link[p].send_tail = &own.link[p].sendq;
+}
+
+/* --------------------------------------------------------------- driving -- */
+
+struct util_ep_prefix {          /* include/ofi_util.h:280-306 */
+	struct fid_ep ep_fid;
+	void *domain, *av, *av_entry[2], *eq, *rx_cq;
+	uint64_t rx_op_flags;
+	void *tx_cq;
+	uint64_t tx_op_flags, inject_op_flags, tx_msg_flags, rx_msg_flags;
+	void *cntrs[6];
+	void (*cntr_inc_funcs[6])(void *);
+	enum fi_ep_type type;
+	uint64_t caps, flags;
+	void (*progress)(void *);
+};
+
+static int manual;
+
+static void drive(void)
+{
+	owner_progress();
+	if (manual)
+		((struct util_ep_prefix *)own.offload)->progress(own.offload);
+}
+
+static int wait_comp(void *ctx)
+{
+	struct timespec t0, t;
+
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	for (;;) {
+		int n = __atomic_load_n(&own.ncomp, __ATOMIC_ACQUIRE);
+
+		for (int i = 0; i < n && i < 256; i++)
+			if (__atomic_load_n(&own.comp[i], __ATOMIC_ACQUIRE) == ctx) {
+				own.comp[i] = NULL;
+				return 0;
+			}
+		drive();
+		clock_gettime(CLOCK_MONOTONIC, &t);
+		if (t.tv_sec - t0.tv_sec > 60) {
+			CHECK(0, "completion %p timed out", ctx);
+			return -1;
+		}
+	}
+}
+
+static int wait_join(struct fid_mc *mc)
+{
+	struct timespec t0, t;
+
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	for (;;) {
+		int n = __atomic_load_n(&own.nev, __ATOMIC_ACQUIRE);
+
+		for (int i = 0; i < n; i++)
+			if (own.eve[i].fid == &mc->fid) {
+				CHECK(own.ev[i] == FI_JOIN_COMPLETE, "event %u", own.ev[i]);
+				own.eve[i].fid = NULL;
+				return 0;
+			}
+		drive();
+		clock_gettime(CLOCK_MONOTONIC, &t);
+		if (t.tv_sec - t0.tv_sec > 60) {
+			CHECK(0, "join timed out");
+			return -1;
+		}
+	}
+}
+
+static const char *outdir;
+
+static void dump(const char *name, const char *io, const void *p, size_t n)
+{
+	char path[4096];
+	FILE *f;
+
+	snprintf(path, sizeof(path), "%s/r%d_%s_%s.bin", outdir, me, name, io);
+	f = fopen(path, "wb");
+	if (!f || fwrite(p, 1, n, f) != n)
+		CHECK(0, "write %s", path);
+	if (f)
+		fclose(f);
+}
+
+static uint64_t lcg_state;
+
+static uint64_t lcg(void)
+{
+	lcg_state = lcg_state * 6364136223846793005ull + 1442695040888963407ull;
+	return lcg_state >> 11;
+}
+
+static double unif(double lo, double hi)
+{
+	return lo + (hi - lo) * (double)lcg() / (double)(1ull << 53);
+}
+
+static void seed(int c)
+{
+	lcg_state = 0x5EEDull + (uint64_t)me * 1000003ull + (uint64_t)c * 7919ull;
+}
+
+typedef struct fi_provider *(*ini_fn)(void);
+
+static int run_rank(const char *prov_path)
+{
+	void *dl;
+	struct fi_provider *prov;
+	struct fi_info *hints, *info = NULL;
+	struct fid_fabric *fabric;
+	struct fid_domain *domain;
+	struct fid_av *av;
+	struct fid_cq *cq;
+	struct fid_eq *eq;
+	struct fid_ep *ep;
+	struct fid_av_set *set, *sub_set;
+	struct fid_mc *mc, *sub;
+	struct fi_peer_domain_context dctx = { sizeof(dctx), NULL };
+	struct fi_peer_av_context actx = { sizeof(actx), NULL };
+	struct fi_peer_cq_context cctx = { sizeof(cctx), NULL };
+	struct fi_peer_eq_context ectx = { sizeof(ectx), NULL };
+	struct fi_peer_transfer_context tctx;
+	struct fi_av_attr av_attr = { 0 };
+	struct fi_cq_attr cq_attr = { 0 };
+	struct fi_eq_attr eq_attr = { 0 };
+	struct fi_av_set_attr sattr = { 0 };
+	fi_addr_t world, subaddr;
+	int req[32], one = 1, ival;
+	size_t len;
+
+	owner_init();
+	dl = dlopen(prov_path, RTLD_NOW);
+	if (!dl) {
+		fprintf(stderr, "dlopen: %s\n", dlerror());
+		return 1;
+	}
+	prov = ((ini_fn)dlsym(dl, "fi_prov_ini"))();
+	hints = calloc(1, sizeof(*hints));
+	hints->fabric_attr = calloc(1, sizeof(*hints->fabric_attr));
+	hints->mode = FI_PEER_TRANSFER;
+	hints->fabric_attr->prov_name = OFF_LFA_PROV_NAME;
+	CHECK(prov->getinfo(FI_VERSION(2, 0), NULL, NULL, 0, hints, &info) == 0, "getinfo");
+	free(hints->fabric_attr);
+	free(hints);
+	if (!info)
+		return 1;
+	CHECK(prov->fabric(info->fabric_attr, &fabric, NULL) == 0, "fabric");
+	dctx.domain = &own.domain;
+	CHECK(fi_domain2(fabric, info, &domain, FI_PEER, &dctx) == 0, "domain2");
+	actx.av = &own.peer_av;
+	av_attr.flags = FI_PEER;
+	CHECK(fi_av_open(domain, &av_attr, &av, &actx) == 0, "av");
+	cctx.cq = &own.peer_cq;
+	cq_attr.flags = FI_PEER;
+	CHECK(fi_cq_open(domain, &cq_attr, &cq, &cctx) == 0, "cq");
+	ectx.eq = &own.eq;
+	eq_attr.flags = FI_PEER;
+	CHECK(fi_eq_open(fabric, &eq_attr, &eq, &ectx) == 0, "eq");
+	memset(&tctx, 0, sizeof(tctx));
+	tctx.size = sizeof(tctx);
+	tctx.info = info;
+	tctx.ep = &own.ep;
+	CHECK(fi_endpoint(domain, info, &ep, &tctx) == 0, "endpoint");
+	own.offload = ep;
+	own.xfer = tctx.peer_ops;
+	CHECK(fi_ep_bind(ep, &av->fid, 0) == 0, "bind av");
+	CHECK(fi_ep_bind(ep, &cq->fid, FI_TRANSMIT | FI_RECV) == 0, "bind cq");
+	CHECK(fi_ep_bind(ep, &eq->fid, 0) == 0, "bind eq");
+	CHECK(fi_enable(ep) == 0, "enable");
+	/* the peer transport: transfers through this owner's tagged ops */
+	CHECK(fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_TRANSPORT, &one,
+			sizeof(one)) == 0, "transport option");
+	ival = -1;
+	len = sizeof(ival);
+	CHECK(fi_getopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_TRANSPORT, &ival, &len) == 0 &&
+	      ival == 1, "transport readback");
+
+	/* world: an av_set of every rank (fabtests core_coll.c:453-521 order) */
+	sattr.count = (size_t)nranks;
+	sattr.start_addr = 0;
+	sattr.end_addr = (fi_addr_t)nranks - 1;
+	sattr.stride = 1;
+	CHECK(fi_av_set(av, &sattr, &set, NULL) == 0, "av_set");
+	CHECK(fi_join_collective(ep, FI_ADDR_NOTAVAIL, set, 0, &mc, &req[0]) == 0, "join");
+	wait_join(mc);
+	CHECK(fi_av_set_addr(set, &world) == 0, "av_set_addr");
+	CHECK(fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_TRANSPORT, &one,
+			sizeof(one)) == -FI_EBUSY, "transport fixed after the join");
+
+	{   /* the reference's known answer: uint64 SUM of 1234 + rank */
+		uint64_t x = 1234 + (uint64_t)me, y = 0, want = 0;
+
+		for (int r = 0; r < nranks; r++)
+			want += 1234 + (uint64_t)r;
+		CHECK(fi_allreduce(ep, &x, 1, NULL, &y, NULL, world, FI_UINT64, FI_SUM, 0,
+				   &req[1]) == 0, "allreduce ka");
+		wait_comp(&req[1]);
+		CHECK(y == want, "known answer %lu vs %lu", (unsigned long)y,
+		      (unsigned long)want);
+	}
+	for (int algo = 0; algo < 2; algo++) {
+		const char *sfx = algo ? "_rd" : "";
+		char name[64];
+		float *fx = malloc(1000 * 4), *fy = calloc(1000, 4);
+		double *dx = malloc(4099 * 8), *dy = calloc(4099, 8);
+		int64_t lx[33], ly[33] = { 0 };
+
+		CHECK(fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_ALGO, &algo,
+				sizeof(algo)) == 0, "algo");
+		seed(1);
+		for (int i = 0; i < 1000; i++)
+			fx[i] = (float)unif(-1, 1);
+		CHECK(fi_allreduce(ep, fx, 1000, NULL, fy, NULL, world, FI_FLOAT, FI_SUM, 0,
+				   &req[2]) == 0, "allreduce f32");
+		seed(2);
+		for (int i = 0; i < 4099; i++)
+			dx[i] = unif(0.9, 1.1);
+		CHECK(fi_allreduce(ep, dx, 4099, NULL, dy, NULL, world, FI_DOUBLE, FI_PROD,
+				   0, &req[3]) == 0, "allreduce f64");
+		seed(3);
+		for (int i = 0; i < 33; i++)
+			lx[i] = (int64_t)(lcg() << 11 ^ lcg());
+		CHECK(fi_allreduce(ep, lx, 33, NULL, ly, NULL, world, FI_INT64, FI_BXOR, 0,
+				   &req[4]) == 0, "allreduce bxor");
+		/* three in flight at once; complete in any order here */
+		wait_comp(&req[2]);
+		wait_comp(&req[3]);
+		wait_comp(&req[4]);
+		snprintf(name, sizeof(name), "sum_f32%s", sfx);
+		dump(name, "in", fx, 1000 * 4);
+		dump(name, "out", fy, 1000 * 4);
+		snprintf(name, sizeof(name), "prod_f64%s", sfx);
+		dump(name, "in", dx, 4099 * 8);
+		dump(name, "out", dy, 4099 * 8);
+		snprintf(name, sizeof(name), "bxor_i64%s", sfx);
+		dump(name, "in", lx, sizeof(lx));
+		dump(name, "out", ly, sizeof(ly));
+		free(fx);
+		free(fy);
+		free(dx);
+		free(dy);
+	}
+	ival = 0;
+	fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_ALGO, &ival, sizeof(ival));
+	{   /* reduce_scatter: rank r gets block r (ragged at N = 3) */
+		size_t count = 1000, base = count / (size_t)nranks, extra = count % (size_t)nranks;
+		size_t mlen = base + ((size_t)me < extra);
+		float *x = malloc(count * 4), *y = calloc(mlen ? mlen : 1, 4);
+
+		seed(4);
+		for (size_t i = 0; i < count; i++)
+			x[i] = (float)unif(-1, 1);
+		CHECK(fi_reduce_scatter(ep, x, count, NULL, y, NULL, world, FI_FLOAT, FI_SUM,
+					0, &req[5]) == 0, "reduce_scatter");
+		wait_comp(&req[5]);
+		dump("rs_f32", "in", x, count * 4);
+		dump("rs_f32", "out", y, mlen * 4);
+		free(x);
+		free(y);
+	}
+	{   /* reduce to the last rank */
+		double *x = malloc(777 * 8), *y = calloc(777, 8);
+
+		seed(5);
+		for (int i = 0; i < 777; i++)
+			x[i] = unif(-1, 1);
+		CHECK(fi_reduce(ep, x, 777, NULL, y, NULL, world, (fi_addr_t)nranks - 1,
+				FI_DOUBLE, FI_SUM, 0, &req[6]) == 0, "reduce");
+		wait_comp(&req[6]);
+		dump("reduce_f64", "in", x, 777 * 8);
+		if (me == nranks - 1)
+			dump("reduce_f64", "out", y, 777 * 8);
+		free(x);
+		free(y);
+	}
+	{   /* allgather, broadcast, barrier */
+		int32_t g[10], all[10 * MAXR];
+		int64_t b[5];
+
+		for (int i = 0; i < 10; i++)
+			g[i] = 100 * me + i;
+		CHECK(fi_allgather(ep, g, 10, NULL, all, NULL, world, FI_INT32, 0,
+				   &req[7]) == 0, "allgather");
+		wait_comp(&req[7]);
+		for (int r = 0; r < nranks; r++)
+			for (int i = 0; i < 10; i++)
+				CHECK(all[r * 10 + i] == 100 * r + i, "allgather [%d][%d]", r, i);
+		for (int i = 0; i < 5; i++)
+			b[i] = me == 0 ? 77 + i : -1;
+		CHECK(fi_broadcast(ep, b, 5, NULL, world, 0, FI_INT64, 0, &req[8]) == 0,
+		      "broadcast");
+		wait_comp(&req[8]);
+		for (int i = 0; i < 5; i++)
+			CHECK(b[i] == 77 + i, "broadcast [%d]", i);
+		CHECK(fi_barrier(ep, world, &req[9]) == 0, "barrier");
+		wait_comp(&req[9]);
+	}
+	/* subset join: the first and the last rank (coll_coll.c:912-995) */
+	sattr.count = 2;
+	sattr.start_addr = 0;
+	sattr.end_addr = (fi_addr_t)nranks - 1;
+	sattr.stride = nranks > 1 ? (uint64_t)nranks - 1 : 1;
+	CHECK(fi_av_set(av, &sattr, &sub_set, NULL) == 0, "subset av_set");
+	CHECK(fi_join_collective(ep, fi_mc_addr(mc), sub_set, 0, &sub, &req[10]) == 0,
+	      "subset join");
+	wait_join(sub);
+	subaddr = fi_mc_addr(sub);
+	if (me == 0 || me == nranks - 1) {
+		float x[100], y[100];
+
+		seed(6);
+		for (int i = 0; i < 100; i++)
+			x[i] = (float)unif(-1, 1);
+		CHECK(fi_allreduce(ep, x, 100, NULL, y, NULL, subaddr, FI_FLOAT, FI_SUM, 0,
+				   &req[11]) == 0, "subset allreduce");
+		wait_comp(&req[11]);
+		dump("sub_f32", "in", x, sizeof(x));
+		dump("sub_f32", "out", y, sizeof(y));
+	} else {
+		float x = 0;
+
+		CHECK(fi_allreduce(ep, &x, 1, NULL, &x, NULL, subaddr, FI_FLOAT, FI_SUM, 0,
+				   &req[11]) == -FI_EINVAL, "non-member refused");
+	}
+	/* let the last transfers drain before anyone closes its sockets */
+	CHECK(fi_barrier(ep, world, &req[12]) == 0, "final barrier");
+	wait_comp(&req[12]);
+	CHECK(own.bytes_sent > 0 || nranks == 1, "the owner carried the transfers");
+	fi_close(&sub->fid);
+	fi_close(&sub_set->fid);
+	fi_close(&mc->fid);
+	fi_close(&set->fid);
+	fi_close(&ep->fid);
+	fi_close(&eq->fid);
+	fi_close(&cq->fid);
+	fi_close(&av->fid);
+	fi_close(&domain->fid);
+	fi_close(&fabric->fid);
+	return failures ? 1 : 0;
+}
+
+int main(int argc, char **argv)
+{
+	int sp[MAXR][MAXR][2], status, bad = 0;
+	pid_t pid[MAXR];
+
+	if (argc < 4) {
+		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> <nranks> <outdir> [manual]\n",
+			argv[0]);
+		return 2;
+	}
+	nranks = atoi(argv[2]);
+	outdir = argv[3];
+	manual = argc > 4 && !strcmp(argv[4], "manual");
+	if (manual)
+		setenv("OFF_LFA_PROGRESS", "manual", 1);
+	if (nranks < 1 || nranks > MAXR)
+		return 2;
+	for (int i = 0; i < nranks; i++)
+		for (int j = i + 1; j < nranks; j++)
+			if (socketpair(AF_UNIX, SOCK_STREAM, 0, sp[i][j]))
+				return 1;
+	for (int r = 0; r < nranks; r++) {
+		pid[r] = fork();
+		if (pid[r] < 0)
+			return 1;
+		if (pid[r] == 0) {
+			me = r;
+			for (int i = 0; i < nranks; i++)
+				for (int j = i + 1; j < nranks; j++) {
+					if (i == r)
+						own.link[j].fd = sp[i][j][0];
+					else
+						close(sp[i][j][0]);
+					if (j == r)
+						own.link[i].fd = sp[i][j][1];
+					else
+						close(sp[i][j][1]);
+				}
+			for (int p = 0; p < nranks; p++)
+				if (p != r)
+					fcntl(own.link[p].fd, F_SETFL,
+					      fcntl(own.link[p].fd, F_GETFL) | O_NONBLOCK);
+			_exit(run_rank(argv[1]));
+		}
+	}
+	for (int i = 0; i < nranks; i++)
+		for (int j = i + 1; j < nranks; j++) {
+			close(sp[i][j][0]);
+			close(sp[i][j][1]);
+		}
+	for (int r = 0; r < nranks; r++) {
+		if (waitpid(pid[r], &status, 0) < 0 || !WIFEXITED(status) ||
+		    WEXITSTATUS(status)) {
+			fprintf(stderr, "rank %d failed (status %#x)\n", r, status);
+			bad = 1;
+		}
+	}
+	if (bad)
+		return 1;
+	printf("OK peer%s\n", manual ? " manual" : "");
+	return 0;
+}

@@ -26,10 +26,20 @@
  * it; <key> = $OFF_LFA_BOOTSTRAP_KEY or "world").  A one-member set needs
  * neither.
  *
+ * Transport.  By default the world group is an RCCL communicator over xGMI
+ * and buffers may be device (or staged host) memory.  With
+ * OFF_LFA_OPT_TRANSPORT = 1 (or OFF_LFA_TRANSPORT=peer) the provider instead
+ * moves every transfer through the OWNER endpoint's tagged messaging with
+ * FI_PEER_TRANSFER, as prov/coll does through rxm (coll_coll.c:770-814): the
+ * owner must then provide fi_tsendmsg / fi_trecvmsg and report each finished
+ * transfer through the peer_ops->complete this provider installs; buffers are
+ * host memory and reductions run in liblfa's host combine.  No unique id is
+ * needed then.
+ *
  * Environment: OFF_LFA_DEVICE (HIP device ordinal; default $LOCAL_RANK,
  * else 0), OFF_LFA_PROGRESS=manual (no progress thread: the owner drives
  * progress through the util_ep progress slot or fi_cq_read on the
- * off_lfa CQ), OFF_LFA_ALGO (enum lfa_coll_algo).
+ * off_lfa CQ), OFF_LFA_ALGO (enum lfa_coll_algo), OFF_LFA_TRANSPORT=peer.
  */
 #ifndef OFF_LFA_H
 #define OFF_LFA_H
@@ -47,6 +57,9 @@ enum {
 	OFF_LFA_OPT_CHUNK,
 	/* int: HIP device ordinal; only before the world join */
 	OFF_LFA_OPT_DEVICE,
+	/* int: 0 = RCCL over xGMI (default), 1 = the owner's peer transfers;
+	 * only before the world join */
+	OFF_LFA_OPT_TRANSPORT,
 };
 
 #endif /* OFF_LFA_H */

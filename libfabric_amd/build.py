@@ -140,6 +140,7 @@ def build_example(verbose: bool = False) -> str | None:
 FABRIC_INC = os.environ.get("LFA_FABRIC_INCLUDE", "/root/reference/include")
 LIB_OFF = os.path.join(PKG, "liboff_lfa-fi.so")
 OFF_HOST = os.path.join(ROOT, "examples", "off_lfa_host")
+OFF_PEER = os.path.join(ROOT, "examples", "off_lfa_peer")
 
 
 def have_fabric_headers() -> bool:
@@ -171,6 +172,13 @@ def build_off_lfa(verbose: bool = False) -> str | None:
               "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-ldl"])
         if verbose:
             print(f"built {OFF_HOST}")
+    if _newer(OFF_PEER, [OFF_PEER + ".c", os.path.join(INC, "off_lfa.h")]):
+        # the multi-process owner with its own tagged transport: no HIP
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              "-I" + INC, "-I" + FABRIC_INC, "-o", OFF_PEER, OFF_PEER + ".c", "-ldl",
+              "-lpthread"])
+        if verbose:
+            print(f"built {OFF_PEER}")
     return LIB_OFF
 
 

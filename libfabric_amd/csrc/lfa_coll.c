@@ -1352,11 +1352,12 @@ struct xrun {
 	uint64_t cid;           /* xport_peer tags: group_id << 16 | seq */
 	size_t pc;
 	void **reqs;            /* the current group's transfers; NULL = done */
-	size_t nreq, creq;
-	int posted;
+	size_t nreq, creq;      /* nreq = steps of the group posted so far */
 };
 
-/* Run the schedule as far as it goes: 1 done, 0 waiting on transfers, <0. */
+/* Run the schedule as far as it goes: 1 done, 0 waiting on transfers, <0.
+ * A post that returns -LFA_EAGAIN (the owner's queue is full: prov/coll
+ * requeues such items, coll_coll.c:845-852) is retried on the next call. */
 static int xrun_advance(struct xrun *r)
 {
 	const struct plan *pl = r->pl;
@@ -1392,7 +1393,7 @@ static int xrun_advance(struct xrun *r)
 		for (end = r->pc; end < pl->nsteps &&
 		     pl->steps[end].type != LFA_STEP_GROUP_END; end++)
 			;
-		if (!r->posted) {
+		if (r->nreq < end - r->pc) {
 			size_t need = end - r->pc;
 
 			if (r->xp->test && need > r->creq) {
@@ -1403,22 +1404,24 @@ static int xrun_advance(struct xrun *r)
 				r->reqs = nr;
 				r->creq = need;
 			}
-			r->nreq = 0;
 			ret = r->xp->group_start(r);
-			for (size_t i = r->pc; i < end && !ret; i++) {
+			while (!ret && r->nreq < need) {
 				void *req = NULL;
 
-				ret = r->xp->post(r, &pl->steps[i], &req);
-				if (r->xp->test)
-					r->reqs[r->nreq++] = req;
+				ret = r->xp->post(r, &pl->steps[r->pc + r->nreq], &req);
+				if (!ret && r->xp->test)
+					r->reqs[r->nreq] = req;
+				if (!ret)
+					r->nreq++;
 			}
 			if (r->xp->group_end(r) && !ret)
 				ret = -LFA_EIO;
-			if (ret)
+			if (ret == -LFA_EAGAIN)
+				pending = 1;
+			else if (ret)
 				return ret;
-			r->posted = 1;
 		}
-		for (size_t i = 0; i < r->nreq; i++) {
+		for (size_t i = 0; r->xp->test && i < r->nreq; i++) {
 			if (!r->reqs[i])
 				continue;
 			ret = r->xp->test(r, r->reqs[i]);
@@ -1431,7 +1434,7 @@ static int xrun_advance(struct xrun *r)
 		}
 		if (pending)
 			return 0;
-		r->posted = 0;
+		r->nreq = 0;
 		r->pc = end < pl->nsteps ? end + 1 : end;
 	}
 	return 1;

@@ -63,6 +63,7 @@
 #include <rdma/fi_endpoint.h>
 #include <rdma/fi_eq.h>
 #include <rdma/fi_errno.h>
+#include <rdma/fi_tagged.h>
 #include <rdma/providers/fi_peer.h>
 #include <rdma/providers/fi_prov.h>
 
@@ -175,6 +176,8 @@ struct olfa_ep {
 	int device;
 	int algo;
 	size_t chunk;
+	int peer_xport;                    /* OFF_LFA_TRANSPORT=peer */
+	fi_addr_t *waddr;                  /* world rank -> owner AV address */
 	int have_uid;
 	unsigned char uid[LFA_UNIQUE_ID_BYTES];
 	struct lfa_coll_domain *ld;
@@ -520,13 +523,97 @@ static int olfa_uid_rendezvous(int rank, unsigned char *id)
 	}
 }
 
-/* Creates the RCCL-backed liblfa_coll domain + endpoint for the world
- * group (blocking, like ncclCommInitRank) and starts progress. */
-static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks)
+/*
+ * Peer transport (OFF_LFA_TRANSPORT=peer): the collective's transfers ride on
+ * the OWNER's tagged messaging, exactly as prov/coll's do on rxm's —
+ * fi_tsendmsg / fi_trecvmsg(FI_PEER_TRANSFER) on the owner endpoint with
+ * prov/coll's tag (coll_coll.c:770-814); the owner reports each finished
+ * transfer through peer_ops->complete (rxm_cq.c:1532-1546, 846-872), which
+ * lands in olfa_peer_complete below.  Buffers are host memory; reductions
+ * run in liblfa's host combine (lfa_coll_domain_open_host).
+ */
+struct olfa_xfer {
+	atomic_int done;                /* 1 ok, -err failed */
+	struct iovec iov;
+};
+
+static int olfa_xpost(struct olfa_ep *ep, int send, int peer, void *buf,
+		      size_t bytes, uint64_t tag, void **req)
+{
+	struct olfa_xfer *x = calloc(1, sizeof(*x));
+	struct fi_msg_tagged msg;
+	ssize_t ret;
+
+	if (!x)
+		return -LFA_ENOMEM;
+	x->iov.iov_base = buf;
+	x->iov.iov_len = bytes;
+	memset(&msg, 0, sizeof(msg));
+	msg.msg_iov = &x->iov;
+	msg.iov_count = 1;
+	msg.addr = ep->waddr[peer];
+	msg.tag = tag;
+	msg.context = x;
+	ret = send ? fi_tsendmsg(ep->peer_ep, &msg, FI_PEER_TRANSFER) :
+		     fi_trecvmsg(ep->peer_ep, &msg, FI_PEER_TRANSFER);
+	if (ret) {
+		free(x);
+		return ret == -FI_EAGAIN ? -LFA_EAGAIN : (int)ret;
+	}
+	*req = x;
+	return 0;
+}
+
+static int olfa_xsend(void *ctx, int peer, const void *buf, size_t bytes,
+		      uint64_t tag, void **req)
+{
+	return olfa_xpost(ctx, 1, peer, (void *)buf, bytes, tag, req);
+}
+
+static int olfa_xrecv(void *ctx, int peer, void *buf, size_t bytes, uint64_t tag,
+		      void **req)
+{
+	return olfa_xpost(ctx, 0, peer, buf, bytes, tag, req);
+}
+
+static int olfa_xtest(void *ctx, void *req)
+{
+	struct olfa_xfer *x = req;
+	int d = atomic_load(&x->done);
+
+	if (!d)
+		return 0;
+	free(x);
+	return d > 0 ? 1 : d;
+}
+
+static const struct lfa_peer_xfer_ops olfa_xops = {
+	olfa_xsend, olfa_xrecv, olfa_xtest,
+};
+
+/* Creates the liblfa_coll domain + endpoint for the world group — over RCCL
+ * (blocking, like ncclCommInitRank) or over the owner's transfers — and
+ * starts progress.  `addrs` are the members' owner AV addresses in rank
+ * order. */
+static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks,
+			  const fi_addr_t *addrs)
 {
 	unsigned char id[LFA_UNIQUE_ID_BYTES];
 	int ret = 0;
 
+	if (ep->peer_xport) {
+		ep->waddr = malloc((size_t)nranks * sizeof(*ep->waddr));
+		if (!ep->waddr)
+			return -FI_ENOMEM;
+		memcpy(ep->waddr, addrs, (size_t)nranks * sizeof(*ep->waddr));
+		ret = lfa_coll_domain_open_host(rank, nranks, &olfa_xops, ep, &ep->ld);
+		if (ret) {
+			free(ep->waddr);
+			ep->waddr = NULL;
+			return ret;
+		}
+		goto open_ep;
+	}
 	if (ep->have_uid)
 		memcpy(id, ep->uid, sizeof(id));
 	else if (nranks == 1)
@@ -541,6 +628,7 @@ static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks)
 	ret = lfa_coll_domain_open(ep->device, rank, nranks, id, sizeof(id), &ep->ld);
 	if (ret)
 		return ret;
+open_ep:
 	ret = lfa_coll_ep_open(ep->ld, &ep->le);
 	if (ret)
 		goto err_dom;
@@ -563,6 +651,8 @@ err_ep:
 err_dom:
 	lfa_coll_domain_close(ep->ld);
 	ep->ld = NULL;
+	free(ep->waddr);
+	ep->waddr = NULL;
 	return ret;
 }
 
@@ -646,7 +736,7 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 			ret = -FI_EINVAL;       /* a world needs this rank in it */
 			goto err;
 		}
-		ret = olfa_bootstrap(ep, (int)rank, (int)n);
+		ret = olfa_bootstrap(ep, (int)rank, (int)n, set->addr);
 		if (ret)
 			goto err;
 		m->members = malloc(n * sizeof(fi_addr_t));
@@ -664,9 +754,11 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 		}
 		memcpy(set->set_mc.members, set->addr, n * sizeof(fi_addr_t));
 		set->set_mc.nmembers = n;
-		pthread_mutex_lock(&ep->lock);
+		/* not under the registry lock: the join's communicator work must
+		 * not hold up the progress thread's EQ hand-off */
 		ret = lfa_join_collective(ep->le, LFA_ADDR_NOTAVAIL, NULL, 0, flags,
 					  &m->lmc, context);
+		pthread_mutex_lock(&ep->lock);
 		if (!ret) {
 			m->laddr = lfa_mc_addr(m->lmc);
 			olfa_mc_register(ep, m);
@@ -712,7 +804,9 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 	for (size_t i = 0; i < n; i++)
 		m->members[i] = parent->members[ranks[i]];
 	m->nmembers = n;
+	pthread_mutex_unlock(&ep->lock);
 	ret = lfa_join_collective(ep->le, paddr, ranks, n, flags, &m->lmc, context);
+	pthread_mutex_lock(&ep->lock);
 	if (!ret) {
 		m->laddr = lfa_mc_addr(m->lmc);
 		olfa_mc_register(ep, m);
@@ -919,6 +1013,7 @@ static int olfa_ep_close(struct fid *fid)
 		lfa_coll_ep_close(ep->le);
 	if (ep->ld)
 		lfa_coll_domain_close(ep->ld);
+	free(ep->waddr);
 	pthread_mutex_destroy(&ep->lock);
 	pthread_mutex_destroy(&ep->plock);
 	free(ep);
@@ -980,9 +1075,11 @@ static int olfa_ep_getopt(fid_t fid, int level, int optname, void *optval,
 		return lfa_coll_get_unique_id(optval, LFA_UNIQUE_ID_BYTES);
 	case OFF_LFA_OPT_ALGO:
 	case OFF_LFA_OPT_DEVICE:
+	case OFF_LFA_OPT_TRANSPORT:
 		if (*optlen < sizeof(int))
 			return -FI_ETOOSMALL;
-		*(int *)optval = optname == OFF_LFA_OPT_ALGO ? ep->algo : ep->device;
+		*(int *)optval = optname == OFF_LFA_OPT_ALGO ? ep->algo :
+				 optname == OFF_LFA_OPT_DEVICE ? ep->device : ep->peer_xport;
 		*optlen = sizeof(int);
 		return 0;
 	case OFF_LFA_OPT_CHUNK:
@@ -1043,6 +1140,13 @@ static int olfa_ep_setopt(fid_t fid, int level, int optname, const void *optval,
 		if (ep->le)
 			return -FI_EBUSY;
 		ep->device = *(const int *)optval;
+		return 0;
+	case OFF_LFA_OPT_TRANSPORT:
+		if (optlen != sizeof(int) || (unsigned)*(const int *)optval > 1)
+			return -FI_EINVAL;
+		if (ep->le)
+			return -FI_EBUSY;
+		ep->peer_xport = *(const int *)optval;
 		return 0;
 	default:
 		return -FI_ENOPROTOOPT;
@@ -1136,20 +1240,37 @@ static struct fi_ops_cm olfa_cm_ops = {
 	.join = olfa_join,
 };
 
-/* Completions of transfers this provider asked the owner to make with
- * FI_PEER_TRANSFER (rxm_cq.c:1936-1947).  off_lfa moves its data over RCCL
- * and never issues such transfers, so nothing should arrive here. */
+/* Completions of the transfers this provider asked the owner to make with
+ * FI_PEER_TRANSFER (coll_peer_xfer_complete, coll_coll.c:1218-1265): the
+ * context is the olfa_xfer the executor's test() polls.  Over RCCL no such
+ * transfer is ever issued. */
 static ssize_t olfa_peer_complete(struct fid_ep *ep, struct fi_cq_tagged_entry *buf,
 				  fi_addr_t src_addr)
 {
-	olfa_warn("unexpected peer-transfer completion", NULL, 0);
-	return -FI_EINVAL;
+	struct olfa_ep *e = (struct olfa_ep *)ep;
+	struct olfa_xfer *x;
+
+	if (!buf || !buf->op_context || !e->peer_xport) {
+		olfa_warn("unexpected peer-transfer completion", NULL, 0);
+		return -FI_EINVAL;
+	}
+	x = buf->op_context;
+	atomic_store(&x->done, 1);
+	return 0;
 }
 
 static ssize_t olfa_peer_comperr(struct fid_ep *ep, struct fi_cq_err_entry *buf)
 {
-	olfa_warn("unexpected peer-transfer error", NULL, buf ? buf->err : 0);
-	return -FI_EINVAL;
+	struct olfa_ep *e = (struct olfa_ep *)ep;
+	struct olfa_xfer *x;
+
+	if (!buf || !buf->op_context || !e->peer_xport) {
+		olfa_warn("unexpected peer-transfer error", NULL, buf ? buf->err : 0);
+		return -FI_EINVAL;
+	}
+	x = buf->op_context;
+	atomic_store(&x->done, -(buf->err ? buf->err : FI_EIO));
+	return 0;
 }
 
 static struct fi_ops_transfer_peer olfa_peer_xfer_ops = {
@@ -1192,6 +1313,8 @@ static int olfa_endpoint(struct fid_domain *domain, struct fi_info *info,
 	ep->algo = algo && *algo ? atoi(algo) : -1;
 	ep->manual_progress = getenv("OFF_LFA_PROGRESS") &&
 			      !strcmp(getenv("OFF_LFA_PROGRESS"), "manual");
+	ep->peer_xport = getenv("OFF_LFA_TRANSPORT") &&
+			 !strcmp(getenv("OFF_LFA_TRANSPORT"), "peer");
 	*ep_fid = &ep->util.ep_fid;
 	return 0;
 }

@@ -63,3 +63,58 @@ def test_host_driver_cpu(mode):
 @pytest.mark.parametrize("mode", [[], ["manual"]])
 def test_host_driver_gpu(mode):
     assert _run("gpu", *mode).startswith("OK gpu")
+
+
+# ------------------------------------------ peer transport, N processes ----
+# off_lfa had only ever run at world size 1, where every
+# collective is an identity copy.  examples/off_lfa_peer forks N ranks, each
+# an owner with its own tagged transport (socket pairs); the provider moves
+# every transfer through it with FI_PEER_TRANSFER, as prov/coll does through
+# rxm.  The outputs must be prov/coll's results bit for bit.
+
+def _peer_run(n, tmp_path, mode):
+    if build.have_fabric_headers():
+        build.build_all()
+    lib, exe = build.LIB_OFF, build.OFF_PEER
+    if not (os.path.exists(lib) and os.path.exists(exe)):
+        pytest.fail("off_lfa provider / peer driver not built")
+    env = dict(os.environ)
+    env.pop("OFF_LFA_PROGRESS", None)
+    r = subprocess.run([exe, lib, str(n), str(tmp_path), *mode], capture_output=True,
+                       text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().splitlines()[-1].startswith("OK peer")
+
+
+def _load(tmp_path, r, name, io, dt):
+    import numpy as np
+    return np.fromfile(tmp_path / f"r{r}_{name}_{io}.bin", dtype=dt)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("mode", [[], ["manual"]])
+def test_peer_transport_collectives(tmp_path, n, mode):
+    import numpy as np
+    import oracle
+    _peer_run(n, tmp_path, mode)
+    for name, op, dt, nd in (("sum_f32", 2, 8, np.float32), ("prod_f64", 3, 9, np.float64),
+                             ("bxor_i64", 9, 6, np.int64)):
+        ins = [_load(tmp_path, r, name, "in", nd) for r in range(n)]
+        want = oracle.allreduce(op, dt, ins)[0]
+        assert ins[0].size and not all(np.array_equal(ins[0], x) for x in ins[1:])
+        for sfx in ("", "_rd"):          # TREE and the reference's own RD schedule
+            for r in range(n):
+                got = _load(tmp_path, r, name + sfx, "out", nd)
+                assert got.tobytes() == want.tobytes(), (name + sfx, r)
+    ins = [_load(tmp_path, r, "rs_f32", "in", np.float32) for r in range(n)]
+    full = oracle.allreduce(2, 8, ins)[0]
+    for r, (a, b) in enumerate(oracle.slice_bounds(full.size, n)):
+        assert _load(tmp_path, r, "rs_f32", "out", np.float32).tobytes() == full[a:b].tobytes()
+    ins = [_load(tmp_path, r, "reduce_f64", "in", np.float64) for r in range(n)]
+    assert (_load(tmp_path, n - 1, "reduce_f64", "out", np.float64).tobytes() ==
+            oracle.allreduce(2, 9, ins)[0].tobytes())
+    members = sorted({0, n - 1})
+    ins = [_load(tmp_path, r, "sub_f32", "in", np.float32) for r in members]
+    want = oracle.allreduce(2, 8, ins)[0]
+    for r in members:
+        assert _load(tmp_path, r, "sub_f32", "out", np.float32).tobytes() == want.tobytes()
