@@ -259,6 +259,38 @@ def cpu_baseline(sample_reps: int = 5):
     return out
 
 
+def cpu_config1_peer(timeout_s: float = 90.0):
+    """BASELINE configs[0]'s shape on the host: a 2-rank 4 KiB float FI_SUM
+    fi_allreduce through the off_lfa provider's PEER transport (the
+    transfers ride on an rxm-like owner's tagged messaging over AF_UNIX
+    sockets, the reductions in liblfa's host combine) — the build's own
+    prov/coll-shaped host path; examples/off_lfa_peer, median of 1000 after
+    100 warm-up, owner-driven progress."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "examples", "off_lfa_peer")
+    lib = os.path.join(ROOT, "libfabric_amd", "liboff_lfa-fi.so")
+    if not (os.path.exists(exe) and os.path.exists(lib)):
+        return {"error": "examples/off_lfa_peer not built"}
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for mode in ("manual", "thread"):
+            args = [exe, lib, "2", td, "latency"] + (["manual"] if mode == "manual" else [])
+            r = subprocess.run(args, capture_output=True, text=True, timeout=timeout_s)
+            line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY_US")]
+            if r.returncode or not line:
+                out[mode] = {"error": (r.stdout + r.stderr)[-200:]}
+                continue
+            med, p10, p90 = (float(v) for v in line[0].split()[1:4])
+            out[mode] = {"us_median": med, "us_p10": p10, "us_p90": p90}
+    out.update({"kind": "port", "cores": 2,
+                "what": "2 processes, fi_allreduce 1024 float FI_SUM through liboff_lfa-fi.so's "
+                        "peer transport (owner tagged messages over AF_UNIX socket pairs, "
+                        "host combine); 'manual' = owner-driven progress, 'thread' = the "
+                        "provider's FI_PROGRESS_AUTO thread"})
+    return out
+
+
 def splitmix64(seed: int, n: int):
     """SURVEY §8(d) config 3 data: full-range splitmix64 stream."""
     import numpy as np
@@ -1082,6 +1114,7 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         line["cpu_baseline"]["config3_int64_64mib"] = cpu_baseline_config3(args.cpu_reps)
+        line["cpu_baseline"]["config1_2rank_4kib_allreduce_host"] = cpu_config1_peer()
 
     # Extras (never the headline).  A watchdog prints the line collected so
     # far and exits if an extra stalls, so the metric is always reported.

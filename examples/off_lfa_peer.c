@@ -7,7 +7,7 @@
  * transfer back through the peer_ops->complete the provider installed
  * (rxm_cq.c:846-872, 1532-1546).
  *
- *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual]
+ *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency]
  *
  * The owner here is a minimal stand-in for rxm over a socket provider: one
  * AF_UNIX socket pair per rank pair (made before fork), non-blocking,
@@ -19,7 +19,9 @@
  * _out .bin) for tests/test_off_lfa.py to check against the oracle; the
  * known answer of fabtests/multinode/src/core_coll.c:230-277 is checked
  * here.  CPU only: no HIP call is made.  Prints "OK peer" and exits 0 when
- * every rank passed.
+ * every rank passed.  With "latency" it instead times BASELINE configs[0]'s
+ * shape — a 4 KiB float FI_SUM fi_allreduce — 100 warm-up then 1000 timed
+ * operations, and rank 0 prints "LATENCY_US <median> <p10> <p90>".
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -367,7 +369,7 @@ struct util_ep_prefix {          /* include/ofi_util.h:280-306 */
 	void (*progress)(void *);
 };
 
-static int manual;
+static int manual, latency;
 
 static void drive(void)
 {
@@ -538,6 +540,41 @@ static int run_rank(const char *prov_path)
 	CHECK(fi_join_collective(ep, FI_ADDR_NOTAVAIL, set, 0, &mc, &req[0]) == 0, "join");
 	wait_join(mc);
 	CHECK(fi_av_set_addr(set, &world) == 0, "av_set_addr");
+	if (latency) {
+		static double us[1000];
+		float x[1024], y[1024];
+		struct timespec a, b;
+
+		seed(0);
+		for (int i = 0; i < 1024; i++)
+			x[i] = (float)unif(-1, 1);
+		for (int it = 0; it < 1100; it++) {
+			clock_gettime(CLOCK_MONOTONIC, &a);
+			CHECK(fi_allreduce(ep, x, 1024, NULL, y, NULL, world, FI_FLOAT, FI_SUM, 0,
+					   &req[1]) == 0, "allreduce");
+			wait_comp(&req[1]);
+			clock_gettime(CLOCK_MONOTONIC, &b);
+			if (it >= 100)
+				us[it - 100] = (b.tv_sec - a.tv_sec) * 1e6 +
+					       (b.tv_nsec - a.tv_nsec) * 1e-3;
+		}
+		for (int i = 1; i < 1000; i++)          /* insertion sort */
+			for (int j = i; j > 0 && us[j - 1] > us[j]; j--) {
+				double t = us[j];
+
+				us[j] = us[j - 1];
+				us[j - 1] = t;
+			}
+		if (me == 0)
+			printf("LATENCY_US %.2f %.2f %.2f\n", us[500], us[100], us[900]);
+		fflush(stdout);
+		CHECK(fi_barrier(ep, world, &req[2]) == 0, "barrier");
+		wait_comp(&req[2]);
+		fi_close(&mc->fid);
+		fi_close(&set->fid);
+		fi_close(&ep->fid);
+		return failures ? 1 : 0;
+	}
 	CHECK(fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_TRANSPORT, &one,
 			sizeof(one)) == -FI_EBUSY, "transport fixed after the join");
 
@@ -705,7 +742,10 @@ int main(int argc, char **argv)
 	}
 	nranks = atoi(argv[2]);
 	outdir = argv[3];
-	manual = argc > 4 && !strcmp(argv[4], "manual");
+	for (int i = 4; i < argc; i++) {
+		manual |= !strcmp(argv[i], "manual");
+		latency |= !strcmp(argv[i], "latency");
+	}
 	if (manual)
 		setenv("OFF_LFA_PROGRESS", "manual", 1);
 	if (nranks < 1 || nranks > MAXR)

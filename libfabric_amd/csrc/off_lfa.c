@@ -47,6 +47,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -467,14 +468,25 @@ static void olfa_util_progress(void *util_ep)
 	olfa_progress((struct olfa_ep *)util_ep);
 }
 
+/* FI_PROGRESS_AUTO.  Spins (yielding) while work came through recently and
+ * backs off to 20 us naps after a quiet spell, so a latency-bound chain of
+ * peer transfers is advanced within microseconds without a busy core when
+ * the endpoint idles. */
 static void *olfa_progress_thread(void *arg)
 {
 	struct olfa_ep *ep = arg;
 	const struct timespec idle = { 0, 20000 };
+	unsigned quiet = 0;
 
-	while (!atomic_load(&ep->stop))
-		if (!olfa_progress(ep))
+	while (!atomic_load(&ep->stop)) {
+		if (olfa_progress(ep)) {
+			quiet = 0;
+		} else if (++quiet < 4096) {
+			sched_yield();
+		} else {
 			nanosleep(&idle, NULL);
+		}
+	}
 	return NULL;
 }
 

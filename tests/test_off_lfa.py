@@ -118,3 +118,16 @@ def test_peer_transport_collectives(tmp_path, n, mode):
     want = oracle.allreduce(2, 8, ins)[0]
     for r in members:
         assert _load(tmp_path, r, "sub_f32", "out", np.float32).tobytes() == want.tobytes()
+
+
+def test_peer_transport_latency_mode(tmp_path):
+    """The config-1 shape (2 ranks, 4 KiB float SUM fi_allreduce) timed
+    through the provider's peer transport: what bench.py reports as the
+    host-path figure."""
+    if build.have_fabric_headers():
+        build.build_all()
+    r = subprocess.run([build.OFF_PEER, build.LIB_OFF, "2", str(tmp_path), "manual",
+                        "latency"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY_US")]
+    assert line and 0 < float(line[0].split()[1]) < 10_000
