@@ -276,6 +276,22 @@ def test_host_chunked_elementwise_geometry(kind, count, chunk):
             assert not res[r].any()
 
 
+@pytest.mark.parametrize("n", range(2, 9))
+@pytest.mark.parametrize("chunk", [8, 4096, 1 << 20, 32 << 20])
+def test_host_staging_is_one_chunk_in_groups(n, chunk):
+    """chunking is a local choice a peer cannot see, so in a
+    group of N > 1 the host path stages ONE chunk, the whole buffer, and its
+    device collective has the shape a device-buffer member issues
+    (dev_count == count), whatever the chunk size."""
+    for kind, count in ((ALLREDUCE, 70_001), (REDUCE, 70_001), (BROADCAST, 513),
+                        (REDUCE_SCATTER, n * 9001)):
+        cs = coll.host_chunks(kind, count, n, 8, chunk)
+        assert len(cs) == 1, (kind, n, chunk)
+        assert cs[0].dev_count == count and cs[0].src_off == 0 and cs[0].dst_off == 0
+    # a one-member group still pipelines
+    assert len(coll.host_chunks(ALLREDUCE, 70_001, 1, 8, 4096)) > 1
+
+
 def test_host_chunk_rejects_unchunked_collectives():
     with pytest.raises(coll.CollError):
         coll.host_chunks(REDUCE_SCATTER, 10, 3, 8, 1 << 20)   # ragged blocks
