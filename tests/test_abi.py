@@ -57,3 +57,73 @@ def test_abi_matches_reference_headers():
                             os.path.join(ROOT, "include"), "-c", src, "-o",
                             os.path.join(d, "abi.o")], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
+
+
+def _struct_body(text, name):
+    import re
+    m = re.search(r"struct\s+" + name + r"\s*\{(.*?)\n\};", text, re.S)
+    assert m, name
+    return m.group(1)
+
+
+def test_util_ep_prefix_matches_reference_layout():
+    """off_lfa starts its endpoint with a restatement of struct util_ep's
+    prefix up to `progress` (rxm calls the offload endpoint's progress through
+    container_of(..., struct util_ep, ep_fid), rxm_cq.c:2095-2098).  The
+    reference header needs configure's config.h, so it cannot be included;
+    instead the reference's field list is taken from include/ofi_util.h's
+    text, its private types replaced by same-size stand-ins (pointers,
+    dlist_entry = two pointers, CNTR_CNT from enum ofi_cntr_index), and the
+    offset of `progress` compiled beside off_lfa.c's own struct."""
+    import re
+    util = open(os.path.join(REF, "ofi_util.h")).read()
+    body = _struct_body(util, "util_ep")
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = []
+    for decl in body.split(";"):
+        decl = " ".join(decl.split())
+        if not decl:
+            continue
+        fields.append(decl)
+        if decl.endswith("progress"):
+            break
+    enum = re.search(r"enum ofi_cntr_index \{(.*?)\};", util, re.S).group(1)
+    cnt = [x.split()[0].rstrip(",") for x in re.sub(r"/\*.*?\*/", "", enum, flags=re.S)
+           .split("\n") if x.strip()].index("CNTR_CNT")
+    ref_struct = ["struct ref_util_ep {"]
+    for f in fields:
+        f = f.replace("CNTR_CNT", str(cnt))
+        if f.startswith("struct fid_ep"):
+            ref_struct.append(f"  {f};")
+        elif f.startswith("struct dlist_entry"):
+            ref_struct.append("  struct { void *next, *prev; } " + f.split()[-1] + ";")
+        elif f.startswith("struct") and "*" in f:
+            ref_struct.append("  void *" + f.split("*", 1)[1] + ";")
+        elif f.startswith("ofi_cntr_inc_func") or f.startswith("ofi_ep_progress_func"):
+            nm = f.split()[-1]
+            arr = nm[nm.index("["):] if "[" in nm else ""
+            base = nm.split("[")[0]
+            ref_struct.append(f"  void (*{base}{arr})(void *);" if not arr else
+                              f"  void (*{base}{arr})(void *);")
+        else:
+            ref_struct.append(f"  {f};")
+    ref_struct.append("};")
+    off = open(os.path.join(ROOT, "libfabric_amd", "csrc", "off_lfa.c")).read()
+    ours = re.search(r"(#define OLFA_UTIL_CNTR_CNT.*?\nstruct olfa_util_ep_prefix \{.*?\n\};)",
+                     off, re.S).group(1)
+    src = "\n".join(["#include <stddef.h>", "#include <stdint.h>", "#include <rdma/fabric.h>",
+                     "#include <rdma/fi_endpoint.h>", *ref_struct, ours,
+                     "_Static_assert(offsetof(struct ref_util_ep, progress) == "
+                     "offsetof(struct olfa_util_ep_prefix, progress), \"progress offset\");",
+                     "_Static_assert(offsetof(struct ref_util_ep, type) == "
+                     "offsetof(struct olfa_util_ep_prefix, type), \"type offset\");",
+                     "_Static_assert(offsetof(struct ref_util_ep, cntrs) == "
+                     "offsetof(struct olfa_util_ep_prefix, cntrs), \"cntrs offset\");",
+                     "int main(void) { return 0; }"])
+    assert len(fields) >= 15 and fields[-1].endswith("progress")
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "layout.c")
+        open(p, "w").write(src)
+        r = subprocess.run(["gcc", "-std=gnu11", "-I", REF, "-c", p, "-o", p + ".o"],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr + src
