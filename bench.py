@@ -675,10 +675,12 @@ def extra_collectives(rank, world, stream):
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
         ref = None
+        # P2P (cross-GPU IPC mappings + system-scope kernel) last: the
+        # RCCL-only forms are measured even if it were to fail
         for name, algo in (("allreduce_tree_exact", coll.ALGO_TREE),
                            ("allreduce_tree_exact_rccl_xfer", coll.ALGO_TREE_COLL),
-                           ("allreduce_p2p_exact", coll.ALGO_P2P),
-                           ("allreduce_rccl", coll.ALGO_RCCL)):
+                           ("allreduce_rccl", coll.ALGO_RCCL),
+                           ("allreduce_p2p_exact", coll.ALGO_P2P)):
             try:
                 ep.set_algo(algo)
                 y.zero_()
@@ -689,6 +691,19 @@ def extra_collectives(rank, world, stream):
                         ref = y.clone()
                     else:
                         row["bitwise_equal_tree"] = bool(torch.equal(y, ref))
+                elif ref is not None:
+                    # RCCL's ring order: within the stated bound of the exact
+                    # tree, |got - ref| <= 2(N-1) 2^-24 sum_r |x_r|
+                    ep.set_algo(coll.ALGO_TREE)
+                    ax, sab = x.abs(), torch.empty_like(x)
+                    ep.wait(ep.allreduce(ax, sab, COUNT, 8, 2))
+                    bound = 2 * max(world - 1, 1) * 2.0 ** -24 * sab
+                    err = (y - ref).abs()
+                    row["within_stated_tolerance_of_tree"] = bool((err <= bound).all())
+                    row["max_abs_err"] = float(err.max())
+                    row["bitwise_equal_tree"] = bool(torch.equal(y, ref))
+                    del ax, sab, err, bound
+                    ep.set_algo(algo)
                 barrier(world)
                 reps = 10
                 t0 = time.perf_counter()
