@@ -189,6 +189,23 @@ def read_traffic():
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+def read_traffic_shard(shard_bytes: int):
+    """Per-launch HBM bytes of the same kernel at the shard's operand size,
+    from the committed PMC passes over `--only-extra sizes`
+    (profiles/r02_pmc_traffic_sizes.json, tools/pmc_sizes.py)."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic_sizes.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    for row in d.get("by_operand_mib", {}).values():
+        if row["operand_bytes"] == shard_bytes:
+            return row["hbm_bytes_per_launch"], (
+                f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the same kernel at a "
+                f"{shard_bytes >> 20} MiB operand on one GPU ({path[len(ROOT) + 1:]})")
+    return None, None
+
+
 def cpu_baseline(sample_reps: int = 5):
     """The reference combine timed on ONE pinned host core (rank 0, N=1).
 
@@ -396,7 +413,7 @@ def extra_config3(dev, stream):
     return out
 
 
-def extra_sizes(dev, stream):
+def extra_sizes(dev, stream, reps: int = 100, prewarm_s: float = 0.1):
     """The product float SUM combine vs size per operand (the shard sizes of
     the strong-scaled headline: 256 MiB / N): average launch duration from an
     event pair around 100 back-to-back launches over >= 1 GiB of rotated
@@ -410,8 +427,9 @@ def extra_sizes(dev, stream):
         def fn(i, sets=sets, n=n):
             d, s = sets[i % len(sets)]
             atomic.write(FI_SUM, FI_FLOAT, d, s, n, stream)
-        prewarm(fn, 0.1)
-        ms = _kernel_events(fn, 100, stream)
+        if prewarm_s > 0:
+            prewarm(fn, prewarm_s)
+        ms = _kernel_events(fn, reps, stream)
         gbps = 3 * n * 4 / (ms * 1e-3) / 1e9
         out[str(mib)] = {"kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
                          "frac": round(gbps / PEAK_GBPS, 4)}
@@ -1017,6 +1035,8 @@ def main() -> None:
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
     ap.add_argument("--extras-timeout", type=float, default=300.0)
+    ap.add_argument("--sizes-reps", type=int, default=100,
+                    help="--only-extra sizes: timed launches per size")
     ap.add_argument("--prewarm-s", type=float, default=0.25,
                     help="untimed clock-ramp launches before the W warmup steps (s)")
     args = ap.parse_args()
@@ -1054,7 +1074,8 @@ def main() -> None:
     if args.only_extra == "sizes":
         torch.cuda.set_device(0)
         print(json.dumps({"sizes": extra_sizes(torch.device("cuda", 0),
-                                               torch.cuda.current_stream())}))
+                                               torch.cuda.current_stream(),
+                                               args.sizes_reps, args.prewarm_s)}))
         return
     if args.only_extra == "tree_put":
         torch.cuda.set_device(0)
@@ -1079,7 +1100,7 @@ def main() -> None:
     shard_bytes = cnt * 4
     value = 3 * S_BYTES * args.steps / elapsed / 2**30
     achieved = 3 * shard_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = read_traffic() if world == 1 else (None, None)
+    traffic, traffic_src = read_traffic() if world == 1 else read_traffic_shard(shard_bytes)
 
     line = {
         "metric": "device-resident GiB/s, float32 FI_SUM reduce, 256 MiB buffers",
