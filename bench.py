@@ -25,7 +25,10 @@ Extra objects on the JSON line:
                 launch stream; peak 8.0 TB/s (MI355X HBM3E spec); ``traffic``
                 from the committed rocprofv3 PMC pass (profiles/) when present.
   cpu_baseline  rank 0, N=1 only: the reference combine on 1 pinned host core,
-                same shape (256 MiB float SUM), median of a bounded sample.
+                same shape (256 MiB float SUM), median of a bounded sample;
+                beside it configs[2] (int64 BOR/MIN 64 MiB), configs[0] (2-rank
+                4 KiB allreduce through the provider's host path) and
+                configs[4]'s per-bucket double PROD combine.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu]
        python bench.py --tune      # kernel-variant sweep (dev tool)
@@ -368,6 +371,49 @@ def cpu_baseline_config3(sample_reps: int = 5):
                 "sample": f"64 MiB int64 (8,388,608 lanes) splitmix64 seeds 3/4 with 1 % "
                           f"INT64_MIN/MAX/0/-1 lanes, median of {sample_reps}, 1 pinned core"})
     return out
+
+
+def cpu_baseline_config5(budget_s: float = 1.0):
+    """BASELINE configs[4]'s CPU column: the reference's per-bucket combine,
+    double FI_PROD (CAS loop, util_atomic.c:266-289 via the PROD row
+    :898/:913), one pinned core, for each bucket of the 4 KiB .. 256 MiB
+    sweep.  prov/coll has no reduce_scatter (coll_ep.c:75-76); an allreduce
+    of the bucket costs log2(N) such combines per rank (coll_coll.c:409-430),
+    so the N-rank compute is this figure x log2(N).  Data uniform[0.9,1.1)
+    (SURVEY §8(d)); median over repetitions bounded by `budget_s` per size."""
+    import numpy as np
+    import oracle
+    try:
+        prev = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {sorted(prev)[-1]})
+    except (AttributeError, OSError):
+        prev = None
+    rng = np.random.default_rng(200)
+    top = 256 * 1024 * 1024 // 8
+    src_all = rng.uniform(0.9, 1.1, top)
+    dst_all = rng.uniform(0.9, 1.1, top)
+    sweep = {}
+    try:
+        for nbytes in [4096 * 4 ** k for k in range(9)]:
+            n = nbytes // 8
+            src, dst0 = src_all[:n], dst_all[:n]
+            dst = dst0.copy()
+            ts, t_end = [], time.perf_counter() + budget_s
+            while len(ts) < 3 or (len(ts) < 200 and time.perf_counter() < t_end):
+                dst[:] = dst0
+                t0 = time.perf_counter()
+                oracle.write(3, 9, dst, src, oracle.CAS)   # FI_PROD, FI_DOUBLE
+                ts.append(time.perf_counter() - t0)
+            t = statistics.median(ts)
+            sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
+                                  "gib_s": round(3 * nbytes / t / 2**30, 3)}
+    finally:
+        if prev is not None:
+            os.sched_setaffinity(0, prev)
+    return {"per_bucket_combine": sweep, "cores": 1, "kind": "port",
+            "sample": "double FI_PROD CAS combine of one bucket (dst *= src), 4 KiB .. "
+                      "256 MiB x4 steps, uniform[0.9,1.1), 1 pinned core; an N-rank "
+                      "allreduce of the bucket is log2(N) of these per rank"}
 
 
 
@@ -1151,6 +1197,7 @@ def main() -> None:
         line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         line["cpu_baseline"]["config3_int64_64mib"] = cpu_baseline_config3(args.cpu_reps)
         line["cpu_baseline"]["config1_2rank_4kib_allreduce_host"] = cpu_config1_peer()
+        line["cpu_baseline"]["config5_double_prod"] = cpu_baseline_config5()
 
     # Extras (never the headline).  A watchdog prints the line collected so
     # far and exits if an extra stalls, so the metric is always reported.
