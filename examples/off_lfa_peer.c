@@ -7,7 +7,7 @@
  * transfer back through the peer_ops->complete the provider installed
  * (rxm_cq.c:846-872, 1532-1546).
  *
- *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency]
+ *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency] [core]
  *
  * The owner here is a minimal stand-in for rxm over a socket provider: one
  * AF_UNIX socket pair per rank pair (made before fork), non-blocking,
@@ -21,7 +21,10 @@
  * here.  CPU only: no HIP call is made.  Prints "OK peer" and exits 0 when
  * every rank passed.  With "latency" it instead times BASELINE configs[0]'s
  * shape — a 4 KiB float FI_SUM fi_allreduce — 100 warm-up then 1000 timed
- * operations, and rank 0 prints "LATENCY_US <median> <p10> <p90>".
+ * operations, and rank 0 prints "LATENCY_US <median> <p10> <p90>".  With
+ * "core" it runs the reference's own multinode suite, fabtests core_coll.c's
+ * test table, unchanged in flow (core_suite below); rank 0 prints
+ * "CORE <test> passed" per test.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -102,16 +105,24 @@ static struct owner {
 					      * posts while we progress */
 	void *comp[256];
 	int ncomp;
-	struct fi_eq_entry eve[8];
-	uint32_t ev[8];
+	struct fi_eq_entry eve[64];
+	uint32_t ev[64];
 	int nev;
 	uint64_t bytes_sent, bytes_recv;
 } own;
+
+/* the harness's own out-of-band messages (pm_barrier) complete here, not
+ * into the provider */
+static int oob_done[2 * MAXR];
 
 static void complete_xfer(void *context, uint64_t flags, size_t len, uint64_t tag)
 {
 	struct fi_cq_tagged_entry e;
 
+	if ((int *)context >= oob_done && (int *)context < oob_done + 2 * MAXR) {
+		*(int *)context = 1;
+		return;
+	}
 	memset(&e, 0, sizeof(e));
 	e.op_context = context;
 	e.flags = flags | FI_TAGGED;
@@ -303,7 +314,7 @@ static ssize_t owner_eq_write(struct fid_eq *eq, uint32_t event, const void *buf
 {
 	int i = own.nev;
 
-	if (i >= 8 || len != sizeof(struct fi_eq_entry))
+	if (i >= 64 || len != sizeof(struct fi_eq_entry))
 		return -FI_EINVAL;
 	own.ev[i] = event;
 	memcpy(&own.eve[i], buf, len);
@@ -369,7 +380,7 @@ struct util_ep_prefix {          /* include/ofi_util.h:280-306 */
 	void (*progress)(void *);
 };
 
-static int manual, latency;
+static int manual, latency, core;
 
 static void drive(void)
 {
@@ -425,6 +436,68 @@ static int wait_join(struct fid_mc *mc)
 
 static const char *outdir;
 
+/* fabtests' pm_barrier (multinode/src/harness.c:164-185) over the owner's
+ * links: everyone tells rank 0, rank 0 releases everyone.  Its tags have bit
+ * 63 set; the provider's (cid | rank << 32, cid < 2^25) never do. */
+static void oob_barrier(void)
+{
+	static uint64_t seq;
+	const uint64_t tag = 1ull << 63 | seq++;
+	unsigned char byte = 0, sink[MAXR];
+	struct iovec iov;
+	struct fi_msg_tagged m;
+	int want = 0;
+
+	memset(oob_done, 0, sizeof(oob_done));
+	memset(&m, 0, sizeof(m));
+	m.msg_iov = &iov;
+	m.iov_count = 1;
+	m.tag = tag;
+	for (int p = 0; p < nranks; p++) {
+		if (p == me || (me != 0 && p != 0))
+			continue;
+		iov.iov_base = &sink[p];
+		iov.iov_len = 1;
+		m.addr = (fi_addr_t)p;
+		m.context = &oob_done[p];
+		CHECK(owner_trecvmsg(&own.ep, &m, FI_PEER_TRANSFER) == 0, "oob recv");
+		want++;
+	}
+	if (me != 0) {                       /* arrive */
+		iov.iov_base = &byte;
+		iov.iov_len = 1;
+		m.addr = 0;
+		m.context = &oob_done[MAXR];
+		CHECK(owner_tsendmsg(&own.ep, &m, FI_PEER_TRANSFER) == 0, "oob send");
+		want++;
+	}
+	for (;;) {                           /* rank 0: all arrived; else released */
+		int got = 0;
+
+		for (int i = 0; i < 2 * MAXR; i++)
+			got += __atomic_load_n(&oob_done[i], __ATOMIC_ACQUIRE);
+		if (got == want)
+			break;
+		owner_progress();
+	}
+	if (me == 0) {                       /* release */
+		memset(oob_done, 0, sizeof(oob_done));
+		for (int p = 1; p < nranks; p++) {
+			iov.iov_base = &byte;
+			iov.iov_len = 1;
+			m.addr = (fi_addr_t)p;
+			m.context = &oob_done[MAXR + p];
+			CHECK(owner_tsendmsg(&own.ep, &m, FI_PEER_TRANSFER) == 0, "oob release");
+		}
+		for (int got = 0; got < nranks - 1;) {
+			owner_progress();
+			got = 0;
+			for (int p = 1; p < nranks; p++)
+				got += __atomic_load_n(&oob_done[MAXR + p], __ATOMIC_ACQUIRE);
+		}
+	}
+}
+
 static void dump(const char *name, const char *io, const void *p, size_t n)
 {
 	char path[4096];
@@ -457,6 +530,149 @@ static void seed(int c)
 }
 
 typedef struct fi_provider *(*ini_fn)(void);
+
+/* ------------------------------------------------ fabtests core_coll.c -- */
+
+/*
+ * The reference's own multinode collective suite, in its order and with its
+ * setup / run / pm_barrier / teardown cycle (fabtests/multinode/src/
+ * core_coll.c:453-521, 607-648): every test builds an av_set (count 0,
+ * start, end = N-1, stride), joins with coll_addr = fi_av_set_addr of that
+ * set — the set's own address — only on the ranks in it (:138-168), runs,
+ * meets the others in pm_barrier, closes mc and set.  Expected values are
+ * the ones core_coll.c checks.
+ */
+enum core_run { CORE_JOIN, CORE_BARRIER, CORE_SUM, CORE_ALLGATHER, CORE_SCATTER,
+		CORE_BROADCAST };
+
+static const struct core_test {
+	const char *name;
+	uint64_t start, stride;
+	enum fi_collective_op coll;
+	enum fi_op op;
+	enum fi_datatype dt;
+	enum core_run run;
+} core_tests[] = {
+	{ "join_test", 0, 1, FI_BARRIER, FI_NOOP, FI_VOID, CORE_JOIN },
+	{ "barrier_test", 0, 1, FI_BARRIER, FI_NOOP, FI_VOID, CORE_BARRIER },
+	{ "sum_all_reduce_test", 0, 1, FI_ALLREDUCE, FI_SUM, FI_UINT64, CORE_SUM },
+	{ "sum_all_reduce_w_stride_test", 1, 2, FI_ALLREDUCE, FI_SUM, FI_UINT64, CORE_SUM },
+	{ "all_gather_test", 0, 1, FI_ALLGATHER, FI_NOOP, FI_UINT64, CORE_ALLGATHER },
+	{ "scatter_test", 0, 1, FI_SCATTER, FI_NOOP, FI_UINT64, CORE_SCATTER },
+	{ "broadcast_test", 0, 1, FI_BROADCAST, FI_NOOP, FI_UINT64, CORE_BROADCAST },
+};
+
+static int core_member(const struct core_test *t)      /* core_coll.c:66-77 */
+{
+	return (uint64_t)me >= t->start && (uint64_t)me <= (uint64_t)nranks - 1 &&
+	       ((uint64_t)me - t->start) % t->stride == 0;
+}
+
+static int core_run_one(struct fid_ep *ep, struct fid_mc *mc, const struct core_test *t)
+{
+	fi_addr_t ca = fi_mc_addr(mc);
+	int ctx = 0, before = failures;
+
+	switch (t->run) {
+	case CORE_JOIN:
+		return 0;
+	case CORE_BARRIER:
+		CHECK(fi_barrier(ep, ca, &ctx) == 0, "barrier");
+		break;
+	case CORE_SUM: {                                /* :230-277 */
+		uint64_t data = 1234 + (uint64_t)me, result = 0, want = 0;
+
+		for (uint64_t i = t->start; i <= (uint64_t)nranks - 1; i += t->stride)
+			want += 1234 + i;
+		CHECK(fi_allreduce(ep, &data, 1, NULL, &result, NULL, ca, FI_UINT64, FI_SUM,
+				   0, &ctx) == 0, "allreduce");
+		wait_comp(&ctx);
+		CHECK(result == want, "%s: %lu vs %lu", t->name, (unsigned long)result,
+		      (unsigned long)want);
+		return failures != before;
+	}
+	case CORE_ALLGATHER: {                          /* :279-334 */
+		uint64_t data = (uint64_t)me, result[MAXR];
+
+		CHECK(fi_allgather(ep, &data, 1, NULL, result, NULL, ca, FI_UINT64, 0,
+				   &ctx) == 0, "allgather");
+		wait_comp(&ctx);
+		for (int i = 0; i < nranks; i++)
+			CHECK(result[i] == (uint64_t)i, "allgather [%d] = %lu", i,
+			      (unsigned long)result[i]);
+		return failures != before;
+	}
+	case CORE_SCATTER: {                            /* :336-387 */
+		uint64_t data[MAXR], result = ~0ull;
+
+		for (int i = 0; i < nranks; i++)
+			data[i] = (uint64_t)i;
+		CHECK(fi_scatter(ep, me == 0 ? data : NULL, 1, NULL, &result, NULL, ca, 0,
+				 FI_UINT64, 0, &ctx) == 0, "scatter");
+		wait_comp(&ctx);
+		CHECK(result == data[me], "scatter %lu", (unsigned long)result);
+		return failures != before;
+	}
+	case CORE_BROADCAST: {                          /* :389-451 */
+		uint64_t data[MAXR], result[MAXR];
+
+		for (int i = 0; i < nranks; i++)
+			data[i] = (uint64_t)(nranks - 1 - i);
+		CHECK(fi_broadcast(ep, me == 0 ? data : result, (size_t)nranks, NULL, ca, 0,
+				   FI_UINT64, 0, &ctx) == 0, "broadcast");
+		wait_comp(&ctx);
+		for (int i = 0; me != 0 && i < nranks; i++)
+			CHECK(result[i] == data[i], "broadcast [%d]", i);
+		return failures != before;
+	}
+	}
+	wait_comp(&ctx);
+	return failures != before;
+}
+
+static int core_suite(struct fid_domain *domain, struct fid_av *av, struct fid_ep *ep)
+{
+	for (size_t k = 0; k < sizeof(core_tests) / sizeof(core_tests[0]); k++) {
+		const struct core_test *t = &core_tests[k];
+		struct fi_collective_attr attr = { 0 };
+		struct fi_av_set_attr sattr = { 0 };
+		struct fid_av_set *set = NULL;
+		struct fid_mc *mc = NULL;
+		fi_addr_t addr;
+		int ret, jctx;
+
+		attr.op = t->op;                       /* test_query, :200-210 */
+		attr.datatype = t->dt;
+		attr.mode = 0;
+		ret = fi_query_collective(domain, t->coll, &attr, 0);
+		CHECK(ret == 0, "%s: query %d", t->name, ret);
+		if (ret)
+			continue;
+		if (core_member(t)) {                  /* setup, :138-168 */
+			sattr.count = 0;
+			sattr.start_addr = t->start;
+			sattr.end_addr = (fi_addr_t)nranks - 1;
+			sattr.stride = t->stride;
+			CHECK(fi_av_set(av, &sattr, &set, NULL) == 0, "%s: av_set", t->name);
+			CHECK(fi_av_set_addr(set, &addr) == 0, "%s: av_set_addr", t->name);
+			ret = fi_join_collective(ep, addr, set, 0, &mc, &jctx);
+			CHECK(ret == 0, "%s: join %d", t->name, ret);
+			if (ret)
+				return 1;
+			wait_join(mc);
+			if (core_run_one(ep, mc, t))
+				return 1;
+		}
+		oob_barrier();                         /* :640 */
+		if (mc) {                              /* teardown, :180-192 */
+			CHECK(fi_close(&mc->fid) == 0, "%s: close mc", t->name);
+			CHECK(fi_close(&set->fid) == 0, "%s: close set", t->name);
+		}
+		if (me == 0)
+			printf("CORE %s passed\n", t->name), fflush(stdout);
+	}
+	return failures ? 1 : 0;
+}
 
 static int run_rank(const char *prov_path)
 {
@@ -530,6 +746,17 @@ static int run_rank(const char *prov_path)
 	len = sizeof(ival);
 	CHECK(fi_getopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_TRANSPORT, &ival, &len) == 0 &&
 	      ival == 1, "transport readback");
+	if (core) {
+		int bad = core_suite(domain, av, ep);
+
+		fi_close(&ep->fid);
+		fi_close(&eq->fid);
+		fi_close(&cq->fid);
+		fi_close(&av->fid);
+		fi_close(&domain->fid);
+		fi_close(&fabric->fid);
+		return bad || failures ? 1 : 0;
+	}
 
 	/* world: an av_set of every rank (fabtests core_coll.c:453-521 order) */
 	sattr.count = (size_t)nranks;
@@ -736,7 +963,7 @@ int main(int argc, char **argv)
 	pid_t pid[MAXR];
 
 	if (argc < 4) {
-		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> <nranks> <outdir> [manual]\n",
+		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency] [core]\n",
 			argv[0]);
 		return 2;
 	}
@@ -745,6 +972,7 @@ int main(int argc, char **argv)
 	for (int i = 4; i < argc; i++) {
 		manual |= !strcmp(argv[i], "manual");
 		latency |= !strcmp(argv[i], "latency");
+		core |= !strcmp(argv[i], "core");
 	}
 	if (manual)
 		setenv("OFF_LFA_PROGRESS", "manual", 1);

@@ -146,6 +146,19 @@ int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
 int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			const int *ranks, size_t nmembers, uint64_t flags,
 			struct lfa_coll_mc **mc, void *context);
+/* The same group formed by its MEMBERS ONLY: prov/coll's join whose parent is
+ * the av_set's own address (coll_av_set_addr, coll_av_set.c:166-175, taken as
+ * the parent at coll_coll.c:939-941), so the free-id BAND runs over the new
+ * group itself and the rest of `coll_addr`'s group does not call anything
+ * (fabtests core_coll.c:138-178, the stride test).  `ranks` are sorted ranks
+ * of `coll_addr`'s group and must include the caller.  The agreement travels
+ * under group id 256 (outside the 0..255 ids a join hands out), so it cannot
+ * meet a joined group's traffic.  Device domains accept the whole group only
+ * (a strict subset would need a communicator created without the
+ * non-members: -LFA_ENOSYS). */
+int lfa_join_members(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+		     const int *ranks, size_t nmembers, uint64_t flags,
+		     struct lfa_coll_mc **mc, void *context);
 lfa_addr_t lfa_mc_addr(struct lfa_coll_mc *mc);
 /* The group id the join agreed on (util_coll_mc.group_id, ofi_util.h:849-856;
  * the world group is 0), or -LFA_EAGAIN before the join completed. */

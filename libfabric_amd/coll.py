@@ -123,6 +123,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_join_collective.restype = c_int
     L.lfa_join_collective.argtypes = [c_void_p, c_uint64, P(c_int), c_size_t,
                                       c_uint64, P(c_void_p), c_void_p]
+    L.lfa_join_members.restype = c_int
+    L.lfa_join_members.argtypes = L.lfa_join_collective.argtypes
     L.lfa_mc_addr.restype = c_uint64
     L.lfa_mc_addr.argtypes = [c_void_p]
     L.lfa_mc_close.restype = c_int
@@ -394,6 +396,18 @@ class Endpoint:
         _chk(lib().lfa_join_collective(self.ep, coll_addr or ADDR_NOTAVAIL, arr,
                                        len(ranks) if ranks else 0, 0,
                                        ctypes.byref(mc), ctx), "lfa_join_collective")
+        return mc.value, ctx
+
+    def join_members(self, ranks: list[int], context: int | None = None,
+                     coll_addr: int | None = None):
+        """lfa_join_members: the group of `ranks` formed by its members only
+        (prov/coll's join over an av_set's own address; the other ranks of
+        `coll_addr`'s group call nothing)."""
+        mc = c_void_p()
+        arr = (c_int * len(ranks))(*ranks)
+        ctx = context or self._next_ctx()
+        _chk(lib().lfa_join_members(self.ep, coll_addr or ADDR_NOTAVAIL, arr, len(ranks),
+                                    0, ctypes.byref(mc), ctx), "lfa_join_members")
         return mc.value, ctx
 
     def mc_addr(self, mc: int) -> int:

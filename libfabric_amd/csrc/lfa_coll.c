@@ -2523,9 +2523,11 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 /* join                                                                    */
 /* ---------------------------------------------------------------------- */
 
-int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
-			const int *ranks, size_t nmembers, uint64_t flags,
-			struct lfa_coll_mc **mcp, void *context)
+/* members_only: lfa_join_members — the agreement runs over the new group
+ * itself, so only its members call (see lfa_coll.h). */
+static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+		     const int *ranks, size_t nmembers, uint64_t flags,
+		     struct lfa_coll_mc **mcp, void *context, int members_only)
 {
 	struct lfa_coll_mc *parent, *mc;
 	int member = 0, pos = -1, ret = 0, host;
@@ -2538,6 +2540,8 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	host = ep->dom->host;
 	parent = mc_of(ep, coll_addr);
 	if (!mc_member(parent))
+		return -LFA_EINVAL;
+	if (members_only && !ranks)
 		return -LFA_EINVAL;
 	if (ranks) {
 		for (size_t i = 0; i < nmembers; i++) {
@@ -2553,6 +2557,14 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		member = 1;
 		pos = parent->rank;
 		nmembers = (size_t)parent->size;
+	}
+	if (members_only) {
+		if (!member)
+			return -LFA_EINVAL;     /* only members call this form */
+		if (!host && nmembers != (size_t)parent->size)
+			return -LFA_ENOSYS;     /* no split without the non-members */
+		if (!host)
+			members_only = 0;       /* the whole group: every rank calls */
 	}
 	mc = calloc(1, sizeof(*mc));
 	if (!mc)
@@ -2616,14 +2628,16 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	}
 	pthread_mutex_lock(&ep->lock);
 	/* agree on the group id: BAND of the free-id masks over the PARENT
-	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 */
+	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 — or,
+	 * members_only, over the new group itself under the reserved id
+	 * LFA_MAX_GROUP_ID (the av_set's own coll_mc as the parent) */
 	if (!ret && host) {
 		mc->mask_host = malloc(2 * LFA_CID_BYTES);
 		if (!mc->mask_host)
 			ret = -LFA_ENOMEM;
 		if (!ret) {
 			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
-			ret = host_submit(ep, parent, LFA_ALLREDUCE,
+			ret = host_submit(ep, members_only ? mc : parent, LFA_ALLREDUCE,
 					  mc->mask_host + LFA_CID_BYTES, mc->mask_host,
 					  LFA_CID_BYTES, -1, LFA_UINT8, LFA_BAND,
 					  context, 1, mc);
@@ -2664,6 +2678,20 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	}
 	*mcp = mc;
 	return 0;
+}
+
+int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+			const int *ranks, size_t nmembers, uint64_t flags,
+			struct lfa_coll_mc **mcp, void *context)
+{
+	return join_impl(ep, coll_addr, ranks, nmembers, flags, mcp, context, 0);
+}
+
+int lfa_join_members(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+		     const int *ranks, size_t nmembers, uint64_t flags,
+		     struct lfa_coll_mc **mcp, void *context)
+{
+	return join_impl(ep, coll_addr, ranks, nmembers, flags, mcp, context, 1);
 }
 
 int lfa_mc_close(struct lfa_coll_mc *mc)

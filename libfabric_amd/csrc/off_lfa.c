@@ -179,6 +179,7 @@ struct olfa_ep {
 	size_t chunk;
 	int peer_xport;                    /* OFF_LFA_TRANSPORT=peer */
 	fi_addr_t *waddr;                  /* world rank -> owner AV address */
+	size_t nworld;                     /* entries of waddr */
 	int have_uid;
 	unsigned char uid[LFA_UNIQUE_ID_BYTES];
 	struct lfa_coll_domain *ld;
@@ -613,17 +614,17 @@ static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks,
 	unsigned char id[LFA_UNIQUE_ID_BYTES];
 	int ret = 0;
 
+	/* the world's addresses: the peer transport's destinations, and the
+	 * rank map of later joins over an av_set's own address */
+	ep->waddr = malloc((size_t)nranks * sizeof(*ep->waddr));
+	if (!ep->waddr)
+		return -FI_ENOMEM;
+	memcpy(ep->waddr, addrs, (size_t)nranks * sizeof(*ep->waddr));
+	ep->nworld = (size_t)nranks;
 	if (ep->peer_xport) {
-		ep->waddr = malloc((size_t)nranks * sizeof(*ep->waddr));
-		if (!ep->waddr)
-			return -FI_ENOMEM;
-		memcpy(ep->waddr, addrs, (size_t)nranks * sizeof(*ep->waddr));
 		ret = lfa_coll_domain_open_host(rank, nranks, &olfa_xops, ep, &ep->ld);
-		if (ret) {
-			free(ep->waddr);
-			ep->waddr = NULL;
-			return ret;
-		}
+		if (ret)
+			goto err_addr;
 		goto open_ep;
 	}
 	if (ep->have_uid)
@@ -635,11 +636,11 @@ static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks,
 	if (!ep->have_uid && ret) {
 		olfa_warn("no unique id: set OFF_LFA_OPT_UNIQUE_ID or "
 			  "OFF_LFA_BOOTSTRAP_DIR", NULL, ret);
-		return ret;
+		goto err_addr;
 	}
 	ret = lfa_coll_domain_open(ep->device, rank, nranks, id, sizeof(id), &ep->ld);
 	if (ret)
-		return ret;
+		goto err_addr;
 open_ep:
 	ret = lfa_coll_ep_open(ep->ld, &ep->le);
 	if (ret)
@@ -663,8 +664,10 @@ err_ep:
 err_dom:
 	lfa_coll_domain_close(ep->ld);
 	ep->ld = NULL;
+err_addr:
 	free(ep->waddr);
 	ep->waddr = NULL;
+	ep->nworld = 0;
 	return ret;
 }
 
@@ -706,9 +709,61 @@ static int olfa_cmp_int(const void *a, const void *b)
 	return *(const int *)a - *(const int *)b;
 }
 
+/* A join whose parent is the set itself: its members, as world ranks, form
+ * the group through lfa_join_members; the other world ranks call nothing. */
+static int olfa_join_self(struct olfa_ep *ep, struct olfa_av_set *set,
+			  struct olfa_mc *m, uint64_t flags, void *context)
+{
+	size_t n = set->count;
+	int *ranks = malloc(n * sizeof(int)), ret = 0;
+
+	m->members = malloc(n * sizeof(fi_addr_t));
+	if (!ranks || !m->members) {
+		ret = -FI_ENOMEM;
+		goto out;
+	}
+	pthread_mutex_lock(&ep->lock);
+	for (size_t i = 0; i < n && !ret; i++) {
+		long r = ep->waddr ? olfa_index(ep->waddr, ep->nworld, set->addr[i]) : -1;
+
+		if (r < 0)
+			ret = -FI_EINVAL;       /* not in the bootstrapped world */
+		else
+			ranks[i] = (int)r;
+	}
+	pthread_mutex_unlock(&ep->lock);
+	if (ret)
+		goto out;
+	qsort(ranks, n, sizeof(int), olfa_cmp_int);
+	for (size_t i = 0; i < n; i++) {
+		if (i && ranks[i] == ranks[i - 1]) {
+			ret = -FI_EINVAL;       /* an address listed twice */
+			goto out;
+		}
+		m->members[i] = ep->waddr[ranks[i]];
+	}
+	m->nmembers = n;
+	ret = lfa_join_members(ep->le, lfa_coll_world_addr(ep->le), ranks, n, flags,
+			       &m->lmc, context);
+	if (!ret) {
+		pthread_mutex_lock(&ep->lock);
+		m->laddr = lfa_mc_addr(m->lmc);
+		olfa_mc_register(ep, m);
+		pthread_mutex_unlock(&ep->lock);
+	}
+out:
+	free(ranks);
+	if (ret) {
+		free(m->members);
+		m->members = NULL;
+	}
+	return ret;
+}
+
 /* fi_join_collective (coll_coll.c:912-995).  The parent group is the one
  * coll_addr names; FI_ADDR_NOTAVAIL means the set's world group, which the
- * first such join creates. */
+ * first such join creates; the set's own address (fi_av_set_addr) means the
+ * set's members alone (olfa_join_self). */
 static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 		     struct fid_mc **mc_fid, void *context)
 {
@@ -717,7 +772,7 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 	struct olfa_av_set *set;
 	struct olfa_mc *parent, *m;
 	fi_addr_t my_addr;
-	int *ranks = NULL, ret;
+	int *ranks = NULL, ret, self;
 	size_t n;
 	lfa_addr_t paddr;
 
@@ -740,7 +795,12 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 	m->mc_fid.fi_addr = (fi_addr_t)(uintptr_t)m;
 	m->laddr = LFA_ADDR_NOTAVAIL;
 
-	if (ca->coll_addr == FI_ADDR_NOTAVAIL && !ep->le) {
+	/* coll_addr = fi_av_set_addr of this very set: prov/coll then takes the
+	 * set's own coll_mc as the parent (coll_av_set.c:166-175,
+	 * coll_coll.c:939-941), so the set's members alone take part — fabtests
+	 * core_coll.c joins every test group this way (:138-178) */
+	self = ca->coll_addr == (fi_addr_t)(uintptr_t)&set->set_mc;
+	if ((ca->coll_addr == FI_ADDR_NOTAVAIL || self) && !ep->le) {
 		/* world bootstrap: every member of the set takes part */
 		long rank = olfa_index(set->addr, n, my_addr);
 
@@ -786,6 +846,13 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 		return 0;
 	}
 
+	if (self) {
+		ret = olfa_join_self(ep, set, m, flags, context);
+		if (ret)
+			goto err;
+		*mc_fid = &m->mc_fid;
+		return 0;
+	}
 	pthread_mutex_lock(&ep->lock);
 	parent = ca->coll_addr == FI_ADDR_NOTAVAIL ? ep->world :
 		 olfa_mc_lookup(ep, ca->coll_addr);

@@ -30,7 +30,9 @@ def _free_port():
 
 class GlooXfer:
     """The owner's tagged transport, over gloo.  prov/coll's tag
-    (cid | sender << 32) is folded into gloo's 31-bit tag space."""
+    (cid | sender << 32, cid = group_id << 16 | seq, group_id <= 256) is
+    folded into gloo's 31-bit tag space: 6 bits of sender, 9 of group id, 16
+    of seq."""
 
     def __init__(self):
         self.reqs, self.next = {}, 1
@@ -38,7 +40,7 @@ class GlooXfer:
 
     @staticmethod
     def _tag(tag):
-        return ((tag >> 32) & 0x7F) << 24 | (tag & 0xFFFFFF)
+        return ((tag >> 32) & 0x3F) << 25 | ((tag >> 16) & 0x1FF) << 16 | (tag & 0xFFFF)
 
     def _put(self, v):
         h = self.next
@@ -201,6 +203,40 @@ def _joins(ep, rank, world, oracle):
     assert int(res[0]) == sum(1234 + k for k in range(world))
 
 
+def _joins_members(ep, rank, world):
+    """lfa_join_members — prov/coll's join with coll_addr = the av_set's own
+    address (coll_coll.c:939-941): the stride set of fabtests core_coll.c
+    (start 1, stride 2, :175-178) forms its group while the other ranks call
+    nothing and run a world collective meanwhile; the group gets the lowest
+    id its members have free, and core_coll.c's expected sum."""
+    from libfabric_amd import coll
+    from libfabric_amd.coll import CollError
+    members = list(range(1, world, 2))
+    if rank in members:
+        mc, ctx = ep.join_members(members)
+        ev = ep.wait_join()
+        assert ev[0] == 6 and ev[2] == ctx
+        assert ep.group_id(mc) == 1
+        x = np.array([1234 + rank], np.uint64)
+        res = np.zeros(1, np.uint64)
+        ep.wait(ep.allreduce(x, res, 1, 7, 2, coll_addr=ep.mc_addr(mc)))
+        assert int(res[0]) == sum(1234 + m for m in members)
+        assert coll.lib().lfa_mc_close(mc) == 0
+    else:
+        with pytest.raises(CollError):        # only members call this form
+            ep.join_members(members or [world])
+    # every rank: the whole group through the same form, then the world
+    mc, _ = ep.join_members(list(range(world)))
+    ep.wait_join()
+    assert ep.group_id(mc) == 1
+    x = np.array([rank + 1], np.uint64)
+    res = np.zeros(1, np.uint64)
+    ep.wait(ep.allreduce(x, res, 1, 7, 2, coll_addr=ep.mc_addr(mc)))
+    assert int(res[0]) == world * (world + 1) // 2
+    assert coll.lib().lfa_mc_close(mc) == 0
+    ep.wait(ep.barrier())
+
+
 def _worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -213,6 +249,7 @@ def _worker(rank, world, port, q):
             _collectives(ep, rank, world, oracle, coll)
             _overlap(ep, rank, world, oracle)
             _joins(ep, rank, world, oracle)
+            _joins_members(ep, rank, world)
             if world > 1:
                 assert xfer.sent > 0 and xfer.received > 0
             assert not xfer.reqs, "transfers left behind"
@@ -226,7 +263,7 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_c_executor_across_processes(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -131,3 +131,28 @@ def test_peer_transport_latency_mode(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY_US")]
     assert line and 0 < float(line[0].split()[1]) < 10_000
+
+
+CORE_TESTS = ("join_test", "barrier_test", "sum_all_reduce_test",
+              "sum_all_reduce_w_stride_test", "all_gather_test", "scatter_test",
+              "broadcast_test")
+
+
+@pytest.mark.parametrize("n,mode", [(1, "thread"), (2, "thread"), (3, "manual"),
+                                    (4, "thread"), (4, "manual"), (5, "thread")])
+def test_reference_multinode_suite(tmp_path, n, mode):
+    """The reference's own collective suite, fabtests/multinode/src/
+    core_coll.c:453-521, in its setup / run / pm_barrier / teardown cycle
+    (:607-648): each test joins with coll_addr = fi_av_set_addr of its own
+    set, on the set's ranks only — at N >= 4 the stride test's {1, 3, ..}
+    forms its group while the other ranks call nothing (the members-only
+    join, lfa_join_members) — and checks core_coll.c's expected values."""
+    if build.have_fabric_headers():
+        build.build_all()
+    args = [build.OFF_PEER, build.LIB_OFF, str(n), str(tmp_path), "core"]
+    if mode == "manual":
+        args.append("manual")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    passed = [x.split()[1] for x in r.stdout.splitlines() if x.startswith("CORE ")]
+    assert tuple(passed) == CORE_TESTS, r.stdout + r.stderr
