@@ -121,6 +121,17 @@ struct lfa_peer_xfer_ops {
 int lfa_coll_domain_open_host(int rank, int nranks,
 			      const struct lfa_peer_xfer_ops *ops, void *ctx,
 			      struct lfa_coll_domain **domain);
+/* The same on GPU `device` (< 0: lfa_coll_domain_open_host): collectives
+ * whose buffers are device memory then run the same schedule with the local
+ * items as the gfx950 kernels on the endpoint's stream, and every transfer
+ * staged through host memory (device -> host before a send, host -> device
+ * after a receive), so the owner only ever moves host bytes — prov/coll over
+ * an owner without FI_HMEM.  Host buffers keep the host combine.  A buffer
+ * pair must be both device or both host memory (-LFA_EINVAL otherwise);
+ * members may differ from one another. */
+int lfa_coll_domain_open_peer(int device, int rank, int nranks,
+			      const struct lfa_peer_xfer_ops *ops, void *ctx,
+			      struct lfa_coll_domain **domain);
 int lfa_coll_domain_close(struct lfa_coll_domain *domain);
 
 /* An endpoint owns one HIP stream (its progress context), a work-item

@@ -102,6 +102,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_domain_open_host.restype = c_int
     L.lfa_coll_domain_open_host.argtypes = [c_int, c_int, P(PeerXferOps), c_void_p,
                                             P(c_void_p)]
+    L.lfa_coll_domain_open_peer.restype = c_int
+    L.lfa_coll_domain_open_peer.argtypes = [c_int] + L.lfa_coll_domain_open_host.argtypes
     L.lfa_mc_group_id.restype = c_int
     L.lfa_mc_group_id.argtypes = [c_void_p]
     L.lfa_coll_domain_close.restype = c_int
@@ -462,9 +464,12 @@ class HostEndpoint(Endpoint):
     handle and test(handle) -> 1 done / 0 pending / <0 error — the way
     prov/coll rides on the owner provider's tagged messages."""
 
-    def __init__(self, rank: int, nranks: int, transport):
+    def __init__(self, rank: int, nranks: int, transport, device: int = -1):
+        """device >= 0: lfa_coll_domain_open_peer — device-tensor buffers run
+        the same schedule with the gfx950 kernels, transfers staged through
+        host memory."""
         L = lib()
-        self.rank, self.nranks, self.device = rank, nranks, -1
+        self.rank, self.nranks, self.device = rank, nranks, device
         self.transport = transport
 
         def _send(ctx, peer, buf, nbytes, tag, req):
@@ -490,8 +495,8 @@ class HostEndpoint(Endpoint):
         # keep the trampolines alive as long as the endpoint
         self._ops = PeerXferOps(XferPost(_send), XferPost(_recv), XferTest(_test))
         self.dom, self.ep = c_void_p(), c_void_p()
-        _chk(L.lfa_coll_domain_open_host(rank, nranks, ctypes.byref(self._ops), None,
-                                         ctypes.byref(self.dom)), "domain_open_host")
+        _chk(L.lfa_coll_domain_open_peer(device, rank, nranks, ctypes.byref(self._ops),
+                                         None, ctypes.byref(self.dom)), "domain_open_peer")
         _chk(L.lfa_coll_ep_open(self.dom, ctypes.byref(self.ep)), "ep_open")
         self.world = L.lfa_coll_world_addr(self.ep)
         self._ctx = 0

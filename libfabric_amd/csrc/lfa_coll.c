@@ -1023,15 +1023,24 @@ int lfa_coll_domain_open_host(int rank, int nranks,
 			      const struct lfa_peer_xfer_ops *ops, void *ctx,
 			      struct lfa_coll_domain **domain)
 {
+	return lfa_coll_domain_open_peer(-1, rank, nranks, ops, ctx, domain);
+}
+
+int lfa_coll_domain_open_peer(int device, int rank, int nranks,
+			      const struct lfa_peer_xfer_ops *ops, void *ctx,
+			      struct lfa_coll_domain **domain)
+{
 	struct lfa_coll_domain *d;
 
 	if (!domain || !ops || !ops->send || !ops->recv || !ops->test ||
 	    nranks < 1 || rank < 0 || rank >= nranks)
 		return -LFA_EINVAL;
+	if (device >= 0 && hipSetDevice(device) != hipSuccess)
+		return -LFA_EINVAL;
 	d = calloc(1, sizeof(*d));
 	if (!d)
 		return -LFA_ENOMEM;
-	d->device = -1;
+	d->device = device < 0 ? -1 : device;
 	d->rank = rank;
 	d->nranks = nranks;
 	d->host = 1;
@@ -1107,6 +1116,14 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 			return -LFA_EIO;
 		}
 		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
+	} else if (d->device >= 0) {
+		/* device buffers on a peer-transfer domain: the local items' kernels
+		 * and the staging copies run on this stream */
+		hipSetDevice(d->device);
+		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess) {
+			ep_release(ep);
+			return -LFA_EIO;
+		}
 	}
 	memset(ep->cid_mask, 0xff, sizeof(ep->cid_mask));
 	ep->cid_mask[0] &= (uint8_t)~1u;            /* world group id 0 taken */
@@ -1135,6 +1152,8 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	if (ep->dom->host) {
 		for (size_t i = 0; i < ep->qlen; i++)
 			hop_free(ep->q[(ep->qhead + i) % ep->qcap].hop);
+		if (ep->stream)
+			hipStreamDestroy(ep->stream);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
 		pthread_mutex_destroy(&ep->comm_lock);
@@ -1507,14 +1526,97 @@ static const struct xport xport_peer = {
 };
 
 /*
+ * ---- xport_peer_dev: device buffers over the owner's transfers ----------
+ * The owner moves host bytes only (an FI_HMEM-less rxm), so every transfer
+ * is staged: a SEND copies its device bytes — as the endpoint stream has
+ * them after the items enqueued before it — into a host bounce buffer and
+ * sends that; a RECV lands in a bounce buffer and is copied to the device
+ * on the stream before the group counts as done.  REDUCE / TREE / COPY are
+ * the gfx950 kernels on the endpoint stream.  The schedule (and so every
+ * tag and size) is the host form's, so members may mix host and device
+ * buffers freely.
+ */
+struct stg {
+	void *inner;            /* the owner's request */
+	char *bounce;
+	void *dst;              /* RECV: device destination */
+	size_t n;
+};
+
+static int pdev_post(struct xrun *r, const struct lfa_step *st, void **req)
+{
+	const struct lfa_coll_domain *d = r->mc->ep->dom;
+	struct stg *g = calloc(1, sizeof(*g));
+	int ret;
+
+	if (!g || !(g->bounce = malloc(st->count ? st->count : 1))) {
+		free(g);
+		return -LFA_ENOMEM;
+	}
+	g->n = st->count;
+	if (st->type == LFA_STEP_SEND) {
+		if (hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
+				   hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
+		    hipStreamSynchronize(r->stream) != hipSuccess)
+			ret = -LFA_EIO;
+		else
+			ret = d->xops.send(d->xctx, world_rank(r->mc, st->peer), g->bounce,
+					   st->count, r->cid | (uint64_t)r->mc->rank << 32,
+					   &g->inner);
+	} else {
+		g->dst = resolve(&r->x, st->dst);
+		ret = d->xops.recv(d->xctx, world_rank(r->mc, st->peer), g->bounce,
+				   st->count, r->cid | (uint64_t)st->peer << 32, &g->inner);
+	}
+	if (ret) {
+		free(g->bounce);
+		free(g);
+		return ret;
+	}
+	*req = g;
+	return 0;
+}
+
+static int pdev_test(struct xrun *r, void *req)
+{
+	const struct lfa_coll_domain *d = r->mc->ep->dom;
+	struct stg *g = req;
+	int ret = d->xops.test(d->xctx, g->inner);
+
+	if (ret == 0)
+		return 0;
+	if (ret > 0 && g->dst &&
+	    (hipMemcpyAsync(g->dst, g->bounce, g->n, hipMemcpyHostToDevice,
+			    r->stream) != hipSuccess ||
+	     hipStreamSynchronize(r->stream) != hipSuccess))
+		ret = -LFA_EIO;
+	free(g->bounce);
+	free(g);
+	return ret;
+}
+
+static int pdev_local(struct xrun *r, const struct lfa_step *st)
+{
+	if (st->type == LFA_STEP_TREE_PUT)
+		return -LFA_EINVAL;     /* P2P plans are not used here */
+	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
+}
+
+static const struct xport xport_peer_dev = {
+	peer_nop, pdev_post, peer_nop, pdev_test, pdev_local, peer_coll,
+};
+
+/*
  * One collective on a host domain: prov/coll's util_coll_operation and its
  * work queue (ofi_coll.h:146-163) — the schedule, its own TMP, and the run.
  */
 struct hop {
 	struct xrun r;
 	struct plan pl;
-	void *tmp;
+	void *tmp;              /* host, or device memory for a device hop */
 	int done, err;
+	int dev;                /* device buffers (xport_peer_dev) */
+	hipEvent_t fin;         /* device hop: the stream reached the end */
 	uint64_t scratch[2];    /* barrier word and its result */
 };
 
@@ -1523,7 +1625,16 @@ static void hop_free(struct hop *h)
 	if (!h)
 		return;
 	plan_free(&h->pl);
-	free(h->tmp);
+	if (h->dev) {
+		/* a failed run may have left items on the stream that use tmp */
+		hipStreamSynchronize(h->r.stream);
+		if (h->tmp)
+			hipFree(h->tmp);
+		if (h->fin)
+			hipEventDestroy(h->fin);
+	} else {
+		free(h->tmp);
+	}
 	free(h->r.reqs);
 	free(h);
 }
@@ -1538,10 +1649,26 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 		if (!h || h->done || h->err)
 			continue;
 		ret = xrun_advance(&h->r);
-		if (ret < 0)
+		if (ret < 0) {
 			h->err = ret;
-		else if (ret)
+		} else if (ret && h->dev) {
+			/* done once the stream has run the last local items */
+			hipError_t e;
+
+			if (!h->fin &&
+			    (hipEventCreateWithFlags(&h->fin, hipEventDisableTiming) != hipSuccess ||
+			     hipEventRecord(h->fin, h->r.stream) != hipSuccess)) {
+				h->err = -LFA_EIO;
+				continue;
+			}
+			e = hipEventQuery(h->fin);
+			if (e == hipSuccess)
+				h->done = 1;
+			else if (e != hipErrorNotReady)
+				h->err = -LFA_EIO;
+		} else if (ret) {
 			h->done = 1;
+		}
 	}
 }
 
@@ -2275,7 +2402,7 @@ static int mc_member(const struct lfa_coll_mc *mc)
 static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 		      const void *buf, void *result, size_t count, int root,
-		      enum lfa_datatype dt, enum lfa_op op)
+		      enum lfa_datatype dt, enum lfa_op op, int dev)
 {
 	enum lfa_coll_algo algo = ep->algo;
 	size_t esz = lfa_datatype_size(dt);
@@ -2291,9 +2418,18 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	plan_free(&raw);
 	if (ret)
 		return ret;
-	if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp)))
+	h->dev = dev;
+	h->r.stream = ep->stream;
+	if (dev) {
+		hipSetDevice(ep->dom->device);
+		if (h->pl.tmp && hipMalloc(&h->tmp, h->pl.tmp) != hipSuccess) {
+			h->tmp = NULL;
+			return -LFA_ENOMEM;
+		}
+	} else if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp))) {
 		return -LFA_ENOMEM;
-	h->r.xp = &xport_peer;
+	}
+	h->r.xp = dev ? &xport_peer_dev : &xport_peer;
 	h->r.pl = &h->pl;
 	h->r.mc = mc;
 	h->r.op = op;
@@ -2309,7 +2445,7 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		       enum lfa_collective_op coll, const void *buf,
 		       void *result, size_t count, int root,
 		       enum lfa_datatype dt, enum lfa_op op, void *context,
-		       int kind, struct lfa_coll_mc *jmc)
+		       int kind, struct lfa_coll_mc *jmc, int dev)
 {
 	struct hop *h = calloc(1, sizeof(*h));
 	int ret;
@@ -2317,7 +2453,7 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	if (!h)
 		return -LFA_ENOMEM;
 	mc->seq++;                              /* coll_get_next_id :48-52 */
-	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op);
+	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op, dev);
 	if (!ret)
 		ret = enqueue_host(ep, h, context, kind, jmc);
 	if (ret)
@@ -2353,13 +2489,24 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		if (ret)
 			return ret;
 	}
-	pthread_mutex_lock(&ep->lock);
 	if (ep->dom->host) {
+		/* device buffers (a peer domain opened on a GPU): both must be
+		 * device memory — the kernels read and write them in place */
+		const void *in = coll == LFA_SCATTER && mc->rank != root ? NULL : buf;
+		const void *out = coll == LFA_REDUCE && mc->rank != root ? NULL : result;
+		int din = ep->dom->device >= 0 && in && count && is_device_ptr(in);
+		int dout = ep->dom->device >= 0 && out && count && is_device_ptr(out);
+		int dev = din || dout;
+
+		if (dev && ((in && count && !din) || (out && count && !dout)))
+			return -LFA_EINVAL;
+		pthread_mutex_lock(&ep->lock);
 		ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
-				  context, 0, NULL);
+				  context, 0, NULL, dev);
 		pthread_mutex_unlock(&ep->lock);
 		return ret;
 	}
+	pthread_mutex_lock(&ep->lock);
 	hipSetDevice(ep->dom->device);
 	mc->seq++;                              /* coll_get_next_id :48-52 */
 	host = (buf && count && !is_device_ptr(buf)) ||
@@ -2495,7 +2642,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 			h->scratch[0] = ~(uint64_t)mc->rank;
 			mc->seq++;
 			ret = host_start(ep, h, mc, LFA_ALLREDUCE, &h->scratch[0],
-					 &h->scratch[1], 1, -1, LFA_UINT64, LFA_BAND);
+					 &h->scratch[1], 1, -1, LFA_UINT64, LFA_BAND, 0);
 			if (!ret)
 				ret = enqueue_host(ep, h, context, 0, NULL);
 			if (ret)
@@ -2640,7 +2787,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			ret = host_submit(ep, members_only ? mc : parent, LFA_ALLREDUCE,
 					  mc->mask_host + LFA_CID_BYTES, mc->mask_host,
 					  LFA_CID_BYTES, -1, LFA_UINT8, LFA_BAND,
-					  context, 1, mc);
+					  context, 1, mc, 0);
 		}
 	} else if (!ret) {
 		hipSetDevice(ep->dom->device);

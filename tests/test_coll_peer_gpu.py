@@ -1,0 +1,167 @@
+"""The C executor with the gfx950 kernels across PROCESSES, on the GPU.
+
+Two and three processes share the box's one MI355X.  Each opens a
+peer-transfer domain on device 0 (lfa_coll_domain_open_peer): the collective
+provider builds the same schedules as on every other path, the owner's
+transport (gloo, tests/gloo_xfer.py) carries every SEND/RECV as host bytes
+(staged device <-> host by the provider), and every REDUCE / TREE / COPY item
+runs as the product kernels on the endpoint's stream.  Results must equal
+prov/coll's (the oracle) bit for bit, including when one member hands in
+host buffers and the others device buffers.  The oracle is only the checker.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(oracle, dt, count, world, seed):
+    nd = oracle.DT_NP[dt]
+    rng = np.random.default_rng(seed)
+    if nd.kind == "f":
+        return [rng.uniform(0.9, 1.1, count).astype(nd) for _ in range(world)]
+    return [rng.integers(0, 255, count).astype(nd) for _ in range(world)]
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _ready(*_):
+    """fi_allreduce takes buffers that are ready when it is called (there is
+    no stream in libfabric's API): torch's copies and fills, on torch's
+    stream, must have finished before the provider's stream touches them."""
+    torch.cuda.synchronize()
+
+
+def _body(ep, rank, world, oracle, coll):
+    torch.cuda.synchronize()
+    for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL):
+        ep.set_algo(algo)
+        for dt, op, count in ((8, 2, 70_001), (9, 3, 4099), (6, 6, 6000), (1, 7, 33),
+                              (8, 0, 1000)):
+            sends = _inputs(oracle, dt, count, world, 4321 + count + algo)
+            want = oracle.allreduce(op, dt, sends)[0]
+            nd = sends[0].dtype
+            # rank 0 hands in host buffers, the others device buffers: one
+            # schedule either way
+            host = rank == 0 and algo == coll.ALGO_TREE
+            x = sends[rank] if host else _dev(sends[rank])
+            res = np.zeros(count, nd) if host else torch.zeros(count, dtype=x.dtype,
+                                                                device="cuda")
+            _ready()
+            ep.wait(ep.allreduce(x, res, count, dt, op))
+            got = res if host else res.cpu().numpy()
+            assert got.tobytes() == want.tobytes(), f"allreduce algo={algo} dt={dt} n={count}"
+            off, ln = coll.block(count, world, rank)
+            xs = _dev(sends[rank])
+            rs = torch.zeros(max(ln, 1), dtype=xs.dtype, device="cuda")
+            _ready()
+            ep.wait(ep.reduce_scatter(xs, rs, count, dt, op))
+            assert rs[:ln].cpu().numpy().tobytes() == want[off:off + ln].tobytes()
+            for root in range(world):
+                r = torch.zeros(count, dtype=rs.dtype, device="cuda")
+                _ready()
+                ep.wait(ep.reduce(xs, r, count, root, dt, op))
+                if rank == root:
+                    assert r.cpu().numpy().tobytes() == want.tobytes(), f"reduce {root}"
+    ep.set_algo(coll.ALGO_TREE)
+    x = torch.arange(10, dtype=torch.int32, device="cuda") + 100 * rank
+    res = torch.zeros(10 * world, dtype=torch.int32, device="cuda")
+    _ready()
+    ep.wait(ep.allgather(x, res, 10, 4))
+    assert torch.equal(res.cpu(), torch.cat([torch.arange(10, dtype=torch.int32) + 100 * k
+                                             for k in range(world)]))
+    for root in range(world):
+        b = (torch.arange(7, dtype=torch.float64, device="cuda") * (root + 1) if rank == root
+             else torch.zeros(7, dtype=torch.float64, device="cuda"))
+        _ready()
+        ep.wait(ep.broadcast(b, 7, root, 9))
+        assert torch.equal(b.cpu(), torch.arange(7, dtype=torch.float64) * (root + 1))
+        src = (torch.arange(5 * world, dtype=torch.int64, device="cuda") if rank == root
+               else None)
+        out = torch.zeros(5, dtype=torch.int64, device="cuda")
+        _ready()
+        ep.wait(ep.scatter(src, out, 5, root, 6))
+        assert torch.equal(out.cpu(), torch.arange(5) + 5 * rank)
+    ep.wait(ep.barrier())
+    # several in flight: completions in issue order, each result exact
+    outs, ctxs = [], []
+    for k in range(4):
+        sends = _inputs(oracle, 8, 5000 + k, world, 99 + k)
+        want = oracle.allreduce(2, 8, sends)[0]
+        r = torch.zeros(want.size, dtype=torch.float32, device="cuda")
+        xs = _dev(sends[rank])
+        _ready()
+        ctxs.append(ep.allreduce(xs, r, want.size, 8, 2))
+        outs.append((r, want, xs))
+    done = []
+    while len(done) < len(ctxs):
+        done += ep.cq_read()
+    assert done == ctxs
+    for r, want, _ in outs:
+        assert r.cpu().numpy().tobytes() == want.tobytes()
+    # a mixed pair on one member is refused
+    from libfabric_amd.coll import CollError
+    with pytest.raises(CollError):
+        ep.allreduce(torch.zeros(4, device="cuda"), np.zeros(4, np.float32), 4, 8, 2)
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        xfer = GlooXfer()
+        ep = coll.HostEndpoint(rank, world, xfer, device=0)
+        try:
+            _body(ep, rank, world, oracle, coll)
+            if world > 1:
+                assert xfer.sent > 0 and xfer.received > 0
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c_executor_gpu_kernels_across_processes(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=100)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
