@@ -296,7 +296,9 @@ def cpu_config1_peer(timeout_s: float = 90.0):
     with tempfile.TemporaryDirectory() as td:
         for mode in ("manual", "thread"):
             args = [exe, lib, "2", td, "latency"] + (["manual"] if mode == "manual" else [])
-            r = subprocess.run(args, capture_output=True, text=True, timeout=timeout_s)
+            # host buffers only: OFF_LFA_DEVICE=-1 keeps the GPU out of it
+            r = subprocess.run(args, capture_output=True, text=True, timeout=timeout_s,
+                               env=dict(os.environ, OFF_LFA_DEVICE="-1"))
             line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY_US")]
             if r.returncode or not line:
                 out[mode] = {"error": (r.stdout + r.stderr)[-200:]}

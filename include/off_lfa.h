@@ -32,12 +32,15 @@
  * moves every transfer through the OWNER endpoint's tagged messaging with
  * FI_PEER_TRANSFER, as prov/coll does through rxm (coll_coll.c:770-814): the
  * owner must then provide fi_tsendmsg / fi_trecvmsg and report each finished
- * transfer through the peer_ops->complete this provider installs; buffers are
- * host memory and reductions run in liblfa's host combine.  No unique id is
- * needed then.
+ * transfer through the peer_ops->complete this provider installs.  Host
+ * buffers reduce in liblfa's host combine; device buffers (on the endpoint's
+ * GPU, OFF_LFA_DEVICE) run the gfx950 kernels, with every transfer staged
+ * through host memory so the owner only moves host bytes.  On a host without
+ * a usable GPU (and no device named) the endpoint takes host buffers only.
+ * No unique id is needed then.
  *
  * Environment: OFF_LFA_DEVICE (HIP device ordinal; default $LOCAL_RANK,
- * else 0), OFF_LFA_PROGRESS=manual (no progress thread: the owner drives
+ * else 0; -1 with the peer transport: host buffers only, no GPU touched), OFF_LFA_PROGRESS=manual (no progress thread: the owner drives
  * progress through the util_ep progress slot or fi_cq_read on the
  * off_lfa CQ), OFF_LFA_ALGO (enum lfa_coll_algo), OFF_LFA_TRANSPORT=peer.
  */

@@ -175,6 +175,7 @@ struct olfa_ep {
 
 	/* bootstrap */
 	int device;
+	int device_set;                    /* OFF_LFA_DEVICE / the option given */
 	int algo;
 	size_t chunk;
 	int peer_xport;                    /* OFF_LFA_TRANSPORT=peer */
@@ -622,7 +623,14 @@ static int olfa_bootstrap(struct olfa_ep *ep, int rank, int nranks,
 	memcpy(ep->waddr, addrs, (size_t)nranks * sizeof(*ep->waddr));
 	ep->nworld = (size_t)nranks;
 	if (ep->peer_xport) {
-		ret = lfa_coll_domain_open_host(rank, nranks, &olfa_xops, ep, &ep->ld);
+		/* on the endpoint's GPU, so device buffers run the kernels with
+		 * staged transfers (lfa_coll_domain_open_peer); a host without a
+		 * usable GPU keeps host buffers only, unless a device was named */
+		ret = lfa_coll_domain_open_peer(ep->device, rank, nranks, &olfa_xops, ep,
+						&ep->ld);
+		if (ret == -LFA_EINVAL && !ep->device_set)
+			ret = lfa_coll_domain_open_peer(-1, rank, nranks, &olfa_xops, ep,
+							&ep->ld);
 		if (ret)
 			goto err_addr;
 		goto open_ep;
@@ -1219,6 +1227,7 @@ static int olfa_ep_setopt(fid_t fid, int level, int optname, const void *optval,
 		if (ep->le)
 			return -FI_EBUSY;
 		ep->device = *(const int *)optval;
+		ep->device_set = 1;
 		return 0;
 	case OFF_LFA_OPT_TRANSPORT:
 		if (optlen != sizeof(int) || (unsigned)*(const int *)optval > 1)
@@ -1388,6 +1397,7 @@ static int olfa_endpoint(struct fid_domain *domain, struct fi_info *info,
 	pthread_mutex_init(&ep->lock, NULL);
 	pthread_mutex_init(&ep->plock, NULL);
 	ep->device = olfa_env_int("OFF_LFA_DEVICE", olfa_env_int("LOCAL_RANK", 0));
+	ep->device_set = getenv("OFF_LFA_DEVICE") != NULL;
 	algo = getenv("OFF_LFA_ALGO");
 	ep->algo = algo && *algo ? atoi(algo) : -1;
 	ep->manual_progress = getenv("OFF_LFA_PROGRESS") &&
