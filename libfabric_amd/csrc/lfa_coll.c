@@ -803,7 +803,8 @@ static int plan_make(struct plan *pl, enum lfa_collective_op coll,
 	return ret;
 }
 
-static int lower_plan(const struct plan *in, int r, int n, struct plan *out);
+static int lower_plan(const struct plan *in, int r, int n, struct plan *out,
+		      int lower_barrier);
 
 /* ====================================================================== */
 /* device helpers                                                          */
@@ -1118,9 +1119,11 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	} else if (d->device >= 0) {
 		/* device buffers on a peer-transfer domain: the local items' kernels
-		 * and the staging copies run on this stream */
+		 * and the staging copies run on this stream; ctl_host holds the P2P
+		 * handshake records */
 		hipSetDevice(d->device);
-		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess) {
+		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
+		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
@@ -1152,8 +1155,10 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	if (ep->dom->host) {
 		for (size_t i = 0; i < ep->qlen; i++)
 			hop_free(ep->q[(ep->qhead + i) % ep->qcap].hop);
+		p2p_release(&ep->world);
 		if (ep->stream)
 			hipStreamDestroy(ep->stream);
+		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
 		pthread_mutex_destroy(&ep->comm_lock);
@@ -1555,16 +1560,20 @@ static int pdev_post(struct xrun *r, const struct lfa_step *st, void **req)
 	}
 	g->n = st->count;
 	if (st->type == LFA_STEP_SEND) {
-		if (hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
-				   hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
-		    hipStreamSynchronize(r->stream) != hipSuccess)
+		/* the stream first: a zero-byte send is a barrier arrival and
+		 * must leave only after this rank's earlier items completed */
+		if (hipStreamSynchronize(r->stream) != hipSuccess ||
+		    (st->count &&
+		     (hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
+				     hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
+		      hipStreamSynchronize(r->stream) != hipSuccess)))
 			ret = -LFA_EIO;
 		else
 			ret = d->xops.send(d->xctx, world_rank(r->mc, st->peer), g->bounce,
 					   st->count, r->cid | (uint64_t)r->mc->rank << 32,
 					   &g->inner);
 	} else {
-		g->dst = resolve(&r->x, st->dst);
+		g->dst = st->count ? resolve(&r->x, st->dst) : NULL;
 		ret = d->xops.recv(d->xctx, world_rank(r->mc, st->peer), g->bounce,
 				   st->count, r->cid | (uint64_t)st->peer << 32, &g->inner);
 	}
@@ -1597,8 +1606,6 @@ static int pdev_test(struct xrun *r, void *req)
 
 static int pdev_local(struct xrun *r, const struct lfa_step *st)
 {
-	if (st->type == LFA_STEP_TREE_PUT)
-		return -LFA_EINVAL;     /* P2P plans are not used here */
 	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
 }
 
@@ -1617,6 +1624,19 @@ struct hop {
 	int done, err;
 	int dev;                /* device buffers (xport_peer_dev) */
 	hipEvent_t fin;         /* device hop: the stream reached the end */
+	/* host buffers run as a device hop (LFA_ALGO_P2P on a GPU peer domain:
+	 * every member must follow the one schedule): staged copies */
+	void *st_in, *st_out, *user_out;
+	size_t out_bytes;
+	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
+	 * (they share the symmetric workspace), then grow it if needed through
+	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
+	int phase;
+	size_t sym_need, sym_size;
+	struct hop *sub;
+	uint16_t sub_seq;
+	int32_t agree_in, agree_out;
+	unsigned char mine[LFA_SYM_REC_BYTES];
 	uint64_t scratch[2];    /* barrier word and its result */
 };
 
@@ -1624,12 +1644,17 @@ static void hop_free(struct hop *h)
 {
 	if (!h)
 		return;
+	hop_free(h->sub);
 	plan_free(&h->pl);
 	if (h->dev) {
 		/* a failed run may have left items on the stream that use tmp */
 		hipStreamSynchronize(h->r.stream);
 		if (h->tmp)
 			hipFree(h->tmp);
+		if (h->st_in)
+			hipFree(h->st_in);
+		if (h->st_out)
+			hipFree(h->st_out);
 		if (h->fin)
 			hipEventDestroy(h->fin);
 	} else {
@@ -1638,6 +1663,9 @@ static void hop_free(struct hop *h)
 	free(h->r.reqs);
 	free(h);
 }
+
+enum { HOP_RUN, HOP_WAIT_PRIOR, HOP_SYM_GATHER, HOP_SYM_AGREE };
+static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx);
 
 /* Advance every in-flight host operation (ep->lock held). */
 static void host_progress_all(struct lfa_coll_ep *ep)
@@ -1648,6 +1676,13 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 
 		if (!h || h->done || h->err)
 			continue;
+		if (h->phase != HOP_RUN) {
+			ret = hop_prologue(ep, h, i);
+			if (ret < 0)
+				h->err = ret;
+			if (h->phase != HOP_RUN || h->err)
+				continue;
+		}
 		ret = xrun_advance(&h->r);
 		if (ret < 0) {
 			h->err = ret;
@@ -1662,7 +1697,11 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 				continue;
 			}
 			e = hipEventQuery(h->fin);
-			if (e == hipSuccess)
+			if (e == hipSuccess && h->out_bytes &&
+			    hipMemcpy(h->user_out, h->st_out, h->out_bytes,
+				      hipMemcpyDeviceToHost) != hipSuccess)
+				h->err = -LFA_EIO;
+			else if (e == hipSuccess)
 				h->done = 1;
 			else if (e != hipErrorNotReady)
 				h->err = -LFA_EIO;
@@ -2022,39 +2061,185 @@ static void p2p_release(struct lfa_coll_mc *mc)
 
 _Static_assert(sizeof(struct sym_rec) <= LFA_SYM_REC_BYTES, "sym_rec");
 
-static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
+/* The workspace size p2p_ensure grows to for a need of `region` bytes. */
+static size_t sym_grow(const struct lfa_coll_mc *mc, size_t region)
 {
-	struct lfa_coll_ep *ep = mc->ep;
-	struct sym_rec *recs = ep->ctl_host;    /* nranks records, from ep open */
-	void *drec = ep->ctl_dev;
-	const size_t rb = sizeof(struct sym_rec);
-	int n = mc->size, ret = 0, ok;
-
-	if (region <= mc->sym_region)
-		return 0;
 	if (region < 2 * mc->sym_region)
 		region = 2 * mc->sym_region;
 	if (region < (8u << 20))
 		region = 8u << 20;
-	region = (region + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-	/*
-	 * A local failure (the old workspace still busy, no memory for the
-	 * new one or its peer table, no IPC handle) is not returned before the
-	 * collective steps below: this rank still takes part in them with
-	 * ok = 0, so every member fails together instead of leaving its peers
-	 * waiting in the allgather.
-	 */
-	ok = hipStreamSynchronize(ep->stream) == hipSuccess;
+	return (region + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+}
+
+/*
+ * p2p_ensure in three local parts around two agreements.  A local failure
+ * (no memory for the new workspace or its peer table, no IPC handle) is not
+ * returned before the agreements: this rank still takes part with ok = 0, so
+ * every member fails together instead of leaving its peers waiting (ADVICE
+ * r1).  `ok` comes in false when the old workspace could not be quiesced.
+ */
+static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
+			struct sym_rec *mine)
+{
+	int n = mc->size;
+
 	p2p_release(mc);
-	memset(recs, 0, (size_t)n * rb);
+	memset(mine, 0, sizeof(*mine));
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
 	ok = ok && hipMalloc((void **)&mc->sym_local, 2 * region) == hipSuccess;
 	if (!ok)
 		mc->sym_local = NULL;
 	if (ok && n > 1)
-		ok = hipIpcGetMemHandle(&recs[mc->rank].h, mc->sym_local) == hipSuccess;
-	recs[mc->rank].ok = ok;
+		ok = hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
+	mine->ok = ok;
+}
+
+/* Every member's record in hand: map the peers' workspaces. */
+static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs)
+{
+	int ret = 0;
+
+	for (int k = 0; k < mc->size && !ret; k++)
+		if (!recs[k].ok)
+			ret = -LFA_ENOMEM;
+	for (int k = 0; k < mc->size && !ret; k++) {
+		if (k == mc->rank) {
+			mc->sym[k] = mc->sym_local;
+		} else if (hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
+					       hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+			mc->sym[k] = NULL;
+			ret = -LFA_EIO;
+		}
+	}
+	return ret;
+}
+
+static int host_start(struct lfa_coll_ep *ep, struct hop *h,
+		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
+		      const void *buf, void *result, size_t count, int root,
+		      enum lfa_datatype dt, enum lfa_op op, int dev);
+
+/* A handshake collective of hop `h` on its reserved seq (host buffers). */
+static int sub_start(struct lfa_coll_ep *ep, struct hop *h, enum lfa_collective_op coll,
+		     const void *buf, void *result, size_t count,
+		     enum lfa_datatype dt, enum lfa_op op, uint16_t seq)
+{
+	struct lfa_coll_mc *mc = h->r.mc;
+	int ret;
+
+	h->sub = calloc(1, sizeof(*h->sub));
+	if (!h->sub)
+		return -LFA_ENOMEM;
+	ret = host_start(ep, h->sub, mc, coll, buf, result, count, -1, dt, op, 0);
+	h->sub->r.cid = (uint64_t)mc->group_id << 16 | seq;
+	return ret;
+}
+
+/* Run the current handshake collective: 1 done, 0 pending, <0 failed. */
+static int sub_advance(struct hop *h)
+{
+	int ret = xrun_advance(&h->sub->r);
+
+	if (ret) {
+		hop_free(h->sub);
+		h->sub = NULL;
+	}
+	return ret;
+}
+
+/*
+ * The P2P prologue of a peer-domain hop, driven from progress calls like the
+ * rest of it (nothing blocks inside a submit: the owner's transfers may only
+ * move when the application drives progress).  WAIT_PRIOR: the operations
+ * queued before this one share the symmetric workspace, so they finish
+ * first — each ends with a barrier, so no peer still reads or writes it.
+ * Then, if the workspace must grow, p2p_ensure's two agreements run as host
+ * collectives on the seqs reserved at submit.
+ */
+static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
+{
+	struct lfa_coll_mc *mc = h->r.mc;
+	struct sym_rec *recs = ep->ctl_host;
+	int ret;
+
+	switch (h->phase) {
+	case HOP_WAIT_PRIOR:
+		for (size_t j = 0; j < idx; j++) {
+			struct hop *p = ep->q[(ep->qhead + j) % ep->qcap].hop;
+
+			if (p && p->err)
+				return p->err;
+			if (p && !p->done)
+				return 0;
+		}
+		if (h->sym_need <= mc->sym_region)
+			break;
+		h->sym_size = sym_grow(mc, h->sym_need);
+		sym_prepare(mc, h->sym_size,
+			    hipStreamSynchronize(ep->stream) == hipSuccess,
+			    (struct sym_rec *)h->mine);
+		if (mc->size == 1) {
+			h->agree_in = h->agree_out = ((struct sym_rec *)h->mine)->ok;
+			recs[0] = *(struct sym_rec *)h->mine;
+			h->agree_out = h->agree_out && sym_open(mc, recs) == 0;
+			goto agreed;
+		}
+		ret = sub_start(ep, h, LFA_ALLGATHER, h->mine, recs, sizeof(struct sym_rec),
+				LFA_UINT8, LFA_NOOP, h->sub_seq);
+		if (ret)
+			return ret;
+		h->phase = HOP_SYM_GATHER;
+		return 0;
+	case HOP_SYM_GATHER:
+		ret = sub_advance(h);
+		if (ret <= 0)
+			return ret;
+		h->agree_in = sym_open(mc, recs) == 0;
+		ret = sub_start(ep, h, LFA_ALLREDUCE, &h->agree_in, &h->agree_out, 1,
+				LFA_INT32, LFA_MIN, (uint16_t)(h->sub_seq + 1));
+		if (ret)
+			return ret;
+		h->phase = HOP_SYM_AGREE;
+		return 0;
+	case HOP_SYM_AGREE:
+		ret = sub_advance(h);
+		if (ret <= 0)
+			return ret;
+agreed:
+		if (!h->agree_out) {
+			p2p_release(mc);
+			return -LFA_EIO;
+		}
+		mc->sym_region = h->sym_size;
+		break;
+	default:
+		return 0;
+	}
+	h->r.x.sym = mc->sym;
+	h->r.x.region = mc->sym_region;
+	h->phase = HOP_RUN;
+	return 0;
+}
+
+/* Device domains: the whole handshake, stream-ordered, over RCCL. */
+static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
+{
+	struct lfa_coll_ep *ep = mc->ep;
+	struct sym_rec *recs = ep->ctl_host;    /* nranks records, from ep open */
+	void *drec = ep->ctl_dev;
+	const size_t rb = sizeof(struct sym_rec);
+	int n = mc->size, ret = 0;
+
+	if (region <= mc->sym_region)
+		return 0;
+	region = sym_grow(mc, region);
+	/* the old workspace is released only after this rank's earlier
+	 * operations have completed — each of which ends with a barrier, so no
+	 * peer still touches it */
+	memset(recs, 0, (size_t)n * rb);
+	sym_prepare(mc, region, hipStreamSynchronize(ep->stream) == hipSuccess,
+		    &recs[mc->rank]);
 	if (n > 1 &&
 	    (hipMemcpyAsync((char *)drec + (size_t)mc->rank * rb, &recs[mc->rank], rb,
 			    hipMemcpyHostToDevice, ep->stream) != hipSuccess ||
@@ -2064,18 +2249,8 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 			    ep->stream) != hipSuccess ||
 	     hipStreamSynchronize(ep->stream) != hipSuccess))
 		ret = -LFA_EIO;
-	for (int k = 0; k < n && !ret; k++)
-		if (!recs[k].ok)
-			ret = -LFA_ENOMEM;
-	for (int k = 0; k < n && !ret; k++) {
-		if (k == mc->rank) {
-			mc->sym[k] = mc->sym_local;
-		} else if (hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
-					       hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-			mc->sym[k] = NULL;
-			ret = -LFA_EIO;
-		}
-	}
+	if (!ret)
+		ret = sym_open(mc, recs);
 	if (n > 1) {
 		/* agree that every member mapped every peer (MIN of the flags) */
 		int32_t all = ret == 0;
@@ -2406,19 +2581,34 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 {
 	enum lfa_coll_algo algo = ep->algo;
 	size_t esz = lfa_datatype_size(dt);
+	/* this operation's sequence number, taken before a P2P handshake below
+	 * draws the next ones */
+	const uint16_t seq = (uint16_t)(mc->seq - 1);
 	struct plan raw;
-	int ret;
+	int ret, sym;
 
-	if (algo == LFA_ALGO_P2P || algo == LFA_ALGO_RCCL)
+	/* P2P keeps its schedule on device buffers (the peers' symmetric
+	 * workspaces are IPC-mapped device memory; its barriers become zero-byte
+	 * messages); host buffers and RCCL run as TREE */
+	if ((algo == LFA_ALGO_P2P && !dev) || algo == LFA_ALGO_RCCL)
 		algo = LFA_ALGO_TREE;
 	ret = plan_make(&raw, coll, algo, mc->rank, mc->size, root, count, esz);
 	if (ret)
 		return ret;
-	ret = lower_plan(&raw, mc->rank, mc->size, &h->pl);
+	sym = plan_uses_sym(raw.steps, raw.nsteps);
+	ret = lower_plan(&raw, mc->rank, mc->size, &h->pl, sym);
 	plan_free(&raw);
 	if (ret)
 		return ret;
-	h->dev = dev;
+	if (sym) {
+		/* the workspace is set up by hop_prologue, from progress; its two
+		 * possible handshakes get the next two seqs on every member */
+		h->phase = HOP_WAIT_PRIOR;
+		h->sym_need = sym_region(count, esz);
+		h->sub_seq = mc->seq;
+		mc->seq += 2;
+	}
+	h->dev = dev != 0;
 	h->r.stream = ep->stream;
 	if (dev) {
 		hipSetDevice(ep->dom->device);
@@ -2429,12 +2619,28 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	} else if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp))) {
 		return -LFA_ENOMEM;
 	}
+	if (dev == 2) {
+		/* host buffers through device copies (reducing collectives) */
+		size_t moff, mlen, in_b = count * esz;
+
+		lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
+		h->out_bytes = coll == LFA_REDUCE_SCATTER ? mlen * esz :
+			       coll == LFA_REDUCE && mc->rank != root ? 0 : count * esz;
+		h->user_out = result;
+		if (hipMalloc(&h->st_in, in_b ? in_b : 1) != hipSuccess ||
+		    hipMalloc(&h->st_out, h->out_bytes ? h->out_bytes : 1) != hipSuccess)
+			return -LFA_ENOMEM;     /* hop_free releases what was made */
+		if (hipMemcpy(h->st_in, buf, in_b, hipMemcpyHostToDevice) != hipSuccess)
+			return -LFA_EIO;
+		buf = h->st_in;
+		result = h->st_out;
+	}
 	h->r.xp = dev ? &xport_peer_dev : &xport_peer;
 	h->r.pl = &h->pl;
 	h->r.mc = mc;
 	h->r.op = op;
 	h->r.dt = dt;
-	h->r.cid = (uint64_t)mc->group_id << 16 | (uint16_t)(mc->seq - 1);
+	h->r.cid = (uint64_t)mc->group_id << 16 | seq;
 	h->r.x.base[LFA_BUF_SEND] = coll == LFA_BROADCAST ? result : (void *)buf;
 	h->r.x.base[LFA_BUF_RESULT] = result;
 	h->r.x.base[LFA_BUF_TMP] = h->tmp;
@@ -2500,6 +2706,13 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 
 		if (dev && ((in && count && !din) || (out && count && !dout)))
 			return -LFA_EINVAL;
+		/* LFA_ALGO_P2P on a GPU peer domain: host buffers follow the
+		 * device schedule too (staged), so members may still mix */
+		if (!dev && ep->dom->device >= 0 && ep->algo == LFA_ALGO_P2P && count &&
+		    mc->size > 1 && mc->size <= LFA_TREE_MAX && mc->size <= LFA_PUT_MAX &&
+		    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER ||
+		     coll == LFA_REDUCE))
+			dev = 2;
 		pthread_mutex_lock(&ep->lock);
 		ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
 				  context, 0, NULL, dev);
@@ -2873,6 +3086,8 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 		if (mc->owns_comm && mc->comm)
 			ncclCommDestroy(mc->comm);
 		pthread_mutex_unlock(&ep->comm_lock);
+	} else {
+		p2p_release(mc);        /* a peer domain's device workspace */
 	}
 	free(mc->members);
 	free(mc);
@@ -2929,13 +3144,19 @@ int lfa_query_collective(struct lfa_coll_domain *domain,
  * COPY items, for executors without RCCL collectives (the loopback below;
  * tests/_plansim.py does the same in Python).
  */
-static int lower_plan(const struct plan *in, int r, int n, struct plan *out)
+/* Collective items -> grouped SEND/RECV items (transports without
+ * collectives).  lower_barrier: BARRIER -> a ring of zero-byte messages,
+ * every rank to every other (peer transports, whose sends leave only after
+ * the rank's earlier items have completed). */
+static int lower_plan(const struct plan *in, int r, int n, struct plan *out,
+		      int lower_barrier)
 {
 	size_t cap = in->nsteps + 1;
 
 	for (size_t i = 0; i < in->nsteps; i++)
 		if (in->steps[i].type == LFA_STEP_ALLTOALL ||
-		    in->steps[i].type == LFA_STEP_ALLGATHER)
+		    in->steps[i].type == LFA_STEP_ALLGATHER ||
+		    (lower_barrier && in->steps[i].type == LFA_STEP_BARRIER))
 			cap += 2 * (size_t)n + 2;
 	memset(out, 0, sizeof(*out));
 	out->steps = calloc(cap, sizeof(*out->steps));
@@ -2952,6 +3173,24 @@ static int lower_plan(const struct plan *in, int r, int n, struct plan *out)
 		int a2a = st->type == LFA_STEP_ALLTOALL;
 		struct lfa_step *o;
 
+		if (lower_barrier && st->type == LFA_STEP_BARRIER) {
+			for (int k = 1; k < n; k++) {
+				o = &out->steps[out->nsteps++];
+				memset(o, 0, sizeof(*o));
+				o->type = LFA_STEP_SEND;
+				o->peer = (r + k) % n;
+				o = &out->steps[out->nsteps++];
+				memset(o, 0, sizeof(*o));
+				o->type = LFA_STEP_RECV;
+				o->peer = (r - k + n) % n;
+			}
+			if (n > 1) {
+				o = &out->steps[out->nsteps++];
+				memset(o, 0, sizeof(*o));
+				o->type = LFA_STEP_GROUP_END;
+			}
+			continue;
+		}
 		if (!a2a && st->type != LFA_STEP_ALLGATHER) {
 			out->steps[out->nsteps++] = *st;
 			continue;
@@ -3045,7 +3284,7 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		ret = plan_make(&raw, coll, algo, r, n, root, count, esz);
 		if (ret)
 			break;
-		ret = lower_plan(&raw, r, n, &pl[r]);
+		ret = lower_plan(&raw, r, n, &pl[r], 0);
 		plan_free(&raw);
 		if (!ret && pl[r].tmp &&
 		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)

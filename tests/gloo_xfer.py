@@ -30,12 +30,14 @@ class GlooXfer:
         return h
 
     def send(self, peer, ptr, nbytes, tag):
-        t = torch.frombuffer(bytearray(ctypes.string_at(ptr, nbytes)), dtype=torch.uint8)
+        # a zero-byte message (a barrier arrival) travels as one byte
+        t = (torch.frombuffer(bytearray(ctypes.string_at(ptr, nbytes)), dtype=torch.uint8)
+             if nbytes else torch.zeros(1, dtype=torch.uint8))
         self.sent += nbytes
         return self._put((dist.isend(t, peer, tag=self._tag(tag)), t, None, 0))
 
     def recv(self, peer, ptr, nbytes, tag):
-        t = torch.empty(nbytes, dtype=torch.uint8)
+        t = torch.empty(max(nbytes, 1), dtype=torch.uint8)
         return self._put((dist.irecv(t, peer, tag=self._tag(tag)), t, ptr, nbytes))
 
     def test(self, h):
@@ -44,7 +46,7 @@ class GlooXfer:
         # tests any, so waiting here cannot deadlock the schedule
         w, t, ptr, n = self.reqs[h]
         w.wait()
-        if ptr:
+        if ptr and n:
             ctypes.memmove(ptr, t.data_ptr(), n)
             self.received += n
         del self.reqs[h]

@@ -5,7 +5,11 @@ peer-transfer domain on device 0 (lfa_coll_domain_open_peer): the collective
 provider builds the same schedules as on every other path, the owner's
 transport (gloo, tests/gloo_xfer.py) carries every SEND/RECV as host bytes
 (staged device <-> host by the provider), and every REDUCE / TREE / COPY item
-runs as the product kernels on the endpoint's stream.  Results must equal
+runs as the product kernels on the endpoint's stream.  With LFA_ALGO_P2P the
+members exchange IPC handles of their symmetric workspaces (the handshake as
+host collectives, from progress), and the system-scope tree_put kernel reads
+the other processes' inputs and writes their outputs through the IPC
+mappings — the P2P path's mechanics, on one device.  Results must equal
 prov/coll's (the oracle) bit for bit, including when one member hands in
 host buffers and the others device buffers.  The oracle is only the checker.
 """
@@ -50,7 +54,7 @@ def _ready(*_):
 
 def _body(ep, rank, world, oracle, coll):
     torch.cuda.synchronize()
-    for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL):
+    for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL, coll.ALGO_P2P):
         ep.set_algo(algo)
         for dt, op, count in ((8, 2, 70_001), (9, 3, 4099), (6, 6, 6000), (1, 7, 33),
                               (8, 0, 1000)):
@@ -59,7 +63,9 @@ def _body(ep, rank, world, oracle, coll):
             nd = sends[0].dtype
             # rank 0 hands in host buffers, the others device buffers: one
             # schedule either way
-            host = rank == 0 and algo == coll.ALGO_TREE
+            # (under P2P the host member's buffers are staged through the
+            # device so it follows the P2P schedule too)
+            host = rank == 0 and algo in (coll.ALGO_TREE, coll.ALGO_P2P)
             x = sends[rank] if host else _dev(sends[rank])
             res = np.zeros(count, nd) if host else torch.zeros(count, dtype=x.dtype,
                                                                 device="cuda")
@@ -115,6 +121,26 @@ def _body(ep, rank, world, oracle, coll):
     assert done == ctxs
     for r, want, _ in outs:
         assert r.cpu().numpy().tobytes() == want.tobytes()
+    # P2P with operations in flight: each waits for the one before it (they
+    # share the symmetric workspace), the middle one grows the workspace
+    # (12 MiB > the 8 MiB first size) through the asynchronous handshake
+    ep.set_algo(coll.ALGO_P2P)
+    outs, ctxs = [], []
+    for k, n in enumerate((5000, 3 << 20, 777)):
+        sends = _inputs(oracle, 8, n, world, 7 + k)
+        want = oracle.allreduce(2, 8, sends)[0]
+        r = torch.zeros(n, dtype=torch.float32, device="cuda")
+        xs = _dev(sends[rank])
+        _ready()
+        ctxs.append(ep.allreduce(xs, r, n, 8, 2))
+        outs.append((r, want, xs))
+    done = []
+    while len(done) < len(ctxs):
+        done += ep.cq_read()
+    assert done == ctxs
+    for r, want, _ in outs:
+        assert r.cpu().numpy().tobytes() == want.tobytes(), "P2P in flight"
+    ep.set_algo(coll.ALGO_TREE)
     # a mixed pair on one member is refused
     from libfabric_amd.coll import CollError
     with pytest.raises(CollError):
