@@ -8,6 +8,7 @@
  * (rxm_cq.c:846-872, 1532-1546).
  *
  *   off_lfa_peer <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency] [core]
+ *                [device]
  *
  * The owner here is a minimal stand-in for rxm over a socket provider: one
  * AF_UNIX socket pair per rank pair (made before fork), non-blocking,
@@ -24,7 +25,9 @@
  * operations, and rank 0 prints "LATENCY_US <median> <p10> <p90>".  With
  * "core" it runs the reference's own multinode suite, fabtests core_coll.c's
  * test table, unchanged in flow (core_suite below); rank 0 prints
- * "CORE <test> passed" per test.
+ * "CORE <test> passed" per test.  With "device" (GPU box) the reducing
+ * collectives take hipMalloc'd buffers and add the P2P algorithm: the
+ * provider runs the gfx950 kernels and stages the owner's transfers.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -531,6 +534,64 @@ static void seed(int c)
 
 typedef struct fi_provider *(*ini_fn)(void);
 
+/* ------------------------------------------- "device": GPU buffers ------- */
+
+/* With "device" the reducing collectives hand the provider hipMalloc'd
+ * buffers: it runs the kernels on them and stages every transfer through
+ * host memory, so this owner still moves host bytes only.  HIP is loaded on
+ * demand (CPU runs never touch it), after fork, in each rank. */
+static int devmode;
+static struct {
+	int (*malloc)(void **, size_t);
+	int (*memcpy)(void *, const void *, size_t, int);   /* 1 H2D, 2 D2H */
+	int (*free)(void *);
+} hip;
+
+static int hip_load(void)
+{
+	void *h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL);
+
+	if (!h)
+		h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_GLOBAL);
+	if (!h)
+		return -1;
+	hip.malloc = (int (*)(void **, size_t))dlsym(h, "hipMalloc");
+	hip.memcpy = (int (*)(void *, const void *, size_t, int))dlsym(h, "hipMemcpy");
+	hip.free = (int (*)(void *))dlsym(h, "hipFree");
+	if (!hip.malloc || !hip.memcpy || !hip.free)
+		return -1;
+	{   /* a usable GPU, or fail now rather than in every collective */
+		void *probe = NULL;
+
+		if (hip.malloc(&probe, 1) != 0)
+			return -1;
+		hip.free(probe);
+	}
+	return 0;
+}
+
+/* the buffer the provider sees: `h` itself, or a device copy of it */
+static void *xbuf(void *h, size_t n)
+{
+	void *d = NULL;
+
+	if (!devmode)
+		return h;
+	CHECK(hip.malloc(&d, n ? n : 1) == 0, "hipMalloc");
+	CHECK(hip.memcpy(d, h, n, 1) == 0, "hipMemcpy H2D");
+	return d;
+}
+
+/* results back into `h` (device mode), and the device copy freed */
+static void xdone(void *h, void *x, size_t n)
+{
+	if (!devmode)
+		return;
+	if (h && n)
+		CHECK(hip.memcpy(h, x, n, 2) == 0, "hipMemcpy D2H");
+	hip.free(x);
+}
+
 /* ------------------------------------------------ fabtests core_coll.c -- */
 
 /*
@@ -701,6 +762,10 @@ static int run_rank(const char *prov_path)
 	size_t len;
 
 	owner_init();
+	if (devmode && hip_load()) {
+		fprintf(stderr, "rank %d: no HIP runtime for device mode\n", me);
+		return 1;
+	}
 	dl = dlopen(prov_path, RTLD_NOW);
 	if (!dl) {
 		fprintf(stderr, "dlopen: %s\n", dlerror());
@@ -816,34 +881,51 @@ static int run_rank(const char *prov_path)
 		CHECK(y == want, "known answer %lu vs %lu", (unsigned long)y,
 		      (unsigned long)want);
 	}
-	for (int algo = 0; algo < 2; algo++) {
-		const char *sfx = algo ? "_rd" : "";
+	/* TREE, the reference's RD schedule, and (device buffers) P2P */
+	for (int k = 0; k < (devmode ? 3 : 2); k++) {
+		static const int algos[3] = { 0, 1, 4 };
+		static const char *const sfxs[3] = { "", "_rd", "_p2p" };
+		int algo = algos[k];
+		const char *sfx = sfxs[k];
 		char name[64];
 		float *fx = malloc(1000 * 4), *fy = calloc(1000, 4);
 		double *dx = malloc(4099 * 8), *dy = calloc(4099, 8);
 		int64_t lx[33], ly[33] = { 0 };
+		void *a[6];
 
 		CHECK(fi_setopt(&ep->fid, FI_OPT_ENDPOINT, OFF_LFA_OPT_ALGO, &algo,
 				sizeof(algo)) == 0, "algo");
 		seed(1);
 		for (int i = 0; i < 1000; i++)
 			fx[i] = (float)unif(-1, 1);
-		CHECK(fi_allreduce(ep, fx, 1000, NULL, fy, NULL, world, FI_FLOAT, FI_SUM, 0,
-				   &req[2]) == 0, "allreduce f32");
 		seed(2);
 		for (int i = 0; i < 4099; i++)
 			dx[i] = unif(0.9, 1.1);
-		CHECK(fi_allreduce(ep, dx, 4099, NULL, dy, NULL, world, FI_DOUBLE, FI_PROD,
-				   0, &req[3]) == 0, "allreduce f64");
 		seed(3);
 		for (int i = 0; i < 33; i++)
 			lx[i] = (int64_t)(lcg() << 11 ^ lcg());
-		CHECK(fi_allreduce(ep, lx, 33, NULL, ly, NULL, world, FI_INT64, FI_BXOR, 0,
+		a[0] = xbuf(fx, 1000 * 4);
+		a[1] = xbuf(fy, 1000 * 4);
+		a[2] = xbuf(dx, 4099 * 8);
+		a[3] = xbuf(dy, 4099 * 8);
+		a[4] = xbuf(lx, sizeof(lx));
+		a[5] = xbuf(ly, sizeof(ly));
+		CHECK(fi_allreduce(ep, a[0], 1000, NULL, a[1], NULL, world, FI_FLOAT, FI_SUM, 0,
+				   &req[2]) == 0, "allreduce f32");
+		CHECK(fi_allreduce(ep, a[2], 4099, NULL, a[3], NULL, world, FI_DOUBLE, FI_PROD,
+				   0, &req[3]) == 0, "allreduce f64");
+		CHECK(fi_allreduce(ep, a[4], 33, NULL, a[5], NULL, world, FI_INT64, FI_BXOR, 0,
 				   &req[4]) == 0, "allreduce bxor");
 		/* three in flight at once; complete in any order here */
 		wait_comp(&req[2]);
 		wait_comp(&req[3]);
 		wait_comp(&req[4]);
+		xdone(NULL, a[0], 0);
+		xdone(fy, a[1], 1000 * 4);
+		xdone(NULL, a[2], 0);
+		xdone(dy, a[3], 4099 * 8);
+		xdone(NULL, a[4], 0);
+		xdone(ly, a[5], sizeof(ly));
 		snprintf(name, sizeof(name), "sum_f32%s", sfx);
 		dump(name, "in", fx, 1000 * 4);
 		dump(name, "out", fy, 1000 * 4);
@@ -864,13 +946,18 @@ static int run_rank(const char *prov_path)
 		size_t count = 1000, base = count / (size_t)nranks, extra = count % (size_t)nranks;
 		size_t mlen = base + ((size_t)me < extra);
 		float *x = malloc(count * 4), *y = calloc(mlen ? mlen : 1, 4);
+		void *ax, *ay;
 
 		seed(4);
 		for (size_t i = 0; i < count; i++)
 			x[i] = (float)unif(-1, 1);
-		CHECK(fi_reduce_scatter(ep, x, count, NULL, y, NULL, world, FI_FLOAT, FI_SUM,
+		ax = xbuf(x, count * 4);
+		ay = xbuf(y, (mlen ? mlen : 1) * 4);
+		CHECK(fi_reduce_scatter(ep, ax, count, NULL, ay, NULL, world, FI_FLOAT, FI_SUM,
 					0, &req[5]) == 0, "reduce_scatter");
 		wait_comp(&req[5]);
+		xdone(NULL, ax, 0);
+		xdone(y, ay, mlen * 4);
 		dump("rs_f32", "in", x, count * 4);
 		dump("rs_f32", "out", y, mlen * 4);
 		free(x);
@@ -879,12 +966,18 @@ static int run_rank(const char *prov_path)
 	{   /* reduce to the last rank */
 		double *x = malloc(777 * 8), *y = calloc(777, 8);
 
+		void *ax, *ay;
+
 		seed(5);
 		for (int i = 0; i < 777; i++)
 			x[i] = unif(-1, 1);
-		CHECK(fi_reduce(ep, x, 777, NULL, y, NULL, world, (fi_addr_t)nranks - 1,
+		ax = xbuf(x, 777 * 8);
+		ay = xbuf(y, 777 * 8);
+		CHECK(fi_reduce(ep, ax, 777, NULL, ay, NULL, world, (fi_addr_t)nranks - 1,
 				FI_DOUBLE, FI_SUM, 0, &req[6]) == 0, "reduce");
 		wait_comp(&req[6]);
+		xdone(NULL, ax, 0);
+		xdone(y, ay, 777 * 8);
 		dump("reduce_f64", "in", x, 777 * 8);
 		if (me == nranks - 1)
 			dump("reduce_f64", "out", y, 777 * 8);
@@ -963,7 +1056,7 @@ int main(int argc, char **argv)
 	pid_t pid[MAXR];
 
 	if (argc < 4) {
-		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency] [core]\n",
+		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> <nranks> <outdir> [manual] [latency] [core] [device]\n",
 			argv[0]);
 		return 2;
 	}
@@ -973,6 +1066,7 @@ int main(int argc, char **argv)
 		manual |= !strcmp(argv[i], "manual");
 		latency |= !strcmp(argv[i], "latency");
 		core |= !strcmp(argv[i], "core");
+		devmode |= !strcmp(argv[i], "device");
 	}
 	if (manual)
 		setenv("OFF_LFA_PROGRESS", "manual", 1);

@@ -94,15 +94,31 @@ def _load(tmp_path, r, name, io, dt):
 @pytest.mark.parametrize("n", [2, 3])
 @pytest.mark.parametrize("mode", [[], ["manual"]])
 def test_peer_transport_collectives(tmp_path, n, mode):
+    _peer_run(n, tmp_path, mode)
+    _check_peer_outputs(tmp_path, n, ("", "_rd"))   # TREE and the reference's RD
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,mode", [(2, []), (3, ["manual"])])
+def test_peer_transport_device_buffers(tmp_path, n, mode):
+    """The provider with DEVICE buffers over the owner's transport, N
+    processes on the one GPU: the reducing collectives (TREE, RD and P2P —
+    the IPC workspace handshake and the system-scope kernel across the
+    processes) run the gfx950 kernels, every transfer staged through host
+    memory for an owner that moves host bytes only."""
+    _peer_run(n, tmp_path, mode + ["device"])
+    _check_peer_outputs(tmp_path, n, ("", "_rd", "_p2p"))
+
+
+def _check_peer_outputs(tmp_path, n, sfxs):
     import numpy as np
     import oracle
-    _peer_run(n, tmp_path, mode)
     for name, op, dt, nd in (("sum_f32", 2, 8, np.float32), ("prod_f64", 3, 9, np.float64),
                              ("bxor_i64", 9, 6, np.int64)):
         ins = [_load(tmp_path, r, name, "in", nd) for r in range(n)]
         want = oracle.allreduce(op, dt, ins)[0]
         assert ins[0].size and not all(np.array_equal(ins[0], x) for x in ins[1:])
-        for sfx in ("", "_rd"):          # TREE and the reference's own RD schedule
+        for sfx in sfxs:
             for r in range(n):
                 got = _load(tmp_path, r, name + sfx, "out", nd)
                 assert got.tobytes() == want.tobytes(), (name + sfx, r)
