@@ -19,10 +19,10 @@ for kind in asan tsan; do
   gcc $SAN -fPIC -std=gnu11 -Wall -I"$R/include" -I"$FAB" -shared -o "$d/liboff_lfa-fi.so" \
       "$R/libfabric_amd/csrc/off_lfa.c" -L"$d" -llfa_coll -lpthread -Wl,-rpath,'$ORIGIN'
   gcc $SAN -std=gnu11 -I"$R/include" -I"$FAB" -o "$d/peer" "$R/examples/off_lfa_peer.c" -ldl -lpthread
-  for args in "3 manual" "3" "2 latency"; do
+  for args in "3 manual" "3" "2 latency" "5 core" "4 core manual"; do
     set -- $args
     LD_LIBRARY_PATH="$R/libfabric_amd" timeout 300 "$d/peer" "$d/liboff_lfa-fi.so" "$1" "$d/out" \
-        "${@:2}" 2>&1 | tee "$d/log.txt" | grep -E "^OK|SUMMARY|WARNING" || true
+        "${@:2}" 2>&1 | tee "$d/log.txt" | grep -E "^OK|^CORE broadcast|SUMMARY|WARNING" || true
     if grep -qE "SUMMARY|WARNING: ThreadSanitizer|ERROR: AddressSanitizer" "$d/log.txt"; then
       echo "$kind: sanitizer report (see $d/log.txt)"; exit 1
     fi
