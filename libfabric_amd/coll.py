@@ -457,6 +457,13 @@ class Endpoint:
                 raise TimeoutError("join did not complete")
 
 
+class TransportAgain(Exception):
+    """Raised by a HostEndpoint transport's send/recv when the owner cannot
+    take the transfer now (its queue is full): the provider retries the post
+    on a later progress call, as prov/coll requeues a SEND that returned
+    -FI_EAGAIN (coll_coll.c:845-852)."""
+
+
 class HostEndpoint(Endpoint):
     """An endpoint of a peer-transfer domain (lfa_coll_domain_open_host):
     host-memory buffers, transfers through `transport` — an object with
@@ -476,6 +483,8 @@ class HostEndpoint(Endpoint):
             try:
                 req[0] = transport.send(peer, buf, nbytes, tag)
                 return 0
+            except TransportAgain:
+                return -EAGAIN
             except Exception:  # noqa: BLE001 — an exception must not cross C
                 return -EIO
 
@@ -483,6 +492,8 @@ class HostEndpoint(Endpoint):
             try:
                 req[0] = transport.recv(peer, buf, nbytes, tag)
                 return 0
+            except TransportAgain:
+                return -EAGAIN
             except Exception:  # noqa: BLE001
                 return -EIO
 
@@ -508,4 +519,4 @@ def esz(dt: int) -> int:
 
 __all__ = ["plan", "block", "host_chunks", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
            "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz",
-           "HostEndpoint", "PeerXferOps"]
+           "HostEndpoint", "PeerXferOps", "TransportAgain"]

@@ -224,6 +224,110 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
+class FlakyXfer(GlooXfer):
+    """The owner pushing back: every `every`-th post is refused with
+    TransportAgain (-EAGAIN, the provider must retry it later), and a chosen
+    receive can be made to complete with an error."""
+
+    def __init__(self, every=3):
+        super().__init__()
+        self.every, self.n, self.refused = every, 0, 0
+        self.fail_recv = False
+        self.failing = set()
+
+    def _gate(self):
+        from libfabric_amd.coll import TransportAgain
+        self.n += 1
+        if self.n % self.every == 0:
+            self.refused += 1
+            raise TransportAgain()
+
+    def send(self, peer, ptr, nbytes, tag):
+        self._gate()
+        return super().send(peer, ptr, nbytes, tag)
+
+    def recv(self, peer, ptr, nbytes, tag):
+        self._gate()
+        h = super().recv(peer, ptr, nbytes, tag)
+        if self.fail_recv:
+            self.failing.add(h)
+        return h
+
+    def test(self, h):
+        bad = h in self.failing
+        r = super().test(h)
+        if bad:
+            self.failing.discard(h)
+            return -5                         # the transfer failed: -EIO
+        return r
+
+
+def _flaky_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from libfabric_amd import coll
+        xfer = FlakyXfer()
+        ep = coll.HostEndpoint(rank, world, xfer)
+        try:
+            for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL):
+                ep.set_algo(algo)
+                sends = _inputs(oracle, 8, 5000, world, 31 + algo)
+                want = oracle.allreduce(2, 8, sends)[0]
+                res = np.zeros(5000, np.float32)
+                ep.wait(ep.allreduce(sends[rank], res, 5000, 8, 2))
+                assert res.tobytes() == want.tobytes(), algo
+            assert xfer.refused > 0, "no post was refused"
+            # a failed transfer fails its operation, on that rank only
+            xfer.every = 10 ** 9
+            xfer.fail_recv = rank == 1
+            x = np.ones(64, np.float32)
+            res = np.zeros(64, np.float32)
+            ctx = ep.allreduce(x, res, 64, 8, 2)
+            if rank == 1:
+                with pytest.raises(coll.CollError):
+                    ep.wait(ctx)
+            else:
+                ep.wait(ctx)
+                assert np.all(res == world)
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_transport_pushback_and_failure():
+    """prov/coll's requeue of a SEND the owner refused with -FI_EAGAIN
+    (coll_coll.c:845-852) — here every third post, sends and receives, over
+    three algorithms, results still exact — and a transfer that completes in
+    error failing its operation through lfa_cq_readerr."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flaky_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=120)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_c_executor_across_processes(world):
     ctx = mp.get_context("spawn")
