@@ -313,6 +313,14 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype dt, void *dst,
     return -LFA_EINVAL;
   for (int k = 0; k < nsrc; k++)
     if (cnt && !srcs[k]) return -LFA_EINVAL;
+  // One input is a copy (a one-member group's allreduce): from 16 MiB the
+  // write table's ATOMIC_WRITE body beats hipMemcpyAsync D2D (83.3 vs 98.8 us
+  // at 256 MiB, profiles/r02_probe_copy.log); below, the tree launcher's
+  // hipMemcpyAsync stays.
+  const size_t bytes = cnt * lfa_datatype_size(dt);
+  if (nsrc == 1 && dst != srcs[0] && bytes >= ((size_t)16 << 20))
+    return lfa_atomic_write_async(LFA_ATOMIC_WRITE, LFA_UINT8, dst, srcs[0], bytes,
+                                  stream);
   return kTree[op](dt, dst, srcs, nsrc, cnt, stream);
 }
 

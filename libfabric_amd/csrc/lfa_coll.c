@@ -828,6 +828,8 @@ static void *resolve(const struct xctx *x, struct lfa_ref r)
 	return (char *)x->base[r.buf] + r.off;
 }
 
+#define LFA_COPY_KERNEL_BYTES ((size_t)16 << 20)
+
 /* Non-communication step on `stream`. */
 static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 		     const struct xctx *x, enum lfa_op op,
@@ -863,6 +865,16 @@ static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 						 (int)s->nsrc, s->count, stream);
 	}
 	case LFA_STEP_COPY:
+		/* large copies through the write table's ATOMIC_WRITE row (the
+		 * LDS-DMA body, no dst read): 83.3 vs 98.8 us at 256 MiB and 12.3
+		 * vs 14.5 us at 32 MiB against hipMemcpyAsync D2D, which stays
+		 * ahead below (4.95 vs 5.43 us at 4 MiB; tools/probe_copy.py,
+		 * profiles/r02_probe_copy.log).  COPY items never touch a peer's
+		 * memory (the planner's copies stay in this rank's buffers). */
+		if (s->count >= LFA_COPY_KERNEL_BYTES)
+			return lfa_atomic_write_async(LFA_ATOMIC_WRITE, LFA_UINT8,
+						      resolve(x, s->dst), resolve(x, s->src),
+						      s->count, stream);
 		return hipMemcpyAsync(resolve(x, s->dst), resolve(x, s->src),
 				      s->count, hipMemcpyDeviceToDevice,
 				      stream) == hipSuccess ? 0 : -LFA_EIO;
