@@ -640,6 +640,7 @@ def extra_host_reduce_scatter(ep, rank, world, reps=3):
     hy = torch.zeros(ln, dtype=torch.float64).pin_memory()
     dx = hx.to("cuda")
     dy = torch.empty(ln, device="cuda", dtype=torch.float64)
+    torch.cuda.synchronize()     # buffers ready: the provider's stream is its own
     ep.wait(ep.reduce_scatter(dx, dy, cnt, 9, 3))
     ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
     row = {"bitwise_equal_device": bool(torch.equal(hy, dy.cpu()))}
@@ -716,6 +717,7 @@ def _rs_sweep(ep, rank, world, algo):
         a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
         off, ln = coll.block(cnt, world, rank)
         b = torch.empty(max(ln, 1), device="cuda", dtype=torch.float64)
+        torch.cuda.synchronize()
         ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
         barrier(world)
         reps = 20 if nbytes < (16 << 20) else 5
@@ -750,6 +752,10 @@ def extra_collectives(rank, world, stream):
             try:
                 ep.set_algo(algo)
                 y.zero_()
+                # fi_allreduce takes ready buffers: torch's fill and the
+                # input's generation run on torch's stream, the provider on
+                # its own
+                torch.cuda.synchronize()
                 ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
                 row = {}
                 if algo != coll.ALGO_RCCL:
@@ -762,6 +768,7 @@ def extra_collectives(rank, world, stream):
                     # tree, |got - ref| <= 2(N-1) 2^-24 sum_r |x_r|
                     ep.set_algo(coll.ALGO_TREE)
                     ax, sab = x.abs(), torch.empty_like(x)
+                    torch.cuda.synchronize()
                     ep.wait(ep.allreduce(ax, sab, COUNT, 8, 2))
                     bound = 2 * max(world - 1, 1) * 2.0 ** -24 * sab
                     err = (y - ref).abs()
@@ -800,6 +807,7 @@ def extra_collectives(rank, world, stream):
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
         a = torch.rand(1024, device="cuda")
         b = torch.empty_like(a)
+        torch.cuda.synchronize()
         for name, algo in (("allreduce_4kib_float_sum_us", coll.ALGO_TREE),
                            ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P)):
             if algo == coll.ALGO_P2P and world == 1:

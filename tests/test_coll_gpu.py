@@ -133,10 +133,33 @@ def test_loopback_16_ranks_int_bitwise(coll):
 
 # ------------------------------------------------ RCCL domain, world = 1 ----
 
+class _ReadyBuffers:
+    """fi_allreduce & co. take buffers that are ready when called: libfabric
+    carries no stream, and the endpoint's stream does not wait for torch's.
+    This wrapper synchronises the device before each collective call, as a
+    caller that filled its buffers with kernels must."""
+
+    _CALLS = {"allreduce", "reduce_scatter", "reduce", "allgather", "scatter",
+              "broadcast", "barrier"}
+
+    def __init__(self, ep):
+        self._ep = ep
+
+    def __getattr__(self, name):
+        a = getattr(self._ep, name)
+        if name not in self._CALLS:
+            return a
+
+        def call(*args, **kw):
+            torch.cuda.synchronize()
+            return a(*args, **kw)
+        return call
+
+
 @pytest.fixture(scope="module")
 def ep(coll):
     e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
-    yield e
+    yield _ReadyBuffers(e)
     e.close()
 
 
