@@ -113,15 +113,28 @@ def check_world(expected: int, world: int) -> None:
         sys.exit(2)
 
 
+# LFA_BENCH_REHEARSE=1: a dry run of the N-rank flow on fewer GPUs than ranks
+# (ranks share devices round-robin, torch.distributed over gloo).  RCCL
+# refuses two ranks on one GPU, so the provider's collectives report errors
+# there; the launch, the sharded headline, the timing and the JSON line are
+# what it exercises.  Never used for a reported number.
+REHEARSE = os.environ.get("LFA_BENCH_REHEARSE") == "1"
+
+
 def init_dist(n_gpus: int):
     if n_gpus > 1 or "RANK" in os.environ:
         rank = int(os.environ.get("RANK", 0))
         world = int(os.environ.get("WORLD_SIZE", 1))
         local = int(os.environ.get("LOCAL_RANK", rank))
         check_world(n_gpus, world)
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if REHEARSE:
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
         check_world(n_gpus, dist.get_world_size())
         return rank, world, local
     torch.cuda.set_device(0)
@@ -145,7 +158,7 @@ def barrier(world: int) -> None:
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if REHEARSE else "cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -1203,6 +1216,8 @@ def main() -> None:
             "traffic_source": traffic_src,
         },
     }
+    if REHEARSE:
+        line["rehearsal"] = "LFA_BENCH_REHEARSE: ranks share GPUs; not a measurement"
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         line["cpu_baseline"]["config3_int64_64mib"] = cpu_baseline_config3(args.cpu_reps)
