@@ -100,14 +100,16 @@ def build_coll(verbose: bool = False) -> str | None:
     src = os.path.join(CSRC, "lfa_coll.c")
     if not os.path.exists(src):
         return None
+    srcs = [src, os.path.join(CSRC, "lfa_coll_plan.c")]   # executor + planner
     hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "lfa_atomic.h"),
-            os.path.join(INC, "lfa_fabric.h"), LIB_LFA]
-    if _newer(LIB_COLL, [src] + hdrs):
+            os.path.join(INC, "lfa_fabric.h"), os.path.join(CSRC, "lfa_coll_plan.h"),
+            LIB_LFA]
+    if _newer(LIB_COLL, srcs + hdrs):
         # Plain C (the reference's host language), calling HIP's and RCCL's
         # C APIs; no HIP device code in this library.
         _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
               "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__", "-I" + INC,
-              "-I" + os.path.join(ROCM, "include"), "-shared", "-o", LIB_COLL, src,
+              "-I" + os.path.join(ROCM, "include"), "-shared", "-o", LIB_COLL, *srcs,
               "-L" + PKG, "-llfa", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64",
               "-lrccl", "-lpthread", "-Wl,-rpath,$ORIGIN",
               "-Wl,-soname,liblfa_coll.so"])

@@ -1,0 +1,32 @@
+/*
+ * lfa_coll_plan.h — internal interface between the schedule builder
+ * (lfa_coll_plan.c) and the executor (lfa_coll.c) of liblfa_coll.so.  Not
+ * installed; nothing here is exported from the library.
+ */
+#ifndef LFA_COLL_PLAN_H
+#define LFA_COLL_PLAN_H
+
+#include <stddef.h>
+
+#include "lfa_coll.h"
+
+#define LFA_INTERNAL __attribute__((visibility("hidden")))
+#define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
+
+/* A heap-allocated plan. */
+struct plan {
+	struct lfa_step *steps;
+	struct lfa_ref *refs;
+	size_t nsteps, nrefs, tmp;
+};
+
+LFA_INTERNAL void plan_free(struct plan *pl);
+/* lfa_coll_plan into freshly allocated arrays */
+LFA_INTERNAL int plan_make(struct plan *pl, enum lfa_collective_op coll,
+			   enum lfa_coll_algo algo, int rank, int n, int root,
+			   size_t count, size_t esz);
+/* Collective items -> grouped SEND/RECV items; lower_barrier: BARRIER too */
+LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, struct plan *out,
+			    int lower_barrier);
+
+#endif
