@@ -109,6 +109,16 @@ static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 						 (int)s->nsrc, s->count, stream);
 	}
 	case LFA_STEP_COPY:
+		if (s->src.buf == LFA_BUF_SYM_IN || s->src.buf == LFA_BUF_SYM_OUT) {
+			/* bytes peers pushed over xGMI into this rank's workspace
+			 * (the P2P unstage): through the P2P kernel's system-scope
+			 * loads, which no cached copy of the line can satisfy */
+			void *d = resolve(x, s->dst);
+			const void *sp = resolve(x, s->src);
+
+			return lfa_reduce_tree_put_async(LFA_BOR, LFA_UINT8, &d, 1, &sp, 1,
+							 s->count, stream);
+		}
 		/* large copies through the write table's ATOMIC_WRITE row (the
 		 * LDS-DMA body, no dst read): 83.3 vs 98.8 us at 256 MiB and 12.3
 		 * vs 14.5 us at 32 MiB against hipMemcpyAsync D2D, which stays
