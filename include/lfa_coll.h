@@ -164,9 +164,10 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
  * (fabtests core_coll.c:138-178, the stride test).  `ranks` are sorted ranks
  * of `coll_addr`'s group and must include the caller.  The agreement travels
  * under group id 256 (outside the 0..255 ids a join hands out), so it cannot
- * meet a joined group's traffic.  Device domains accept the whole group only
- * (a strict subset would need a communicator created without the
- * non-members: -LFA_ENOSYS). */
+ * meet a joined group's traffic.  On a device domain a strict subset gets an
+ * RCCL communicator of its own (the first member's unique id sent to the
+ * others point-to-point over the parent's communicator, then
+ * ncclCommInitRank among the members); the whole group splits as usual. */
 int lfa_join_members(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		     const int *ranks, size_t nmembers, uint64_t flags,
 		     struct lfa_coll_mc **mc, void *context);

@@ -2149,6 +2149,69 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 /* join                                                                    */
 /* ---------------------------------------------------------------------- */
 
+/*
+ * A device domain's communicator for a group formed by its members alone
+ * (lfa_join_members on a strict subset): the first member's RCCL unique id
+ * reaches the others point-to-point over the parent's communicator — only
+ * the members take part in those transfers — and the members then create
+ * their communicator together.  The transfers are enqueued under ep->lock
+ * (this rank's position in the parent's operation order); the waits run
+ * outside it, so progress keeps reaping completions meanwhile.
+ */
+static int members_comm(struct lfa_coll_ep *ep, struct lfa_coll_mc *parent,
+			const int *ranks, size_t n, int pos, ncclComm_t *out)
+{
+	ncclUniqueId uid;
+	hipEvent_t ev = NULL;
+	void *d = NULL;
+	int ret = 0;
+
+	memset(&uid, 0, sizeof(uid));
+	hipSetDevice(ep->dom->device);
+	if (pos == 0 && ncclGetUniqueId(&uid) != ncclSuccess)
+		ret = -LFA_EIO;         /* the others still get (and fail on) zeros */
+	if (hipMalloc(&d, sizeof(uid)) != hipSuccess ||
+	    hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+		if (d)
+			hipFree(d);
+		return -LFA_ENOMEM;
+	}
+	pthread_mutex_lock(&ep->lock);
+	if ((pos == 0 && hipMemcpyAsync(d, &uid, sizeof(uid), hipMemcpyHostToDevice,
+					ep->stream) != hipSuccess) ||
+	    ncclGroupStart() != ncclSuccess)
+		ret = -LFA_EIO;
+	for (size_t k = 1; k < n && pos == 0; k++)
+		if (ncclSend(d, sizeof(uid), ncclUint8, ranks[k], parent->comm,
+			     ep->stream) != ncclSuccess)
+			ret = -LFA_EIO;
+	if (pos != 0 && ncclRecv(d, sizeof(uid), ncclUint8, ranks[0], parent->comm,
+				 ep->stream) != ncclSuccess)
+		ret = -LFA_EIO;
+	if (ncclGroupEnd() != ncclSuccess ||
+	    hipMemcpyAsync(&uid, d, sizeof(uid), hipMemcpyDeviceToHost,
+			   ep->stream) != hipSuccess ||
+	    hipEventRecord(ev, ep->stream) != hipSuccess)
+		ret = -LFA_EIO;
+	pthread_mutex_unlock(&ep->lock);
+	if (hipEventSynchronize(ev) != hipSuccess)
+		ret = -LFA_EIO;
+	hipEventDestroy(ev);
+	hipFree(d);
+	{
+		/* a first member without an id sent zeros: everyone stops here */
+		static const ncclUniqueId none;
+
+		if (!memcmp(&uid, &none, sizeof(uid)))
+			return ret ? ret : -LFA_EIO;
+	}
+	pthread_mutex_lock(&ep->comm_lock);
+	if (ncclCommInitRank(out, (int)n, uid, pos) != ncclSuccess)
+		ret = ret ? ret : -LFA_EIO;
+	pthread_mutex_unlock(&ep->comm_lock);
+	return ret;
+}
+
 /* members_only: lfa_join_members — the agreement runs over the new group
  * itself, so only its members call (see lfa_coll.h). */
 static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
@@ -2187,9 +2250,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	if (members_only) {
 		if (!member)
 			return -LFA_EINVAL;     /* only members call this form */
-		if (!host && nmembers != (size_t)parent->size)
-			return -LFA_ENOSYS;     /* no split without the non-members */
-		if (!host)
+		if (!host && nmembers == (size_t)parent->size)
 			members_only = 0;       /* the whole group: every rank calls */
 	}
 	mc = calloc(1, sizeof(*mc));
@@ -2220,6 +2281,13 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			ret = -LFA_ENOMEM;
 		for (size_t i = 0; !ret && i < nmembers; i++)
 			mc->members[i] = world_rank(parent, ranks[i]);
+	} else if (members_only) {
+		/* a strict subset formed by its members alone: no split (that
+		 * needs every parent rank) but a communicator of its own */
+		ret = members_comm(ep, parent, ranks, nmembers, pos, &mc->comm);
+		mc->owns_comm = !ret;
+		mc->rank = pos;
+		mc->size = (int)nmembers;
 	} else {
 		/*
 		 * Every parent rank takes part in the split (non-members with
@@ -2279,7 +2347,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
 			hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
 				       hipMemcpyHostToDevice, ep->stream);
-			ret = run_device(ep, parent, LFA_ALLREDUCE, dmask,
+			ret = run_device(ep, members_only ? mc : parent, LFA_ALLREDUCE, dmask,
 					 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
 					 LFA_UINT8, LFA_BAND, ep->stream);
 			if (!ret)
