@@ -107,9 +107,10 @@ int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
  * Endpoints of such a domain run each collective's schedule on the host:
  * transfers through these callbacks, REDUCE / TREE items through
  * lfa_host_write / lfa_host_reduce_tree (include/lfa_atomic.h), progressed by
- * lfa_cq_read as prov/coll progresses in fi_cq_read.  LFA_ALGO_P2P and
- * LFA_ALGO_RCCL run as LFA_ALGO_TREE; LFA_ALGO_TREE_COLL's collective items
- * become grouped sends/receives.
+ * lfa_cq_read as prov/coll progresses in fi_cq_read.  LFA_ALGO_RCCL runs as
+ * LFA_ALGO_TREE, and so does LFA_ALGO_P2P on a domain without a GPU (on a
+ * GPU peer domain it keeps its schedule, see lfa_coll_domain_open_peer);
+ * LFA_ALGO_TREE_COLL's collective items become grouped sends/receives.
  */
 struct lfa_peer_xfer_ops {
 	int (*send)(void *ctx, int peer, const void *buf, size_t bytes,
@@ -128,7 +129,11 @@ int lfa_coll_domain_open_host(int rank, int nranks,
  * after a receive), so the owner only ever moves host bytes — prov/coll over
  * an owner without FI_HMEM.  Host buffers keep the host combine.  A buffer
  * pair must be both device or both host memory (-LFA_EINVAL otherwise);
- * members may differ from one another. */
+ * members may differ from one another.  LFA_ALGO_P2P keeps its schedule
+ * here: the members map each other's symmetric workspaces over IPC (the
+ * handshake runs from progress calls), its barriers are zero-byte message
+ * rings, a host-buffer member is staged through device copies, and a P2P
+ * operation starts once the endpoint's earlier operations have finished. */
 int lfa_coll_domain_open_peer(int device, int rank, int nranks,
 			      const struct lfa_peer_xfer_ops *ops, void *ctx,
 			      struct lfa_coll_domain **domain);
