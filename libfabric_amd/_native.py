@@ -71,6 +71,9 @@ def _bind_tune(L):
     for fn in (L.lfa__tune_sum_f32, L.lfa__tune2_sum_f32):
         fn.restype = c_int
         fn.argtypes = [c_int, c_void_p, c_void_p, c_size_t, c_void_p]
+    L.lfa__tune_fetch_f32.restype = c_int
+    L.lfa__tune_fetch_f32.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_size_t, c_void_p]
 
 
 def lib(name: str = "lfa") -> ctypes.CDLL:

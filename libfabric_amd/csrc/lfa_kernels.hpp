@@ -496,6 +496,13 @@ struct RwF {
   u32x4 *dv;
   const u32x4 *sv;
   u32x4 *rv;
+  // fetch_lds interface: inputs dst, src; outputs res (old dst), dst
+  static constexpr int kIn = OP == OP_READ ? 1 : 2;
+  static constexpr bool kWriteDst = OP != OP_READ;
+  __device__ __forceinline__ const u32x4 *in(int k) const { return k ? sv : dv; }
+  __device__ __forceinline__ u32x4 op(u32x4 a, u32x4 b, u32x4) const {
+    return apply_vec<OP, T>(a, b);
+  }
   __device__ __forceinline__ void vec(size_t i) const {
     u32x4 a = ld<true>(dv + i);
     st<true>(rv + i, a);
@@ -543,6 +550,15 @@ struct SwapF {
   const u32x4 *sv;
   const u32x4 *cv;
   u32x4 *rv;
+  // fetch_lds interface: inputs dst, src, cmp; outputs res, dst
+  static constexpr int kIn = 3;
+  static constexpr bool kWriteDst = true;
+  __device__ __forceinline__ const u32x4 *in(int k) const {
+    return k == 0 ? dv : k == 1 ? sv : cv;
+  }
+  __device__ __forceinline__ u32x4 op(u32x4 a, u32x4 b, u32x4 m) const {
+    return swap_vec<OP, T>(a, b, m);
+  }
   __device__ __forceinline__ void vec(size_t i) const {
     u32x4 a = ld<true>(dv + i);
     u32x4 b = ld<true>(sv + i);
@@ -587,6 +603,55 @@ __global__ __launch_bounds__(kBlock) void fetch_elem(F f, size_t n0, size_t off1
   size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
   size_t stride = (size_t)gridDim.x * kBlock;
   for (; i < n0 + n1; i += stride) f.elem(i < n0 ? i : off1 + (i - n0));
+}
+
+// LDS-DMA staged fetch / compare body, combine_lds's shape: each wave moves
+// U KiB of each of its F::kIn inputs (dst, src[, cmp]) HBM -> LDS with nt
+// global_load_lds (all in flight together), then writes res = the old dst
+// and, unless ATOMIC_READ, the new dst, with SAUX stores.  The register form
+// above interleaves its loads with stores that may alias them, so each lane
+// had only one or two loads in flight (75.7 % of HBM peak for a 256 MiB float
+// SUM readwrite, tools/probe_fetch.py).
+template <int U, int SAUX, typename F>
+__global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds(F f, size_t nvec) {
+  __shared__ u32x4 lds[F::kIn][kLdsWaves][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base =
+      (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int k = 0; k < F::kIn; k++)
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(f.in(k) + base + u * 64 + l),
+                                         (lds_void *)&lds[k][w][u][0], 16, 0,
+                                         /*aux: nt*/ 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u32x4 a = lds[0][w][u][l];
+      const u32x4 b = F::kIn > 1 ? lds[F::kIn > 1 ? 1 : 0][w][u][l] : a;
+      const u32x4 c = F::kIn > 2 ? lds[F::kIn > 2 ? 2 : 0][w][u][l] : a;
+      const unsigned off = (unsigned)(u * 64 + l) * 16;
+      if constexpr (SAUX == kStoreNt) {
+        st<true>(f.rv + base + u * 64 + l, a);
+        if constexpr (F::kWriteDst) st<true>(f.dv + base + u * 64 + l, f.op(a, b, c));
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
+        if constexpr (F::kWriteDst)
+          __builtin_amdgcn_raw_buffer_store_b128(f.op(a, b, c), rd, off, 0, SAUX);
+      }
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec) f.vec(i);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -870,10 +935,19 @@ static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
     size_t nvec = (cnt - head) * E / 16, body = nvec * 16 / E;
     size_t tail = cnt - head - body;
     auto f = make(std::integral_constant<bool, true>(), head);
+    using FF = decltype(f);
+    // 4 KiB per input per wave and write-through (sc1) stores at every size:
+    // at 256 MiB per operand 168.0 us (79.9 %) for a float SUM readwrite and
+    // 199.9 us (83.9 %) for a float CSWAP, against 174.3 / 204.8 us for the
+    // round-1 register form and 174.6 / 201.1 us with nt stores
+    // (tools/probe_fetch.py --tune, profiles/r02_tune_fetch.log).  Two
+    // output streams make write-through win even where combine_lds (one
+    // output) keeps nt.
+    constexpr int U = 4;
     if (nvec)
-      hipLaunchKernelGGL(fetch_vec<decltype(f)>,
-                         dim3(grid_for(nvec, (size_t)kBlock * kFetchUnroll, 0x7fffffffu)),
-                         dim3(kBlock), 0, s, f, nvec);
+      hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF>),
+                         dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu)),
+                         dim3(kLdsWaves * 64), 0, s, f, nvec);
     if (head + tail)
       hipLaunchKernelGGL(fetch_elem<decltype(f)>,
                          dim3(grid_for(head + tail, kBlock, kElemGridCap)),

@@ -615,3 +615,52 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
 #undef TPP
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
+
+// ---------------------------------------------------------------------------
+// fetch / compare table bodies (tools/probe_fetch.py --tune): float SUM
+// readwrite (swap = 0) or float CSWAP (swap = 1) over nvec co-aligned 16-B
+// vectors.  0 = the round-1 register form (fetch_vec, 2 vectors per lane),
+// 1..3 = fetch_lds U = 4 / 2 / 1 with nt stores, 4..5 = U = 4 / 2 with sc1
+// write-through stores.
+// ---------------------------------------------------------------------------
+extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void *src,
+                                   const void *cmp, void *res, size_t nvec,
+                                   void *stream) {
+  using namespace lfa;
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto f) -> int {
+    using FF = decltype(f);
+    auto lds = [&](auto u, auto aux) {
+      constexpr int U = decltype(u)::value, A = decltype(aux)::value;
+      hipLaunchKernelGGL((fetch_lds<U, A, FF>),
+                         dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu)),
+                         dim3(kLdsWaves * 64), 0, s, f, nvec);
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I2 = std::integral_constant<int, 2>;
+    using I1 = std::integral_constant<int, 1>;
+    using NT = std::integral_constant<int, kStoreNt>;
+    using SC1 = std::integral_constant<int, kStoreSc1>;
+    switch (variant) {
+      case 0:
+        hipLaunchKernelGGL(fetch_vec<FF>,
+                           dim3(grid_for(nvec, (size_t)kBlock * kFetchUnroll, 0x7fffffffu)),
+                           dim3(kBlock), 0, s, f, nvec);
+        break;
+      case 1: lds(I4(), NT()); break;
+      case 2: lds(I2(), NT()); break;
+      case 3: lds(I1(), NT()); break;
+      case 4: lds(I4(), SC1()); break;
+      case 5: lds(I2(), SC1()); break;
+      default: return -LFA_EINVAL;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+  };
+  if (swap)
+    return go(SwapF<OP_CSWAP, float, true>{(char *)dst, (const char *)src,
+                                           (const char *)cmp, (char *)res, (u32x4 *)dst,
+                                           (const u32x4 *)src, (const u32x4 *)cmp,
+                                           (u32x4 *)res});
+  return go(RwF<OP_SUM, float, true>{(char *)dst, (const char *)src, (char *)res,
+                                     (u32x4 *)dst, (const u32x4 *)src, (u32x4 *)res});
+}

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Fetch and compare tables at 256 MiB per operand (dev probe, GPU box):
+lfa_atomic_readwrite_async (res = dst; dst = dst OP src: 2 reads + 2 writes
+per element) and lfa_atomic_swap_async (res = dst; dst = src where cmp OP
+dst: 3 reads + 2 writes), float / int64, rotated over >= 1 GiB per operand
+kind; one HIP event pair around 20 launches, median of 5 rounds.  Prints one
+JSON line per (table, op, datatype) with the HBM roofline fraction of the
+algorithmic bytes."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from libfabric_amd import atomic  # noqa: E402
+
+S = 256 << 20
+
+
+def run(name, fn, nbytes_per_launch):
+    for i in range(6):
+        fn(i)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for i in range(20):
+            fn(i)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 20)
+    t = statistics.median(ts)
+    print(json.dumps({"case": name, "us": round(t * 1e3, 1),
+                      "frac": round(nbytes_per_launch / (t * 1e-3) / 8e12, 4)}), flush=True)
+
+
+def main():
+    torch.cuda.set_device(0)
+    for dtn, dt, tdt in (("float", 8, torch.float32), ("int64", 6, torch.int64)):
+        n = S // torch.tensor([], dtype=tdt).element_size()
+        sets = [[torch.ones(n, dtype=tdt, device="cuda") for _ in range(4)]
+                for _ in range(2)]
+        # readwrite: SUM (float) / BOR (int64); ATOMIC_READ (1 read + 1 write)
+        op = 2 if dt == 8 else 6
+        run(f"readwrite_{dtn}_{'sum' if op == 2 else 'bor'}",
+            lambda i: atomic.readwrite(op, dt, sets[i % 2][0], sets[i % 2][1], sets[i % 2][2]),
+            4 * S)
+        run(f"readwrite_{dtn}_atomic_read",
+            lambda i: atomic.readwrite(10, dt, sets[i % 2][0], None, sets[i % 2][2]), 2 * S)
+        # swap: CSWAP (op 12 = FI_CSWAP): reads dst, src, cmp; writes res, dst
+        run(f"swap_{dtn}_cswap",
+            lambda i: atomic.swap(12, dt, sets[i % 2][0], sets[i % 2][1], sets[i % 2][3],
+                                  sets[i % 2][2]), 5 * S)
+        del sets
+        torch.cuda.empty_cache()
+
+
+def tune():
+    """--tune: the fetch bodies of liblfa_tune.so (lfa__tune_fetch_f32),
+    interleaved rounds, float SUM readwrite and float CSWAP, 256 MiB each
+    operand, two rotating sets; every variant checked against variant 0."""
+    from libfabric_amd import _native
+    L = _native.lib("tune")
+    torch.cuda.set_device(0)
+    h = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    nvec = n // 4
+    variants = [0, 1, 2, 3, 4, 5]
+    for swap, nbytes in ((0, 4 * S), (1, 5 * S)):
+        g = torch.Generator(device="cuda").manual_seed(3)
+        sets = [[torch.rand(n, device="cuda", generator=g) for _ in range(4)]
+                for _ in range(2)]
+        for t in sets:                      # cmp == dst on half the lanes
+            t[3][::2] = t[0][::2]
+        ref = None
+        for v in variants:                  # correctness on a fresh copy
+            d, sr, c, r = (x.clone() for x in sets[0])
+            assert L.lfa__tune_fetch_f32(v, swap, d.data_ptr(), sr.data_ptr(), c.data_ptr(),
+                                         r.data_ptr(), nvec, h) == 0
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (d, r)
+            elif not (torch.equal(ref[0], d) and torch.equal(ref[1], r)):
+                raise SystemExit(f"fetch variant {v} swap={swap} WRONG")
+        del ref
+        times = {v: [] for v in variants}
+        for _ in range(8):
+            for v in variants:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for i in range(10):
+                    d, sr, c, r = sets[i % 2]
+                    L.lfa__tune_fetch_f32(v, swap, d.data_ptr(), sr.data_ptr(), c.data_ptr(),
+                                          r.data_ptr(), nvec, h)
+                b.record()
+                torch.cuda.synchronize()
+                times[v].append(a.elapsed_time(b) / 10)
+        for v in variants:
+            t = statistics.median(times[v][2:])
+            print(json.dumps({"tune_fetch": "cswap" if swap else "readwrite_sum", "variant": v,
+                              "us": round(t * 1e3, 1),
+                              "frac": round(nbytes / (t * 1e-3) / 8e12, 4)}), flush=True)
+        del sets
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    tune() if "--tune" in sys.argv else main()
