@@ -107,5 +107,51 @@ def tune():
         torch.cuda.empty_cache()
 
 
+def sweep():
+    """--sweep: every entry of the fetch (readwrite) and compare (swap)
+    tables at 256 MiB per operand; entries the table lacks are skipped (the
+    product's -EOPNOTSUPP).  Bytes: readwrite 4·S (ATOMIC_READ 2·S), swap
+    5·S."""
+    from libfabric_amd.atomic import LfaError
+    torch.cuda.set_device(0)
+    sets = [[torch.randint(0, 255, (S,), dtype=torch.uint8, device="cuda")
+             for _ in range(4)] for _ in range(2)]
+    rows = []
+    for dt in range(16):
+        if not atomic.datatype_size(dt):
+            continue
+        for op in list(range(12)) + list(range(12, 19)):
+            if op < 12:
+                fn = lambda i, op=op, dt=dt: atomic.readwrite(
+                    op, dt, sets[i % 2][0], sets[i % 2][1], sets[i % 2][2],
+                    S // atomic.datatype_size(dt))
+                nb = 2 * S if op == 10 else 4 * S
+            else:
+                fn = lambda i, op=op, dt=dt: atomic.swap(
+                    op, dt, sets[i % 2][0], sets[i % 2][1], sets[i % 2][3], sets[i % 2][2],
+                    S // atomic.datatype_size(dt))
+                nb = 5 * S
+            try:
+                fn(0)
+            except LfaError:
+                continue
+            for i in range(3):
+                fn(i)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            for i in range(8):
+                fn(i)
+            b.record()
+            torch.cuda.synchronize()
+            t = a.elapsed_time(b) / 8
+            rows.append({"table": "readwrite" if op < 12 else "swap", "op": op, "dt": dt,
+                         "us": round(t * 1e3, 1),
+                         "frac": round(nb / (t * 1e-3) / 8e12, 4)})
+    fr = [r["frac"] for r in rows]
+    print(json.dumps({"sweep_fetch": rows, "entries": len(rows), "min_frac": min(fr),
+                      "median_frac": statistics.median(fr)}), flush=True)
+
+
 if __name__ == "__main__":
-    tune() if "--tune" in sys.argv else main()
+    tune() if "--tune" in sys.argv else sweep() if "--sweep" in sys.argv else main()
