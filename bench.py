@@ -474,6 +474,33 @@ def extra_config3(dev, stream):
     return out
 
 
+def extra_fetch_tables(dev, stream):
+    """§8(f) row 4 on the bench line: the fetch table (float SUM readwrite:
+    res = dst, dst += src; 4·S bytes) and the compare table (float CSWAP:
+    res = dst, dst = src where cmp == dst; 5·S bytes) at 256 MiB per operand,
+    two rotating sets (2 GiB) so the MALL cannot serve repeats."""
+    from libfabric_amd import atomic
+    g = torch.Generator(device=dev).manual_seed(5)
+    sets = [[torch.rand(COUNT, device=dev, generator=g) for _ in range(4)] for _ in range(2)]
+    out = {}
+    for name, nb, fn in (
+            ("readwrite_float_sum", 4 * S_BYTES,
+             lambda i: atomic.readwrite(FI_SUM, FI_FLOAT, sets[i % 2][0], sets[i % 2][1],
+                                        sets[i % 2][2], COUNT, stream)),
+            ("swap_float_cswap", 5 * S_BYTES,
+             lambda i: atomic.swap(12, FI_FLOAT, sets[i % 2][0], sets[i % 2][1],
+                                   sets[i % 2][3], sets[i % 2][2], COUNT, stream))):
+        for i in range(4):
+            fn(i)
+        ms = _kernel_events(fn, 20, stream)
+        gbps = nb / (ms * 1e-3) / 1e9
+        out[name] = {"kernel_us": round(ms * 1e3, 1), "achieved_gbs": round(gbps, 1),
+                     "frac": round(gbps / PEAK_GBPS, 4)}
+    del sets
+    torch.cuda.empty_cache()
+    return out
+
+
 def extra_sizes(dev, stream, reps: int = 100, prewarm_s: float = 0.1):
     """The product float SUM combine vs size per operand (the shard sizes of
     the strong-scaled headline: 256 MiB / N): average launch duration from an
@@ -1257,6 +1284,7 @@ def main() -> None:
                 ex["config1_2rank_4kib_loopback"] = extra_config1_loopback(dev, stream)
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
                 ex["tree8_put_p2p_kernel_local"] = extra_tree_put(dev, stream)
+                ex["fetch_compare_tables_256mib"] = extra_fetch_tables(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
                 ex["e2e_host_staged_float_sum_256mib"] = extra_e2e_staged()
             if world > 1 or not args.no_extras_coll:
