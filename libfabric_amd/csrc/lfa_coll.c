@@ -936,6 +936,10 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx);
 /* Advance every in-flight host operation (ep->lock held). */
 static void host_progress_all(struct lfa_coll_ep *ep)
 {
+	/* device hops issue HIP calls from whichever thread progresses (e.g.
+	 * off_lfa's progress thread): make the domain's GPU current there */
+	if (ep->dom->device >= 0 && ep->qlen)
+		hipSetDevice(ep->dom->device);
 	for (size_t i = 0; i < ep->qlen; i++) {
 		struct hop *h = ep->q[(ep->qhead + i) % ep->qcap].hop;
 		int ret;
