@@ -333,6 +333,36 @@ def test_fetch_swap_alignment(lfa, n):
         assert np.array_equal(rd.cpu().numpy().view(np.int32)[od:od + n], want_r)
 
 
+@pytest.mark.parametrize("n", [5000, 70_001, (1 << 20) + 1234])
+def test_fetch_swap_partial_tiles(lfa, n):
+    """The LDS-staged fetch / compare body on sizes whose last workgroup tile
+    is partial (its waves take the guarded register path), float SUM
+    readwrite, ATOMIC_READ and int64 CSWAP_LT, against the oracle."""
+    rng = np.random.default_rng(n)
+    d = rng.uniform(-1, 1, n).astype(np.float32)
+    s = rng.uniform(-1, 1, n).astype(np.float32)
+    for op in (2, 10):
+        want_d, want_r = d.copy(), np.zeros(n, np.float32)
+        oracle.readwrite(op, 8, want_d, s.copy(), want_r)
+        dd, sd = _dev(d), _dev(s)
+        rd = torch.zeros_like(dd)
+        lfa.readwrite(op, 8, dd, sd, rd)
+        torch.cuda.synchronize()
+        assert np.array_equal(dd.cpu().numpy().view(np.float32), want_d), op
+        assert np.array_equal(rd.cpu().numpy().view(np.float32), want_r), op
+    d8 = rng.integers(-2**40, 2**40, n)
+    s8 = rng.integers(-2**40, 2**40, n)
+    c8 = d8 + rng.integers(-1, 2, n)
+    want_d, want_r = d8.copy(), np.zeros(n, np.int64)
+    oracle.swap(15, 6, want_d, s8.copy(), c8.copy(), want_r)
+    dd, sd, cd = _dev(d8), _dev(s8), _dev(c8)
+    rd = torch.zeros_like(dd)
+    lfa.swap(15, 6, dd, sd, cd, rd)
+    torch.cuda.synchronize()
+    assert np.array_equal(dd.cpu().numpy().view(np.int64), want_d)
+    assert np.array_equal(rd.cpu().numpy().view(np.int64), want_r)
+
+
 # ------------------------------------- size-independent properties at size ----
 
 def test_full_size_properties(lfa):
