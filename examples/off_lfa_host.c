@@ -474,7 +474,7 @@ int main(int argc, char **argv)
 		struct fid_mc *mc, *sub;
 		fi_addr_t world, setaddr;
 		float *d_x, *d_y, *h_x, *h_y;
-		int req[16], err = -1;
+		int req[20], err = -1;
 		unsigned char uid[128];
 		struct fi_cq_err_entry dummy;
 
@@ -580,6 +580,35 @@ int main(int argc, char **argv)
 		CHECK(!memcmp(h_x, h_y, n * 4), "allreduce on subset group");
 		CHECK_RC(fi_close(&sub->fid), 0);
 		CHECK_RC(fi_barrier(ep, fi_mc_addr(sub), NULL), -FI_EINVAL);
+
+		/* a join over a new set's OWN address (fabtests core_coll.c:138-168:
+		 * the set's members alone form the group, lfa_join_members), then
+		 * core_coll.c's known answer on it */
+		{
+			struct fid_av_set *own_set;
+			struct fid_mc *own_mc;
+			fi_addr_t own_addr;
+			uint64_t ka = 1234, kr = 0, *d_ka;
+
+			sattr.count = 0;
+			sattr.start_addr = 0;
+			sattr.end_addr = 0;
+			sattr.stride = 1;
+			CHECK_RC(fi_av_set(av, &sattr, &own_set, NULL), 0);
+			CHECK_RC(fi_av_set_addr(own_set, &own_addr), 0);
+			CHECK_RC(fi_join_collective(ep, own_addr, own_set, 0, &own_mc, &req[14]), 0);
+			CHECK_RC(wait_join(ep, own_mc, &req[14]), 0);
+			hipMalloc((void **)&d_ka, 2 * sizeof(uint64_t));
+			hipMemcpy(d_ka, &ka, sizeof(ka), hipMemcpyHostToDevice);
+			CHECK_RC(fi_allreduce(ep, d_ka, 1, NULL, d_ka + 1, NULL, fi_mc_addr(own_mc),
+					      FI_UINT64, FI_SUM, 0, &req[15]), 0);
+			CHECK_RC(wait_comp(ep, &req[15], NULL), 0);
+			hipMemcpy(&kr, d_ka + 1, sizeof(kr), hipMemcpyDeviceToHost);
+			CHECK(kr == 1234, "self-joined group known answer %lu", (unsigned long)kr);
+			hipFree(d_ka);
+			CHECK_RC(fi_close(&own_mc->fid), 0);
+			CHECK_RC(fi_close(&own_set->fid), 0);
+		}
 
 		CHECK_RC(fi_close(&mc->fid), 0);
 		CHECK_RC(fi_close(&set->fid), 0);
