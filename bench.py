@@ -770,6 +770,45 @@ def _rs_sweep(ep, rank, world, algo):
     return sweep
 
 
+def extra_xgmi(rank, world, device="cuda", nbytes=S_BYTES):
+    """SURVEY §8(d) config 4's bound, measured: per-GPU xGMI egress with every
+    GPU sending to every other at once (RCCL all-to-all of 256 MiB per rank:
+    (N-1)/N·S leaves each GPU), and one link alone (each rank sends 256 MiB
+    to its ring neighbour while receiving from the other).  The allreduce
+    extras report their time against the all-to-all figure: an allreduce
+    moves 2(N-1)/N·S out of every GPU."""
+    x = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    y = torch.empty_like(x)
+    out = {}
+    sync = torch.cuda.synchronize if device == "cuda" else (lambda: None)
+
+    def timed(fn, reps):
+        fn()
+        sync()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        sync()
+        return max_over_ranks(time.perf_counter() - t0, world) / reps
+
+    t = timed(lambda: dist.all_to_all_single(y, x), 5)
+    out["alltoall_egress_gbs"] = round((world - 1) / world * nbytes / t / 1e9, 1)
+    out["alltoall_ms"] = round(t * 1e3, 3)
+
+    def ring():
+        reqs = dist.batch_isend_irecv([
+            dist.P2POp(dist.isend, x, (rank + 1) % world),
+            dist.P2POp(dist.irecv, y, (rank - 1) % world)])
+        for r in reqs:
+            r.wait()
+    t = timed(ring, 5)
+    out["one_link_gbs"] = round(nbytes / t / 1e9, 1)
+    out["what"] = ("RCCL all_to_all_single and a ring send/recv of 256 MiB per rank "
+                   "(torch.distributed over RCCL); GB/s leaving each GPU")
+    return out
+
+
 def extra_collectives(rank, world, stream):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
@@ -777,8 +816,14 @@ def extra_collectives(rank, world, stream):
     algorithms (TREE, TREE_COLL, P2P) must agree bit for bit; the line says
     whether they did on this run."""
     from libfabric_amd import coll
+    xgmi = {}
+    if world > 1 and not REHEARSE:
+        try:
+            xgmi = extra_xgmi(rank, world)
+        except Exception as e:  # noqa: BLE001 — a probe must not hide the rest
+            xgmi = {"error": f"{type(e).__name__}: {e}"[:200]}
     ep = coll.Endpoint.from_torch_dist()
-    out = {}
+    out = {"xgmi_peer_copy_256mib": xgmi} if xgmi else {}
     try:
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
@@ -826,6 +871,11 @@ def extra_collectives(rank, world, stream):
                 row.update({"ms": round(t * 1e3, 3),
                             "algbw_gbs": round(S_BYTES / t / 1e9, 1),
                             "busbw_gbs": round(2 * (world - 1) / world * S_BYTES / t / 1e9, 1)})
+                if xgmi.get("alltoall_egress_gbs"):
+                    # the xGMI floor: 2(N-1)/N·S out of each GPU at the
+                    # measured all-to-all egress rate
+                    floor = 2 * (world - 1) / world * S_BYTES / (xgmi["alltoall_egress_gbs"] * 1e9)
+                    row["frac_of_xgmi_bound"] = round(floor / t, 4)
                 out[name] = row
             except Exception as e:  # noqa: BLE001 — one algorithm must not hide the rest
                 out[name] = {"error": f"{type(e).__name__}: {e}"[:200]}

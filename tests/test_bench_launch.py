@@ -100,3 +100,41 @@ def test_config3_data_distribution():
     special = np.isin(x, [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]).sum()
     assert 0.009 < special / x.size < 0.011
     assert x.min() < -(1 << 60) and x.max() > (1 << 60)   # full range
+
+
+def _xgmi_worker(rank, world, port, q):
+    try:
+        import os as _os
+        _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        import bench
+        bench.REHEARSE = True               # max over ranks on the CPU
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out = bench.extra_xgmi(rank, world, device="cpu", nbytes=1 << 20)
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_xgmi_probe_flow_on_gloo():
+    """bench.extra_xgmi's all-to-all and ring send/recv, run over gloo on
+    CPU tensors (the flow; the numbers come from RCCL on a GPU node)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+        assert res[r]["alltoall_egress_gbs"] > 0 and res[r]["one_link_gbs"] > 0
