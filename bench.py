@@ -747,7 +747,7 @@ def extra_e2e_staged(reps=3):
             "note": "pinned host dst/src, pipelined H2D / combine / D2H on two streams"}
 
 
-def _rs_sweep(ep, rank, world, algo):
+def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
     """double PROD reduce_scatter, 4 KiB .. 256 MiB per rank (configs[4])."""
     from libfabric_amd import coll
     ep.set_algo(algo)
@@ -767,6 +767,10 @@ def _rs_sweep(ep, rank, world, algo):
         t = max_over_ranks(time.perf_counter() - t0, world) / reps
         sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+        if egress_gbs and world > 1:
+            # reduce_scatter moves (N-1)/N of the bucket out of every GPU
+            floor = (world - 1) / world * nbytes / (egress_gbs * 1e9)
+            sweep[str(nbytes)]["frac_of_xgmi_bound"] = round(floor / t, 4)
     return sweep
 
 
@@ -887,11 +891,13 @@ def extra_collectives(rank, world, stream):
                 ep, rank, world)
         except Exception as e:  # noqa: BLE001
             out["reduce_scatter_host_buffers_256mib"] = {"error": f"{e}"[:200]}
-        out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE)
+        egress = xgmi.get("alltoall_egress_gbs")
+        out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE,
+                                                           egress)
         if world > 1:
             try:
                 out["reduce_scatter_double_prod_p2p"] = _rs_sweep(ep, rank, world,
-                                                                  coll.ALGO_P2P)
+                                                                  coll.ALGO_P2P, egress)
             except Exception as e:  # noqa: BLE001
                 out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
