@@ -813,6 +813,35 @@ def extra_xgmi(rank, world, device="cuda", nbytes=S_BYTES):
     return out
 
 
+def _allreduce_sweep(ep, world):
+    """float SUM allreduce time per algorithm at 64 KiB, 1 MiB and 16 MiB per
+    rank (N > 1): the data the choice of a default per size needs."""
+    from libfabric_amd import coll
+    out = {}
+    for nbytes, reps in ((64 << 10, 50), (1 << 20, 30), (16 << 20, 10)):
+        n = nbytes // 4
+        x = torch.rand(n, device="cuda")
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        row = {}
+        for name, algo in (("tree", coll.ALGO_TREE), ("tree_coll", coll.ALGO_TREE_COLL),
+                           ("p2p", coll.ALGO_P2P), ("rccl", coll.ALGO_RCCL)):
+            try:
+                ep.set_algo(algo)
+                ep.wait(ep.allreduce(x, y, n, 8, 2))
+                barrier(world)
+                t0 = time.perf_counter()
+                ctxs = [ep.allreduce(x, y, n, 8, 2) for _ in range(reps)]
+                ep.wait(ctxs[-1])
+                t = max_over_ranks(time.perf_counter() - t0, world) / reps
+                row[name + "_us"] = round(t * 1e6, 1)
+            except Exception as e:  # noqa: BLE001
+                row[name + "_error"] = f"{e}"[:120]
+        out[str(nbytes)] = row
+    ep.set_algo(coll.ALGO_TREE)
+    return out
+
+
 def extra_collectives(rank, world, stream):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
@@ -892,6 +921,8 @@ def extra_collectives(rank, world, stream):
         except Exception as e:  # noqa: BLE001
             out["reduce_scatter_host_buffers_256mib"] = {"error": f"{e}"[:200]}
         egress = xgmi.get("alltoall_egress_gbs")
+        if world > 1:
+            out["allreduce_float_sum_by_size_us"] = _allreduce_sweep(ep, world)
         out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE,
                                                            egress)
         if world > 1:
