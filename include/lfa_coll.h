@@ -68,7 +68,8 @@ enum lfa_coll_algo {
 	/* LFA_ALGO_TREE with the block exchange and the block all-gather done
 	 * by RCCL's own ncclAllToAll / in-place ncclAllGather instead of
 	 * grouped ncclSend/ncclRecv (when count divides evenly over the
-	 * group; otherwise identical to LFA_ALGO_TREE).  Same bits. */
+	 * group), and small allreduces gathering every input with one
+	 * ncclAllGather; otherwise identical to LFA_ALGO_TREE.  Same bits. */
 	LFA_ALGO_TREE_COLL = 3,
 	/* direct xGMI peer access, same tree and bits as LFA_ALGO_TREE: each
 	 * rank stages its input in a symmetric workspace whose peers map it

@@ -582,6 +582,27 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 			   !(coll == LFA_ALLREDUCE &&
 			     bytes * (size_t)n <= LFA_SMALL_AG_BYTES);
 
+		if (coll == LFA_ALLREDUCE && n > 1 && n <= LFA_TREE_MAX &&
+		    bytes * (size_t)n <= LFA_SMALL_AG_BYTES) {
+			uint32_t first;
+
+			/* small: every rank's whole input through ONE RCCL
+			 * allgather (TMP slot k <- rank k), then the tree over the
+			 * slots in rank order — the grouped-send form's bits */
+			p_coll(&p, LFA_STEP_ALLGATHER, ref(LFA_BUF_TMP, 0),
+			       ref(LFA_BUF_SEND, 0), bytes);
+			first = p_tree_begin(&p);
+			for (int k = 0; k < n; k++)
+				p_tree_src(&p, ref(LFA_BUF_TMP, (uint64_t)k * bytes));
+			p_tree_end(&p, first, ref(LFA_BUF_RESULT, 0), count);
+			*tmp_bytes = (size_t)n * bytes;
+			*nsteps = p.n;
+			*nrefs = p.nr;
+			if (!steps || !refs)
+				return 0;
+			return (p.n > p.cap || p.nr > p.rcap) ? -LFA_ETOOSMALL : 0;
+		}
+
 		if (even && (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER)) {
 			uint32_t first;
 
