@@ -936,8 +936,10 @@ def extra_collectives(rank, world, stream):
         b = torch.empty_like(a)
         torch.cuda.synchronize()
         for name, algo in (("allreduce_4kib_float_sum_us", coll.ALGO_TREE),
-                           ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P)):
-            if algo == coll.ALGO_P2P and world == 1:
+                           ("allreduce_4kib_float_sum_tree_coll_us", coll.ALGO_TREE_COLL),
+                           ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P),
+                           ("allreduce_4kib_float_sum_rccl_us", coll.ALGO_RCCL)):
+            if algo != coll.ALGO_TREE and world == 1:
                 continue
             ep.set_algo(algo)
             ep.wait(ep.allreduce(a, b, 1024, 8, 2))
