@@ -131,6 +131,63 @@ def test_loopback_16_ranks_int_bitwise(coll):
             assert np.array_equal(rd[r].cpu().numpy(), want.view(np.uint8))
 
 
+@pytest.fixture(scope="module")
+def full_size_sum():
+    """BASELINE.json configs[3]'s shape on loopback: 8 ranks, 256 MiB of
+    float32 per rank, FI_SUM. The C oracle (oracle_allreduce, the
+    coll_coll.c:364-420 schedule) finishes this in seconds."""
+    n, count = 8, (256 << 20) // 4
+    sends = _inputs(8, n, count, 2026)
+    return n, count, sends, oracle.allreduce(2, 8, sends)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+def test_loopback_allreduce_full_size(coll, full_size_sum, algo):
+    """Full-size parity: every algorithm (TREE, RD, TREE_COLL, P2P) returns
+    the oracle's bits on every rank at 256 MiB per rank, so the per-size
+    choices bench.py measures (sweep rows) never change a result."""
+    n, count, sends, want = full_size_sum
+    sd = [_dev(s) for s in sends]
+    rd = [torch.empty_like(x) for x in sd]
+    coll.loopback(ALLREDUCE, algo, n, -1, 8, 2, count, sd, rd)
+    torch.cuda.synchronize()
+    del sd
+    for r in range(n):
+        assert_parity(8, rd[r].cpu().numpy(), want[r], f"algo={algo} r={r}")
+
+
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+def test_loopback_prod_reduce_scatter_full_size(coll, algo):
+    """BASELINE.json configs[4]'s largest bucket: double FI_PROD
+    reduce_scatter, 256 MiB per rank, 8 ranks, bit-exact per block."""
+    n, dt, op = 8, 9, 3
+    count = (256 << 20) // 8
+    sends = _inputs(dt, n, count, 4242, 0.999, 1.001)
+    want = oracle.reduce_scatter(op, dt, sends)
+    sd = [_dev(s) for s in sends]
+    rd = [torch.empty(coll.block(count, n, r)[1] * 8, dtype=torch.uint8,
+                      device=DEV) for r in range(n)]
+    coll.loopback(REDUCE_SCATTER, algo, n, -1, dt, op, count, sd, rd)
+    torch.cuda.synchronize()
+    for r in range(n):
+        assert_parity(dt, rd[r].cpu().numpy(), want[r], f"algo={algo} rs r={r}")
+
+
+def test_loopback_int64_min_bor_64mib(coll):
+    """BASELINE.json configs[2]'s dtype/ops and size through the 8-rank
+    allreduce: int64 FI_MIN and FI_BOR over 64 MiB, bit-exact."""
+    n, dt, count = 8, 6, (64 << 20) // 8
+    for op in (0, 6):
+        sends = _inputs(dt, n, count, 7 + op)
+        want = oracle.allreduce(op, dt, sends)[0]
+        sd = [_dev(s) for s in sends]
+        rd = [torch.empty_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, 0, n, -1, dt, op, count, sd, rd)
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert np.array_equal(rd[r].cpu().numpy(), want.view(np.uint8)), (op, r)
+
+
 # ------------------------------------------------ RCCL domain, world = 1 ----
 
 class _ReadyBuffers:
