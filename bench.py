@@ -40,6 +40,7 @@ import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 import torch
@@ -105,6 +106,73 @@ def launch_ranks(n: int, cmd: list[str], timeout_s: float | None = None) -> int:
     for p in procs:
         p.wait()
     return rc
+
+
+_CHILD = None                          # the running isolated child (watchdog kills it)
+_ISO_SEQ = [0]
+
+
+def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float) -> dict:
+    """Run `cmd` as this rank's member of a NEW N-rank job (fresh rendezvous
+    port, same RANK / LOCAL_RANK / WORLD_SIZE) in a child process, and return
+    rank 0's last JSON line from it.
+
+    The N > 1 provider extras run this way: they are the first run of the
+    RCCL / xGMI / IPC transports on N GPUs, and a GPU fault or crash there
+    aborts its process — here the child, not the rank that holds the headline,
+    so the one JSON line is still printed.  The ranks coordinate through the
+    job's store only (no GPU collective): rank 0 publishes the port, and a
+    rank whose child fails or overruns posts it, so every rank stops its child
+    (by PID) instead of leaving it waiting in a collective.  Each rank returns
+    only after its own child has exited."""
+    import subprocess
+    import tempfile
+    global _CHILD
+    store = dist.distributed_c10d._get_default_store()
+    _ISO_SEQ[0] += 1
+    key = f"lfa_iso{_ISO_SEQ[0]}"
+    if rank == 0:
+        store.set(key + "_port", str(_free_port()))
+    port = store.get(key + "_port").decode()
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=port, LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)),
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    status = "ok"
+    with tempfile.TemporaryFile("w+") as out:
+        p = _CHILD = subprocess.Popen(cmd, env=env, stdout=out)
+        deadline = time.time() + budget_s
+        while True:
+            rc = p.poll()
+            if rc is not None:
+                if rc != 0:
+                    status = f"rank {rank}: child exited with code {rc}"
+                    store.set(key + "_fail", status)
+                break
+            if store.check([key + "_fail"]):
+                status = "stopped: " + store.get(key + "_fail").decode()
+                p.kill()
+                p.wait()
+                break
+            if time.time() > deadline:
+                status = f"rank {rank}: child overran {budget_s:.0f} s"
+                store.set(key + "_fail", status)
+                p.kill()
+                p.wait()
+                break
+            time.sleep(0.1)
+        _CHILD = None
+        out.seek(0)
+        lines = [x for x in out.read().splitlines() if x.startswith("{")]
+    res = {}
+    if lines:
+        try:
+            res = json.loads(lines[-1])
+        except ValueError:
+            status += "; last line unparsable"
+    if status != "ok":
+        res["isolated_status"] = status
+    return res
 
 
 def check_world(expected: int, world: int) -> None:
@@ -842,21 +910,24 @@ def _allreduce_sweep(ep, world):
     return out
 
 
-def extra_collectives(rank, world, stream):
+def extra_collectives(rank, world, stream, emit=None):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
     (liblfa_coll.so).  algbw = S/t, busbw = 2(N-1)/N·S/t.  The exact
     algorithms (TREE, TREE_COLL, P2P) must agree bit for bit; the line says
-    whether they did on this run."""
+    whether they did on this run.  `emit(out)` is called after each section
+    (the isolated child prints the rows collected so far)."""
     from libfabric_amd import coll
+    emit = emit or (lambda _o: None)
     xgmi = {}
     if world > 1 and not REHEARSE:
         try:
             xgmi = extra_xgmi(rank, world)
         except Exception as e:  # noqa: BLE001 — a probe must not hide the rest
             xgmi = {"error": f"{type(e).__name__}: {e}"[:200]}
-    ep = coll.Endpoint.from_torch_dist()
     out = {"xgmi_peer_copy_256mib": xgmi} if xgmi else {}
+    emit(out)
+    ep = coll.Endpoint.from_torch_dist()
     try:
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
@@ -912,6 +983,7 @@ def extra_collectives(rank, world, stream):
                 out[name] = row
             except Exception as e:  # noqa: BLE001 — one algorithm must not hide the rest
                 out[name] = {"error": f"{type(e).__name__}: {e}"[:200]}
+            emit(out)
         del ref
         ep.set_algo(coll.ALGO_TREE)
         out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
@@ -920,17 +992,21 @@ def extra_collectives(rank, world, stream):
                 ep, rank, world)
         except Exception as e:  # noqa: BLE001
             out["reduce_scatter_host_buffers_256mib"] = {"error": f"{e}"[:200]}
+        emit(out)
         egress = xgmi.get("alltoall_egress_gbs")
         if world > 1:
             out["allreduce_float_sum_by_size_us"] = _allreduce_sweep(ep, world)
+            emit(out)
         out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE,
                                                            egress)
+        emit(out)
         if world > 1:
             try:
                 out["reduce_scatter_double_prod_p2p"] = _rs_sweep(ep, rank, world,
                                                                   coll.ALGO_P2P, egress)
             except Exception as e:  # noqa: BLE001
                 out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
+            emit(out)
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
         a = torch.rand(1024, device="cuda")
         b = torch.empty_like(a)
@@ -951,6 +1027,7 @@ def extra_collectives(rank, world, stream):
             out[name] = round(t * 1e6, 1)
         if rank == 0:
             out["cpu_model_allreduce_256mib"] = cpu_model_allreduce(world)
+        emit(out)
     finally:
         ep.close()
     return out
@@ -1215,7 +1292,8 @@ def main() -> None:
     ap.add_argument("--tune-treeput", action="store_true")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
-    ap.add_argument("--only-extra", default="", help="run one extra (dev): tree_put, host_rs")
+    ap.add_argument("--only-extra", default="", help="run one extra: tree_put, host_rs, config3, sizes (dev); "
+                    "coll (the isolated N>1 provider extras, started by run_isolated)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
                     help="skip the provider (RCCL) extras at N=1")
@@ -1277,6 +1355,22 @@ def main() -> None:
     lib()  # no fallback: raises if liblfa.so is missing
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
+    if args.only_extra == "coll":
+        # the isolated child of run_isolated: the provider extras only
+        def show(o):
+            if rank == 0:
+                print(json.dumps(o), flush=True)
+        try:
+            extra_collectives(rank, world, stream, show)
+        except Exception as e:  # noqa: BLE001
+            show({"error": f"{type(e).__name__}: {e}"[:300]})
+        finally:
+            if world > 1:
+                bye = threading.Timer(60.0, lambda: os._exit(0))
+                bye.daemon = True
+                bye.start()
+                dist.destroy_process_group()
+        return
 
     # Headline: ONE 256 MiB buffer pair, sharded over the N GPUs (strong).
     off, cnt = shard_of(COUNT, world, rank)
@@ -1342,18 +1436,22 @@ def main() -> None:
 
     # Extras (never the headline).  A watchdog prints the line collected so
     # far and exits if an extra stalls, so the metric is always reported.
-    import threading
-
     def _emit(note=None):
         if note:
             line.setdefault("extras", {})["status"] = note
         if rank == 0:
             print(json.dumps(line), flush=True)
 
+    def _overrun():
+        if _CHILD is not None:
+            _CHILD.kill()
+        _emit("extras timed out")
+        os._exit(0)
+
     if not args.no_extras:
         torch.cuda.empty_cache()
-        wd = threading.Timer(args.extras_timeout, lambda: (_emit("extras timed out"),
-                                                           os._exit(0)))
+        t_extras = time.time()
+        wd = threading.Timer(args.extras_timeout, _overrun)
         wd.daemon = True
         wd.start()
         ex = line.setdefault("extras", {})
@@ -1376,7 +1474,14 @@ def main() -> None:
                 ex["fetch_compare_tables_256mib"] = extra_fetch_tables(dev, stream)
                 ex["e2e_host_float_sum_256mib"] = extra_e2e_host(dev, stream)
                 ex["e2e_host_staged_float_sum_256mib"] = extra_e2e_staged()
-            if world > 1 or not args.no_extras_coll:
+            if world > 1:
+                # first N-GPU run of the transports: in a child job, so a
+                # fault there cannot take the headline with it
+                budget = args.extras_timeout - (time.time() - t_extras) - 20.0
+                ex.update(run_isolated(
+                    [sys.executable, os.path.abspath(__file__), "--gpus", str(world),
+                     "--only-extra", "coll"], rank, world, max(budget, 10.0)))
+            elif not args.no_extras_coll:
                 ex.update(extra_collectives(rank, world, stream))
         except Exception as e:  # noqa: BLE001 — extras must not hide the metric
             ex["error"] = f"{type(e).__name__}: {e}"[:300]

@@ -138,3 +138,82 @@ def test_xgmi_probe_flow_on_gloo():
     for r in range(2):
         assert isinstance(res[r], dict), res[r]
         assert res[r]["alltoall_egress_gbs"] > 0 and res[r]["one_link_gbs"] > 0
+
+
+_ISO_CHILD = (
+    "import json, os, sys, time\n"
+    "mode, rank = sys.argv[1], int(os.environ['RANK'])\n"
+    "if mode == 'crash' and rank == 1:\n"
+    "    os.abort()\n"
+    "if mode in ('crash', 'hang'):\n"
+    "    time.sleep(120)\n"
+    "import torch, torch.distributed as dist\n"
+    "dist.init_process_group('gloo')\n"
+    "t = torch.tensor([rank + 1.0])\n"
+    "dist.all_reduce(t)\n"
+    "if rank == 0:\n"
+    "    print(json.dumps({'partial': 1}), flush=True)\n"
+    "    print(json.dumps({'sum': float(t), 'port': os.environ['MASTER_PORT'],\n"
+    "                      'elastic': [k for k in os.environ if k.startswith('TORCHELASTIC_')]}),\n"
+    "          flush=True)\n"
+    "dist.destroy_process_group()\n"
+)
+
+
+def _iso_worker(rank, world, port, mode, q):
+    try:
+        import os as _os
+        _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        import bench
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # as under torch.distributed.run: the child must not inherit it
+        _os.environ["TORCHELASTIC_USE_AGENT_STORE"] = "True"
+        t0 = time.time()
+        out = bench.run_isolated([sys.executable, "-c", _ISO_CHILD, mode], rank, world,
+                                 budget_s=20.0)
+        dt = time.time() - t0
+        dist.destroy_process_group()
+        q.put((rank, (out, dt)))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("mode", ["ok", "crash", "hang"])
+def test_isolated_extras_child_job(mode):
+    """bench.run_isolated (the N>1 provider extras' child job) over gloo:
+    a fresh rendezvous that works without the elastic agent's store; rank 0's
+    last JSON line comes back; a child that aborts on one rank stops every
+    rank's child at once; a hung child is stopped at the budget."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_iso_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=120) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        assert isinstance(res[r], tuple), res[r]
+    (out0, dt0), (out1, dt1) = res[0], res[1]
+    if mode == "ok":
+        assert out0["sum"] == 3.0 and out0["elastic"] == [] and out0["port"] != str(port)
+        assert "isolated_status" not in out0 and out1 == {}
+    elif mode == "crash":
+        assert "code" in out1["isolated_status"]
+        assert "stopped" in out0["isolated_status"]
+        assert max(dt0, dt1) < 15
+    else:
+        assert "overran" in out0["isolated_status"] or "stopped" in out0["isolated_status"]
+        assert max(dt0, dt1) < 40
