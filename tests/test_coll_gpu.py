@@ -131,6 +131,29 @@ def test_loopback_16_ranks_int_bitwise(coll):
             assert np.array_equal(rd[r].cpu().numpy(), want.view(np.uint8))
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+def test_loopback_reference_known_answers(coll, algo):
+    """prov/cxi/test/multinode/test_coll.c's fi_allreduce checks, every rank
+    count 2..8 on the kernels: int64 SUM of 4r+v exact (:722-792), double SUM
+    of (4r+v)/1000 within 1e-8 (:795-865)."""
+    for n in range(2, 9):
+        sd = [_dev(np.array([4 * r + v for v in range(4)], np.int64)) for r in range(n)]
+        rd = [torch.zeros_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, algo, n, -1, 6, 2, 4, sd, rd)
+        torch.cuda.synchronize()
+        comp = [sum(4 * r + v for r in range(n)) for v in range(4)]
+        for r in range(n):
+            assert rd[r].cpu().numpy().view(np.int64).tolist() == comp, (n, r)
+        sd = [_dev(np.array([(4 * r + v) / 1000.0 for v in range(4)])) for r in range(n)]
+        rd = [torch.zeros_like(x) for x in sd]
+        coll.loopback(ALLREDUCE, algo, n, -1, 9, 2, 4, sd, rd)
+        torch.cuda.synchronize()
+        comp = [sum((4 * r + v) / 1000.0 for r in range(n)) for v in range(4)]
+        for r in range(n):
+            got = rd[r].cpu().numpy().view(np.float64)
+            assert all(abs(a - b) <= 1e-8 for a, b in zip(got, comp)), (n, r)
+
+
 @pytest.fixture(scope="module")
 def full_size_sum():
     """BASELINE.json configs[3]'s shape on loopback: 8 ranks, 256 MiB of

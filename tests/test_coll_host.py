@@ -198,6 +198,34 @@ def _joins_members(ep, rank, world):
     ep.wait(ep.barrier())
 
 
+def _reference_known_answers(ep, rank, world, coll):
+    """The reference's own acceptance checks for fi_allreduce / fi_broadcast /
+    fi_barrier, from prov/cxi/test/multinode/test_coll.c (a provider's test of
+    the same fi_collective API): int64 SUM of data[4r+v] = 4r+v, exact
+    (:722-792); double SUM of (4r+v)/1000 within 1e-8 (:795-865); a 4-word
+    uint64 broadcast from every root (:656-717); barrier (:608-654)."""
+    for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL, coll.ALGO_P2P):
+        ep.set_algo(algo)
+        data = np.array([4 * rank + v for v in range(4)], np.int64)
+        res = np.zeros(4, np.int64)
+        ep.wait(ep.allreduce(data, res, 4, 6, 2))
+        comp = [sum(4 * r + v for r in range(world)) for v in range(4)]
+        assert res.tolist() == comp, ("isum", algo)
+        data = np.array([(4 * rank + v) / 1000.0 for v in range(4)])
+        res = np.zeros(4)
+        ep.wait(ep.allreduce(data, res, 4, 9, 2))
+        comp = [sum((4 * r + v) / 1000.0 for r in range(world)) for v in range(4)]
+        assert all(abs(a - b) <= 1e-8 for a, b in zip(res, comp)), ("dsum", algo)
+        for i in range(2):
+            for root in range(world):
+                want = np.array([i, root, 0x13579bdf, 0x10101010], np.uint64)
+                buf = want.copy() if rank == root else np.zeros(4, np.uint64)
+                ep.wait(ep.broadcast(buf, 4, root, 7))
+                assert np.array_equal(buf, want), ("broadcast", algo, root)
+        ep.wait(ep.barrier())
+    ep.set_algo(coll.ALGO_TREE)
+
+
 def _worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -208,6 +236,7 @@ def _worker(rank, world, port, q):
         ep = coll.HostEndpoint(rank, world, xfer)
         try:
             _collectives(ep, rank, world, oracle, coll)
+            _reference_known_answers(ep, rank, world, coll)
             _overlap(ep, rank, world, oracle)
             _joins(ep, rank, world, oracle)
             _joins_members(ep, rank, world)
@@ -328,7 +357,7 @@ def test_transport_pushback_and_failure():
         assert results.get(r) == "ok", results.get(r)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5])
 def test_c_executor_across_processes(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
