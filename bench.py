@@ -881,19 +881,19 @@ def extra_xgmi(rank, world, device="cuda", nbytes=S_BYTES):
     return out
 
 
-def _allreduce_sweep(ep, world):
+def _allreduce_sweep(ep, world, algos, out=None):
     """float SUM allreduce time per algorithm at 64 KiB, 1 MiB and 16 MiB per
-    rank (N > 1): the data the choice of a default per size needs."""
+    rank (N > 1): the data the choice of a default per size needs.  `algos`:
+    (name, algo) pairs; rows merge into `out`."""
     from libfabric_amd import coll
-    out = {}
+    out = {} if out is None else out
     for nbytes, reps in ((64 << 10, 50), (1 << 20, 30), (16 << 20, 10)):
         n = nbytes // 4
         x = torch.rand(n, device="cuda")
         y = torch.empty_like(x)
         torch.cuda.synchronize()
-        row = {}
-        for name, algo in (("tree", coll.ALGO_TREE), ("tree_coll", coll.ALGO_TREE_COLL),
-                           ("p2p", coll.ALGO_P2P), ("rccl", coll.ALGO_RCCL)):
+        row = out.setdefault(str(nbytes), {})
+        for name, algo in algos:
             try:
                 ep.set_algo(algo)
                 ep.wait(ep.allreduce(x, y, n, 8, 2))
@@ -905,7 +905,6 @@ def _allreduce_sweep(ep, world):
                 row[name + "_us"] = round(t * 1e6, 1)
             except Exception as e:  # noqa: BLE001
                 row[name + "_error"] = f"{e}"[:120]
-        out[str(nbytes)] = row
     ep.set_algo(coll.ALGO_TREE)
     return out
 
@@ -994,37 +993,50 @@ def extra_collectives(rank, world, stream, emit=None):
             out["reduce_scatter_host_buffers_256mib"] = {"error": f"{e}"[:200]}
         emit(out)
         egress = xgmi.get("alltoall_egress_gbs")
+        # the P2P forms (cross-GPU IPC mappings + system-scope kernels) come
+        # last in every group below: if one stalled, the rows before it are out
+        sizes = {}
         if world > 1:
-            out["allreduce_float_sum_by_size_us"] = _allreduce_sweep(ep, world)
+            out["allreduce_float_sum_by_size_us"] = _allreduce_sweep(
+                ep, world, (("tree", coll.ALGO_TREE), ("tree_coll", coll.ALGO_TREE_COLL),
+                            ("rccl", coll.ALGO_RCCL)), sizes)
             emit(out)
         out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE,
                                                            egress)
         emit(out)
-        if world > 1:
-            try:
-                out["reduce_scatter_double_prod_p2p"] = _rs_sweep(ep, rank, world,
-                                                                  coll.ALGO_P2P, egress)
-            except Exception as e:  # noqa: BLE001
-                out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
-            emit(out)
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
         a = torch.rand(1024, device="cuda")
         b = torch.empty_like(a)
         torch.cuda.synchronize()
         for name, algo in (("allreduce_4kib_float_sum_us", coll.ALGO_TREE),
                            ("allreduce_4kib_float_sum_tree_coll_us", coll.ALGO_TREE_COLL),
-                           ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P),
-                           ("allreduce_4kib_float_sum_rccl_us", coll.ALGO_RCCL)):
+                           ("allreduce_4kib_float_sum_rccl_us", coll.ALGO_RCCL),
+                           ("allreduce_4kib_float_sum_p2p_us", coll.ALGO_P2P)):
             if algo != coll.ALGO_TREE and world == 1:
                 continue
-            ep.set_algo(algo)
-            ep.wait(ep.allreduce(a, b, 1024, 8, 2))
-            barrier(world)
-            t0 = time.perf_counter()
-            for _ in range(200):
+            try:
+                ep.set_algo(algo)
                 ep.wait(ep.allreduce(a, b, 1024, 8, 2))
-            t = max_over_ranks(time.perf_counter() - t0, world) / 200
-            out[name] = round(t * 1e6, 1)
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(200):
+                    ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+                t = max_over_ranks(time.perf_counter() - t0, world) / 200
+                out[name] = round(t * 1e6, 1)
+            except Exception as e:  # noqa: BLE001
+                out[name] = {"error": f"{e}"[:120]}
+            emit(out)
+        ep.set_algo(coll.ALGO_TREE)
+        if world > 1:
+            _allreduce_sweep(ep, world, (("p2p", coll.ALGO_P2P),), sizes)
+            emit(out)
+            try:
+                out["reduce_scatter_double_prod_p2p"] = _rs_sweep(ep, rank, world,
+                                                                  coll.ALGO_P2P, egress)
+            except Exception as e:  # noqa: BLE001
+                out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
+            ep.set_algo(coll.ALGO_TREE)
+            emit(out)
         if rank == 0:
             out["cpu_model_allreduce_256mib"] = cpu_model_allreduce(world)
         emit(out)
