@@ -100,10 +100,12 @@ def build_coll(verbose: bool = False) -> str | None:
     src = os.path.join(CSRC, "lfa_coll.c")
     if not os.path.exists(src):
         return None
-    srcs = [src, os.path.join(CSRC, "lfa_coll_plan.c")]   # executor + planner
+    # API + groups, executor + transports, planner, single-GPU loopback
+    srcs = [src] + [os.path.join(CSRC, f) for f in
+                    ("lfa_coll_exec.c", "lfa_coll_plan.c", "lfa_coll_loopback.c")]
     hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "lfa_atomic.h"),
             os.path.join(INC, "lfa_fabric.h"), os.path.join(CSRC, "lfa_coll_plan.h"),
-            LIB_LFA]
+            os.path.join(CSRC, "lfa_coll_int.h"), LIB_LFA]
     if _newer(LIB_COLL, srcs + hdrs):
         # Plain C (the reference's host language), calling HIP's and RCCL's
         # C APIs; no HIP device code in this library.

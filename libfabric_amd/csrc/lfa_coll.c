@@ -36,121 +36,11 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
+#include "lfa_coll_int.h"
 
-#include "lfa_atomic.h"
-#include "lfa_coll.h"
-
-#define LFA_MAX_GROUP_ID 256            /* OFI_MAX_GROUP_ID, ofi_coll.h:44 */
-#define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
 /* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
  * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
 #define LFA_DEFAULT_CHUNK (32u << 20)
-
-#include "lfa_coll_plan.h"
-
-/* ====================================================================== */
-/* device helpers                                                          */
-/* ====================================================================== */
-
-/* Where a plan's refs point for one execution: the operation's buffers and,
- * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
- * (IN region at 0, OUT region at `region`). */
-struct xctx {
-	void *base[3];          /* SEND, RESULT, TMP */
-	char *const *sym;       /* [group rank] */
-	size_t region;
-};
-
-static void *resolve(const struct xctx *x, struct lfa_ref r)
-{
-	if (r.buf == LFA_BUF_SYM_IN)
-		return x->sym[r.rank] + r.off;
-	if (r.buf == LFA_BUF_SYM_OUT)
-		return x->sym[r.rank] + x->region + r.off;
-	return (char *)x->base[r.buf] + r.off;
-}
-
-#define LFA_COPY_KERNEL_BYTES ((size_t)16 << 20)
-
-/* Non-communication step on `stream`. */
-static int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
-		     const struct xctx *x, enum lfa_op op,
-		     enum lfa_datatype dt, hipStream_t stream)
-{
-	switch (s->type) {
-	case LFA_STEP_REDUCE:
-		return lfa_atomic_write_async(op, dt, resolve(x, s->dst),
-					      resolve(x, s->src), s->count,
-					      stream);
-	case LFA_STEP_TREE: {
-		const void *srcs[LFA_TREE_MAX];
-
-		if (s->nsrc > LFA_TREE_MAX)
-			return -LFA_EINVAL;
-		for (uint32_t k = 0; k < s->nsrc; k++)
-			srcs[k] = resolve(x, refs[s->first + k]);
-		return lfa_reduce_tree_async(op, dt, resolve(x, s->dst), srcs,
-					     (int)s->nsrc, s->count, stream);
-	}
-	case LFA_STEP_TREE_PUT: {
-		const void *srcs[LFA_TREE_MAX];
-		void *dsts[LFA_PUT_MAX];
-
-		if (s->nsrc > LFA_TREE_MAX || s->peer < 0 || s->peer + 1 > LFA_PUT_MAX)
-			return -LFA_EINVAL;
-		for (uint32_t k = 0; k < s->nsrc; k++)
-			srcs[k] = resolve(x, refs[s->first + k]);
-		dsts[0] = resolve(x, s->dst);
-		for (int j = 0; j < s->peer; j++)
-			dsts[1 + j] = resolve(x, refs[s->first + s->nsrc + (uint32_t)j]);
-		return lfa_reduce_tree_put_async(op, dt, dsts, 1 + s->peer, srcs,
-						 (int)s->nsrc, s->count, stream);
-	}
-	case LFA_STEP_COPY:
-		if (s->src.buf == LFA_BUF_SYM_IN || s->src.buf == LFA_BUF_SYM_OUT) {
-			/* bytes peers pushed over xGMI into this rank's workspace
-			 * (the P2P unstage): through the P2P kernel's system-scope
-			 * loads, which no cached copy of the line can satisfy */
-			void *d = resolve(x, s->dst);
-			const void *sp = resolve(x, s->src);
-
-			return lfa_reduce_tree_put_async(LFA_BOR, LFA_UINT8, &d, 1, &sp, 1,
-							 s->count, stream);
-		}
-		/* large copies through the write table's ATOMIC_WRITE row (the
-		 * LDS-DMA body, no dst read): 83.3 vs 98.8 us at 256 MiB and 12.3
-		 * vs 14.5 us at 32 MiB against hipMemcpyAsync D2D, which stays
-		 * ahead below (4.95 vs 5.43 us at 4 MiB; tools/probe_copy.py,
-		 * profiles/r02_probe_copy.log).  COPY items never touch a peer's
-		 * memory (the planner's copies stay in this rank's buffers). */
-		if (s->count >= LFA_COPY_KERNEL_BYTES)
-			return lfa_atomic_write_async(LFA_ATOMIC_WRITE, LFA_UINT8,
-						      resolve(x, s->dst), resolve(x, s->src),
-						      s->count, stream);
-		return hipMemcpyAsync(resolve(x, s->dst), resolve(x, s->src),
-				      s->count, hipMemcpyDeviceToDevice,
-				      stream) == hipSuccess ? 0 : -LFA_EIO;
-	default:
-		return -LFA_EINVAL;
-	}
-}
-
-/* Does the plan address the symmetric workspace? */
-static int plan_uses_sym(const struct lfa_step *st, size_t nsteps)
-{
-	for (size_t i = 0; i < nsteps; i++)
-		if (st[i].type == LFA_STEP_BARRIER || st[i].type == LFA_STEP_TREE_PUT)
-			return 1;
-	return 0;
-}
-
-/* Bytes of one symmetric-workspace region for `count` elements. */
-static size_t sym_region(size_t count, size_t esz)
-{
-	return (count * esz + 255) & ~(size_t)255;
-}
 
 static int is_device_ptr(const void *p)
 {
@@ -165,85 +55,6 @@ static int is_device_ptr(const void *p)
 	return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
-/* ====================================================================== */
-/* domain / endpoint                                                       */
-/* ====================================================================== */
-
-struct lfa_coll_mc {
-	struct lfa_coll_ep *ep;
-	ncclComm_t comm;
-	int owns_comm;
-	int rank, size;
-	uint16_t group_id;
-	uint16_t seq;
-	int is_world;
-	/* host (peer-transfer) domains: group rank -> domain rank, NULL for
-	 * the world group (prov/coll's av_set fi_addr_array) */
-	int *members;
-	/* join in flight */
-	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
-	void *join_context;
-	/* LFA_ALGO_P2P symmetric workspace: `sym_local` (2 regions, hipMalloc,
-	 * IPC-exported) and every member's as mapped here (sym[rank] = local) */
-	char *sym_local;
-	char **sym;
-	size_t sym_region;
-};
-
-struct lfa_coll_domain {
-	int device, rank, nranks;
-	ncclComm_t comm;
-	int host;                       /* peer-transfer domain (host memory) */
-	struct lfa_peer_xfer_ops xops;
-	void *xctx;
-};
-
-struct hop;
-
-struct pending {
-	hipEvent_t ev;          /* device domains */
-	struct hop *hop;        /* host domains: the operation's state */
-	void *context;
-	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
-	struct lfa_coll_mc *mc;
-};
-
-struct lfa_coll_ep {
-	struct lfa_coll_domain *dom;
-	pthread_mutex_t lock;       /* queue, CQ/EQ, stream enqueue order */
-	pthread_mutex_t comm_lock;  /* communicator management (split/destroy,
-				     * P2P workspace exchange), in call order */
-	hipStream_t stream;         /* executor stream (RCCL + kernels) */
-	hipStream_t copy_stream;    /* host staging copies, H2D */
-	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
-				     * PCIe direction runs concurrently) */
-	enum lfa_coll_algo algo;
-	size_t chunk;
-	void *ws;                   /* device workspace */
-	size_t ws_size;
-	void *hs[2];                /* device staging for host buffers */
-	size_t hs_size;
-	uint64_t *barrier_host;     /* pinned ~rank for barrier */
-	void *barrier_dev;          /* 2 x uint64 */
-	void *ctl_dev;              /* P2P handle exchange, nranks records */
-	void *ctl_host;
-	uint8_t cid_mask[LFA_CID_BYTES];
-	struct lfa_coll_mc world;
-	hipEvent_t evpool[64];      /* recycled completion events */
-	int nev;
-	struct plan_cache {         /* last schedules built, keyed by shape */
-		int valid, coll, algo, rank, n, root;
-		size_t count, esz;
-		struct plan pl;
-	} pc[8];
-	unsigned pc_next;
-	struct pending *q;          /* FIFO ring of in-flight ops */
-	size_t qcap, qhead, qlen;
-	struct lfa_cq_err_entry err;
-	int have_err;
-	struct { uint32_t event; struct lfa_eq_entry entry; } eq[64];
-	size_t eqh, eqn;
-};
 
 static void p2p_release(struct lfa_coll_mc *mc);
 
@@ -348,9 +159,6 @@ static void ep_release(struct lfa_coll_ep *ep)
 	pthread_mutex_destroy(&ep->comm_lock);
 	free(ep);
 }
-
-/* Bytes of one P2P handle-exchange record (struct sym_rec, below). */
-#define LFA_SYM_REC_BYTES 80
 
 int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 {
@@ -600,284 +408,6 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 	return 0;
 }
 
-/* ---------------------------------------------------------------------- */
-/* host (peer-transfer) executor                                          */
-/* ---------------------------------------------------------------------- */
-
-/*
- * The executor.  A schedule (struct plan) runs through ONE loop,
- * xrun_advance, whatever carries its transfers; a transport table (xport)
- * supplies the transfers and the local items:
- *   xport_rccl  device buffers: SEND/RECV groups are RCCL grouped
- *               ncclSend/ncclRecv, ALLTOALL/ALLGATHER/BARRIER RCCL
- *               collectives, REDUCE/TREE/TREE_PUT/COPY gfx950 kernels — all
- *               enqueued on the endpoint's stream, so a group "completes" as
- *               soon as it is posted and one call runs the whole schedule;
- *   xport_peer  host buffers of a peer-transfer domain: SEND/RECV are the
- *               owner's tagged transfers (lfa_peer_xfer_ops), REDUCE/TREE the
- *               host combine; a group is waited on with test() and the run
- *               resumes there on the next progress call (prov/coll's fenced
- *               work queue, coll_coll.c:153-227, 816-890).
- * The multi-process CPU tests (tests/test_coll_host.py) therefore run this
- * same loop, planner and tag scheme that the GPU endpoints run.
- */
-struct xrun;
-struct xport {
-	int (*group_start)(struct xrun *r);
-	int (*post)(struct xrun *r, const struct lfa_step *st, void **req);
-	int (*group_end)(struct xrun *r);
-	int (*test)(struct xrun *r, void *req);       /* NULL: stream-ordered */
-	int (*local)(struct xrun *r, const struct lfa_step *st);
-	int (*coll)(struct xrun *r, const struct lfa_step *st);
-};
-
-struct xrun {
-	const struct xport *xp;
-	const struct plan *pl;
-	struct xctx x;
-	struct lfa_coll_mc *mc;
-	enum lfa_op op;
-	enum lfa_datatype dt;
-	hipStream_t stream;     /* xport_rccl */
-	uint64_t cid;           /* xport_peer tags: group_id << 16 | seq */
-	size_t pc;
-	void **reqs;            /* the current group's transfers; NULL = done */
-	size_t nreq, creq;      /* nreq = steps of the group posted so far */
-};
-
-/* Run the schedule as far as it goes: 1 done, 0 waiting on transfers, <0.
- * A post that returns -LFA_EAGAIN (the owner's queue is full: prov/coll
- * requeues such items, coll_coll.c:845-852) is retried on the next call. */
-static int xrun_advance(struct xrun *r)
-{
-	const struct plan *pl = r->pl;
-	int ret;
-
-	while (r->pc < pl->nsteps) {
-		const struct lfa_step *st = &pl->steps[r->pc];
-		size_t end;
-		int pending = 0;
-
-		switch (st->type) {
-		case LFA_STEP_GROUP_END:
-			r->pc++;
-			continue;
-		case LFA_STEP_SEND:
-		case LFA_STEP_RECV:
-			break;
-		case LFA_STEP_ALLTOALL:
-		case LFA_STEP_ALLGATHER:
-		case LFA_STEP_BARRIER:
-			ret = r->xp->coll(r, st);
-			if (ret)
-				return ret;
-			r->pc++;
-			continue;
-		default:
-			ret = r->xp->local(r, st);
-			if (ret)
-				return ret;
-			r->pc++;
-			continue;
-		}
-		for (end = r->pc; end < pl->nsteps &&
-		     pl->steps[end].type != LFA_STEP_GROUP_END; end++)
-			;
-		if (r->nreq < end - r->pc) {
-			size_t need = end - r->pc;
-
-			if (r->xp->test && need > r->creq) {
-				void **nr = realloc(r->reqs, need * sizeof(*nr));
-
-				if (!nr)
-					return -LFA_ENOMEM;
-				r->reqs = nr;
-				r->creq = need;
-			}
-			ret = r->xp->group_start(r);
-			while (!ret && r->nreq < need) {
-				void *req = NULL;
-
-				ret = r->xp->post(r, &pl->steps[r->pc + r->nreq], &req);
-				if (!ret && r->xp->test)
-					r->reqs[r->nreq] = req;
-				if (!ret)
-					r->nreq++;
-			}
-			if (r->xp->group_end(r) && !ret)
-				ret = -LFA_EIO;
-			if (ret == -LFA_EAGAIN)
-				pending = 1;
-			else if (ret)
-				return ret;
-		}
-		for (size_t i = 0; r->xp->test && i < r->nreq; i++) {
-			if (!r->reqs[i])
-				continue;
-			ret = r->xp->test(r, r->reqs[i]);
-			if (ret < 0)
-				return ret;
-			if (ret)
-				r->reqs[i] = NULL;
-			else
-				pending = 1;
-		}
-		if (pending)
-			return 0;
-		r->nreq = 0;
-		r->pc = end < pl->nsteps ? end + 1 : end;
-	}
-	return 1;
-}
-
-/* ---- xport_peer: the owner's tagged transfers + the host combine ------ */
-
-static int world_rank(const struct lfa_coll_mc *mc, int grank)
-{
-	return mc->members ? mc->members[grank] : grank;
-}
-
-static int peer_nop(struct xrun *r)
-{
-	return 0;
-}
-
-static int peer_post(struct xrun *r, const struct lfa_step *st, void **req)
-{
-	const struct lfa_coll_domain *d = r->mc->ep->dom;
-
-	/* coll_form_tag (coll_coll.c:37-45): cid | the SENDING rank << 32 */
-	if (st->type == LFA_STEP_SEND)
-		return d->xops.send(d->xctx, world_rank(r->mc, st->peer),
-				    resolve(&r->x, st->src), st->count,
-				    r->cid | (uint64_t)r->mc->rank << 32, req);
-	return d->xops.recv(d->xctx, world_rank(r->mc, st->peer),
-			    resolve(&r->x, st->dst), st->count,
-			    r->cid | (uint64_t)st->peer << 32, req);
-}
-
-static int peer_test(struct xrun *r, void *req)
-{
-	const struct lfa_coll_domain *d = r->mc->ep->dom;
-
-	return d->xops.test(d->xctx, req);
-}
-
-static int peer_local(struct xrun *r, const struct lfa_step *st)
-{
-	switch (st->type) {
-	case LFA_STEP_REDUCE:
-		return lfa_host_write(r->op, r->dt, resolve(&r->x, st->dst),
-				      resolve(&r->x, st->src), st->count);
-	case LFA_STEP_TREE: {
-		const void *srcs[LFA_TREE_MAX];
-
-		if (st->nsrc > LFA_TREE_MAX)
-			return -LFA_EINVAL;
-		for (uint32_t k = 0; k < st->nsrc; k++)
-			srcs[k] = resolve(&r->x, r->pl->refs[st->first + k]);
-		return lfa_host_reduce_tree(r->op, r->dt, resolve(&r->x, st->dst),
-					    srcs, (int)st->nsrc, st->count);
-	}
-	case LFA_STEP_COPY:
-		memmove(resolve(&r->x, st->dst), resolve(&r->x, st->src), st->count);
-		return 0;
-	default:
-		return -LFA_EINVAL;     /* TREE_PUT: P2P plans are not used here */
-	}
-}
-
-static int peer_coll(struct xrun *r, const struct lfa_step *st)
-{
-	return -LFA_EINVAL;             /* lowered to SEND/RECV by host_start */
-}
-
-static const struct xport xport_peer = {
-	peer_nop, peer_post, peer_nop, peer_test, peer_local, peer_coll,
-};
-
-/*
- * ---- xport_peer_dev: device buffers over the owner's transfers ----------
- * The owner moves host bytes only (an FI_HMEM-less rxm), so every transfer
- * is staged: a SEND copies its device bytes — as the endpoint stream has
- * them after the items enqueued before it — into a host bounce buffer and
- * sends that; a RECV lands in a bounce buffer and is copied to the device
- * on the stream before the group counts as done.  REDUCE / TREE / COPY are
- * the gfx950 kernels on the endpoint stream.  The schedule (and so every
- * tag and size) is the host form's, so members may mix host and device
- * buffers freely.
- */
-struct stg {
-	void *inner;            /* the owner's request */
-	char *bounce;
-	void *dst;              /* RECV: device destination */
-	size_t n;
-};
-
-static int pdev_post(struct xrun *r, const struct lfa_step *st, void **req)
-{
-	const struct lfa_coll_domain *d = r->mc->ep->dom;
-	struct stg *g = calloc(1, sizeof(*g));
-	int ret;
-
-	if (!g || !(g->bounce = malloc(st->count ? st->count : 1))) {
-		free(g);
-		return -LFA_ENOMEM;
-	}
-	g->n = st->count;
-	if (st->type == LFA_STEP_SEND) {
-		/* the stream first: a zero-byte send is a barrier arrival and
-		 * must leave only after this rank's earlier items completed */
-		if (hipStreamSynchronize(r->stream) != hipSuccess ||
-		    (st->count &&
-		     (hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
-				     hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
-		      hipStreamSynchronize(r->stream) != hipSuccess)))
-			ret = -LFA_EIO;
-		else
-			ret = d->xops.send(d->xctx, world_rank(r->mc, st->peer), g->bounce,
-					   st->count, r->cid | (uint64_t)r->mc->rank << 32,
-					   &g->inner);
-	} else {
-		g->dst = st->count ? resolve(&r->x, st->dst) : NULL;
-		ret = d->xops.recv(d->xctx, world_rank(r->mc, st->peer), g->bounce,
-				   st->count, r->cid | (uint64_t)st->peer << 32, &g->inner);
-	}
-	if (ret) {
-		free(g->bounce);
-		free(g);
-		return ret;
-	}
-	*req = g;
-	return 0;
-}
-
-static int pdev_test(struct xrun *r, void *req)
-{
-	const struct lfa_coll_domain *d = r->mc->ep->dom;
-	struct stg *g = req;
-	int ret = d->xops.test(d->xctx, g->inner);
-
-	if (ret == 0)
-		return 0;
-	if (ret > 0 && g->dst &&
-	    (hipMemcpyAsync(g->dst, g->bounce, g->n, hipMemcpyHostToDevice,
-			    r->stream) != hipSuccess ||
-	     hipStreamSynchronize(r->stream) != hipSuccess))
-		ret = -LFA_EIO;
-	free(g->bounce);
-	free(g);
-	return ret;
-}
-
-static int pdev_local(struct xrun *r, const struct lfa_step *st)
-{
-	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
-}
-
-static const struct xport xport_peer_dev = {
-	peer_nop, pdev_post, peer_nop, pdev_test, pdev_local, peer_coll,
-};
 
 /*
  * One collective on a host domain: prov/coll's util_coll_operation and its
@@ -1215,88 +745,6 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 	       hipStreamSynchronize(ep->d2h_stream) == hipSuccess ? 0 : -LFA_EIO;
 }
 
-/* ---------------------------------------------------------------------- */
-/* executor: schedule -> RCCL + kernels on the endpoint stream             */
-/* ---------------------------------------------------------------------- */
-
-/* ---- xport_rccl: RCCL over xGMI + the gfx950 kernels, stream-ordered -- */
-
-static int rccl_group_start(struct xrun *r)
-{
-	return ncclGroupStart() == ncclSuccess ? 0 : -LFA_EIO;
-}
-
-static int rccl_group_end(struct xrun *r)
-{
-	return ncclGroupEnd() == ncclSuccess ? 0 : -LFA_EIO;
-}
-
-static int rccl_post(struct xrun *r, const struct lfa_step *st, void **req)
-{
-	ncclResult_t e;
-
-	if (st->type == LFA_STEP_SEND)
-		e = ncclSend(resolve(&r->x, st->src), st->count, ncclUint8, st->peer,
-			     r->mc->comm, r->stream);
-	else
-		e = ncclRecv(resolve(&r->x, st->dst), st->count, ncclUint8, st->peer,
-			     r->mc->comm, r->stream);
-	return e == ncclSuccess ? 0 : -LFA_EIO;
-}
-
-static int rccl_local(struct xrun *r, const struct lfa_step *st)
-{
-	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
-}
-
-static int rccl_coll(struct xrun *r, const struct lfa_step *st)
-{
-	ncclComm_t c = r->mc->comm;
-	ncclResult_t e;
-
-	switch (st->type) {
-	case LFA_STEP_ALLTOALL:
-		e = ncclAllToAll(resolve(&r->x, st->src), resolve(&r->x, st->dst),
-				 st->count, ncclUint8, c, r->stream);
-		break;
-	case LFA_STEP_ALLGATHER:
-		e = ncclAllGather(resolve(&r->x, st->src), resolve(&r->x, st->dst),
-				  st->count, ncclUint8, c, r->stream);
-		break;
-	default: {
-		/* BARRIER, stream-ordered: a one-word allreduce completes on a
-		 * rank only after every member's stream has reached it */
-		uint64_t *w = (uint64_t *)r->mc->ep->barrier_dev + 2;
-
-		e = ncclAllReduce(w, w, 1, ncclUint64, ncclSum, c, r->stream);
-	}
-	}
-	return e == ncclSuccess ? 0 : -LFA_EIO;
-}
-
-static const struct xport xport_rccl = {
-	rccl_group_start, rccl_post, rccl_group_end, NULL, rccl_local, rccl_coll,
-};
-
-/* Enqueue a whole schedule on `s` (one xrun_advance pass runs it all). */
-static int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
-		     const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
-		     hipStream_t s)
-{
-	struct xrun r;
-	int ret;
-
-	memset(&r, 0, sizeof(r));
-	r.xp = &xport_rccl;
-	r.pl = pl;
-	r.x = *x;
-	r.mc = mc;
-	r.op = op;
-	r.dt = dt;
-	r.stream = s;
-	ret = xrun_advance(&r);
-	return ret == 1 ? 0 : ret ? ret : -LFA_EIO;
-}
 
 /*
  * The P2P symmetric workspace of `mc`, grown to `region` bytes per region.
@@ -1817,7 +1265,7 @@ static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	return ret;
 }
 
-static int check_reduce_args(enum lfa_datatype dt, enum lfa_op op)
+LFA_INTERNAL int check_reduce_args(enum lfa_datatype dt, enum lfa_op op)
 {
 	if (op < LFA_MIN || op > LFA_BXOR)
 		return -LFA_ENOSYS;   /* coll_process_reduce_item :760-761 */
@@ -2483,211 +1931,3 @@ int lfa_query_collective(struct lfa_coll_domain *domain,
  * tests/_plansim.py does the same in Python).
  */
 
-/* ====================================================================== */
-/* single-GPU multi-rank executor (loopback transport)                     */
-/* ====================================================================== */
-
-struct lb_msg {
-	struct lb_msg *next;
-	void *data;
-	size_t bytes;
-};
-
-int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
-		      int n, int root, enum lfa_datatype dt, enum lfa_op op,
-		      size_t count, void *const *send, void *const *result,
-		      void *stream)
-{
-	hipStream_t s = (hipStream_t)stream;
-	size_t esz = lfa_datatype_size(dt);
-	struct plan *pl = NULL;
-	size_t *pc = NULL, *arrived = NULL, region = sym_region(count, esz);
-	void **tmp = NULL;
-	char **sym = NULL;
-	struct lb_msg **box = NULL;
-	int ret = 0, done, progressed;
-
-	if (n < 1 || n > 64 || !send || !result || !esz)
-		return -LFA_EINVAL;
-	if ((coll == LFA_ALLREDUCE || coll == LFA_REDUCE ||
-	     coll == LFA_REDUCE_SCATTER) && (ret = check_reduce_args(dt, op)))
-		return ret;
-	if (algo == LFA_ALGO_RCCL)
-		algo = LFA_ALGO_TREE;
-	if (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
-	    algo != LFA_ALGO_TREE_COLL && algo != LFA_ALGO_P2P)
-		return -LFA_EINVAL;
-	pl = calloc((size_t)n, sizeof(*pl));
-	pc = calloc((size_t)n, sizeof(*pc));
-	arrived = calloc((size_t)n, sizeof(*arrived));
-	tmp = calloc((size_t)n, sizeof(*tmp));
-	sym = calloc((size_t)n, sizeof(*sym));
-	box = calloc((size_t)n * (size_t)n, sizeof(*box));
-	if (!pl || !pc || !arrived || !tmp || !sym || !box) {
-		ret = -LFA_ENOMEM;
-		goto out;
-	}
-	for (int r = 0; r < n && !ret; r++) {
-		struct plan raw;
-
-		ret = plan_make(&raw, coll, algo, r, n, root, count, esz);
-		if (ret)
-			break;
-		ret = lower_plan(&raw, r, n, &pl[r], 0);
-		plan_free(&raw);
-		if (!ret && pl[r].tmp &&
-		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)
-			ret = -LFA_ENOMEM;
-		/* P2P: every rank's symmetric workspace, plain pointers here */
-		if (!ret && plan_uses_sym(pl[r].steps, pl[r].nsteps) &&
-		    hipMallocAsync((void **)&sym[r], 2 * region, s) != hipSuccess)
-			ret = -LFA_ENOMEM;
-	}
-	/*
-	 * Lockstep: a rank runs local steps freely; at a comm group it posts
-	 * all its SENDs (snapshot copies) and completes once every RECV of the
-	 * group has a message waiting — RCCL group semantics.
-	 */
-	do {
-		done = 1;
-		progressed = 0;
-		for (int r = 0; r < n && !ret; r++) {
-			struct xctx xc = {{send[r], result[r], tmp[r]}, sym, region};
-
-			if (coll == LFA_BROADCAST)
-				xc.base[LFA_BUF_SEND] = result[r];
-			while (pc[r] < pl[r].nsteps && !ret) {
-				struct lfa_step *st = &pl[r].steps[pc[r]];
-
-				if (st->type == LFA_STEP_BARRIER) {
-					/* one stream: a rank passes barrier b once every
-					 * rank has enqueued everything before its b-th */
-					int all = 1;
-
-					if (!(arrived[r] & 1)) {
-						arrived[r] += 3;   /* count in bits 1.., flag 1 */
-						progressed = 1;
-					}
-					for (int q = 0; q < n; q++)
-						if ((arrived[q] >> 1) < (arrived[r] >> 1))
-							all = 0;
-					if (!all)
-						break;
-					arrived[r] &= ~(size_t)1;
-					pc[r]++;
-					progressed = 1;
-					continue;
-				}
-				if (st->type != LFA_STEP_SEND && st->type != LFA_STEP_RECV &&
-				    st->type != LFA_STEP_GROUP_END) {
-					ret = run_local(st, pl[r].refs, &xc, op, dt, s);
-					pc[r]++;
-					progressed = 1;
-					continue;
-				}
-				/* a group: [pc, end) up to GROUP_END */
-				size_t end = pc[r];
-				int ready = 1;
-
-				while (end < pl[r].nsteps &&
-				       pl[r].steps[end].type != LFA_STEP_GROUP_END)
-					end++;
-				/* post sends once (mark by negating peer) */
-				for (size_t i = pc[r]; i < end; i++) {
-					struct lfa_step *x = &pl[r].steps[i];
-
-					if (x->type != LFA_STEP_SEND || x->peer < 0)
-						continue;
-					struct lb_msg *m = calloc(1, sizeof(*m)), **t;
-
-					if (!m || hipMallocAsync(&m->data, x->count, s) != hipSuccess) {
-						free(m);
-						ret = -LFA_ENOMEM;
-						break;
-					}
-					m->bytes = x->count;
-					hipMemcpyAsync(m->data, resolve(&xc, x->src), x->count,
-						       hipMemcpyDeviceToDevice, s);
-					t = &box[(size_t)r * n + x->peer];
-					while (*t)
-						t = &(*t)->next;
-					*t = m;
-					x->peer = -x->peer - 1;
-					progressed = 1;
-				}
-				/* every recv matched? (count per peer in order) */
-				for (size_t i = pc[r]; i < end && ready; i++) {
-					struct lfa_step *x = &pl[r].steps[i];
-					int need = 0;
-
-					if (x->type != LFA_STEP_RECV)
-						continue;
-					for (size_t j = pc[r]; j <= i; j++)
-						if (pl[r].steps[j].type == LFA_STEP_RECV &&
-						    pl[r].steps[j].peer == x->peer)
-							need++;
-					struct lb_msg *m = box[(size_t)x->peer * n + r];
-
-					while (m && --need)
-						m = m->next;
-					if (!m)
-						ready = 0;
-				}
-				if (!ready || ret)
-					break;
-				for (size_t i = pc[r]; i < end; i++) {
-					struct lfa_step *x = &pl[r].steps[i];
-					struct lb_msg *m;
-
-					if (x->type == LFA_STEP_SEND) {
-						x->peer = -x->peer - 1;  /* restore */
-						continue;
-					}
-					m = box[(size_t)x->peer * n + r];
-					box[(size_t)x->peer * n + r] = m->next;
-					if (m->bytes != x->count)
-						ret = -LFA_EIO;
-					hipMemcpyAsync(resolve(&xc, x->dst), m->data, x->count,
-						       hipMemcpyDeviceToDevice, s);
-					hipFreeAsync(m->data, s);
-					free(m);
-				}
-				pc[r] = end < pl[r].nsteps ? end + 1 : end;
-				progressed = 1;
-			}
-			if (pc[r] < pl[r].nsteps)
-				done = 0;
-		}
-		if (!done && !progressed && !ret)
-			ret = -LFA_EIO;   /* schedule deadlock: a bug */
-	} while (!done && !ret);
-out:
-	if (box) {
-		for (size_t k = 0; k < (size_t)n * (size_t)n; k++)
-			while (box[k]) {
-				struct lb_msg *m = box[k];
-
-				box[k] = m->next;
-				hipFreeAsync(m->data, s);
-				free(m);
-			}
-	}
-	if (tmp)
-		for (int r = 0; r < n; r++)
-			if (tmp[r])
-				hipFreeAsync(tmp[r], s);
-	if (sym)
-		for (int r = 0; r < n; r++)
-			if (sym[r])
-				hipFreeAsync(sym[r], s);
-	if (pl)
-		for (int r = 0; r < n; r++)
-			plan_free(&pl[r]);
-	free(pl);
-	free(pc);
-	free(arrived);
-	free(tmp);
-	free(sym);
-	free(box);
-	return ret;
-}

@@ -1,0 +1,182 @@
+/*
+ * lfa_coll_int.h — internal types shared by the collective provider's
+ * translation units (liblfa_coll.so): the domain / endpoint / group state
+ * (lfa_coll.c), the executor and its transports (lfa_coll_exec.c) and the
+ * single-GPU loopback (lfa_coll_loopback.c).  Not installed.
+ */
+#ifndef LFA_COLL_INT_H
+#define LFA_COLL_INT_H
+
+#include <pthread.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "lfa_atomic.h"
+#include "lfa_coll.h"
+#include "lfa_coll_plan.h"
+
+#define LFA_MAX_GROUP_ID 256            /* OFI_MAX_GROUP_ID, ofi_coll.h:44 */
+#define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
+/* Bytes of one P2P handle-exchange record (struct sym_rec, lfa_coll.c). */
+#define LFA_SYM_REC_BYTES 80
+
+/* Where a plan's refs point for one execution: the operation's buffers and,
+ * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
+ * (IN region at 0, OUT region at `region`). */
+struct xctx {
+	void *base[3];          /* SEND, RESULT, TMP */
+	char *const *sym;       /* [group rank] */
+	size_t region;
+};
+
+/* ====================================================================== */
+/* domain / endpoint                                                       */
+/* ====================================================================== */
+
+struct lfa_coll_mc {
+	struct lfa_coll_ep *ep;
+	ncclComm_t comm;
+	int owns_comm;
+	int rank, size;
+	uint16_t group_id;
+	uint16_t seq;
+	int is_world;
+	/* host (peer-transfer) domains: group rank -> domain rank, NULL for
+	 * the world group (prov/coll's av_set fi_addr_array) */
+	int *members;
+	/* join in flight */
+	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
+	void *join_context;
+	/* LFA_ALGO_P2P symmetric workspace: `sym_local` (2 regions, hipMalloc,
+	 * IPC-exported) and every member's as mapped here (sym[rank] = local) */
+	char *sym_local;
+	char **sym;
+	size_t sym_region;
+};
+
+struct lfa_coll_domain {
+	int device, rank, nranks;
+	ncclComm_t comm;
+	int host;                       /* peer-transfer domain (host memory) */
+	struct lfa_peer_xfer_ops xops;
+	void *xctx;
+};
+
+struct hop;
+
+struct pending {
+	hipEvent_t ev;          /* device domains */
+	struct hop *hop;        /* host domains: the operation's state */
+	void *context;
+	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
+	struct lfa_coll_mc *mc;
+};
+
+struct lfa_coll_ep {
+	struct lfa_coll_domain *dom;
+	pthread_mutex_t lock;       /* queue, CQ/EQ, stream enqueue order */
+	pthread_mutex_t comm_lock;  /* communicator management (split/destroy,
+				     * P2P workspace exchange), in call order */
+	hipStream_t stream;         /* executor stream (RCCL + kernels) */
+	hipStream_t copy_stream;    /* host staging copies, H2D */
+	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
+				     * PCIe direction runs concurrently) */
+	enum lfa_coll_algo algo;
+	size_t chunk;
+	void *ws;                   /* device workspace */
+	size_t ws_size;
+	void *hs[2];                /* device staging for host buffers */
+	size_t hs_size;
+	uint64_t *barrier_host;     /* pinned ~rank for barrier */
+	void *barrier_dev;          /* 2 x uint64 */
+	void *ctl_dev;              /* P2P handle exchange, nranks records */
+	void *ctl_host;
+	uint8_t cid_mask[LFA_CID_BYTES];
+	struct lfa_coll_mc world;
+	hipEvent_t evpool[64];      /* recycled completion events */
+	int nev;
+	struct plan_cache {         /* last schedules built, keyed by shape */
+		int valid, coll, algo, rank, n, root;
+		size_t count, esz;
+		struct plan pl;
+	} pc[8];
+	unsigned pc_next;
+	struct pending *q;          /* FIFO ring of in-flight ops */
+	size_t qcap, qhead, qlen;
+	struct lfa_cq_err_entry err;
+	int have_err;
+	struct { uint32_t event; struct lfa_eq_entry entry; } eq[64];
+	size_t eqh, eqn;
+};
+
+/* group rank -> domain rank (host domains; identity for the world) */
+static inline int world_rank(const struct lfa_coll_mc *mc, int grank)
+{
+	return mc->members ? mc->members[grank] : grank;
+}
+
+/* ---------------------------------------------------------------------- */
+/* host (peer-transfer) executor                                          */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * The executor.  A schedule (struct plan) runs through ONE loop,
+ * xrun_advance, whatever carries its transfers; a transport table (xport)
+ * supplies the transfers and the local items:
+ *   xport_rccl  device buffers: SEND/RECV groups are RCCL grouped
+ *               ncclSend/ncclRecv, ALLTOALL/ALLGATHER/BARRIER RCCL
+ *               collectives, REDUCE/TREE/TREE_PUT/COPY gfx950 kernels — all
+ *               enqueued on the endpoint's stream, so a group "completes" as
+ *               soon as it is posted and one call runs the whole schedule;
+ *   xport_peer  host buffers of a peer-transfer domain: SEND/RECV are the
+ *               owner's tagged transfers (lfa_peer_xfer_ops), REDUCE/TREE the
+ *               host combine; a group is waited on with test() and the run
+ *               resumes there on the next progress call (prov/coll's fenced
+ *               work queue, coll_coll.c:153-227, 816-890).
+ * The multi-process CPU tests (tests/test_coll_host.py) therefore run this
+ * same loop, planner and tag scheme that the GPU endpoints run.
+ */
+struct xrun;
+struct xport {
+	int (*group_start)(struct xrun *r);
+	int (*post)(struct xrun *r, const struct lfa_step *st, void **req);
+	int (*group_end)(struct xrun *r);
+	int (*test)(struct xrun *r, void *req);       /* NULL: stream-ordered */
+	int (*local)(struct xrun *r, const struct lfa_step *st);
+	int (*coll)(struct xrun *r, const struct lfa_step *st);
+};
+
+struct xrun {
+	const struct xport *xp;
+	const struct plan *pl;
+	struct xctx x;
+	struct lfa_coll_mc *mc;
+	enum lfa_op op;
+	enum lfa_datatype dt;
+	hipStream_t stream;     /* xport_rccl */
+	uint64_t cid;           /* xport_peer tags: group_id << 16 | seq */
+	size_t pc;
+	void **reqs;            /* the current group's transfers; NULL = done */
+	size_t nreq, creq;      /* nreq = steps of the group posted so far */
+};
+
+/* lfa_coll_exec.c */
+LFA_INTERNAL void *resolve(const struct xctx *x, struct lfa_ref r);
+/* Non-communication step on `stream`. */
+LFA_INTERNAL int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
+			   const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
+			   hipStream_t stream);
+LFA_INTERNAL int plan_uses_sym(const struct lfa_step *st, size_t nsteps);
+LFA_INTERNAL size_t sym_region(size_t count, size_t esz);
+LFA_INTERNAL int xrun_advance(struct xrun *r);
+LFA_INTERNAL int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
+			   const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
+			   hipStream_t s);
+LFA_INTERNAL extern const struct xport xport_peer, xport_peer_dev;
+
+/* lfa_coll.c */
+LFA_INTERNAL int check_reduce_args(enum lfa_datatype dt, enum lfa_op op);
+
+#endif

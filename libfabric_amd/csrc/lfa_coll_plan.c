@@ -4,7 +4,7 @@
  * include/lfa_coll.h), host-only and testable on CPU.  prov/coll builds the
  * same thing as a work queue per operation (include/ofi_coll.h:64-119,
  * coll_coll.c:229-343); the executor that runs these schedules over RCCL or
- * the owner's transfers is lfa_coll.c.
+ * the owner's transfers is lfa_coll_exec.c.
  */
 #define _GNU_SOURCE
 #include <stdint.h>

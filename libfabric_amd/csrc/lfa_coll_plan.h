@@ -1,6 +1,7 @@
 /*
  * lfa_coll_plan.h — internal interface between the schedule builder
- * (lfa_coll_plan.c) and the executor (lfa_coll.c) of liblfa_coll.so.  Not
+ * (lfa_coll_plan.c) and the executor (lfa_coll.c, lfa_coll_exec.c,
+ * lfa_coll_loopback.c) of liblfa_coll.so.  Not
  * installed; nothing here is exported from the library.
  */
 #ifndef LFA_COLL_PLAN_H

@@ -14,7 +14,7 @@ for kind in asan tsan; do
   if [ $kind = asan ]; then SAN="-fsanitize=address,undefined -fno-omit-frame-pointer -g -O1"
   else SAN="-fsanitize=thread -g -O1"; fi
   gcc $SAN -fPIC -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I"$R/include" -I/opt/rocm/include \
-      -shared -o "$d/liblfa_coll.so" "$R/libfabric_amd/csrc/lfa_coll.c" "$R/libfabric_amd/csrc/lfa_coll_plan.c" -L"$R/libfabric_amd" -llfa \
+      -shared -o "$d/liblfa_coll.so" "$R/libfabric_amd/csrc/lfa_coll.c" "$R/libfabric_amd/csrc/lfa_coll_exec.c" "$R/libfabric_amd/csrc/lfa_coll_plan.c" "$R/libfabric_amd/csrc/lfa_coll_loopback.c" -L"$R/libfabric_amd" -llfa \
       -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,"$R/libfabric_amd" -Wl,-soname,liblfa_coll.so
   gcc $SAN -fPIC -std=gnu11 -Wall -I"$R/include" -I"$FAB" -shared -o "$d/liboff_lfa-fi.so" \
       "$R/libfabric_amd/csrc/off_lfa.c" -L"$d" -llfa_coll -lpthread -Wl,-rpath,'$ORIGIN'
