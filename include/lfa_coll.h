@@ -146,6 +146,12 @@ int lfa_coll_ep_open(struct lfa_coll_domain *domain, struct lfa_coll_ep **ep);
 int lfa_coll_ep_close(struct lfa_coll_ep *ep);
 /* The endpoint's HIP stream (hipStream_t), for callers that order work. */
 void *lfa_coll_ep_stream(struct lfa_coll_ep *ep);
+/* The algorithm picks the schedule, so every member of a group must use the
+ * same one when it issues a collective (as every rank of an RCCL
+ * communicator issues the same calls); the buffers' memory type and the
+ * chunk size need not agree.  LFA_ALGO_P2P on peer domains also needs every
+ * member's domain on a GPU (lfa_coll_domain_open_peer with a device): a
+ * domain without one runs it as LFA_ALGO_TREE, a different schedule. */
 int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo);
 /* Host-staging chunk size in bytes (0 = default 32 MiB). */
 int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
