@@ -1004,6 +1004,15 @@ def extra_collectives(rank, world, stream, emit=None):
         out["reduce_scatter_double_prod_tree"] = _rs_sweep(ep, rank, world, coll.ALGO_TREE,
                                                            egress)
         emit(out)
+        if world > 1:
+            # the same schedule with the block exchange as one ncclAllToAll
+            try:
+                out["reduce_scatter_double_prod_tree_coll"] = _rs_sweep(
+                    ep, rank, world, coll.ALGO_TREE_COLL, egress)
+            except Exception as e:  # noqa: BLE001
+                out["reduce_scatter_double_prod_tree_coll"] = {"error": f"{e}"[:200]}
+            ep.set_algo(coll.ALGO_TREE)
+            emit(out)
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
         a = torch.rand(1024, device="cuda")
         b = torch.empty_like(a)
