@@ -641,8 +641,31 @@ def extra_tree(dev, stream, nsrc=8):
         fn(i)
     ms = _kernel_events(fn, 30, stream)
     gbps = (nsrc + 1) * blk * 4 / (ms * 1e-3) / 1e9
-    return {"nsrc": nsrc, "block_bytes": blk * 4, "kernel_us": round(ms * 1e3, 2),
-            "achieved_gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
+    out = {"nsrc": nsrc, "block_bytes": blk * 4, "kernel_us": round(ms * 1e3, 2),
+           "achieved_gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4),
+           "layout": "separate allocations (the caller's buffers)"}
+    del sets
+    # the collective's own layout: the N slots of one TMP workspace sit
+    # round_up(B, 256) + 6 KiB apart (lfa_coll_plan.c blk_stride)
+    stride = (blk * 4 + 255) // 256 * 256 + 6 * 1024
+    ws = [torch.empty(nsrc * stride, dtype=torch.uint8, device=dev) for _ in range(2)]
+    for w in ws:
+        w.view(torch.float32)[: w.numel() // 4].uniform_()
+    wsets = [([w[k * stride:k * stride + blk * 4].view(torch.float32) for k in range(nsrc)],
+              torch.empty(blk, device=dev)) for w in ws]
+
+    def fw(i):
+        srcs, o = wsets[i % 2]
+        atomic.reduce_tree(2, 8, o, srcs, blk, stream)
+    for i in range(4):
+        fw(i)
+    ms = _kernel_events(fw, 30, stream)
+    gbps = (nsrc + 1) * blk * 4 / (ms * 1e-3) / 1e9
+    out["collective_workspace_layout"] = {
+        "kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
+        "frac": round(gbps / PEAK_GBPS, 4),
+        "layout": "8 slots of one allocation, round_up(B, 256) + 6 KiB apart (TREE's TMP)"}
+    return out
 
 
 def extra_tree_put(dev, stream, nsrc=8):
