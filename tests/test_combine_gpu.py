@@ -516,3 +516,66 @@ def test_sync_table_host_pointers(lfa, nbytes, kind):
             fn(td.data_ptr(), s.ctypes.data, n)
             got = td.cpu().numpy()
         assert_parity(dt, got.view(np.uint8), want.view(np.uint8), f"{kind} {nbytes}")
+
+
+def _shape(rng):
+    """A random (count, dst offset, src offset) in elements: sizes across the
+    element-only, one-tile and many-tile ranges, offsets co-aligned or not."""
+    n = int(rng.choice([int(rng.integers(0, 70)), int(rng.integers(70, 5000)),
+                        int(rng.integers(5000, 200_000))]))
+    return n, int(rng.integers(0, 8)), int(rng.integers(0, 8))
+
+
+def test_every_write_entry_random_shapes(lfa, manifest):
+    """Each of the 132 write-table entries on three seeded random counts and
+    offsets (heads, tails, vector body, non-co-aligned) against the oracle."""
+    rng = np.random.default_rng(2026)
+    for case in manifest["combine"] * 3:
+        op, dt = case["op"], case["dt"]
+        esz = oracle.datatype_size(dt)
+        n, od, os_ = _shape(rng)
+        d, s = _rand(dt, n + 8, rng), _rand(dt, n + 8, rng)
+        want = d.copy()
+        oracle.write(op, dt, want[od:od + n], s[os_:os_ + n].copy())
+        dd, sd = _dev(d), _dev(s)
+        assert lfa.write_ptr(op, dt, dd.data_ptr() + od * esz,
+                             sd.data_ptr() + os_ * esz, n) == 0
+        torch.cuda.synchronize()
+        assert_parity(dt, dd.cpu().numpy(), want, f"{case['file']} n={n} off={od},{os_}")
+
+
+def test_every_fetch_and_compare_entry_random_shapes(lfa, manifest):
+    """Each of the 145 readwrite and 84 swap entries on three seeded random
+    counts and offsets; res receives the old destination (shipping semantics)."""
+    from libfabric_amd import _native
+    L = _native.lib()
+    rng = np.random.default_rng(4052)
+    for case in (manifest["readwrite"] + manifest["swap"]) * 3:
+        op, dt = case["op"], case["dt"]
+        esz = oracle.datatype_size(dt)
+        n, od, os_ = _shape(rng)
+        d, s = _rand(dt, n + 8, rng), _rand(dt, n + 8, rng)
+        want_d, want_r = d[od:od + n].copy(), np.zeros_like(d[:n])
+        dd, sd = _dev(d), _dev(s)
+        rd = torch.zeros((n + 8) * esz, dtype=torch.uint8, device=DEV)
+        if op >= 12:
+            c = d.copy()
+            flip = rng.random(n + 8) < 0.5
+            c[flip] = _rand(dt, int(flip.sum()), rng)
+            cd = _dev(c)
+            oracle.swap(op, dt, want_d, s[os_:os_ + n].copy(), c[os_:os_ + n].copy(),
+                        want_r, oracle.CAS)
+            rc = L.lfa_atomic_swap_async(op, dt, dd.data_ptr() + od * esz,
+                                         sd.data_ptr() + os_ * esz,
+                                         cd.data_ptr() + os_ * esz,
+                                         rd.data_ptr() + os_ * esz, n, None)
+        else:
+            oracle.readwrite(op, dt, want_d, s[os_:os_ + n].copy(), want_r)
+            rc = L.lfa_atomic_readwrite_async(op, dt, dd.data_ptr() + od * esz,
+                                              sd.data_ptr() + os_ * esz,
+                                              rd.data_ptr() + os_ * esz, n, None)
+        assert rc == 0, case["file"]
+        torch.cuda.synchronize()
+        what = f"{case['file']} n={n} off={od},{os_}"
+        assert_parity(dt, dd.cpu().numpy()[od * esz:(od + n) * esz], want_d, what)
+        assert_parity(dt, rd.cpu().numpy()[os_ * esz:(os_ + n) * esz], want_r, what + " res")
