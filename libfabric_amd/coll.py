@@ -17,6 +17,7 @@ ships it to the other ranks over torch.distributed's store/gloo group.
 from __future__ import annotations
 
 import ctypes
+import sys
 from dataclasses import dataclass
 
 import torch
@@ -479,14 +480,25 @@ class HostEndpoint(Endpoint):
         self.rank, self.nranks, self.device = rank, nranks, device
         self.transport = transport
 
+        self.transport_errors = []     # tracebacks of transport exceptions
+
+        def _failed(what):
+            # an exception must not cross C: it becomes -EIO for the
+            # operation, and its traceback is kept (and shown) for diagnosis
+            import traceback
+            tb = f"{what}: " + traceback.format_exc()
+            self.transport_errors.append(tb)
+            sys.stderr.write(f"lfa HostEndpoint rank {rank}: transport {tb}")
+            return -EIO
+
         def _send(ctx, peer, buf, nbytes, tag, req):
             try:
                 req[0] = transport.send(peer, buf, nbytes, tag)
                 return 0
             except TransportAgain:
                 return -EAGAIN
-            except Exception:  # noqa: BLE001 — an exception must not cross C
-                return -EIO
+            except Exception:  # noqa: BLE001
+                return _failed(f"send(peer={peer}, {nbytes} B, tag={tag:#x})")
 
         def _recv(ctx, peer, buf, nbytes, tag, req):
             try:
@@ -495,13 +507,13 @@ class HostEndpoint(Endpoint):
             except TransportAgain:
                 return -EAGAIN
             except Exception:  # noqa: BLE001
-                return -EIO
+                return _failed(f"recv(peer={peer}, {nbytes} B, tag={tag:#x})")
 
         def _test(ctx, req):
             try:
                 return int(transport.test(req))
             except Exception:  # noqa: BLE001
-                return -EIO
+                return _failed("test")
 
         # keep the trampolines alive as long as the endpoint
         self._ops = PeerXferOps(XferPost(_send), XferPost(_recv), XferTest(_test))

@@ -491,19 +491,25 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 			hipError_t e;
 
 			if (!h->fin &&
-			    (hipEventCreateWithFlags(&h->fin, hipEventDisableTiming) != hipSuccess ||
-			     hipEventRecord(h->fin, h->r.stream) != hipSuccess)) {
+			    (lfa_hip_note(&h->r.hip_err,
+					  hipEventCreateWithFlags(&h->fin, hipEventDisableTiming),
+					  "completion event create") != hipSuccess ||
+			     lfa_hip_note(&h->r.hip_err, hipEventRecord(h->fin, h->r.stream),
+					  "completion event record") != hipSuccess)) {
 				h->err = -LFA_EIO;
 				continue;
 			}
 			e = hipEventQuery(h->fin);
 			if (e == hipSuccess && h->out_bytes &&
-			    hipMemcpy(h->user_out, h->st_out, h->out_bytes,
-				      hipMemcpyDeviceToHost) != hipSuccess)
+			    lfa_hip_note(&h->r.hip_err,
+					 hipMemcpy(h->user_out, h->st_out, h->out_bytes,
+						   hipMemcpyDeviceToHost),
+					 "staged result D2H") != hipSuccess)
 				h->err = -LFA_EIO;
 			else if (e == hipSuccess)
 				h->done = 1;
-			else if (e != hipErrorNotReady)
+			else if (e != hipErrorNotReady &&
+				 lfa_hip_note(&h->r.hip_err, e, "completion event query"))
 				h->err = -LFA_EIO;
 		} else if (ret) {
 			h->done = 1;
@@ -575,7 +581,8 @@ static int pending_state(const struct pending *p, int *perr)
 {
 	if (p->hop) {
 		if (p->hop->err) {
-			*perr = -p->hop->err;
+			/* the failing HIP call's code when there was one */
+			*perr = p->hop->r.hip_err ? p->hop->r.hip_err : -p->hop->err;
 			return -1;
 		}
 		return p->hop->done ? 0 : 1;
@@ -797,7 +804,7 @@ static size_t sym_grow(const struct lfa_coll_mc *mc, size_t region)
  * r1).  `ok` comes in false when the old workspace could not be quiesced.
  */
 static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
-			struct sym_rec *mine)
+			struct sym_rec *mine, int *why)
 {
 	int n = mc->size;
 
@@ -805,16 +812,18 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	memset(mine, 0, sizeof(*mine));
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
-	ok = ok && hipMalloc((void **)&mc->sym_local, 2 * region) == hipSuccess;
+	ok = ok && lfa_hip_note(why, hipMalloc((void **)&mc->sym_local, 2 * region),
+				"P2P workspace hipMalloc") == hipSuccess;
 	if (!ok)
 		mc->sym_local = NULL;
 	if (ok && n > 1)
-		ok = hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
+		ok = lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
+				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
 	mine->ok = ok;
 }
 
 /* Every member's record in hand: map the peers' workspaces. */
-static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs)
+static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, int *why)
 {
 	int ret = 0;
 
@@ -824,8 +833,9 @@ static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs)
 	for (int k = 0; k < mc->size && !ret; k++) {
 		if (k == mc->rank) {
 			mc->sym[k] = mc->sym_local;
-		} else if (hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
-					       hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+		} else if (lfa_hip_note(why, hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
+								  hipIpcMemLazyEnablePeerAccess),
+					"P2P hipIpcOpenMemHandle") != hipSuccess) {
 			mc->sym[k] = NULL;
 			ret = -LFA_EIO;
 		}
@@ -895,12 +905,13 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 			break;
 		h->sym_size = sym_grow(mc, h->sym_need);
 		sym_prepare(mc, h->sym_size,
-			    hipStreamSynchronize(ep->stream) == hipSuccess,
-			    (struct sym_rec *)h->mine);
+			    lfa_hip_note(&h->r.hip_err, hipStreamSynchronize(ep->stream),
+					 "P2P prologue stream sync") == hipSuccess,
+			    (struct sym_rec *)h->mine, &h->r.hip_err);
 		if (mc->size == 1) {
 			h->agree_in = h->agree_out = ((struct sym_rec *)h->mine)->ok;
 			recs[0] = *(struct sym_rec *)h->mine;
-			h->agree_out = h->agree_out && sym_open(mc, recs) == 0;
+			h->agree_out = h->agree_out && sym_open(mc, recs, &h->r.hip_err) == 0;
 			goto agreed;
 		}
 		ret = sub_start(ep, h, LFA_ALLGATHER, h->mine, recs, sizeof(struct sym_rec),
@@ -913,7 +924,7 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 		ret = sub_advance(h);
 		if (ret <= 0)
 			return ret;
-		h->agree_in = sym_open(mc, recs) == 0;
+		h->agree_in = sym_open(mc, recs, &h->r.hip_err) == 0;
 		ret = sub_start(ep, h, LFA_ALLREDUCE, &h->agree_in, &h->agree_out, 1,
 				LFA_INT32, LFA_MIN, (uint16_t)(h->sub_seq + 1));
 		if (ret)
@@ -957,7 +968,7 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 	 * peer still touches it */
 	memset(recs, 0, (size_t)n * rb);
 	sym_prepare(mc, region, hipStreamSynchronize(ep->stream) == hipSuccess,
-		    &recs[mc->rank]);
+		    &recs[mc->rank], NULL);
 	if (n > 1 &&
 	    (hipMemcpyAsync((char *)drec + (size_t)mc->rank * rb, &recs[mc->rank], rb,
 			    hipMemcpyHostToDevice, ep->stream) != hipSuccess ||
@@ -968,7 +979,7 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 	     hipStreamSynchronize(ep->stream) != hipSuccess))
 		ret = -LFA_EIO;
 	if (!ret)
-		ret = sym_open(mc, recs);
+		ret = sym_open(mc, recs, NULL);
 	if (n > 1) {
 		/* agree that every member mapped every peer (MIN of the flags) */
 		int32_t all = ret == 0;

@@ -9,10 +9,23 @@
  * FI_PEER_TRANSFER sends and receives (coll_coll.c:770-814).
  */
 #define _GNU_SOURCE
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "lfa_coll_int.h"
+
+LFA_INTERNAL hipError_t lfa_hip_note(int *slot, hipError_t e, const char *what)
+{
+	if (e != hipSuccess) {
+		if (slot && !*slot)
+			*slot = (int)e;
+		if (getenv("LFA_DEBUG"))
+			fprintf(stderr, "lfa: %s failed: %s (%d)\n", what,
+				hipGetErrorString(e), (int)e);
+	}
+	return e;
+}
 
 LFA_INTERNAL void *resolve(const struct xctx *x, struct lfa_ref r)
 {
@@ -283,11 +296,15 @@ static int pdev_post(struct xrun *r, const struct lfa_step *st, void **req)
 	if (st->type == LFA_STEP_SEND) {
 		/* the stream first: a zero-byte send is a barrier arrival and
 		 * must leave only after this rank's earlier items completed */
-		if (hipStreamSynchronize(r->stream) != hipSuccess ||
+		if (lfa_hip_note(&r->hip_err, hipStreamSynchronize(r->stream),
+				 "send: stream sync") != hipSuccess ||
 		    (st->count &&
-		     (hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
-				     hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
-		      hipStreamSynchronize(r->stream) != hipSuccess)))
+		     (lfa_hip_note(&r->hip_err,
+				   hipMemcpyAsync(g->bounce, resolve(&r->x, st->src), st->count,
+						  hipMemcpyDeviceToHost, r->stream),
+				   "send: D2H staging") != hipSuccess ||
+		      lfa_hip_note(&r->hip_err, hipStreamSynchronize(r->stream),
+				   "send: stream sync after D2H") != hipSuccess)))
 			ret = -LFA_EIO;
 		else
 			ret = d->xops.send(d->xctx, world_rank(r->mc, st->peer), g->bounce,
@@ -316,9 +333,11 @@ static int pdev_test(struct xrun *r, void *req)
 	if (ret == 0)
 		return 0;
 	if (ret > 0 && g->dst &&
-	    (hipMemcpyAsync(g->dst, g->bounce, g->n, hipMemcpyHostToDevice,
-			    r->stream) != hipSuccess ||
-	     hipStreamSynchronize(r->stream) != hipSuccess))
+	    (lfa_hip_note(&r->hip_err,
+			  hipMemcpyAsync(g->dst, g->bounce, g->n, hipMemcpyHostToDevice,
+					 r->stream), "recv: H2D staging") != hipSuccess ||
+	     lfa_hip_note(&r->hip_err, hipStreamSynchronize(r->stream),
+			  "recv: stream sync after H2D") != hipSuccess))
 		ret = -LFA_EIO;
 	free(g->bounce);
 	free(g);

@@ -160,7 +160,15 @@ struct xrun {
 	size_t pc;
 	void **reqs;            /* the current group's transfers; NULL = done */
 	size_t nreq, creq;      /* nreq = steps of the group posted so far */
+	int hip_err;            /* first failing HIP call's code (prov_errno) */
 };
+
+/*
+ * A HIP call of an operation failed: keep the first code (it becomes the
+ * completion's prov_errno, fi_cq_err_entry's provider-specific error) and,
+ * with LFA_DEBUG set, name the call on stderr.  Returns the call's result.
+ */
+LFA_INTERNAL hipError_t lfa_hip_note(int *slot, hipError_t e, const char *what);
 
 /* lfa_coll_exec.c */
 LFA_INTERNAL void *resolve(const struct xctx *x, struct lfa_ref r);

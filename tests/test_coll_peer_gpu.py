@@ -149,7 +149,9 @@ def _body(ep, rank, world, oracle, coll):
 
 def _worker(rank, world, port, q):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # LFA_DEBUG: a failing HIP call is named on stderr (and its code is
+        # the completion's prov_errno)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
