@@ -769,17 +769,23 @@ struct sym_rec {
 	hipIpcMemHandle_t h;
 };
 
+/* Unmap the peers' workspaces in `sym` and free this rank's `local`. */
+static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
+{
+	if (sym) {
+		for (int k = 0; k < mc->size; k++)
+			if (k != mc->rank && sym[k])
+				hipIpcCloseMemHandle(sym[k]);
+		free(sym);
+	}
+	if (local)
+		hipFree(local);
+}
+
 static void p2p_release(struct lfa_coll_mc *mc)
 {
-	if (mc->sym) {
-		for (int k = 0; k < mc->size; k++)
-			if (k != mc->rank && mc->sym[k])
-				hipIpcCloseMemHandle(mc->sym[k]);
-		free(mc->sym);
-		mc->sym = NULL;
-	}
-	if (mc->sym_local)
-		hipFree(mc->sym_local);
+	sym_free(mc, mc->sym, mc->sym_local);
+	mc->sym = NULL;
 	mc->sym_local = NULL;
 	mc->sym_region = 0;
 }
@@ -807,8 +813,15 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 			struct sym_rec *mine, int *why)
 {
 	int n = mc->size;
+	char **old_sym = mc->sym, *old_local = mc->sym_local;
 
-	p2p_release(mc);
+	/* the new workspace is allocated and exported while the old one is
+	 * still held, so its IPC handle can never repeat the old one's (an
+	 * exporter resource freed and reused at once); the old mappings and
+	 * memory go right after */
+	mc->sym = NULL;
+	mc->sym_local = NULL;
+	mc->sym_region = 0;
 	memset(mine, 0, sizeof(*mine));
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
@@ -820,6 +833,7 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 		ok = lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
 				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
 	mine->ok = ok;
+	sym_free(mc, old_sym, old_local);
 }
 
 /* Every member's record in hand: map the peers' workspaces. */
