@@ -17,7 +17,9 @@ N > 1  : one process per GPU.  The headline is STRONG-scaled (SURVEY §8(e),
          extras.  `python bench.py --gpus N` without RANK in the environment
          starts the N rank processes itself (before any GPU call); under
          torch.distributed.run it is one of them.  A world size that differs
-         from --gpus is an error (exit 2).
+         from --gpus is an error (exit 2).  The N > 1 provider extras
+         (allreduce / reduce_scatter over RCCL, xGMI P2P) run as a child job
+         of the ranks (run_isolated), so a fault there cannot lose the line.
 
 Extra objects on the JSON line:
   roofline      dominant kernel (combine_lds<SUM,float>): algorithmic bytes per
