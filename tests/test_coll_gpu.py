@@ -154,6 +154,44 @@ def test_loopback_reference_known_answers(coll, algo):
             assert all(abs(a - b) <= 1e-8 for a, b in zip(got, comp)), (n, r)
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_loopback_ragged_counts_every_root(coll, algo, n):
+    """Counts of 0, 1, n-1 and 7n+3 (empty, fewer elements than ranks,
+    ragged blocks) through allreduce, reduce_scatter and reduce to EVERY
+    root, bit-exact with the oracle; int64 SUM and double PROD."""
+    for dt, op in ((6, 2), (9, 3)):
+        esz = 8
+        for count in (0, 1, n - 1, 7 * n + 3):
+            sends = _inputs(dt, n, count, 17 * n + count + op,
+                            *((0.9, 1.1) if op == 3 else (-1, 1)))
+            want = oracle.allreduce(op, dt, sends)[0] if count else np.zeros(0)
+            sd = [_dev(s) if count else torch.zeros(8, dtype=torch.uint8, device=DEV)
+                  for s in sends]
+            rd = [torch.zeros(max(count, 1) * esz, dtype=torch.uint8, device=DEV)
+                  for _ in range(n)]
+            coll.loopback(ALLREDUCE, algo, n, -1, dt, op, count, sd, rd)
+            torch.cuda.synchronize()
+            for r in range(n):
+                assert_parity(dt, rd[r].cpu().numpy()[:count * esz], want,
+                              f"allreduce n={n} count={count} r={r}")
+            rd = [torch.zeros(max(coll.block(count, n, r)[1], 1) * esz, dtype=torch.uint8,
+                              device=DEV) for r in range(n)]
+            coll.loopback(REDUCE_SCATTER, algo, n, -1, dt, op, count, sd, rd)
+            torch.cuda.synchronize()
+            for r in range(n):
+                off, ln = coll.block(count, n, r)
+                assert_parity(dt, rd[r].cpu().numpy()[:ln * esz], want[off:off + ln],
+                              f"reduce_scatter n={n} count={count} r={r}")
+            for root in range(n):
+                rd = [torch.zeros(max(count, 1) * esz, dtype=torch.uint8, device=DEV)
+                      for _ in range(n)]
+                coll.loopback(REDUCE, algo, n, root, dt, op, count, sd, rd)
+                torch.cuda.synchronize()
+                assert_parity(dt, rd[root].cpu().numpy()[:count * esz], want,
+                              f"reduce n={n} count={count} root={root}")
+
+
 @pytest.fixture(scope="module")
 def full_size_sum():
     """BASELINE.json configs[3]'s shape on loopback: 8 ranks, 256 MiB of
