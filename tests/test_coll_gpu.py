@@ -192,6 +192,35 @@ def test_loopback_ragged_counts_every_root(coll, algo, n):
                               f"reduce n={n} count={count} root={root}")
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+def test_loopback_edge_values_minmax(coll, algo):
+    """NaN, +-inf and +-0 lanes in some ranks' inputs through float and
+    double MIN / MAX / SUM allreduces: the dst-biased compare of the
+    reference (util_atomic.c:291-316: a NaN partial on the hi side stays, one
+    on the lo side is ignored; ties keep hi) at every level of the tree."""
+    edge = [np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 1.0, -1.0]
+    for n in (2, 3, 5, 8):
+        for dt in (8, 9):
+            nd = oracle.DT_NP[dt]
+            rng = np.random.default_rng(n * 10 + dt)
+            count = 4099
+            sends = []
+            for _ in range(n):
+                x = rng.uniform(-1, 1, count).astype(nd)
+                lanes = rng.random(count) < 0.3
+                x[lanes] = rng.choice(np.array(edge, nd), int(lanes.sum()))
+                sends.append(x)
+            for op in (0, 1, 2):
+                want = oracle.allreduce(op, dt, sends)[0]
+                sd = [_dev(x) for x in sends]
+                rd = [torch.zeros_like(x) for x in sd]
+                coll.loopback(ALLREDUCE, algo, n, -1, dt, op, count, sd, rd)
+                torch.cuda.synchronize()
+                for r in range(n):
+                    assert_parity(dt, rd[r].cpu().numpy(), want,
+                                  f"n={n} dt={dt} op={op} r={r}")
+
+
 @pytest.fixture(scope="module")
 def full_size_sum():
     """BASELINE.json configs[3]'s shape on loopback: 8 ranks, 256 MiB of
