@@ -193,3 +193,71 @@ def test_c_executor_gpu_kernels_across_processes(world):
                 p.kill()
     for r in range(world):
         assert results.get(r) == "ok", results.get(r)
+
+
+def _growth_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            # sizes that grow the symmetric workspace again and again, with
+            # small operations between them, all in flight at once
+            sizes = (1000, 3 << 20, 777, 6 << 20, 5, 11 << 20, 4096, 23 << 20, 3 << 20)
+            for rep in range(2):
+                outs, ctxs = [], []
+                for k, n in enumerate(sizes):
+                    sends = _inputs(oracle, 8, n, world, 1000 * rep + k)
+                    want = oracle.allreduce(2, 8, sends)[0]
+                    r = torch.zeros(n, dtype=torch.float32, device="cuda")
+                    xs = _dev(sends[rank])
+                    _ready()
+                    ctxs.append(ep.allreduce(xs, r, n, 8, 2))
+                    outs.append((r, want, xs))
+                done = []
+                while len(done) < len(ctxs):
+                    done += ep.cq_read()
+                assert done == ctxs
+                for (r, want, _), n in zip(outs, sizes):
+                    assert r.cpu().numpy().tobytes() == want.tobytes(), f"P2P n={n} rep={rep}"
+            assert not ep.transport_errors, ep.transport_errors
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_p2p_workspace_growth_in_flight():
+    """LFA_ALGO_P2P across two processes: nine allreduces queued at once, four
+    of which grow the IPC-shared symmetric workspace (the asynchronous
+    handshake from progress, each after the operations before it), twice
+    over; every result bit-exact."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_growth_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=110)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
