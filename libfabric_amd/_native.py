@@ -74,6 +74,8 @@ def _bind_tune(L):
     L.lfa__tune_fetch_f32.restype = c_int
     L.lfa__tune_fetch_f32.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_size_t, c_void_p]
+    L.lfa__tune_stream.restype = c_int
+    L.lfa__tune_stream.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
 
 
 def lib(name: str = "lfa") -> ctypes.CDLL:

@@ -664,3 +664,79 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
   return go(RwF<OP_SUM, float, true>{(char *)dst, (const char *)src, (char *)res,
                                      (u32x4 *)dst, (const u32x4 *)src, (u32x4 *)res});
 }
+
+// ---------------------------------------------------------------------------
+// Pure streams, to bound the combine by what HBM gives each access mix on
+// this part (tools/probe_hbm.py): NIN inputs read HBM -> LDS with nt
+// global_load_lds (the combine's load path, nothing stored but one vector
+// per workgroup that no real data reaches), or a write-only stream of U KiB
+// per wave with the combine's store policies.  Same tile shape as
+// combine_lds: 4 waves per workgroup, U KiB per operand per wave.
+// ---------------------------------------------------------------------------
+namespace lfa_stream {
+using lfa::u32x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int NIN, int U>
+__global__ __launch_bounds__(256) void read_lds(const u32x4 *a, const u32x4 *b,
+                                                u32x4 *sink, size_t nvec) {
+  __shared__ u32x4 lds[NIN][4][U][64];
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (4 * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U > nvec) return;
+#pragma unroll
+  for (int k = 0; k < NIN; k++)
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)((k ? b : a) + base + u * 64 + l),
+                                       (lds_void *)&lds[k][w][u][0], 16, 0, 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const u32x4 x = lds[NIN - 1][w][U - 1][l];
+  if (x.x == 0x9e3779b9u && x.y == 0x7f4a7c15u && x.z == 0x2545f491u && x.w == 1u)
+    sink[blockIdx.x] = x;
+}
+
+template <int U, int SAUX>
+__global__ __launch_bounds__(256) void write_only(u32x4 *dst, size_t nvec) {
+  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (4 * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U > nvec) return;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+  const u32x4 v = {l, w, (unsigned)blockIdx.x, 0x3f800000u};
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+}
+}  // namespace lfa_stream
+
+// kind 0: read a; 1: read a and b; 2: write dst, nt; 3: write dst, sc1.
+// nvec 16-B vectors per operand, a multiple of the 16 KiB workgroup tile.
+extern "C" int lfa__tune_stream(int kind, void *dst, const void *a, const void *b,
+                                size_t nvec, void *stream) {
+  using namespace lfa_stream;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t tile = 4 * 64 * 4;
+  if (!nvec || nvec % tile) return -LFA_EINVAL;
+  const dim3 grid((unsigned)(nvec / tile)), block(256);
+  switch (kind) {
+    case 0:
+      hipLaunchKernelGGL((read_lds<1, 4>), grid, block, 0, s, (const u32x4 *)a,
+                         (const u32x4 *)a, (u32x4 *)dst, nvec);
+      break;
+    case 1:
+      hipLaunchKernelGGL((read_lds<2, 4>), grid, block, 0, s, (const u32x4 *)a,
+                         (const u32x4 *)b, (u32x4 *)dst, nvec);
+      break;
+    case 2:
+      hipLaunchKernelGGL((write_only<4, lfa::kStoreNt>), grid, block, 0, s, (u32x4 *)dst, nvec);
+      break;
+    case 3:
+      hipLaunchKernelGGL((write_only<4, lfa::kStoreSc1>), grid, block, 0, s, (u32x4 *)dst,
+                         nvec);
+      break;
+    default:
+      return -LFA_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
