@@ -55,6 +55,7 @@ S_BYTES = 256 * 1024 * 1024            # BASELINE config 2: 256 MiB buffers
 COUNT = S_BYTES // 4                   # 67,108,864 float
 BUFFER_SETS = 4                        # rotate: 2 GiB of inputs >> 256 MiB MALL
 PEAK_GBPS = 8000.0                     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+ACCESS_MIX_CEILING_GBPS = 6756.0       # 2 reads + 1 write, tools/probe_hbm.py
 FI_SUM, FI_FLOAT = 2, 8
 
 
@@ -1470,6 +1471,13 @@ def main() -> None:
                       "kernel-trace summary in profiles/",
             "algorithmic_bytes_per_launch": 3 * shard_bytes,
             "traffic_source": traffic_src,
+            # HBM's own rate for this 2-read/1-write mix, measured apart
+            # (tools/probe_hbm.py): the practical ceiling beside the 8 TB/s spec
+            "access_mix_ceiling": {
+                "gb_s": ACCESS_MIX_CEILING_GBPS,
+                "frac": round(achieved / ACCESS_MIX_CEILING_GBPS, 4),
+                "source": "reads 7.00 TB/s, writes 6.32 TB/s alone; 3/(2/7.00+1/6.32) "
+                          "(profiles/r02_probe_hbm_access_mix.log)"},
         },
     }
     if REHEARSE:
