@@ -165,6 +165,13 @@ def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float) -> dict
                 break
             time.sleep(0.1)
         _CHILD = None
+        # rank 0 hosts the store: it leaves last, after every peer's final
+        # store call (this add) has been answered, so no peer still polling
+        # the fail key sees the store torn down under it
+        n_done = store.add(key + "_done", 1)
+        while rank == 0 and n_done < world:
+            time.sleep(0.05)
+            n_done = store.add(key + "_done", 0)
         out.seek(0)
         lines = [x for x in out.read().splitlines() if x.startswith("{")]
     res = {}
