@@ -283,6 +283,15 @@ enum lfa_step_type {
 	LFA_STEP_TREE_PUT = 9, /* TREE whose result also goes to `peer` more
 				  destinations: refs[first+nsrc ..
 				  first+nsrc+peer) (LFA_ALGO_P2P pushes)      */
+	LFA_STEP_ONESHOT = 10, /* dst = TREE over every rank's src (count
+				  elements, rank order), ONE kernel: src goes
+				  to slot `rank` of every member's SYM_IN
+				  (slots of count·esz rounded up to 256 B,
+				  double-buffered by the group's one-shot
+				  count), flags in the workspace order it.
+				  Same result as COPY src -> own slot, BARRIER,
+				  TREE over the slots, BARRIER.  LFA_ALGO_P2P
+				  small allreduces, 2..8 members.            */
 };
 /* SYM_IN / SYM_OUT: the symmetric workspace of group rank `ref.rank`, two
  * regions of count·esz bytes each (input staging, gathered result), mapped

@@ -65,6 +65,12 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     tune_o = os.path.join(BUILD, "lfa_tune.o")
     if _newer(tune_o, [tune] + hdrs):
         steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", tune_o])
+    # op-independent device code: the P2P flag barrier
+    sig = os.path.join(CSRC, "lfa_signal.hip")
+    o = os.path.join(BUILD, "lfa_signal.o")
+    objs.append(o)
+    if _newer(o, [sig, os.path.join(CSRC, "lfa_signal.h"), os.path.join(INC, "lfa_fabric.h")]):
+        steps.append([HIPCC, *HIP_FLAGS, "-c", sig, "-o", o])
     capi = os.path.join(CSRC, "lfa_capi.cpp")
     o = os.path.join(BUILD, "lfa_capi.o")
     objs.append(o)
@@ -105,7 +111,7 @@ def build_coll(verbose: bool = False) -> str | None:
                     ("lfa_coll_exec.c", "lfa_coll_plan.c", "lfa_coll_loopback.c")]
     hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "lfa_atomic.h"),
             os.path.join(INC, "lfa_fabric.h"), os.path.join(CSRC, "lfa_coll_plan.h"),
-            os.path.join(CSRC, "lfa_coll_int.h"), LIB_LFA]
+            os.path.join(CSRC, "lfa_coll_int.h"), os.path.join(CSRC, "lfa_signal.h"), LIB_LFA]
     if _newer(LIB_COLL, srcs + hdrs):
         # Plain C (the reference's host language), calling HIP's and RCCL's
         # C APIs; no HIP device code in this library.

@@ -32,7 +32,7 @@ c_ssize_t = ctypes.c_ssize_t
 
 ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL, ALGO_P2P = 0, 1, 2, 3, 4
 (STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY,
- STEP_ALLTOALL, STEP_ALLGATHER, STEP_BARRIER, STEP_TREE_PUT) = range(10)
+ STEP_ALLTOALL, STEP_ALLGATHER, STEP_BARRIER, STEP_TREE_PUT, STEP_ONESHOT) = range(11)
 BUF_SEND, BUF_RESULT, BUF_TMP, BUF_SYM_IN, BUF_SYM_OUT = 0, 1, 2, 3, 4
 ADDR_NOTAVAIL = (1 << 64) - 1
 EAGAIN, EIO = 11, 5

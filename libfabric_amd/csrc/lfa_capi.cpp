@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include "../../include/lfa_atomic.h"
+#include "lfa_signal.h"
 
 extern "C" {
 #define LFA_DECL_W(N)                                                          \
@@ -21,6 +22,7 @@ extern "C" {
 #define LFA_DECL_TP(N)                                                         \
   int lfa__treeput_op##N(int, void *const *, int, const void *const *, int,    \
                          size_t, void *);
+#define LFA_DECL_OS(N) int lfa__oneshot_op##N(int, const lfa_oneshot *, void *);
 #define LFA_DECL_RW(N)                                                         \
   int lfa__readwrite_op##N(int, void *, const void *, void *, size_t, void *);
 #define LFA_DECL_SW(N)                                                         \
@@ -33,6 +35,8 @@ LFA_DECL_T(0) LFA_DECL_T(1) LFA_DECL_T(2) LFA_DECL_T(3) LFA_DECL_T(4)
 LFA_DECL_T(5) LFA_DECL_T(6) LFA_DECL_T(7) LFA_DECL_T(8) LFA_DECL_T(9)
 LFA_DECL_TP(0) LFA_DECL_TP(1) LFA_DECL_TP(2) LFA_DECL_TP(3) LFA_DECL_TP(4)
 LFA_DECL_TP(5) LFA_DECL_TP(6) LFA_DECL_TP(7) LFA_DECL_TP(8) LFA_DECL_TP(9)
+LFA_DECL_OS(0) LFA_DECL_OS(1) LFA_DECL_OS(2) LFA_DECL_OS(3) LFA_DECL_OS(4)
+LFA_DECL_OS(5) LFA_DECL_OS(6) LFA_DECL_OS(7) LFA_DECL_OS(8) LFA_DECL_OS(9)
 LFA_DECL_RW(0) LFA_DECL_RW(1) LFA_DECL_RW(2) LFA_DECL_RW(3) LFA_DECL_RW(4)
 LFA_DECL_RW(5) LFA_DECL_RW(6) LFA_DECL_RW(7) LFA_DECL_RW(8) LFA_DECL_RW(9)
 LFA_DECL_RW(10) LFA_DECL_RW(11)
@@ -41,6 +45,7 @@ LFA_DECL_SW(16) LFA_DECL_SW(17) LFA_DECL_SW(18)
 #undef LFA_DECL_W
 #undef LFA_DECL_T
 #undef LFA_DECL_TP
+#undef LFA_DECL_OS
 #undef LFA_DECL_RW
 #undef LFA_DECL_SW
 }
@@ -77,6 +82,12 @@ const treeput_launch_t kTreePut[LFA_BXOR + 1] = {
     lfa__treeput_op0, lfa__treeput_op1, lfa__treeput_op2, lfa__treeput_op3,
     lfa__treeput_op4, lfa__treeput_op5, lfa__treeput_op6, lfa__treeput_op7,
     lfa__treeput_op8, lfa__treeput_op9};
+
+typedef int (*oneshot_launch_t)(int, const lfa_oneshot *, void *);
+const oneshot_launch_t kOneShot[LFA_BXOR + 1] = {
+    lfa__oneshot_op0, lfa__oneshot_op1, lfa__oneshot_op2, lfa__oneshot_op3,
+    lfa__oneshot_op4, lfa__oneshot_op5, lfa__oneshot_op6, lfa__oneshot_op7,
+    lfa__oneshot_op8, lfa__oneshot_op9};
 
 // Table membership (util_atomic.c:907-922, HAVE_BUILTIN_MM_ATOMICS build with
 // 128-bit atomics): REALNO = int8..double + int128; ALL = REALNO + float
@@ -338,6 +349,15 @@ int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype dt,
   for (int j = 0; j < ndst; j++)
     if (cnt && !dsts[j]) return -LFA_EINVAL;
   return kTreePut[op](dt, dsts, ndst, srcs, nsrc, cnt, stream);
+}
+
+int lfa_oneshot_allreduce_async(int op, int dt, const struct lfa_oneshot *a,
+                                void *stream) {
+  if ((unsigned)op > LFA_BXOR || (unsigned)dt >= LFA_DATATYPE_CNT ||
+      !in_table(op, dt))
+    return -LFA_EOPNOTSUPP;
+  if (!a) return -LFA_EINVAL;
+  return kOneShot[op](dt, a, stream);
 }
 
 }  // extern "C"

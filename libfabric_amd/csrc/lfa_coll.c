@@ -147,6 +147,8 @@ static void ep_release(struct lfa_coll_ep *ep)
 		hipFree(ep->ctl_dev);
 	if (ep->barrier_host)
 		hipHostFree(ep->barrier_host);
+	if (ep->sig_status)
+		hipHostFree(ep->sig_status);
 	if (ep->copy_stream)
 		hipStreamDestroy(ep->copy_stream);
 	if (ep->d2h_stream)
@@ -186,10 +188,13 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
 		    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess ||
 		    hipMalloc(&ep->ctl_dev, ctl) != hipSuccess ||
+		    hipHostMalloc((void **)&ep->sig_status, sizeof(uint32_t),
+				  hipHostMallocCoherent) != hipSuccess ||
 		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
+		*ep->sig_status = 0;
 		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	} else if (d->device >= 0) {
 		/* device buffers on a peer-transfer domain: the local items' kernels
@@ -197,10 +202,13 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		 * handshake records */
 		hipSetDevice(d->device);
 		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipHostMalloc((void **)&ep->sig_status, sizeof(uint32_t),
+				  hipHostMallocCoherent) != hipSuccess ||
 		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
+		*ep->sig_status = 0;
 	}
 	memset(ep->cid_mask, 0xff, sizeof(ep->cid_mask));
 	ep->cid_mask[0] &= (uint8_t)~1u;            /* world group id 0 taken */
@@ -232,6 +240,8 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		p2p_release(&ep->world);
 		if (ep->stream)
 			hipStreamDestroy(ep->stream);
+		if (ep->sig_status)
+			hipHostFree(ep->sig_status);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -258,6 +268,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	hipFree(ep->ctl_dev);
 	free(ep->ctl_host);
 	hipHostFree(ep->barrier_host);
+	hipHostFree(ep->sig_status);
 	hipStreamDestroy(ep->stream);
 	hipStreamDestroy(ep->copy_stream);
 	hipStreamDestroy(ep->d2h_stream);
@@ -620,6 +631,13 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 
 		if (st > 0)
 			break;
+		if (st == 0 && ep->sig_status && *(volatile uint32_t *)ep->sig_status) {
+			/* a flag barrier of this or an earlier operation gave up
+			 * waiting for a member (lfa_signal.hip) */
+			*ep->sig_status = 0;
+			st = -1;
+			perr = ETIMEDOUT;
+		}
 		if (p->kind == 0 && st == 0 && *nout >= count)
 			break;
 		if (st < 0) {
@@ -825,10 +843,18 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	memset(mine, 0, sizeof(*mine));
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
-	ok = ok && lfa_hip_note(why, hipMalloc((void **)&mc->sym_local, 2 * region),
+	ok = ok && lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
+					      2 * region + LFA_SIG_AREA_BYTES),
 				"P2P workspace hipMalloc") == hipSuccess;
 	if (!ok)
 		mc->sym_local = NULL;
+	/* the flag area starts at epoch 0, and is zero before any peer can
+	 * learn the handle and post into it (the agreement follows) */
+	ok = ok && lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
+						    LFA_SIG_AREA_BYTES, mc->ep->stream),
+				"P2P flag area memset") == hipSuccess &&
+	     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
+			  "P2P flag area memset sync") == hipSuccess;
 	if (ok && n > 1)
 		ok = lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
 				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
@@ -1137,7 +1163,8 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		return ret;
 	memset(&x, 0, sizeof(x));
 	if (plan_uses_sym(pl->steps, pl->nsteps)) {
-		ret = p2p_ensure(mc, sym_region(count, esz));
+		ret = p2p_ensure(mc, plan_sym_need(pl->steps, pl->nsteps, mc->size,
+						   count, esz));
 		if (ret)
 			return ret;
 		x.sym = mc->sym;
@@ -1339,7 +1366,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	if (ret)
 		return ret;
 	sym = plan_uses_sym(raw.steps, raw.nsteps);
-	ret = lower_plan(&raw, mc->rank, mc->size, &h->pl, sym);
+	/* a device hop's BARRIER stays: the flag kernel (sig_barrier) */
+	ret = lower_plan(&raw, mc->rank, mc->size, esz, &h->pl, sym && !dev, !dev);
 	plan_free(&raw);
 	if (ret)
 		return ret;
@@ -1347,7 +1375,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		/* the workspace is set up by hop_prologue, from progress; its two
 		 * possible handshakes get the next two seqs on every member */
 		h->phase = HOP_WAIT_PRIOR;
-		h->sym_need = sym_region(count, esz);
+		h->sym_need = plan_sym_need(h->pl.steps, h->pl.nsteps, mc->size,
+					    count, esz);
 		h->sub_seq = mc->seq;
 		mc->seq += 2;
 	}

@@ -105,7 +105,8 @@ LFA_INTERNAL int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 LFA_INTERNAL int plan_uses_sym(const struct lfa_step *st, size_t nsteps)
 {
 	for (size_t i = 0; i < nsteps; i++)
-		if (st[i].type == LFA_STEP_BARRIER || st[i].type == LFA_STEP_TREE_PUT)
+		if (st[i].type == LFA_STEP_BARRIER || st[i].type == LFA_STEP_TREE_PUT ||
+		    st[i].type == LFA_STEP_ONESHOT)
 			return 1;
 	return 0;
 }
@@ -116,6 +117,89 @@ LFA_INTERNAL size_t sym_region(size_t count, size_t esz)
 	return (count * esz + 255) & ~(size_t)255;
 }
 
+LFA_INTERNAL size_t plan_sym_need(const struct lfa_step *st, size_t nsteps, int n,
+				  size_t count, size_t esz)
+{
+	size_t need = sym_region(count, esz);
+
+	for (size_t i = 0; i < nsteps; i++)
+		if (st[i].type == LFA_STEP_ONESHOT &&
+		    2 * (size_t)n * sym_region(st[i].count, esz) > need)
+			need = 2 * (size_t)n * sym_region(st[i].count, esz);
+	return need;
+}
+
+
+/* How long a flag barrier waits for a member before failing the operation
+ * (LFA_SIG_TIMEOUT_MS, default 20 s). */
+static uint64_t sig_timeout_us(void)
+{
+	static uint64_t us;
+
+	if (!us) {
+		const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+		long ms = e ? atol(e) : 0;
+
+		us = (uint64_t)(ms > 0 ? ms : 20000) * 1000;
+	}
+	return us;
+}
+
+/*
+ * BARRIER of a plan on the symmetric workspace, stream-ordered: the one-wave
+ * flag kernel (lfa_signal.hip) posts this group's next epoch into every
+ * peer's barrier row and waits for theirs in its own — no RCCL collective,
+ * no host round trip.  The peers' rows are the IPC mappings the workspace
+ * handshake set up, so it runs wherever the P2P kernels do (RCCL device
+ * domains and GPU peer domains alike).
+ */
+LFA_INTERNAL int sig_barrier(struct xrun *r)
+{
+	struct lfa_coll_mc *mc = r->mc;
+	const size_t row = 2 * r->x.region + LFA_SIG_BAR_OFF;
+	uint32_t *post[LFA_SIG_MAX];
+	int ret;
+
+	if (!r->x.sym || mc->size > LFA_SIG_MAX || !mc->ep->sig_status)
+		return -LFA_EINVAL;
+	for (int k = 0; k < mc->size; k++)
+		post[k] = k == mc->rank ? NULL :
+			  (uint32_t *)(r->x.sym[k] + row) + mc->rank;
+	ret = lfa_flag_barrier_async(post, (const uint32_t *)(r->x.sym[mc->rank] + row),
+				     mc->size, mc->rank, mc->bar_epoch + 1,
+				     mc->ep->sig_status, sig_timeout_us(), r->stream);
+	if (!ret)
+		mc->bar_epoch++;
+	return ret;
+}
+
+LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
+{
+	struct lfa_coll_mc *mc = r->mc;
+	size_t esz = lfa_datatype_size(r->dt);
+	struct lfa_oneshot a;
+	int ret;
+
+	if (!r->x.sym || !mc->ep->sig_status || !esz || (int)st->nsrc != mc->size ||
+	    2 * (size_t)mc->size * sym_region(st->count, esz) > r->x.region)
+		return -LFA_EINVAL;
+	memset(&a, 0, sizeof(a));
+	a.send = resolve(&r->x, st->src);
+	a.result = resolve(&r->x, st->dst);
+	a.count = st->count;
+	a.sym = r->x.sym;
+	a.slot_bytes = sym_region(st->count, esz);
+	a.flag_off = 2 * r->x.region;
+	a.n = mc->size;
+	a.rank = mc->rank;
+	a.epoch = mc->os_epoch + 1;
+	a.status = mc->ep->sig_status;
+	a.timeout_us = sig_timeout_us();
+	ret = lfa_oneshot_allreduce_async(r->op, r->dt, &a, r->stream);
+	if (!ret)
+		mc->os_epoch++;
+	return ret;
+}
 
 /* Run the schedule as far as it goes: 1 done, 0 waiting on transfers, <0.
  * A post that returns -LFA_EAGAIN (the owner's queue is full: prov/coll
@@ -264,6 +348,15 @@ LFA_INTERNAL const struct xport xport_peer = {
 	peer_nop, peer_post, peer_nop, peer_test, peer_local, peer_coll,
 };
 
+/* device hops: a P2P plan's BARRIER is the flag kernel (host_start keeps it
+ * unlowered); ALLTOALL / ALLGATHER were lowered to transfers */
+static int pdev_coll(struct xrun *r, const struct lfa_step *st)
+{
+	if (st->type != LFA_STEP_BARRIER)
+		return -LFA_EINVAL;
+	return sig_barrier(r);
+}
+
 /*
  * ---- xport_peer_dev: device buffers over the owner's transfers ----------
  * The owner moves host bytes only (an FI_HMEM-less rxm), so every transfer
@@ -346,11 +439,13 @@ static int pdev_test(struct xrun *r, void *req)
 
 static int pdev_local(struct xrun *r, const struct lfa_step *st)
 {
+	if (st->type == LFA_STEP_ONESHOT)
+		return sig_oneshot(r, st);
 	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
 }
 
 LFA_INTERNAL const struct xport xport_peer_dev = {
-	peer_nop, pdev_post, peer_nop, pdev_test, pdev_local, peer_coll,
+	peer_nop, pdev_post, peer_nop, pdev_test, pdev_local, pdev_coll,
 };
 
 /* ---------------------------------------------------------------------- */
@@ -384,6 +479,8 @@ static int rccl_post(struct xrun *r, const struct lfa_step *st, void **req)
 
 static int rccl_local(struct xrun *r, const struct lfa_step *st)
 {
+	if (st->type == LFA_STEP_ONESHOT)
+		return sig_oneshot(r, st);
 	return run_local(st, r->pl->refs, &r->x, r->op, r->dt, r->stream);
 }
 
@@ -402,10 +499,14 @@ static int rccl_coll(struct xrun *r, const struct lfa_step *st)
 				  st->count, ncclUint8, c, r->stream);
 		break;
 	default: {
-		/* BARRIER, stream-ordered: a one-word allreduce completes on a
-		 * rank only after every member's stream has reached it */
+		/* BARRIER, stream-ordered.  On the symmetric workspace (P2P
+		 * plans): the flag kernel.  Otherwise a one-word allreduce,
+		 * which completes on a rank only after every member's stream
+		 * has reached it. */
 		uint64_t *w = (uint64_t *)r->mc->ep->barrier_dev + 2;
 
+		if (r->x.sym)
+			return sig_barrier(r);
 		e = ncclAllReduce(w, w, 1, ncclUint64, ncclSum, c, r->stream);
 	}
 	}

@@ -16,6 +16,7 @@
 #include "lfa_atomic.h"
 #include "lfa_coll.h"
 #include "lfa_coll_plan.h"
+#include "lfa_signal.h"
 
 #define LFA_MAX_GROUP_ID 256            /* OFI_MAX_GROUP_ID, ofi_coll.h:44 */
 #define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
@@ -24,7 +25,7 @@
 
 /* Where a plan's refs point for one execution: the operation's buffers and,
  * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
- * (IN region at 0, OUT region at `region`). */
+ * (IN region at 0, OUT region at `region`, flag area at 2·region). */
 struct xctx {
 	void *base[3];          /* SEND, RESULT, TMP */
 	char *const *sym;       /* [group rank] */
@@ -49,11 +50,16 @@ struct lfa_coll_mc {
 	/* join in flight */
 	uint8_t *mask_host;     /* pinned result of the cid-mask BAND */
 	void *join_context;
-	/* LFA_ALGO_P2P symmetric workspace: `sym_local` (2 regions, hipMalloc,
-	 * IPC-exported) and every member's as mapped here (sym[rank] = local) */
+	/* LFA_ALGO_P2P symmetric workspace: `sym_local` (2 regions + the flag
+	 * area, hipMalloc, IPC-exported) and every member's as mapped here
+	 * (sym[rank] = local) */
 	char *sym_local;
 	char **sym;
 	size_t sym_region;
+	/* flag barriers enqueued on this group so far (the epoch of the next
+	 * is one more; equal on every member, collectives being ordered) */
+	uint32_t bar_epoch;
+	uint32_t os_epoch;      /* one-shot operations, likewise */
 };
 
 struct lfa_coll_domain {
@@ -93,6 +99,7 @@ struct lfa_coll_ep {
 	void *barrier_dev;          /* 2 x uint64 */
 	void *ctl_dev;              /* P2P handle exchange, nranks records */
 	void *ctl_host;
+	uint32_t *sig_status;       /* host-mapped: a flag barrier timed out */
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
 	hipEvent_t evpool[64];      /* recycled completion events */
@@ -178,7 +185,14 @@ LFA_INTERNAL int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 			   hipStream_t stream);
 LFA_INTERNAL int plan_uses_sym(const struct lfa_step *st, size_t nsteps);
 LFA_INTERNAL size_t sym_region(size_t count, size_t esz);
+/* Bytes per workspace region the plan needs (ONESHOT: 2·n slots). */
+LFA_INTERNAL size_t plan_sym_need(const struct lfa_step *st, size_t nsteps, int n,
+				  size_t count, size_t esz);
 LFA_INTERNAL int xrun_advance(struct xrun *r);
+/* BARRIER of a plan on the symmetric workspace: the flag-barrier kernel. */
+LFA_INTERNAL int sig_barrier(struct xrun *r);
+/* ONESHOT step: the one-kernel small allreduce (lfa_signal.h). */
+LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st);
 LFA_INTERNAL int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 			   const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
 			   hipStream_t s);

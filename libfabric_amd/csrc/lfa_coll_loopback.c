@@ -60,7 +60,7 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		ret = plan_make(&raw, coll, algo, r, n, root, count, esz);
 		if (ret)
 			break;
-		ret = lower_plan(&raw, r, n, &pl[r], 0);
+		ret = lower_plan(&raw, r, n, esz, &pl[r], 0, 1);
 		plan_free(&raw);
 		if (!ret && pl[r].tmp &&
 		    hipMallocAsync(&tmp[r], pl[r].tmp, s) != hipSuccess)

@@ -14,6 +14,7 @@
 #include "lfa_atomic.h"
 #include "lfa_coll.h"
 #include "lfa_coll_plan.h"
+#include "lfa_signal.h"
 
 /* ====================================================================== */
 /* schedule builder                                                        */
@@ -176,6 +177,23 @@ static void p_tree_put_end(struct planner *p, uint32_t first, uint32_t nsrc,
 		s->first = first;
 		s->nsrc = nsrc;
 		s->peer = (int32_t)(p->nr - first - nsrc);
+		s->count = count;
+	}
+}
+
+static void p_oneshot(struct planner *p, struct lfa_ref dst, struct lfa_ref src,
+		      int n, uint64_t count)
+{
+	struct lfa_step *s;
+
+	p_group_end(p);
+	if (!count)
+		return;
+	s = push(p, LFA_STEP_ONESHOT);
+	if (s) {
+		s->dst = dst;
+		s->src = src;
+		s->nsrc = (uint32_t)n;
 		s->count = count;
 	}
 }
@@ -495,6 +513,12 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 	lfa_coll_block(count, n, r, &moff, &mlen);
 	switch (coll) {
 	case LFA_ALLREDUCE:
+		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES && n <= LFA_OS_MAX_RANKS) {
+			/* one kernel: push into the peers' slots, flags, tree */
+			p_oneshot(p, ref(LFA_BUF_RESULT, 0), ref(LFA_BUF_SEND, 0), n,
+				  count);
+			return 0;
+		}
 		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES) {
 			/* one phase: every rank reduces the whole vector */
 			p_copy(p, sref(LFA_BUF_SYM_IN, r, 0), ref(LFA_BUF_SEND, 0),
@@ -786,20 +810,28 @@ LFA_INTERNAL int plan_make(struct plan *pl, enum lfa_collective_op coll,
 /* Collective items -> grouped SEND/RECV items (transports without
  * collectives).  lower_barrier: BARRIER -> a ring of zero-byte messages,
  * every rank to every other (peer transports, whose sends leave only after
- * the rank's earlier items have completed). */
-LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, struct plan *out,
-			    int lower_barrier)
+ * the rank's earlier items have completed).  lower_oneshot: ONESHOT -> the
+ * items it is defined by (COPY src -> own SYM_IN, BARRIER, TREE over every
+ * rank's SYM_IN, BARRIER), for executors that run all ranks on one stream
+ * (the loopback), where one rank's kernel cannot wait for another's. */
+LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, size_t esz,
+			    struct plan *out, int lower_barrier, int lower_oneshot)
 {
-	size_t cap = in->nsteps + 1;
+	size_t cap = in->nsteps + 1, rcap = in->nrefs + 1;
 
-	for (size_t i = 0; i < in->nsteps; i++)
+	for (size_t i = 0; i < in->nsteps; i++) {
 		if (in->steps[i].type == LFA_STEP_ALLTOALL ||
 		    in->steps[i].type == LFA_STEP_ALLGATHER ||
 		    (lower_barrier && in->steps[i].type == LFA_STEP_BARRIER))
 			cap += 2 * (size_t)n + 2;
+		if (lower_oneshot && in->steps[i].type == LFA_STEP_ONESHOT) {
+			cap += 4;
+			rcap += (size_t)n;
+		}
+	}
 	memset(out, 0, sizeof(*out));
 	out->steps = calloc(cap, sizeof(*out->steps));
-	out->refs = calloc(in->nrefs ? in->nrefs : 1, sizeof(*out->refs));
+	out->refs = calloc(rcap, sizeof(*out->refs));
 	if (!out->steps || !out->refs) {
 		plan_free(out);
 		return -LFA_ENOMEM;
@@ -811,6 +843,32 @@ LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, struct plan *ou
 		const struct lfa_step *st = &in->steps[i];
 		int a2a = st->type == LFA_STEP_ALLTOALL;
 		struct lfa_step *o;
+
+		if (lower_oneshot && st->type == LFA_STEP_ONESHOT) {
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_COPY;
+			o->dst = sref(LFA_BUF_SYM_IN, r, 0);
+			o->src = st->src;
+			o->count = st->count * esz;     /* COPY counts bytes */
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_BARRIER;
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_TREE;
+			o->dst = st->dst;
+			o->first = (uint32_t)out->nrefs;
+			o->nsrc = st->nsrc;
+			o->count = st->count;
+			for (int k = 0; k < (int)st->nsrc; k++)
+				out->refs[out->nrefs++] = k == r ? st->src :
+							   sref(LFA_BUF_SYM_IN, k, 0);
+			o = &out->steps[out->nsteps++];
+			memset(o, 0, sizeof(*o));
+			o->type = LFA_STEP_BARRIER;
+			continue;
+		}
 
 		if (lower_barrier && st->type == LFA_STEP_BARRIER) {
 			for (int k = 1; k < n; k++) {

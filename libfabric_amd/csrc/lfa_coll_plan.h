@@ -26,8 +26,9 @@ LFA_INTERNAL void plan_free(struct plan *pl);
 LFA_INTERNAL int plan_make(struct plan *pl, enum lfa_collective_op coll,
 			   enum lfa_coll_algo algo, int rank, int n, int root,
 			   size_t count, size_t esz);
-/* Collective items -> grouped SEND/RECV items; lower_barrier: BARRIER too */
-LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, struct plan *out,
-			    int lower_barrier);
+/* Collective items -> grouped SEND/RECV items; lower_barrier: BARRIER too;
+ * lower_oneshot: ONESHOT -> COPY, BARRIER, TREE, BARRIER */
+LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, size_t esz,
+			    struct plan *out, int lower_barrier, int lower_oneshot);
 
 #endif

@@ -91,6 +91,14 @@ extern "C" int LFA_CAT(lfa__tree_op, LFA_OP)(int dt, void *dst,
   });
 }
 
+extern "C" int LFA_CAT(lfa__oneshot_op, LFA_OP)(int dt, const lfa_oneshot *a,
+                                                void *stream) {
+  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    return lfa::launch_oneshot<LFA_OP, T>(*a, (hipStream_t)stream);
+  });
+}
+
 extern "C" int LFA_CAT(lfa__treeput_op, LFA_OP)(int dt, void *const *dsts, int ndst,
                                                 const void *const *srcs, int nsrc,
                                                 size_t cnt, void *stream) {

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "lfa_ops.hpp"
+#include "lfa_signal.h"
 #include "../../include/lfa_atomic.h"
 
 namespace lfa {
@@ -482,6 +483,84 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t
 }
 
 // ---------------------------------------------------------------------------
+// one-shot allreduce (LFA_STEP_ONESHOT, lfa_signal.h): push, post, wait,
+// reduce — one launch for a small bucket instead of copy + barrier + tree +
+// barrier.  Workgroup b owns bytes [b·chunk, (b+1)·chunk) of the vector on
+// every rank, and synchronises only with the peers' workgroup b.
+// ---------------------------------------------------------------------------
+constexpr int kOsMax = LFA_OS_MAX_RANKS;
+
+struct OsArgs {
+  TreeArgs t;                  // in[k]: own input (k == rank) or own slot k
+  char *push[kOsMax];          // peer k's slot of this rank (k != rank)
+  uint32_t *post[kOsMax];      // peer k's one-shot rows, column `rank`
+  const uint32_t *wait;        // own one-shot rows
+  const char *send;
+  char *result;
+  uint32_t *status;
+  uint64_t timeout;            // wall-clock ticks
+  size_t bytes, chunk;         // chunk: a multiple of 16
+  uint32_t epoch;
+  int n, rank;
+  int vec;                     // input, result 16-B aligned (slots are)
+};
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void oneshot_allreduce(OsArgs a) {
+  constexpr size_t E = sizeof(T);
+  const unsigned t = threadIdx.x;
+  const size_t b = blockIdx.x;
+  const size_t lo = b * a.chunk;
+  const size_t hi = lo + a.chunk < a.bytes ? lo + a.chunk : a.bytes;
+  const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;   // end of the 16-B body
+  // 1. push this rank's chunk into its slot on every peer (write-through)
+  for (int k = 0; k < a.n; k++) {  // wave-uniform
+    if (k == a.rank) continue;
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(a.push[k], (unsigned)a.bytes);
+    for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16)
+      __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(a.send + o), r,
+                                             (unsigned)o, 0, kSysAux);
+    for (size_t o = vhi + t; o < hi; o += kBlock)
+      sys_store<uint8_t>((uint8_t *)a.push[k] + o, (uint8_t)a.send[o]);
+  }
+  // 2. every wave's pushes complete and visible, then one post per peer
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if ((int)t < a.n && (int)t != a.rank) {
+    __hip_atomic_store(a.post[t] + b * LFA_SIG_MAX, a.epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    // 3. wait for peer t's workgroup b (bounded: *status on timeout)
+    const uint32_t *w = a.wait + b * LFA_SIG_MAX + t;
+    const uint64_t t0 = wall_clock64();
+    while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
+                     a.epoch) < 0) {
+      if (wall_clock64() - t0 > a.timeout) {
+        __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // 4. reduce chunk b over every rank's input, rank order (system-scope
+  //    loads: the slots were written by peers over xGMI)
+  for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16) {
+    u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)a.bytes),
+                                                       (unsigned)o, 0, kSysLoadAux));
+    });
+    *(u32x4 *)(a.result + o) = v;
+  }
+  for (size_t e = vhi / E + t; e < hi / E; e += kBlock) {
+    T v = tree_eval_with<OP, T, T, NLEAF>(
+        a.t, [&](int k) { return sys_load<T>((const T *)a.t.in[k] + e); });
+    ((T *)a.result)[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // fetch (readwrite) and compare-swap tables
 // ---------------------------------------------------------------------------
 // One launch shape for both: a functor F carries the operand pointers and
@@ -910,6 +989,64 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
       case 32: return launch_tree_put_n<OP, T, 32>(a, cnt, vec, head, s);
       default: return -LFA_EINVAL;
     }
+  }
+}
+
+template <int OP, typename T>
+static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
+  if constexpr (!supported<OP, T>()) {
+    return -LFA_EOPNOTSUPP;
+  } else {
+    constexpr size_t E = sizeof(T);
+    const int n = h.n, r = h.rank;
+    if (n < 2 || n > kOsMax || r < 0 || r >= n || !h.sym || !h.status) return -LFA_EINVAL;
+    if (h.count == 0) return 0;
+    const size_t bytes = h.count * E;
+    if (!h.send || !h.result || (uintptr_t)h.send % E || (uintptr_t)h.result % E ||
+        h.slot_bytes < bytes || h.slot_bytes % 256 || bytes > 0xffffffffu)
+      return -LFA_EINVAL;
+    for (int k = 0; k < n; k++)
+      if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
+    OsArgs a;
+    memset(&a, 0, sizeof(a));
+    const void *srcs[kOsMax];
+    const size_t par = (size_t)(h.epoch & 1) * (size_t)n;
+    for (int k = 0; k < n; k++) {
+      srcs[k] = k == r ? h.send : h.sym[r] + (par + (size_t)k) * h.slot_bytes;
+      if (k != r) {
+        a.push[k] = h.sym[k] + (par + (size_t)r) * h.slot_bytes;
+        a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
+      }
+    }
+    const int pof2 = tree_leaves(a.t, srcs, n);
+    a.wait = (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF);
+    a.send = (const char *)h.send;
+    a.result = (char *)h.result;
+    a.status = h.status;
+    a.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
+    a.bytes = bytes;
+    size_t chunk = (bytes + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
+    chunk = (chunk + 15) & ~(size_t)15;
+    a.chunk = chunk < 4096 ? 4096 : chunk;
+    a.epoch = h.epoch;
+    a.n = n;
+    a.rank = r;
+    a.vec = (uintptr_t)h.send % 16 == 0 && (uintptr_t)h.result % 16 == 0 && E <= 16;
+    const unsigned grid = (unsigned)((bytes + a.chunk - 1) / a.chunk);
+    switch (pof2) {
+      case 2:
+        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, a);
+        break;
+      case 4:
+        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, a);
+        break;
+      case 8:
+        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+        break;
+      default:
+        return -LFA_EINVAL;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
   }
 }
 

@@ -1,0 +1,76 @@
+/*
+ * lfa_signal.h — device-side synchronisation over the LFA_ALGO_P2P symmetric
+ * workspace (liblfa.so; called by liblfa_coll.so, not installed).
+ *
+ * Every member's workspace ends in a flag area of LFA_SIG_AREA_BYTES that its
+ * peers map over IPC.  Word k of the barrier row is written only by group rank
+ * k, with a per-group epoch that grows by one per barrier, so a rank waits on
+ * its OWN memory (local polling) while its peers post into it over xGMI.
+ * prov/coll's barrier is a zero-byte allreduce through the work queue
+ * (coll_coll.c:997-1038); on device buffers the same ordering point is this
+ * one-wave kernel on the endpoint stream instead of an RCCL collective.
+ */
+#ifndef LFA_SIGNAL_H
+#define LFA_SIGNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LFA_SIG_MAX 32                  /* ranks (= LFA_TREE_MAX) */
+#define LFA_SIG_AREA_BYTES (64u << 10)  /* flag area after the two regions */
+#define LFA_SIG_BAR_OFF 0               /* barrier row: uint32[LFA_SIG_MAX] */
+/* one-shot rows: uint32[LFA_SIG_OS_CHUNKS][LFA_SIG_MAX], word [b][k] written
+ * by rank k's workgroup b */
+#define LFA_SIG_OS_OFF 256
+#define LFA_SIG_OS_CHUNKS 128
+#define LFA_OS_MAX_RANKS 8              /* one-shot groups: 2..8 members */
+
+/*
+ * Enqueue a barrier on `stream`: after the steps before it on every member's
+ * stream, before the steps after it.  post[k] (k != rank) = this rank's word
+ * in peer k's barrier row (IPC-mapped); wait = this rank's own barrier row.
+ * A peer that has not posted `epoch` within timeout_us makes the kernel store
+ * 1 into *status (host-mapped memory) and return.  0 or -LFA_E*.
+ */
+int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
+			   int rank, uint32_t epoch, uint32_t *status,
+			   uint64_t timeout_us, void *stream);
+
+/*
+ * One-shot allreduce (LFA_STEP_ONESHOT) of `count` elements, ONE kernel:
+ * workgroup b pushes chunk b of this rank's input into slot `rank` of every
+ * peer's SYM_IN (system-scope stores over xGMI), posts `epoch` into row b of
+ * every peer's one-shot rows, waits for every peer's post in its own row b,
+ * then reduces chunk b of all ranks' inputs — its own slots, its own input
+ * for itself — in prov/coll's association order into `result`.  Slots are
+ * double-buffered by epoch parity: member j holds rank k's input of epoch e
+ * at sym[j] + ((e & 1)·n + k)·slot_bytes, so a peer one operation ahead
+ * never overwrites a slot still being read.  Needs 2·n·slot_bytes of SYM_IN.
+ */
+struct lfa_oneshot {
+	const void *send;       /* this rank's input, count elements */
+	void *result;           /* count elements */
+	size_t count;
+	char *const *sym;       /* [n]: every member's workspace as mapped here */
+	size_t slot_bytes;      /* one slot: count·esz rounded up to 256 */
+	size_t flag_off;        /* the flag area's offset in a workspace */
+	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
+	uint32_t epoch;         /* this group's one-shot operations so far + 1 */
+	uint32_t *status;       /* host-mapped; 1 after a timed-out wait */
+	uint64_t timeout_us;
+};
+int lfa_oneshot_allreduce_async(int op, int datatype, const struct lfa_oneshot *a,
+				void *stream);
+
+/* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
+uint64_t lfa__wallclock_ticks_per_us(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

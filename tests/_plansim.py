@@ -11,15 +11,28 @@ import numpy as np
 import oracle
 from libfabric_amd import coll
 
-SEND, RECV, GEND, REDUCE, TREE, COPY, ALLTOALL, ALLGATHER, BARRIER, TREE_PUT = range(10)
+SEND, RECV, GEND, REDUCE, TREE, COPY, ALLTOALL, ALLGATHER, BARRIER, TREE_PUT, ONESHOT = \
+    range(11)
 SYM_IN, SYM_OUT = 3, 4
 
 
-def lower(steps, r, n):
-    """ALLTOALL / ALLGATHER -> grouped SEND/RECV + COPY (as lfa_coll.c's
-    lower_plan does for its loopback executor)."""
+def lower(steps, r, n, refs=None, esz=None):
+    """ALLTOALL / ALLGATHER -> grouped SEND/RECV + COPY, and ONESHOT -> the
+    COPY / BARRIER / TREE / BARRIER it is defined by (as lfa_coll_plan.c's
+    lower_plan does for its loopback executor); ONESHOT's tree inputs are
+    appended to `refs`."""
     out = []
     for s in steps:
+        if s["type"] == ONESHOT:
+            first = len(refs)
+            refs.extend(s["src"] if k == r else (SYM_IN, 0, k) for k in range(s["nsrc"]))
+            out.append({"type": COPY, "count": s["count"] * esz, "src": s["src"],
+                        "dst": (SYM_IN, 0, r), "peer": 0})
+            out.append({"type": BARRIER, "count": 0, "src": (0, 0), "dst": (0, 0), "peer": 0})
+            out.append({"type": TREE, "count": s["count"], "dst": s["dst"], "first": first,
+                        "nsrc": s["nsrc"], "src": (0, 0), "peer": 0})
+            out.append({"type": BARRIER, "count": 0, "src": (0, 0), "dst": (0, 0), "peer": 0})
+            continue
         if s["type"] not in (ALLTOALL, ALLGATHER):
             out.append(s)
             continue
@@ -63,7 +76,8 @@ def run(coll_op, algo, n, root, dt, op, count, sends, results):
     nd = oracle.DT_NP[dt]
     plans = [coll.plan(coll_op, algo, r, n, root, count, esz) for r in range(n)]
     for r in range(n):
-        plans[r].steps = lower(plans[r].steps, r, n)
+        plans[r].refs = list(plans[r].refs)
+        plans[r].steps = lower(plans[r].steps, r, n, plans[r].refs, esz)
     region = (count * esz + 255) // 256 * 256
     # symmetric workspaces (LFA_ALGO_P2P), poisoned so stale reads show
     sym = [np.full(2 * region, 0xA5, np.uint8) for _ in range(n)]

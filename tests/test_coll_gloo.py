@@ -46,7 +46,8 @@ def _exec_plan(pl, bufs, op, dt, esz, nd, seq, jitter=None):
     import time
     import oracle
     from tests._plansim import lower
-    st = lower(pl.steps, dist.get_rank(), dist.get_world_size())
+    pl.refs = list(pl.refs)
+    st = lower(pl.steps, dist.get_rank(), dist.get_world_size(), pl.refs, esz)
     i = 0
     while i < len(st):
         s = st[i]

@@ -261,3 +261,72 @@ def test_p2p_workspace_growth_in_flight():
                 p.kill()
     for r in range(world):
         assert results.get(r) == "ok", results.get(r)
+
+
+def _timeout_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                          LFA_SIG_TIMEOUT_MS="300")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            sends = _inputs(oracle, 8, 4096, world, 5)
+            want = oracle.allreduce(2, 8, sends)[0]
+            r = torch.zeros(4096, dtype=torch.float32, device="cuda")
+            xs = _dev(sends[rank])
+            _ready()
+            ep.wait(ep.allreduce(xs, r, 4096, 8, 2))
+            assert r.cpu().numpy().tobytes() == want.tobytes()
+            msg = "ok"
+            if rank == 1:
+                # rank 0 skips this collective: the flag barrier gives up
+                # after LFA_SIG_TIMEOUT_MS and the operation completes in
+                # error (prov_errno ETIMEDOUT) instead of spinning forever
+                import time
+                t0 = time.time()
+                try:
+                    ep.wait(ep.allreduce(xs, r, 4096, 8, 2), timeout_s=30)
+                    msg = "no error"
+                except coll.CollError as e:
+                    msg = "ok" if "prov_errno 110" in str(e) else f"wrong error {e}"
+                if time.time() - t0 > 10:
+                    msg = f"took {time.time() - t0:.1f} s"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_flag_barrier_timeout_is_an_error_completion():
+    """LFA_ALGO_P2P's device-side flag barrier (lfa_signal.hip) is bounded:
+    when a member never joins the collective, the waiting rank's operation
+    completes with an error after LFA_SIG_TIMEOUT_MS, and the kernel retires."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=100)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)

@@ -155,7 +155,21 @@ def test_p2p_schedule_shape():
 
 
 def test_p2p_small_allreduce_is_one_phase():
+    """Small P2P allreduces of 2..8 members are ONE step (the one-shot
+    kernel: push into the peers' slots, flags, tree); above 8 members the
+    one-phase copy / barrier / tree / barrier form."""
     n, count = 4, 1000
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 1, n, -1, count, 4)
+    assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT]
+    s = p.steps[0]
+    assert s["count"] == count and s["nsrc"] == n
+    assert s["src"] == (coll.BUF_SEND, 0) and s["dst"] == (coll.BUF_RESULT, 0)
+    # the largest bucket that still fits 256 KiB over all members
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, (256 << 10) // 32, 4)
+    assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT]
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, (256 << 10) // 32 + 1, 4)
+    assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
+    n = 9
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 1, n, -1, count, 4)
     assert [s["type"] for s in p.steps] == [coll.STEP_COPY, coll.STEP_BARRIER,
                                             coll.STEP_TREE_PUT, coll.STEP_BARRIER]

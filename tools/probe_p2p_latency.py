@@ -1,0 +1,103 @@
+"""Small-bucket latency of LFA_ALGO_P2P across PROCESSES on one MI355X.
+
+N processes (default 2) share device 0 through GPU peer domains
+(lfa_coll_domain_open_peer, the gloo owner transport of the tests): with
+LFA_ALGO_P2P every operation runs on the GPU alone — staging copy, flag
+barrier (lfa_signal.hip), the system-scope tree kernel over the peers'
+IPC-mapped workspaces, closing flag barrier — so this times that path's
+kernels and its host submit/complete cost.  Beside it, the TREE schedule on
+the same domain, whose transfers go through the owner's (gloo) transport.
+Not xGMI: the peers' workspaces are this GPU's own HBM.
+
+  python tools/probe_p2p_latency.py [--world 2] [--reps 300]
+prints one JSON line (median / p10 / p90 us per allreduce, per size).
+"""
+import argparse
+import json
+import os
+import socket
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, reps, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        out = {}
+        try:
+            for name, algo, sizes, n in (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                                         ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10))):
+                ep.set_algo(algo)
+                for nbytes in sizes:
+                    cnt = nbytes // 4
+                    x = torch.rand(cnt, device="cuda")
+                    r = torch.empty_like(x)
+                    torch.cuda.synchronize()
+                    for _ in range(20):
+                        ep.wait(ep.allreduce(x, r, cnt, 8, 2))
+                    dist.barrier()
+                    ts = []
+                    for _ in range(n):
+                        t0 = time.perf_counter()
+                        ep.wait(ep.allreduce(x, r, cnt, 8, 2))
+                        ts.append(time.perf_counter() - t0)
+                    ts.sort()
+                    out[f"{name}_{nbytes}"] = {
+                        "median_us": round(statistics.median(ts) * 1e6, 1),
+                        "p10_us": round(ts[len(ts) // 10] * 1e6, 1),
+                        "p90_us": round(ts[9 * len(ts) // 10] * 1e6, 1), "reps": n}
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=300)
+    a = ap.parse_args()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.reps, q))
+             for r in range(a.world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(a.world))
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    print(json.dumps({"world": a.world, "device": "one MI355X shared by all ranks",
+                      "rank0": res[0], "rank1": res.get(1)}), flush=True)
+    if not all(isinstance(v, dict) for v in res.values()):
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
