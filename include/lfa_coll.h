@@ -283,16 +283,23 @@ enum lfa_step_type {
 	LFA_STEP_TREE_PUT = 9, /* TREE whose result also goes to `peer` more
 				  destinations: refs[first+nsrc ..
 				  first+nsrc+peer) (LFA_ALGO_P2P pushes)      */
-	LFA_STEP_ONESHOT = 10, /* dst = TREE over every rank's src (count
-				  elements, rank order), ONE kernel: src goes
-				  to slot `rank` of every member's SYM_IN
-				  (slots of count·esz rounded up to 256 B,
+	LFA_STEP_ONESHOT = 10, /* ONE kernel for a small reducing collective
+				  over `count` elements of src, rank order:
+				  peer = LFA_ONESHOT_ALL: dst = the whole
+				  result (allreduce); LFA_ONESHOT_SCATTER:
+				  dst = block `rank` (reduce_scatter); root
+				  >= 0: dst = the whole result on the root
+				  only (reduce).  Each rank's part for member
+				  k goes to slot `rank` of k's SYM_IN (slots
 				  double-buffered by the group's one-shot
 				  count), flags in the workspace order it.
-				  Same result as COPY src -> own slot, BARRIER,
-				  TREE over the slots, BARRIER.  LFA_ALGO_P2P
-				  small allreduces, 2..8 members.            */
+				  Same result as COPY src -> own SYM_IN,
+				  BARRIER, TREE of the part over every rank's
+				  SYM_IN, BARRIER.  LFA_ALGO_P2P, 2..8
+				  members.                                   */
 };
+#define LFA_ONESHOT_ALL (-1)
+#define LFA_ONESHOT_SCATTER (-2)
 /* SYM_IN / SYM_OUT: the symmetric workspace of group rank `ref.rank`, two
  * regions of count·esz bytes each (input staging, gathered result), mapped
  * into every member's address space; offsets mirror SEND / RESULT. */

@@ -117,6 +117,16 @@ LFA_INTERNAL size_t sym_region(size_t count, size_t esz)
 	return (count * esz + 255) & ~(size_t)255;
 }
 
+/* One ONESHOT slot: the largest part any member reduces. */
+static size_t os_slot(const struct lfa_step *st, int n, size_t esz)
+{
+	size_t part = st->count;
+
+	if (st->peer == LFA_ONESHOT_SCATTER)
+		part = (st->count + (size_t)n - 1) / (size_t)n;
+	return sym_region(part, esz);
+}
+
 LFA_INTERNAL size_t plan_sym_need(const struct lfa_step *st, size_t nsteps, int n,
 				  size_t count, size_t esz)
 {
@@ -124,8 +134,8 @@ LFA_INTERNAL size_t plan_sym_need(const struct lfa_step *st, size_t nsteps, int 
 
 	for (size_t i = 0; i < nsteps; i++)
 		if (st[i].type == LFA_STEP_ONESHOT &&
-		    2 * (size_t)n * sym_region(st[i].count, esz) > need)
-			need = 2 * (size_t)n * sym_region(st[i].count, esz);
+		    2 * (size_t)n * os_slot(&st[i], n, esz) > need)
+			need = 2 * (size_t)n * os_slot(&st[i], n, esz);
 	return need;
 }
 
@@ -181,14 +191,16 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	int ret;
 
 	if (!r->x.sym || !mc->ep->sig_status || !esz || (int)st->nsrc != mc->size ||
-	    2 * (size_t)mc->size * sym_region(st->count, esz) > r->x.region)
+	    2 * (size_t)mc->size * os_slot(st, mc->size, esz) > r->x.region)
 		return -LFA_EINVAL;
 	memset(&a, 0, sizeof(a));
 	a.send = resolve(&r->x, st->src);
-	a.result = resolve(&r->x, st->dst);
+	/* reduce: a non-root has no result */
+	a.result = st->peer >= 0 && st->peer != mc->rank ? NULL : resolve(&r->x, st->dst);
 	a.count = st->count;
+	a.mode = st->peer;
 	a.sym = r->x.sym;
-	a.slot_bytes = sym_region(st->count, esz);
+	a.slot_bytes = os_slot(st, mc->size, esz);
 	a.flag_off = 2 * r->x.region;
 	a.n = mc->size;
 	a.rank = mc->rank;

@@ -181,8 +181,7 @@ static void p_tree_put_end(struct planner *p, uint32_t first, uint32_t nsrc,
 	}
 }
 
-static void p_oneshot(struct planner *p, struct lfa_ref dst, struct lfa_ref src,
-		      int n, uint64_t count)
+static void p_oneshot(struct planner *p, int mode, int n, uint64_t count)
 {
 	struct lfa_step *s;
 
@@ -191,8 +190,9 @@ static void p_oneshot(struct planner *p, struct lfa_ref dst, struct lfa_ref src,
 		return;
 	s = push(p, LFA_STEP_ONESHOT);
 	if (s) {
-		s->dst = dst;
-		s->src = src;
+		s->dst = ref(LFA_BUF_RESULT, 0);
+		s->src = ref(LFA_BUF_SEND, 0);
+		s->peer = mode;
 		s->nsrc = (uint32_t)n;
 		s->count = count;
 	}
@@ -515,8 +515,7 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 	case LFA_ALLREDUCE:
 		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES && n <= LFA_OS_MAX_RANKS) {
 			/* one kernel: push into the peers' slots, flags, tree */
-			p_oneshot(p, ref(LFA_BUF_RESULT, 0), ref(LFA_BUF_SEND, 0), n,
-				  count);
+			p_oneshot(p, LFA_ONESHOT_ALL, n, count);
 			return 0;
 		}
 		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES) {
@@ -540,11 +539,19 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 		p2p_unstage_output(p, r, n, count, esz, r);
 		return 0;
 	case LFA_REDUCE_SCATTER:
+		if (bytes <= LFA_OS_RS_BYTES && n <= LFA_OS_MAX_RANKS) {
+			p_oneshot(p, LFA_ONESHOT_SCATTER, n, count);
+			return 0;
+		}
 		p2p_stage_input(p, r, n, count, esz);
 		p2p_tree_block(p, r, n, count, esz, ref(LFA_BUF_RESULT, 0), 0);
 		p_barrier(p);
 		return 0;
 	case LFA_REDUCE:
+		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES && n <= LFA_OS_MAX_RANKS) {
+			p_oneshot(p, root, n, count);
+			return 0;
+		}
 		p2p_stage_input(p, r, n, count, esz);
 		p2p_tree_block(p, r, n, count, esz,
 			       r == root ? ref(LFA_BUF_RESULT, moff * esz) :
@@ -845,6 +852,13 @@ LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, size_t esz,
 		struct lfa_step *o;
 
 		if (lower_oneshot && st->type == LFA_STEP_ONESHOT) {
+			/* this rank's part: [moff, moff + mlen) of the vector */
+			size_t moff = 0, mlen = st->count;
+
+			if (st->peer == LFA_ONESHOT_SCATTER)
+				lfa_coll_block(st->count, n, r, &moff, &mlen);
+			else if (st->peer >= 0 && st->peer != r)
+				mlen = 0;
 			o = &out->steps[out->nsteps++];
 			memset(o, 0, sizeof(*o));
 			o->type = LFA_STEP_COPY;
@@ -854,16 +868,22 @@ LFA_INTERNAL int lower_plan(const struct plan *in, int r, int n, size_t esz,
 			o = &out->steps[out->nsteps++];
 			memset(o, 0, sizeof(*o));
 			o->type = LFA_STEP_BARRIER;
-			o = &out->steps[out->nsteps++];
-			memset(o, 0, sizeof(*o));
-			o->type = LFA_STEP_TREE;
-			o->dst = st->dst;
-			o->first = (uint32_t)out->nrefs;
-			o->nsrc = st->nsrc;
-			o->count = st->count;
-			for (int k = 0; k < (int)st->nsrc; k++)
-				out->refs[out->nrefs++] = k == r ? st->src :
-							   sref(LFA_BUF_SYM_IN, k, 0);
+			if (mlen) {
+				o = &out->steps[out->nsteps++];
+				memset(o, 0, sizeof(*o));
+				o->type = LFA_STEP_TREE;
+				o->dst = st->dst;
+				o->first = (uint32_t)out->nrefs;
+				o->nsrc = st->nsrc;
+				o->count = mlen;
+				for (int k = 0; k < (int)st->nsrc; k++) {
+					struct lfa_ref in = k == r ? st->src :
+							    sref(LFA_BUF_SYM_IN, k, 0);
+
+					in.off += moff * esz;
+					out->refs[out->nrefs++] = in;
+				}
+			}
 			o = &out->steps[out->nsteps++];
 			memset(o, 0, sizeof(*o));
 			o->type = LFA_STEP_BARRIER;

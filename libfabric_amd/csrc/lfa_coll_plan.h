@@ -13,6 +13,7 @@
 
 #define LFA_INTERNAL __attribute__((visibility("hidden")))
 #define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
+#define LFA_OS_RS_BYTES (1u << 20)      /* P2P reduce_scatter: one-shot */
 
 /* A heap-allocated plan. */
 struct plan {

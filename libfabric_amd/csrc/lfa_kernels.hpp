@@ -483,45 +483,51 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t
 }
 
 // ---------------------------------------------------------------------------
-// one-shot allreduce (LFA_STEP_ONESHOT, lfa_signal.h): push, post, wait,
+// one-shot reduction (LFA_STEP_ONESHOT, lfa_signal.h): push, post, wait,
 // reduce — one launch for a small bucket instead of copy + barrier + tree +
-// barrier.  Workgroup b owns bytes [b·chunk, (b+1)·chunk) of the vector on
-// every rank, and synchronises only with the peers' workgroup b.
+// barrier.  Destination k receives bytes [soff[k], soff[k] + slen[k]) of this
+// rank's input (the whole vector for allreduce, block k for reduce_scatter,
+// the root alone for reduce).  Workgroup b owns bytes [b·chunk, (b+1)·chunk)
+// of every such range and synchronises only with the peers' workgroup b.
 // ---------------------------------------------------------------------------
 constexpr int kOsMax = LFA_OS_MAX_RANKS;
 
 struct OsArgs {
-  TreeArgs t;                  // in[k]: own input (k == rank) or own slot k
+  TreeArgs t;                  // in[k]: own input range (k == rank) or own slot k
   char *push[kOsMax];          // peer k's slot of this rank (k != rank)
   uint32_t *post[kOsMax];      // peer k's one-shot rows, column `rank`
+  size_t soff[kOsMax];         // input range pushed to k (k == rank: reduced)
+  size_t slen[kOsMax];
   const uint32_t *wait;        // own one-shot rows
   const char *send;
   char *result;
   uint32_t *status;
   uint64_t timeout;            // wall-clock ticks
-  size_t bytes, chunk;         // chunk: a multiple of 16
+  size_t chunk;                // a multiple of 16
   uint32_t epoch;
   int n, rank;
-  int vec;                     // input, result 16-B aligned (slots are)
+  int vec;                     // every range start and result 16-B aligned
 };
 
 template <int OP, typename T, int NLEAF>
-__global__ __launch_bounds__(kBlock) void oneshot_allreduce(OsArgs a) {
+__global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   constexpr size_t E = sizeof(T);
   const unsigned t = threadIdx.x;
   const size_t b = blockIdx.x;
   const size_t lo = b * a.chunk;
-  const size_t hi = lo + a.chunk < a.bytes ? lo + a.chunk : a.bytes;
-  const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;   // end of the 16-B body
-  // 1. push this rank's chunk into its slot on every peer (write-through)
+  // 1. push this rank's chunk of each destination's range into its slot on
+  //    that peer (system-scope write-through stores over xGMI)
   for (int k = 0; k < a.n; k++) {  // wave-uniform
-    if (k == a.rank) continue;
-    const __amdgpu_buffer_rsrc_t r = tile_rsrc(a.push[k], (unsigned)a.bytes);
+    if (k == a.rank || lo >= a.slen[k]) continue;
+    const size_t hi = lo + a.chunk < a.slen[k] ? lo + a.chunk : a.slen[k];
+    const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;
+    const char *src = a.send + a.soff[k];
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(a.push[k], (unsigned)a.slen[k]);
     for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16)
-      __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(a.send + o), r,
-                                             (unsigned)o, 0, kSysAux);
+      __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(src + o), r, (unsigned)o, 0,
+                                             kSysAux);
     for (size_t o = vhi + t; o < hi; o += kBlock)
-      sys_store<uint8_t>((uint8_t *)a.push[k] + o, (uint8_t)a.send[o]);
+      sys_store<uint8_t>((uint8_t *)a.push[k] + o, (uint8_t)src[o]);
   }
   // 2. every wave's pushes complete and visible, then one post per peer
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -543,12 +549,16 @@ __global__ __launch_bounds__(kBlock) void oneshot_allreduce(OsArgs a) {
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  // 4. reduce chunk b over every rank's input, rank order (system-scope
-  //    loads: the slots were written by peers over xGMI)
+  // 4. reduce chunk b of this rank's own range over every rank's input, rank
+  //    order (system-scope loads: the slots were written by peers over xGMI)
+  const size_t own = a.slen[a.rank];
+  if (lo >= own) return;
+  const size_t hi = lo + a.chunk < own ? lo + a.chunk : own;
+  const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;
   for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16) {
     u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
       return __builtin_bit_cast(
-          u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)a.bytes),
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)own),
                                                        (unsigned)o, 0, kSysLoadAux));
     });
     *(u32x4 *)(a.result + o) = v;
@@ -999,20 +1009,37 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
   } else {
     constexpr size_t E = sizeof(T);
     const int n = h.n, r = h.rank;
-    if (n < 2 || n > kOsMax || r < 0 || r >= n || !h.sym || !h.status) return -LFA_EINVAL;
+    if (n < 2 || n > kOsMax || r < 0 || r >= n || !h.sym || !h.status ||
+        h.mode < LFA_ONESHOT_SCATTER || h.mode >= n)
+      return -LFA_EINVAL;
     if (h.count == 0) return 0;
-    const size_t bytes = h.count * E;
-    if (!h.send || !h.result || (uintptr_t)h.send % E || (uintptr_t)h.result % E ||
-        h.slot_bytes < bytes || h.slot_bytes % 256 || bytes > 0xffffffffu)
+    OsArgs a;
+    memset(&a, 0, sizeof(a));
+    size_t most = 0;
+    for (int k = 0; k < n; k++) {
+      if (h.mode == LFA_ONESHOT_SCATTER) {  // lfa_coll_block's partition
+        const size_t base = h.count / (size_t)n, extra = h.count % (size_t)n;
+        const size_t kk = (size_t)k;
+        a.slen[k] = (base + (kk < extra ? 1 : 0)) * E;
+        a.soff[k] = (kk * base + (kk < extra ? kk : extra)) * E;
+      } else {
+        a.slen[k] = h.mode == LFA_ONESHOT_ALL || h.mode == k ? h.count * E : 0;
+      }
+      if (a.slen[k] > most) most = a.slen[k];
+    }
+    if (!h.send || (!h.result && a.slen[r]) || (uintptr_t)h.send % E ||
+        (uintptr_t)h.result % E ||
+        h.slot_bytes < most || h.slot_bytes % 256 || most > 0xffffffffu)
       return -LFA_EINVAL;
     for (int k = 0; k < n; k++)
       if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
-    OsArgs a;
-    memset(&a, 0, sizeof(a));
     const void *srcs[kOsMax];
     const size_t par = (size_t)(h.epoch & 1) * (size_t)n;
+    uintptr_t mis = (uintptr_t)h.result % 16;
     for (int k = 0; k < n; k++) {
-      srcs[k] = k == r ? h.send : h.sym[r] + (par + (size_t)k) * h.slot_bytes;
+      mis |= ((uintptr_t)h.send + a.soff[k]) % 16;
+      srcs[k] = k == r ? (const char *)h.send + a.soff[r]
+                       : h.sym[r] + (par + (size_t)k) * h.slot_bytes;
       if (k != r) {
         a.push[k] = h.sym[k] + (par + (size_t)r) * h.slot_bytes;
         a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
@@ -1024,24 +1051,24 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     a.result = (char *)h.result;
     a.status = h.status;
     a.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
-    a.bytes = bytes;
-    size_t chunk = (bytes + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
+    size_t chunk = (most + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
     chunk = (chunk + 15) & ~(size_t)15;
     a.chunk = chunk < 4096 ? 4096 : chunk;
     a.epoch = h.epoch;
     a.n = n;
     a.rank = r;
-    a.vec = (uintptr_t)h.send % 16 == 0 && (uintptr_t)h.result % 16 == 0 && E <= 16;
-    const unsigned grid = (unsigned)((bytes + a.chunk - 1) / a.chunk);
+    a.vec = mis == 0 && E <= 16;
+    // the same grid on every member: `most` depends only on count and n
+    const unsigned grid = (unsigned)((most + a.chunk - 1) / a.chunk);
     switch (pof2) {
       case 2:
-        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((oneshot_reduce<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, a);
         break;
       case 4:
-        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((oneshot_reduce<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, a);
         break;
       case 8:
-        hipLaunchKernelGGL((oneshot_allreduce<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((oneshot_reduce<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, a);
         break;
       default:
         return -LFA_EINVAL;

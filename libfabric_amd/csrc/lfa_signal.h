@@ -41,22 +41,32 @@ int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
 			   uint64_t timeout_us, void *stream);
 
 /*
- * One-shot allreduce (LFA_STEP_ONESHOT) of `count` elements, ONE kernel:
- * workgroup b pushes chunk b of this rank's input into slot `rank` of every
- * peer's SYM_IN (system-scope stores over xGMI), posts `epoch` into row b of
- * every peer's one-shot rows, waits for every peer's post in its own row b,
- * then reduces chunk b of all ranks' inputs — its own slots, its own input
- * for itself — in prov/coll's association order into `result`.  Slots are
- * double-buffered by epoch parity: member j holds rank k's input of epoch e
- * at sym[j] + ((e & 1)·n + k)·slot_bytes, so a peer one operation ahead
- * never overwrites a slot still being read.  Needs 2·n·slot_bytes of SYM_IN.
+ * One-shot reduction (LFA_STEP_ONESHOT) of `count` elements, ONE kernel:
+ * workgroup b pushes chunk b of the part of this rank's input that member k
+ * reduces into slot `rank` of member k's SYM_IN (system-scope stores over
+ * xGMI), posts `epoch` into row b of every peer's one-shot rows, waits for
+ * every peer's post in its own row b, then reduces chunk b of its own part
+ * over all ranks' inputs — its own slots, its own input for itself — in
+ * prov/coll's association order into `result`.  The part of member k: the
+ * whole vector (mode LFA_ONESHOT_ALL, allreduce), block k of
+ * lfa_coll_block's partition (LFA_ONESHOT_SCATTER, reduce_scatter: result
+ * receives this rank's block), or the whole vector for k == mode only
+ * (reduce to root `mode`).  Slots are double-buffered by epoch parity:
+ * member j holds rank k's part of epoch e at sym[j] + ((e & 1)·n + k)·
+ * slot_bytes, so a peer one operation ahead never overwrites a slot still
+ * being read.  Needs 2·n·slot_bytes of SYM_IN.
  */
+#ifndef LFA_ONESHOT_ALL                 /* also in lfa_coll.h */
+#define LFA_ONESHOT_ALL (-1)
+#define LFA_ONESHOT_SCATTER (-2)
+#endif
 struct lfa_oneshot {
 	const void *send;       /* this rank's input, count elements */
-	void *result;           /* count elements */
+	void *result;           /* this rank's part of the result */
 	size_t count;
+	int mode;               /* LFA_ONESHOT_ALL / _SCATTER / root */
 	char *const *sym;       /* [n]: every member's workspace as mapped here */
-	size_t slot_bytes;      /* one slot: count·esz rounded up to 256 */
+	size_t slot_bytes;      /* one slot: the largest part, rounded up to 256 */
 	size_t flag_off;        /* the flag area's offset in a workspace */
 	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
 	uint32_t epoch;         /* this group's one-shot operations so far + 1 */

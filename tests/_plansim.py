@@ -24,13 +24,23 @@ def lower(steps, r, n, refs=None, esz=None):
     out = []
     for s in steps:
         if s["type"] == ONESHOT:
-            first = len(refs)
-            refs.extend(s["src"] if k == r else (SYM_IN, 0, k) for k in range(s["nsrc"]))
+            # this rank's part: the whole vector (peer -1), block r (-2), or
+            # the whole vector on the root `peer` only
+            moff, mlen = 0, s["count"]
+            if s["peer"] == -2:
+                moff, mlen = coll.block(s["count"], n, r)
+            elif s["peer"] >= 0 and s["peer"] != r:
+                mlen = 0
             out.append({"type": COPY, "count": s["count"] * esz, "src": s["src"],
                         "dst": (SYM_IN, 0, r), "peer": 0})
             out.append({"type": BARRIER, "count": 0, "src": (0, 0), "dst": (0, 0), "peer": 0})
-            out.append({"type": TREE, "count": s["count"], "dst": s["dst"], "first": first,
-                        "nsrc": s["nsrc"], "src": (0, 0), "peer": 0})
+            if mlen:
+                first = len(refs)
+                sb, so = s["src"]
+                refs.extend((sb, so + moff * esz) if k == r else (SYM_IN, moff * esz, k)
+                            for k in range(s["nsrc"]))
+                out.append({"type": TREE, "count": mlen, "dst": s["dst"], "first": first,
+                            "nsrc": s["nsrc"], "src": (0, 0), "peer": 0})
             out.append({"type": BARRIER, "count": 0, "src": (0, 0), "dst": (0, 0), "peer": 0})
             continue
         if s["type"] not in (ALLTOALL, ALLGATHER):

@@ -169,6 +169,14 @@ def test_p2p_small_allreduce_is_one_phase():
     assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT]
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, (256 << 10) // 32 + 1, 4)
     assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
+    # reduce_scatter up to 1 MiB, reduce up to 256 KiB over all members:
+    # one step too, `peer` naming what this rank keeps
+    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, (1 << 20) // 8, 8)
+    assert [(s["type"], s["peer"]) for s in p.steps] == [(coll.STEP_ONESHOT, -2)]
+    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, (1 << 20) // 8 + 1, 8)
+    assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
+    p = coll.plan(REDUCE, coll.ALGO_P2P, 2, 4, 3, 1000, 8)       # root 3
+    assert [(s["type"], s["peer"]) for s in p.steps] == [(coll.STEP_ONESHOT, 3)]
     n = 9
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 1, n, -1, count, 4)
     assert [s["type"] for s in p.steps] == [coll.STEP_COPY, coll.STEP_BARRIER,

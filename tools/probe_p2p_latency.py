@@ -45,20 +45,33 @@ def _worker(rank, world, port, reps, q):
         out = {}
         try:
             for name, algo, sizes, n in (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                                         ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                                          ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10))):
                 ep.set_algo(algo)
                 for nbytes in sizes:
-                    cnt = nbytes // 4
-                    x = torch.rand(cnt, device="cuda")
-                    r = torch.empty_like(x)
+                    if name == "p2p_rs":   # double PROD reduce_scatter (config 5's op)
+                        cnt = nbytes // 8
+                        x = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
+                        r = torch.empty(max(coll.block(cnt, world, rank)[1], 1),
+                                        device="cuda", dtype=torch.float64)
+
+                        def op():
+                            return ep.reduce_scatter(x, r, cnt, 9, 3)
+                    else:
+                        cnt = nbytes // 4
+                        x = torch.rand(cnt, device="cuda")
+                        r = torch.empty_like(x)
+
+                        def op():
+                            return ep.allreduce(x, r, cnt, 8, 2)
                     torch.cuda.synchronize()
                     for _ in range(20):
-                        ep.wait(ep.allreduce(x, r, cnt, 8, 2))
+                        ep.wait(op())
                     dist.barrier()
                     ts = []
                     for _ in range(n):
                         t0 = time.perf_counter()
-                        ep.wait(ep.allreduce(x, r, cnt, 8, 2))
+                        ep.wait(op())
                         ts.append(time.perf_counter() - t0)
                     ts.sort()
                     out[f"{name}_{nbytes}"] = {
