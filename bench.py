@@ -1065,6 +1065,13 @@ def extra_collectives(rank, world, stream, emit=None):
                     ep.wait(ep.allreduce(a, b, 1024, 8, 2))
                 t = max_over_ranks(time.perf_counter() - t0, world) / 200
                 out[name] = round(t * 1e6, 1)
+                if algo == coll.ALGO_TREE:
+                    ref4k = b.clone()
+                elif algo == coll.ALGO_P2P and world > 1:
+                    # the one-shot kernel (push, flags, tree) against TREE's bits
+                    differ = 0.0 if torch.equal(b, ref4k) else 1.0
+                    out["allreduce_4kib_p2p_bitwise_equal_tree"] = \
+                        max_over_ranks(differ, world) == 0.0
             except Exception as e:  # noqa: BLE001
                 out[name] = {"error": f"{e}"[:120]}
             emit(out)
