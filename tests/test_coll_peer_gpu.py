@@ -330,3 +330,88 @@ def test_flag_barrier_timeout_is_an_error_completion():
                 p.kill()
     for r in range(world):
         assert results.get(r) == "ok", results.get(r)
+
+
+def _oneshot_stream_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            rng = np.random.default_rng(77)         # the same sequence on every rank
+            ops, ctxs = [], []
+            for i in range(48):
+                kind = rng.choice(["allreduce", "reduce_scatter", "reduce", "big"])
+                dt, op = [(8, 2), (9, 3), (6, 1), (2, 0), (4, 7), (1, 9)][rng.integers(6)]
+                count = int(rng.integers(1, 3000)) if kind != "big" else 300_001
+                sends = _inputs(oracle, dt, count, world, 1000 + i)
+                want = oracle.allreduce(op, dt, sends)[0]
+                xs = _dev(sends[rank])
+                if kind in ("allreduce", "big"):
+                    r = torch.zeros(count, dtype=xs.dtype, device="cuda")
+                    exp = want
+                    _ready()
+                    ctxs.append(ep.allreduce(xs, r, count, dt, op))
+                elif kind == "reduce_scatter":
+                    off, ln = coll.block(count, world, rank)
+                    r = torch.zeros(max(ln, 1), dtype=xs.dtype, device="cuda")
+                    exp = want[off:off + ln]
+                    _ready()
+                    ctxs.append(ep.reduce_scatter(xs, r, count, dt, op))
+                else:
+                    root = int(rng.integers(world))
+                    r = torch.zeros(count, dtype=xs.dtype, device="cuda")
+                    exp = want if rank == root else None
+                    _ready()
+                    ctxs.append(ep.reduce(xs, r, count, root, dt, op))
+                ops.append((kind, r, exp, xs))
+            done = []
+            while len(done) < len(ctxs):
+                done += ep.cq_read()
+            assert done == ctxs
+            for i, (kind, r, exp, _) in enumerate(ops):
+                if exp is not None:
+                    got = r[:exp.size].cpu().numpy()
+                    assert got.tobytes() == exp.tobytes(), f"op {i} {kind}"
+            assert not ep.transport_errors, ep.transport_errors
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_oneshot_ops_in_flight_mixed(world):
+    """48 LFA_ALGO_P2P operations queued at once across processes: one-shot
+    allreduce / reduce_scatter / reduce (every root) of ragged small counts
+    over six (datatype, op) pairs, with large two-barrier allreduces between
+    them — so consecutive one-shots alternate slot parity while a member may
+    still be reducing the previous one — every result bit-exact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oneshot_stream_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=110)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
