@@ -526,6 +526,56 @@ def _kernel_events(fn, reps, stream):
     return a.elapsed_time(b) / reps
 
 
+def _two_streams_s(launch, k: int = 100) -> float:
+    """Per-launch wall time of K independent launches round-robin over two
+    streams (buckets in flight, as a provider progressing several operations
+    at once), between device synchronizes; median of 5.  One stream makes
+    every launch pay its own ramp and drain; two let the next
+    launch's waves fill the CUs the previous one's are leaving
+    (tools/probe_streams.py: a win up to 64 MiB per operand, a loss at
+    256 MiB, where two concurrent streams contend)."""
+    ss = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(10):
+        launch(i, ss[i % 2])
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(k):
+            launch(i, ss[i % 2])
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) / k)
+    return statistics.median(ts)
+
+
+def extra_two_streams(dev, counts) -> dict:
+    """The headline combine (float SUM) at the given operand counts, K
+    independent launches over two streams vs one (beside the single-stream
+    headline, never instead of it)."""
+    from libfabric_amd import atomic
+    out = {}
+    for count in counts:
+        sets = make_buffers(dev, 3000, count)
+        nsets = len(sets)
+
+        def launch(i, st):
+            d, s_ = sets[i % nsets]
+            atomic.write(FI_SUM, FI_FLOAT, d, s_, count, st)
+        one = torch.cuda.Stream()
+        prewarm(lambda i: launch(i, one), 0.1)
+        t1 = _two_streams_s(lambda i, st: launch(i, one))
+        t2 = _two_streams_s(launch)
+        nb = 3 * count * 4
+        out[f"{count * 4 >> 20}mib"] = {
+            "one_stream_us": round(t1 * 1e6, 2), "two_streams_us": round(t2 * 1e6, 2),
+            "one_stream_frac": round(nb / t1 / 1e9 / PEAK_GBPS, 4),
+            "two_streams_frac": round(nb / t2 / 1e9 / PEAK_GBPS, 4)}
+        del sets
+        torch.cuda.empty_cache()
+    return out
+
+
 def extra_config3(dev, stream):
     """BASELINE configs[2]: int64 FI_BOR and FI_MIN, 64 MiB, bit-exact path.
     8 rotating buffer pairs (1 GiB) so the 256 MiB MALL cannot serve reruns."""
@@ -549,6 +599,11 @@ def extra_config3(dev, stream):
         out[name] = {"kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(gbps, 1),
                      "frac": round(gbps / PEAK_GBPS, 4),
                      "gib_s": round(3 * n * 8 / (ms * 1e-3) / 2**30, 1)}
+        # the same independent buckets two streams at a time
+        t2 = _two_streams_s(lambda i, st, op=op: atomic.write(op, 6, sets[i % 8][0],
+                                                                sets[i % 8][1], n, st))
+        out[name]["two_streams_us"] = round(t2 * 1e6, 2)
+        out[name]["two_streams_frac"] = round(3 * n * 8 / t2 / 1e9 / PEAK_GBPS, 4)
     return out
 
 
@@ -1534,6 +1589,11 @@ def main() -> None:
                     "kernel_us": round(w["kern_ms"] * 1e3, 2),
                     "frac": round(3 * S_BYTES / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4)}
                 torch.cuda.empty_cache()
+            # independent buckets two streams at a time, at this rank's
+            # shard (and at N = 1 also at the N = 8 shard, 32 MiB)
+            ex["buckets_two_streams"] = extra_two_streams(
+                dev, [cnt] + ([COUNT // 8] if world == 1 else []))
+            torch.cuda.empty_cache()
             if world == 1:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
                 ex["config1_2rank_4kib_loopback"] = extra_config1_loopback(dev, stream)
