@@ -351,7 +351,7 @@ int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype dt,
   return kTreePut[op](dt, dsts, ndst, srcs, nsrc, cnt, stream);
 }
 
-int lfa_oneshot_allreduce_async(int op, int dt, const struct lfa_oneshot *a,
+int lfa_oneshot_reduce_async(int op, int dt, const struct lfa_oneshot *a,
                                 void *stream) {
   if ((unsigned)op > LFA_BXOR || (unsigned)dt >= LFA_DATATYPE_CNT ||
       !in_table(op, dt))

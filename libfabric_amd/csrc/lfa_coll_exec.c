@@ -207,7 +207,7 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	a.epoch = mc->os_epoch + 1;
 	a.status = mc->ep->sig_status;
 	a.timeout_us = sig_timeout_us();
-	ret = lfa_oneshot_allreduce_async(r->op, r->dt, &a, r->stream);
+	ret = lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
 	if (!ret)
 		mc->os_epoch++;
 	return ret;

@@ -73,7 +73,7 @@ struct lfa_oneshot {
 	uint32_t *status;       /* host-mapped; 1 after a timed-out wait */
 	uint64_t timeout_us;
 };
-int lfa_oneshot_allreduce_async(int op, int datatype, const struct lfa_oneshot *a,
+int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 				void *stream);
 
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
