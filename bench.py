@@ -1590,9 +1590,13 @@ def main() -> None:
                     "frac": round(3 * S_BYTES / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4)}
                 torch.cuda.empty_cache()
             # independent buckets two streams at a time, at this rank's
-            # shard (and at N = 1 also at the N = 8 shard, 32 MiB)
+            # shard (and at N = 1 at the N = 8 shard, 32 MiB) — only below
+            # 192 MiB per operand: at 256 MiB two streams contend and lose
+            # (tools/probe_streams.py), and the headline kernel's rocprofv3
+            # statistics stay those of the one-stream headline
             ex["buckets_two_streams"] = extra_two_streams(
-                dev, [cnt] + ([COUNT // 8] if world == 1 else []))
+                dev, [c for c in [cnt] + ([COUNT // 8] if world == 1 else [])
+                      if c * 4 < (192 << 20)])
             torch.cuda.empty_cache()
             if world == 1:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
