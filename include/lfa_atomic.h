@@ -62,6 +62,16 @@ int lfa_atomic_valid(enum lfa_datatype datatype, enum lfa_op op, uint64_t flags)
 extern lfa_write_fn const lfa_atomic_write_handlers[LFA_WRITE_OP_CNT][LFA_DATATYPE_CNT];
 
 /*
+ * The synchronous tables keep the reference's void signature, which has no
+ * way to fail on the CPU.  On the GPU a call can (a HIP error, operands
+ * mixing host and device memory): the first failure since the last call of
+ * this function is kept per thread and returned here (a negative LFA_E*
+ * code; -LFA_EIO for a HIP error, also named on stderr), and cleared.  0 when
+ * every table call of this thread since then succeeded.
+ */
+int lfa_atomic_last_error(void);
+
+/*
  * dst[i] = dst[i] OP src[i] for i < cnt, on `stream`.
  * Returns 0, -LFA_EOPNOTSUPP (no handler), -LFA_EINVAL (bad pointer/args),
  * -LFA_EIO (launch failure).

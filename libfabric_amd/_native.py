@@ -31,6 +31,8 @@ def _bind_lfa(L):
     L.lfa_datatype_size.argtypes = [c_int]
     L.lfa_atomic_valid.restype = c_int
     L.lfa_atomic_valid.argtypes = [c_int, c_int, c_uint64]
+    L.lfa_atomic_last_error.restype = c_int
+    L.lfa_atomic_last_error.argtypes = []
     L.lfa_atomic_write_async.restype = c_int
     L.lfa_atomic_write_async.argtypes = [c_int, c_int, c_void_p, c_void_p,
                                          c_size_t, c_void_p]

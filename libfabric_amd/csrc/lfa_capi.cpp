@@ -140,16 +140,25 @@ int ptr_kind(const void *p) {
   return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? kDev : kHost;
 }
 
+// First failure of a synchronous table call on this thread (lfa_atomic_last_error).
+thread_local int t_last_error = 0;
+
+inline void note_error(int rc) {
+  if (rc && !t_last_error) t_last_error = rc < 0 ? rc : -LFA_EIO;
+}
+
 template <int OP, int DT>
 void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
   const int k = ptr_kind(dst) | ptr_kind(res) | (OP == LFA_ATOMIC_READ ? 0 : ptr_kind(src));
   if (cnt && k == kHost) {
     int rc = lfa_host_readwrite((lfa_op)OP, (lfa_datatype)DT, dst, src, res, cnt);
     if (rc) fprintf(stderr, "lfa: host fetch op=%d dt=%d failed (%d)\n", OP, DT, rc);
+    note_error(rc);
     return;
   }
   if (cnt && k != kDev) {
     fprintf(stderr, "lfa: fetch op=%d dt=%d: mixed host/device operands\n", OP, DT);
+    note_error(-LFA_EINVAL);
     return;
   }
   int rc = kReadWrite[OP](DT, dst, src, res, cnt, nullptr);
@@ -157,6 +166,7 @@ void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
   if (rc || e != hipSuccess)
     fprintf(stderr, "lfa: fetch op=%d dt=%d failed (%d, %s)\n", OP, DT, rc,
             hipGetErrorString(e));
+  note_error(rc ? rc : e != hipSuccess ? -LFA_EIO : 0);
 }
 
 template <int OP, int DT>
@@ -166,10 +176,12 @@ void sync_swap_entry(void *dst, const void *src, const void *cmp, void *res,
   if (cnt && k == kHost) {
     int rc = lfa_host_swap((lfa_op)OP, (lfa_datatype)DT, dst, src, cmp, res, cnt);
     if (rc) fprintf(stderr, "lfa: host swap op=%d dt=%d failed (%d)\n", OP, DT, rc);
+    note_error(rc);
     return;
   }
   if (cnt && k != kDev) {
     fprintf(stderr, "lfa: swap op=%d dt=%d: mixed host/device operands\n", OP, DT);
+    note_error(-LFA_EINVAL);
     return;
   }
   int rc = kSwap[OP - LFA_CSWAP](DT, dst, src, cmp, res, cnt, nullptr);
@@ -177,6 +189,7 @@ void sync_swap_entry(void *dst, const void *src, const void *cmp, void *res,
   if (rc || e != hipSuccess)
     fprintf(stderr, "lfa: swap op=%d dt=%d failed (%d, %s)\n", OP, DT, rc,
             hipGetErrorString(e));
+  note_error(rc ? rc : e != hipSuccess ? -LFA_EIO : 0);
 }
 
 template <int OP, int DT>
@@ -202,6 +215,7 @@ void sync_entry(void *dst, const void *src, size_t cnt) {
                  ? lfa_host_write((lfa_op)OP, (lfa_datatype)DT, dst, src, cnt)
                  : lfa_atomic_write_staged((lfa_op)OP, (lfa_datatype)DT, dst, src, cnt, 0);
     if (rc) fprintf(stderr, "lfa: combine op=%d dt=%d (host operands) failed (%d)\n", OP, DT, rc);
+    note_error(rc);
     return;
   }
   int rc = kWrite[OP](DT, dst, src, cnt, nullptr);
@@ -209,6 +223,7 @@ void sync_entry(void *dst, const void *src, size_t cnt) {
   if (rc || e != hipSuccess)
     fprintf(stderr, "lfa: combine op=%d dt=%d failed (%d, %s)\n", OP, DT, rc,
             hipGetErrorString(e));
+  note_error(rc ? rc : e != hipSuccess ? -LFA_EIO : 0);
 }
 
 template <int OP, int DT>
@@ -349,6 +364,12 @@ int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype dt,
   for (int j = 0; j < ndst; j++)
     if (cnt && !dsts[j]) return -LFA_EINVAL;
   return kTreePut[op](dt, dsts, ndst, srcs, nsrc, cnt, stream);
+}
+
+int lfa_atomic_last_error(void) {
+  int rc = t_last_error;
+  t_last_error = 0;
+  return rc;
 }
 
 int lfa_oneshot_reduce_async(int op, int dt, const struct lfa_oneshot *a,

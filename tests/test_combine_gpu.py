@@ -5,6 +5,8 @@ lfa_reduce_tree_async / the synchronous lfa_atomic_write_handlers table).
 Bar: bit-exact for integer ops; float/double/complex bit-exact on every
 non-NaN lane with NaN-class agreement on NaN lanes (tests/_cmp.py).
 """
+import ctypes
+import errno
 import json
 import os
 
@@ -516,6 +518,32 @@ def test_sync_table_host_pointers(lfa, nbytes, kind):
             fn(td.data_ptr(), s.ctypes.data, n)
             got = td.cpu().numpy()
         assert_parity(dt, got.view(np.uint8), want.view(np.uint8), f"{kind} {nbytes}")
+
+
+def test_sync_table_failure_is_reported_per_thread(lfa):
+    """The synchronous tables keep libfabric's void signature; a failure
+    (here: a fetch whose dst is device memory and whose result is host
+    memory, which no single path can serve) is kept per thread and returned
+    once by lfa_atomic_last_error, and a later success leaves it at 0."""
+    from libfabric_amd import lib
+    L = lib()
+    assert L.lfa_atomic_last_error() == 0
+    d = torch.ones(64, device=DEV)
+    s = torch.ones(64, device=DEV)
+    r = np.zeros(64, np.float32)
+    torch.cuda.synchronize()
+    rw = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                          ctypes.c_size_t)
+    tbl = (ctypes.c_void_p * (12 * 16)).in_dll(L, "lfa_atomic_readwrite_handlers")
+    fn = rw(tbl[2 * 16 + 8])                       # FI_SUM, FI_FLOAT
+    fn(d.data_ptr(), s.data_ptr(), r.ctypes.data, 64)
+    assert L.lfa_atomic_last_error() == -errno.EINVAL
+    assert L.lfa_atomic_last_error() == 0          # cleared by the read
+    rd = torch.zeros(64, device=DEV)
+    fn(d.data_ptr(), s.data_ptr(), rd.data_ptr(), 64)
+    assert L.lfa_atomic_last_error() == 0
+    assert torch.equal(rd, torch.ones(64, device=DEV))
+    assert torch.equal(d, torch.full((64,), 2.0, device=DEV))
 
 
 def _shape(rng):
