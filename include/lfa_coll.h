@@ -76,8 +76,12 @@ enum lfa_coll_algo {
 	 * over IPC (hipIpcOpenMemHandle); rank r's kernel reads block r of
 	 * every rank's input straight from peer HBM, reduces it and writes
 	 * (pushes) the result block into every rank's workspace in the same
-	 * pass; two stream-ordered barriers per operation.  No intermediate
-	 * transport copies, xGMI in and out directions busy at once. */
+	 * pass; two stream-ordered barriers per operation, each a one-wave
+	 * flag kernel on the workspace (no RCCL collective).  Small buckets
+	 * (allreduce / reduce <= 256 KiB over all members, reduce_scatter <=
+	 * 1 MiB, 2..8 members) are ONE kernel: push into the peers' slots,
+	 * flags, tree.  No intermediate transport copies, xGMI in and out
+	 * directions busy at once. */
 	LFA_ALGO_P2P = 4,
 };
 
