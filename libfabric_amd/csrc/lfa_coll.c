@@ -635,6 +635,7 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			/* a flag barrier of this or an earlier operation gave up
 			 * waiting for a member (lfa_signal.hip) */
 			*ep->sig_status = 0;
+			ep->sig_failed = 1;
 			st = -1;
 			perr = ETIMEDOUT;
 		}
@@ -1163,6 +1164,10 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		return ret;
 	memset(&x, 0, sizeof(x));
 	if (plan_uses_sym(pl->steps, pl->nsteps)) {
+		/* after a timed-out wait the members' flag epochs disagree: a
+		 * P2P operation could pass a barrier on stale posts */
+		if (ep->sig_failed)
+			return -LFA_EIO;
 		ret = p2p_ensure(mc, plan_sym_need(pl->steps, pl->nsteps, mc->size,
 						   count, esz));
 		if (ret)
@@ -1366,6 +1371,10 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	if (ret)
 		return ret;
 	sym = plan_uses_sym(raw.steps, raw.nsteps);
+	if (sym && ep->sig_failed) {
+		plan_free(&raw);
+		return -LFA_EIO;        /* epochs disagree since a timed-out wait */
+	}
 	/* a device hop's BARRIER stays: the flag kernel (sig_barrier) */
 	ret = lower_plan(&raw, mc->rank, mc->size, esz, &h->pl, sym && !dev, !dev);
 	plan_free(&raw);

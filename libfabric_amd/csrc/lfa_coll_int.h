@@ -100,6 +100,8 @@ struct lfa_coll_ep {
 	void *ctl_dev;              /* P2P handle exchange, nranks records */
 	void *ctl_host;
 	uint32_t *sig_status;       /* host-mapped: a flag barrier timed out */
+	int sig_failed;             /* one did: the groups' flag epochs are no
+				     * longer agreed, P2P operations refused */
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
 	hipEvent_t evpool[64];      /* recycled completion events */

@@ -296,6 +296,14 @@ def _timeout_worker(rank, world, port, q):
                     msg = "ok" if "prov_errno 110" in str(e) else f"wrong error {e}"
                 if time.time() - t0 > 10:
                     msg = f"took {time.time() - t0:.1f} s"
+                # the members' flag epochs now disagree: further P2P
+                # operations on this endpoint are refused at submit
+                if msg == "ok":
+                    try:
+                        ep.allreduce(xs, r, 4096, 8, 2)
+                        msg = "P2P accepted after a timeout"
+                    except coll.CollError:
+                        pass
         finally:
             ep.close()
         dist.barrier()
@@ -309,7 +317,9 @@ def _timeout_worker(rank, world, port, q):
 def test_flag_barrier_timeout_is_an_error_completion():
     """LFA_ALGO_P2P's device-side flag barrier (lfa_signal.hip) is bounded:
     when a member never joins the collective, the waiting rank's operation
-    completes with an error after LFA_SIG_TIMEOUT_MS, and the kernel retires."""
+    completes with an error after LFA_SIG_TIMEOUT_MS, and the kernel retires;
+    the endpoint then refuses further P2P operations (the members' flag
+    epochs no longer agree)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
