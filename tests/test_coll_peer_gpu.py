@@ -425,3 +425,78 @@ def test_oneshot_ops_in_flight_mixed(world):
                 p.kill()
     for r in range(world):
         assert results.get(r) == "ok", results.get(r)
+
+
+def _every_entry_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import json as _json
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        from tests._cmp import assert_parity
+        gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+        with open(os.path.join(gdir, "manifest.json")) as f:
+            cases = [c for c in _json.load(f)["combine"] if c["op"] <= 9]   # reducing ops
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            for c in cases:
+                z = np.load(os.path.join(gdir, c["file"]))
+                esz = oracle.datatype_size(c["dt"])
+                # the fixture's edge-lane operands as the ranks' inputs
+                pool = [np.ascontiguousarray(z[k]).view(np.uint8) for k in ("dst", "src", "out")]
+                sends = [pool[k % 3].copy() for k in range(world)]
+                n = sends[0].nbytes // esz
+                want = oracle.allreduce(c["op"], c["dt"], [s.view(oracle.DT_NP[c["dt"]])
+                                                          for s in sends])[0].view(np.uint8)
+                x = torch.from_numpy(sends[rank]).cuda()
+                r = torch.zeros_like(x)
+                _ready()
+                ep.wait(ep.allreduce(x, r, n, c["dt"], c["op"]))
+                assert_parity(c["dt"], r.cpu().numpy(), want, f"allreduce {c['file']}")
+                off, ln = coll.block(n, world, rank)
+                rs = torch.zeros(max(ln, 1) * esz, dtype=torch.uint8, device="cuda")
+                _ready()
+                ep.wait(ep.reduce_scatter(x, rs, n, c["dt"], c["op"]))
+                assert_parity(c["dt"], rs[:ln * esz].cpu().numpy(),
+                              want[off * esz:(off + ln) * esz], f"reduce_scatter {c['file']}")
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, f"ok {len(cases)}"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_oneshot_every_reducing_entry(world):
+    """Every (op, datatype) of the write table with a reducing op (MIN..BXOR,
+    int8..uint64, float, double, float complex, int128) through LFA_ALGO_P2P's
+    one-shot allreduce and reduce_scatter across processes, on the golden
+    fixtures' operands with their edge lanes (±0, ±inf, NaN, extremes):
+    equal to prov/coll's recursive-doubling result (the oracle), bit for bit
+    (NaN lanes: NaN on both sides)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_every_entry_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=140)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert str(results.get(r)).startswith("ok"), results.get(r)
