@@ -463,6 +463,12 @@ def _every_entry_worker(rank, world, port, q):
                 ep.wait(ep.reduce_scatter(x, rs, n, c["dt"], c["op"]))
                 assert_parity(c["dt"], rs[:ln * esz].cpu().numpy(),
                               want[off * esz:(off + ln) * esz], f"reduce_scatter {c['file']}")
+                root = cases.index(c) % world
+                rr = torch.zeros_like(x)
+                _ready()
+                ep.wait(ep.reduce(x, rr if rank == root else None, n, root, c["dt"], c["op"]))
+                if rank == root:
+                    assert_parity(c["dt"], rr.cpu().numpy(), want, f"reduce {c['file']}")
         finally:
             ep.close()
         dist.barrier()
@@ -477,7 +483,8 @@ def _every_entry_worker(rank, world, port, q):
 def test_oneshot_every_reducing_entry(world):
     """Every (op, datatype) of the write table with a reducing op (MIN..BXOR,
     int8..uint64, float, double, float complex, int128) through LFA_ALGO_P2P's
-    one-shot allreduce and reduce_scatter across processes, on the golden
+    one-shot allreduce, reduce_scatter and reduce (roots in turn, non-roots
+    passing no result buffer) across processes, on the golden
     fixtures' operands with their edge lanes (±0, ±inf, NaN, extremes):
     equal to prov/coll's recursive-doubling result (the oracle), bit for bit
     (NaN lanes: NaN on both sides)."""
