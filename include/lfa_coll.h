@@ -136,8 +136,9 @@ int lfa_coll_domain_open_host(int rank, int nranks,
  * pair must be both device or both host memory (-LFA_EINVAL otherwise);
  * members may differ from one another.  LFA_ALGO_P2P keeps its schedule
  * here: the members map each other's symmetric workspaces over IPC (the
- * handshake runs from progress calls), its barriers are zero-byte message
- * rings, a host-buffer member is staged through device copies, and a P2P
+ * handshake runs from progress calls), its barriers and small buckets are
+ * GPU-side flag kernels on those workspaces (no owner transfers), a
+ * host-buffer member is staged through device copies, and a P2P
  * operation starts once the endpoint's earlier operations have finished. */
 int lfa_coll_domain_open_peer(int device, int rank, int nranks,
 			      const struct lfa_peer_xfer_ops *ops, void *ctx,
