@@ -686,6 +686,39 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
         out[name.replace("_us", "_bitwise_ok")] = bool(ok)
     out["note"] = ("2 ranks on one GPU, loopback transport; median of 1000 after 100 "
                    "warm-up; wall time incl. hipStreamSynchronize")
+    # LFA_ALGO_P2P's one-shot kernel (push, flags, tree) for the same shape:
+    # the two ranks on two streams of this process, each with its own
+    # symmetric workspace (the loopback runs every rank on one stream, where
+    # one rank's kernel could not wait for the other's)
+    import ctypes
+    region, flag_off = 1 << 20, 2 << 20
+    ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device=dev) for _ in range(2)]
+    sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
+    status = torch.zeros(1, dtype=torch.int32).pin_memory()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    for r in results:
+        r.zero_()
+    torch.cuda.synchronize()
+    ts = []
+    for i in range(warm + reps):
+        t0 = time.perf_counter()
+        for r in range(2):
+            coll.oneshot_reduce(FI_SUM, FI_FLOAT, coll.OneShot(
+                sends[r].data_ptr(), results[r].data_ptr(), 1024, -1,
+                ctypes.cast(sym, ctypes.c_void_p), 4096, flag_off, 2, r, i + 1,
+                status.data_ptr(), 2_000_000), streams[r])
+        for st in streams:
+            st.synchronize()
+        if i >= warm:
+            ts.append(time.perf_counter() - t0)
+        if i == warm and int(status.item()):
+            break            # a wait timed out: the two streams did not run together
+    out["oneshot_us"] = round(statistics.median(ts) * 1e6, 1) if ts else None
+    out["oneshot_bitwise_ok"] = bool(all(torch.equal(r, want) for r in results)
+                                     and not int(status.item()))
+    out["oneshot_note"] = ("LFA_ALGO_P2P one-shot kernel, the 2 ranks on two streams of one "
+                           "process with their own workspaces; wall time of both launches "
+                           "+ both stream syncs; region %d B" % region)
     return out
 
 

@@ -270,6 +270,32 @@ def _ptr(x) -> int | None:
     return int(x)
 
 
+class OneShot(ctypes.Structure):
+    """struct lfa_oneshot (libfabric_amd/csrc/lfa_signal.h): one rank's
+    one-shot reduction over the members' symmetric workspaces."""
+    _fields_ = [("send", ctypes.c_void_p), ("result", ctypes.c_void_p),
+                ("count", ctypes.c_size_t), ("mode", ctypes.c_int),
+                ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
+                ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
+                ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
+                ("timeout_us", ctypes.c_uint64)]
+
+
+def oneshot_reduce(op: int, dt: int, a: OneShot, stream) -> None:
+    """lfa_oneshot_reduce_async (liblfa.so): the LFA_STEP_ONESHOT kernel
+    launched directly, for probes and benches that lay out the workspaces
+    themselves (the provider does this inside its executor)."""
+    L = _lib()
+    if not getattr(L, "_oneshot_bound", False):
+        L.lfa_oneshot_reduce_async.restype = ctypes.c_int
+        L.lfa_oneshot_reduce_async.argtypes = [ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(OneShot), ctypes.c_void_p]
+        L._oneshot_bound = True
+    h = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    _chk(L.lfa_oneshot_reduce_async(op, dt, ctypes.byref(a), ctypes.c_void_p(h)),
+         "lfa_oneshot_reduce_async")
+
+
 class Endpoint:
     """One rank's domain + endpoint.  Buffers: torch tensors (device or host)
     or numpy arrays (host).  Calls return after enqueueing; completions come
