@@ -529,9 +529,12 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
     for (size_t o = vhi + t; o < hi; o += kBlock)
       sys_store<uint8_t>((uint8_t *)a.push[k] + o, (uint8_t)src[o]);
   }
-  // 2. every wave's pushes complete and visible, then one post per peer
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // 2. every wave's pushes acknowledged (write-through, so in the peer's
+  //    memory), then ONE system-scope release for the workgroup — its waves
+  //    share a CU and so an L2 — and one post per peer
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (t < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // wave 0: the posting lanes
   if ((int)t < a.n && (int)t != a.rank) {
     __hip_atomic_store(a.post[t] + b * LFA_SIG_MAX, a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -547,8 +550,10 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
       __builtin_amdgcn_s_sleep(2);
     }
   }
+  // the waiting wave acquires for the workgroup (same CU, same L2), then
+  // every wave may read what the peers pushed
+  if (t < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   // 4. reduce chunk b of this rank's own range over every rank's input, rank
   //    order (system-scope loads: the slots were written by peers over xGMI)
   const size_t own = a.slen[a.rank];
