@@ -121,21 +121,22 @@ def test_tree_coll_uses_rccl_collectives_when_even():
 
 
 def test_p2p_schedule_shape():
-    """LFA_ALGO_P2P allreduce, big path: stage the N-1 foreign blocks,
+    """LFA_ALGO_P2P allreduce, big path: stage the input (one copy),
     barrier, ONE tree over every rank's SYM_IN pushing its result into all
     N-1 peers' SYM_OUT, barrier, copy the gathered blocks out.  Bytes staged
-    in and out are (N-1)/N·S each; no RCCL data transfers at all."""
+    in S (own block included: one launch), out (N-1)/N·S; no RCCL data
+    transfers at all."""
     n, count, esz, r = 8, 8 * 1_000_000, 4, 3
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, r, n, -1, count, esz)
     kinds = [s["type"] for s in p.steps]
-    assert kinds == [coll.STEP_COPY, coll.STEP_COPY, coll.STEP_BARRIER,
+    assert kinds == [coll.STEP_COPY, coll.STEP_BARRIER,
                      coll.STEP_TREE_PUT, coll.STEP_BARRIER,
                      coll.STEP_COPY, coll.STEP_COPY]
     assert p.tmp_bytes == 0
     copies = [s for s in p.steps if s["type"] == coll.STEP_COPY]
-    assert sum(c["count"] for c in copies[:2]) == (n - 1) * count * esz // n
-    assert sum(c["count"] for c in copies[2:]) == (n - 1) * count * esz // n
-    t = p.steps[3]
+    assert copies[0]["count"] == count * esz
+    assert sum(c["count"] for c in copies[1:]) == (n - 1) * count * esz // n
+    t = p.steps[2]
     assert t["nsrc"] == n and t["peer"] == n - 1
     off, ln = coll.block(count, n, r)
     ins = p.refs[t["first"]:t["first"] + n]
