@@ -490,17 +490,11 @@ static void p2p_tree_block(struct planner *p, int r, int n, size_t count,
 	p_tree_put_end(p, first, (uint32_t)n, dst, mlen);
 }
 
-/* Copy the gathered blocks (all but block `skip`) from rank r's SYM_OUT. */
-static void p2p_unstage_output(struct planner *p, int r, int n, size_t count,
-			       size_t esz, int skip)
+/* Copy the whole gathered result from rank r's SYM_OUT: its own block was
+ * written there by its own tree, so one launch covers every block. */
+static void p2p_unstage_output(struct planner *p, int r, size_t count, size_t esz)
 {
-	size_t moff, mlen;
-
-	lfa_coll_block(count, n, skip, &moff, &mlen);
-	p_copy(p, ref(LFA_BUF_RESULT, 0), sref(LFA_BUF_SYM_OUT, r, 0), moff * esz);
-	p_copy(p, ref(LFA_BUF_RESULT, (moff + mlen) * esz),
-	       sref(LFA_BUF_SYM_OUT, r, (moff + mlen) * esz),
-	       (count - moff - mlen) * esz);
+	p_copy(p, ref(LFA_BUF_RESULT, 0), sref(LFA_BUF_SYM_OUT, r, 0), count * esz);
 }
 
 static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
@@ -532,10 +526,10 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 			return 0;
 		}
 		p2p_stage_input(p, r, n, count, esz);
-		p2p_tree_block(p, r, n, count, esz, ref(LFA_BUF_RESULT, moff * esz),
+		p2p_tree_block(p, r, n, count, esz, sref(LFA_BUF_SYM_OUT, r, moff * esz),
 			       1);
 		p_barrier(p);
-		p2p_unstage_output(p, r, n, count, esz, r);
+		p2p_unstage_output(p, r, count, esz);
 		return 0;
 	case LFA_REDUCE_SCATTER:
 		if (bytes <= LFA_OS_RS_BYTES && n <= LFA_OS_MAX_RANKS) {
@@ -552,12 +546,11 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 			return 0;
 		}
 		p2p_stage_input(p, r, n, count, esz);
-		p2p_tree_block(p, r, n, count, esz,
-			       r == root ? ref(LFA_BUF_RESULT, moff * esz) :
-			       sref(LFA_BUF_SYM_OUT, root, moff * esz), 0);
+		p2p_tree_block(p, r, n, count, esz, sref(LFA_BUF_SYM_OUT, root, moff * esz),
+			       0);
 		p_barrier(p);
 		if (r == root)
-			p2p_unstage_output(p, r, n, count, esz, root);
+			p2p_unstage_output(p, r, count, esz);
 		return 0;
 	default:
 		return -LFA_ENOSYS;

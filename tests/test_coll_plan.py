@@ -130,12 +130,11 @@ def test_p2p_schedule_shape():
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, r, n, -1, count, esz)
     kinds = [s["type"] for s in p.steps]
     assert kinds == [coll.STEP_COPY, coll.STEP_BARRIER,
-                     coll.STEP_TREE_PUT, coll.STEP_BARRIER,
-                     coll.STEP_COPY, coll.STEP_COPY]
+                     coll.STEP_TREE_PUT, coll.STEP_BARRIER, coll.STEP_COPY]
     assert p.tmp_bytes == 0
     copies = [s for s in p.steps if s["type"] == coll.STEP_COPY]
-    assert copies[0]["count"] == count * esz
-    assert sum(c["count"] for c in copies[1:]) == (n - 1) * count * esz // n
+    assert copies[0]["count"] == count * esz and copies[1]["count"] == count * esz
+    assert copies[1]["src"] == (coll.BUF_SYM_OUT, 0, r)
     t = p.steps[2]
     assert t["nsrc"] == n and t["peer"] == n - 1
     off, ln = coll.block(count, n, r)
@@ -145,7 +144,7 @@ def test_p2p_schedule_shape():
     assert all(ins[k] == (coll.BUF_SYM_IN, off * esz, k) for k in range(n) if k != r)
     assert sorted(o[2] for o in outs) == [k for k in range(n) if k != r]
     assert all(o[:2] == (coll.BUF_SYM_OUT, off * esz) for o in outs)
-    assert t["dst"] == (coll.BUF_RESULT, off * esz)
+    assert t["dst"] == (coll.BUF_SYM_OUT, off * esz, r)     # own block too
     # reduce_scatter: one tree into the result, closing barrier, no pushes
     p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, r, n, -1, count, esz)
     assert [s["type"] for s in p.steps][-2:] == [coll.STEP_TREE_PUT, coll.STEP_BARRIER]
