@@ -40,7 +40,7 @@ __global__ __launch_bounds__(64) void flag_barrier(BarArgs a) {
       __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
-    __builtin_amdgcn_s_sleep(4);
+    __builtin_amdgcn_s_sleep(1);
   }
   // later steps read what the peers wrote before posting
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
