@@ -694,7 +694,7 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     region, flag_off = 1 << 20, 2 << 20
     ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device=dev) for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
-    status = torch.zeros(1, dtype=torch.int32).pin_memory()
+    status = torch.full((1,), -1, dtype=torch.int32).pin_memory()   # LFA_SIG_NONE
     streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
     for r in results:
         r.zero_()
@@ -706,19 +706,22 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
             coll.oneshot_reduce(FI_SUM, FI_FLOAT, coll.OneShot(
                 sends[r].data_ptr(), results[r].data_ptr(), 1024, -1,
                 ctypes.cast(sym, ctypes.c_void_p), 4096, flag_off, 2, r, i + 1,
-                status.data_ptr(), 2_000_000), streams[r])
+                status.data_ptr(), i + 1, 2_000_000), streams[r])
         for st in streams:
             st.synchronize()
+        if int(status.item()) != -1:
+            break            # a wait timed out: the two streams did not run together
         if i >= warm:
             ts.append(time.perf_counter() - t0)
-        if i == warm and int(status.item()):
-            break            # a wait timed out: the two streams did not run together
-    out["oneshot_us"] = round(statistics.median(ts) * 1e6, 1) if ts else None
+    out["oneshot_kernel_only_us"] = round(statistics.median(ts) * 1e6, 1) if ts else None
     out["oneshot_bitwise_ok"] = bool(all(torch.equal(r, want) for r in results)
-                                     and not int(status.item()))
-    out["oneshot_note"] = ("LFA_ALGO_P2P one-shot kernel, the 2 ranks on two streams of one "
-                           "process with their own workspaces; wall time of both launches "
-                           "+ both stream syncs; region %d B" % region)
+                                     and int(status.item()) == -1)
+    out["oneshot_note"] = ("KERNEL ONLY: the LFA_ALGO_P2P one-shot kernel launched directly, "
+                           "the 2 ranks on two streams of one process with hand-built "
+                           "workspaces — no provider submit / completion path (that is "
+                           "probe_p2p_latency's figure); wall time of both launches + both "
+                           "stream syncs, every iteration's status checked; region %d B"
+                           % region)
     return out
 
 
@@ -1198,7 +1201,8 @@ def tune(args) -> None:
     variants = [int(v) for v in args.variants.split(',')] if args.variants else list(range(30))
 
     def run(v, d, s, n):
-        fn = L.lfa__tune_sum_f32 if v < 12 or v == 30 else L.lfa__tune2_sum_f32
+        fn = (L.lfa__tune_sum_f32 if v < 12 or v == 30 else
+              L.lfa__tune3_sum_f32 if 70 <= v < 80 else L.lfa__tune2_sum_f32)
         return fn(v, d.data_ptr(), s.data_ptr(), n, h)
 
     # correctness of every variant first (odd size: exercises the tail path)

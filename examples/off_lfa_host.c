@@ -428,14 +428,14 @@ int main(int argc, char **argv)
 	CHECK_RC(fi_av_set_insert(set, 2), -FI_EINVAL);
 	CHECK_RC(fi_av_set_insert(set, 7), 0);                   /* {0,2,4,6,7} */
 	CHECK_RC(fi_av_set_remove(set, 3), -FI_EINVAL);
-	CHECK_RC(fi_av_set_remove(set, 4), 0);                   /* {0,2,6,7} */
+	CHECK_RC(fi_av_set_remove(set, 4), 0);                   /* {0,2,7,6} */
 	sattr.start_addr = 1;
 	sattr.end_addr = 2;
 	sattr.stride = 1;
 	CHECK_RC(fi_av_set(av, &sattr, &set2, NULL), 0);         /* {1,2} */
 	CHECK_RC(fi_av_set_intersect(set2, set), 0);             /* {2} */
-	CHECK_RC(fi_av_set_union(set2, set), 0);                 /* {2,0,6,7} */
-	CHECK_RC(fi_av_set_remove(set2, 2), 0);
+	CHECK_RC(fi_av_set_union(set2, set), 0);                 /* {2,0,7,6} */
+	CHECK_RC(fi_av_set_remove(set2, 2), 0);                  /* {6,0,7} */
 	CHECK_RC(fi_av_set_diff(set, set2), 0);                  /* {2} */
 	CHECK_RC(fi_close(&set2->fid), 0);
 	CHECK_RC(fi_av_set_remove(set, 2), 0);                   /* {} */

@@ -735,6 +735,144 @@ static int core_suite(struct fid_domain *domain, struct fid_av *av, struct fid_e
 	return failures ? 1 : 0;
 }
 
+/*
+ * Groups over sets whose address order is not ascending.
+ * prov/coll numbers a group's members by their index in the joined av_set's
+ * address array (coll_find_local_rank, coll_coll.c:669-689); insert appends
+ * and remove moves the last address into the hole (coll_av_set.c:127-164),
+ * so the order is the one these calls leave.  Two sets:
+ *   A: stride {0, 2, 4, ...}, insert 1 (and 3), then remove 2 when N >= 4
+ *      — e.g. N = 5: {0,2,4} +1 +3 = {0,2,4,1,3}, -2 = {0,3,4,1};
+ *      joined over the world group (every rank calls; non-members refused);
+ *   B: every rank, diff {0}: {N-1, 1, 2, ..., N-2}; joined over its own
+ *      address (members only).
+ * Each group runs an allgather of the parent ranks (the block order shows
+ * the numbering), a float SUM allreduce (association order), a reduce to
+ * group rank 1 and a broadcast from the last group rank, and dumps the set's
+ * order and every input and output (tests/test_off_lfa.py checks them).
+ */
+static void ordered_group(struct fid_ep *ep, struct fid_mc *g, const char *tag,
+			  const fi_addr_t *order, size_t n)
+{
+	fi_addr_t ga = fi_mc_addr(g);
+	int pos = -1, req[4];
+	char name[64];
+
+	for (size_t i = 0; i < n; i++)
+		if ((int)order[i] == me)
+			pos = (int)i;
+	if (pos < 0) {
+		float x = 0;
+
+		CHECK(fi_allreduce(ep, &x, 1, NULL, &x, NULL, ga, FI_FLOAT, FI_SUM, 0,
+				   &req[0]) == -FI_EINVAL, "%s: non-member refused", tag);
+		return;
+	}
+	{
+		int32_t mine[3] = { me, 10 * me, pos }, all[3 * MAXR];
+
+		CHECK(fi_allgather(ep, mine, 3, NULL, all, NULL, ga, FI_INT32, 0,
+				   &req[0]) == 0, "%s allgather", tag);
+		wait_comp(&req[0]);
+		for (size_t k = 0; k < n; k++)
+			CHECK(all[3 * k] == (int32_t)order[k] && all[3 * k + 2] == (int32_t)k,
+			      "%s allgather block %zu holds rank %d", tag, k, all[3 * k]);
+		snprintf(name, sizeof(name), "%s_allgather", tag);
+		dump(name, "out", all, 3 * n * 4);
+	}
+	{
+		float x[4099], y[4099];
+		double d[333], e[333], b[9];
+
+		seed(40 + me);
+		for (int i = 0; i < 4099; i++)
+			x[i] = (float)unif(-1, 1);
+		CHECK(fi_allreduce(ep, x, 4099, NULL, y, NULL, ga, FI_FLOAT, FI_SUM, 0,
+				   &req[1]) == 0, "%s allreduce", tag);
+		wait_comp(&req[1]);
+		snprintf(name, sizeof(name), "%s_sum_f32", tag);
+		dump(name, "in", x, sizeof(x));
+		dump(name, "out", y, sizeof(y));
+		seed(60 + me);
+		for (int i = 0; i < 333; i++)
+			d[i] = unif(-1, 1);
+		memset(e, 0, sizeof(e));
+		CHECK(fi_reduce(ep, d, 333, NULL, e, NULL, ga, n > 1 ? 1 : 0, FI_DOUBLE,
+				FI_SUM, 0, &req[2]) == 0, "%s reduce", tag);
+		wait_comp(&req[2]);
+		snprintf(name, sizeof(name), "%s_reduce_f64", tag);
+		dump(name, "in", d, sizeof(d));
+		if (pos == (n > 1 ? 1 : 0))
+			dump(name, "out", e, sizeof(e));
+		for (int i = 0; i < 9; i++)
+			b[i] = pos == (int)n - 1 ? 1000.0 * me + i : -1.0;
+		CHECK(fi_broadcast(ep, b, 9, NULL, ga, (fi_addr_t)n - 1, FI_DOUBLE, 0,
+				   &req[3]) == 0, "%s broadcast", tag);
+		wait_comp(&req[3]);
+		for (int i = 0; i < 9; i++)
+			CHECK(b[i] == 1000.0 * (double)order[n - 1] + i,
+			      "%s broadcast from group rank %zu", tag, n - 1);
+	}
+}
+
+static void ordered_sets(struct fid_av *av, struct fid_ep *ep, struct fid_mc *world_mc)
+{
+	struct fi_av_set_attr sattr = { 0 };
+	struct fid_av_set *a, *b, *zero;
+	struct fid_mc *ga, *gb;
+	fi_addr_t order[MAXR], self_addr;
+	size_t n = 0;
+	int req[2];
+
+	sattr.count = (size_t)nranks;
+	sattr.start_addr = 0;
+	sattr.end_addr = (fi_addr_t)nranks - 1;
+	sattr.stride = 2;
+	CHECK(fi_av_set(av, &sattr, &a, NULL) == 0, "set A");
+	/* the expected order, by the reference's rules */
+	for (int r = 0; r < nranks; r += 2)
+		order[n++] = (fi_addr_t)r;
+	if (nranks > 1) {
+		CHECK(fi_av_set_insert(a, 1) == 0, "insert 1");
+		order[n++] = 1;
+	}
+	if (nranks > 3) {
+		CHECK(fi_av_set_insert(a, 3) == 0, "insert 3");
+		order[n++] = 3;
+		CHECK(fi_av_set_remove(a, 2) == 0, "remove 2");
+		order[1] = order[--n];          /* 2 sat at index 1 */
+	}
+	dump("setA", "order", order, n * sizeof(fi_addr_t));
+	CHECK(fi_join_collective(ep, fi_mc_addr(world_mc), a, 0, &ga, &req[0]) == 0,
+	      "join A");
+	wait_join(ga);
+	ordered_group(ep, ga, "setA", order, n);
+
+	/* B = every rank diff {0} */
+	sattr.stride = 1;
+	CHECK(fi_av_set(av, &sattr, &b, NULL) == 0, "set B");
+	sattr.end_addr = 0;
+	CHECK(fi_av_set(av, &sattr, &zero, NULL) == 0, "set {0}");
+	CHECK(fi_av_set_diff(b, zero) == 0, "diff");
+	n = 0;
+	for (int r = 0; r < nranks; r++)
+		order[n++] = (fi_addr_t)r;
+	order[0] = order[--n];
+	dump("setB", "order", order, n * sizeof(fi_addr_t));
+	if (me != 0 && n) {
+		/* coll_addr = the set's own address: its members alone join */
+		CHECK(fi_av_set_addr(b, &self_addr) == 0, "set B addr");
+		CHECK(fi_join_collective(ep, self_addr, b, 0, &gb, &req[1]) == 0, "join B");
+		wait_join(gb);
+		ordered_group(ep, gb, "setB", order, n);
+		fi_close(&gb->fid);
+	}
+	fi_close(&ga->fid);
+	fi_close(&zero->fid);
+	fi_close(&b->fid);
+	fi_close(&a->fid);
+}
+
 static int run_rank(const char *prov_path)
 {
 	void *dl;
@@ -1033,6 +1171,7 @@ static int run_rank(const char *prov_path)
 		CHECK(fi_allreduce(ep, &x, 1, NULL, &x, NULL, subaddr, FI_FLOAT, FI_SUM, 0,
 				   &req[11]) == -FI_EINVAL, "non-member refused");
 	}
+	ordered_sets(av, ep, mc);
 	/* let the last transfers drain before anyone closes its sockets */
 	CHECK(fi_barrier(ep, world, &req[12]) == 0, "final barrier");
 	wait_comp(&req[12]);

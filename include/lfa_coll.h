@@ -164,8 +164,14 @@ int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
 /* ---- groups (fi_join_collective) -------------------------------------- */
 
 /* Form a group from the parent `coll_addr` (LFA_ADDR_NOTAVAIL = the world
- * group).  `ranks` (sorted parent ranks, `nmembers` entries) selects the
- * members; NULL = all.  EVERY parent rank calls it with the same list — the
+ * group).  `ranks` (`nmembers` distinct parent ranks, in any order) selects
+ * the members and numbers them: ranks[i] becomes group rank i — prov/coll's
+ * local_rank is the member's index in the joined av_set's address array
+ * (coll_find_local_rank, coll_coll.c:669-689), so a set built as stride
+ * {0, 2, 4} plus an inserted 1 numbers parent rank 1 as group rank 3.  Group
+ * ranks decide the block order of allgather / scatter / reduce_scatter, the
+ * tree's association order and what a root_addr names.  NULL = all, in parent
+ * order.  EVERY parent rank calls it with the same list — the
  * group id is agreed by a UINT8 BAND allreduce of the free-id masks over the
  * parent, as coll_join_collective does (coll_coll.c:969-973).  Non-members
  * get a handle too, but collectives on it return -LFA_EINVAL.
@@ -178,8 +184,9 @@ int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
  * the av_set's own address (coll_av_set_addr, coll_av_set.c:166-175, taken as
  * the parent at coll_coll.c:939-941), so the free-id BAND runs over the new
  * group itself and the rest of `coll_addr`'s group does not call anything
- * (fabtests core_coll.c:138-178, the stride test).  `ranks` are sorted ranks
- * of `coll_addr`'s group and must include the caller.  The agreement travels
+ * (fabtests core_coll.c:138-178, the stride test).  `ranks` are distinct ranks
+ * of `coll_addr`'s group in group-rank order, as above, and must include the
+ * caller.  The agreement travels
  * under group id 256 (outside the 0..255 ids a join hands out), so it cannot
  * meet a joined group's traffic.  On a device domain a strict subset gets an
  * RCCL communicator of its own (the first member's unique id sent to the
@@ -195,6 +202,20 @@ int lfa_mc_group_id(struct lfa_coll_mc *mc);
 int lfa_mc_close(struct lfa_coll_mc *mc);
 /* The world group, usable without a join (the reference's av_set coll_mc). */
 lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep);
+
+/* What the group's LFA_ALGO_P2P operations ran on this member so far
+ * (prov/coll keeps no collective counters; these let a caller see which
+ * path a bucket took): one-shot kernels (small buckets in one launch),
+ * flag barriers, and P2P operations in total.  timed_out is 1 once a wait
+ * of the group gave up (the group then refuses P2P operations). */
+struct lfa_mc_counters {
+	uint64_t p2p_ops;
+	uint64_t oneshot;
+	uint64_t flag_barriers;
+	int timed_out;
+};
+int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+		    struct lfa_mc_counters *out);
 
 /* ---- fi_ops_collective ------------------------------------------------ */
 

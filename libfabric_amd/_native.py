@@ -70,7 +70,13 @@ def _bind_tune(L):
     L.lfa__tune_treeput_f32.restype = c_int
     L.lfa__tune_treeput_f32.argtypes = [c_int, ctypes.POINTER(c_void_p), c_int,
                                         ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]
-    for fn in (L.lfa__tune_sum_f32, L.lfa__tune2_sum_f32):
+    L.lfa__tp_probe.restype = c_int
+    L.lfa__tp_probe.argtypes = [c_int, ctypes.POINTER(c_void_p), c_int,
+                                ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]
+    L.lfa__tune_treeput_u.restype = c_int
+    L.lfa__tune_treeput_u.argtypes = [c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int,
+                                      ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]
+    for fn in (L.lfa__tune_sum_f32, L.lfa__tune2_sum_f32, L.lfa__tune3_sum_f32):
         fn.restype = c_int
         fn.argtypes = [c_int, c_void_p, c_void_p, c_size_t, c_void_p]
     L.lfa__tune_fetch_f32.restype = c_int

@@ -65,6 +65,12 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     tune_o = os.path.join(BUILD, "lfa_tune.o")
     if _newer(tune_o, [tune] + hdrs):
         steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", tune_o])
+    # the tree_put register-pressure probe (tools/probe_treeput_narrow.py)
+    probe = os.path.join(CSRC, "lfa_probe.hip")
+    probe_o = os.path.join(BUILD, "lfa_probe.o")
+    tune_objs = [tune_o, probe_o]
+    if _newer(probe_o, [probe] + hdrs):
+        steps.append([HIPCC, *HIP_FLAGS, "-c", probe, "-o", probe_o])
     # op-independent device code: the P2P flag barrier
     sig = os.path.join(CSRC, "lfa_signal.hip")
     o = os.path.join(BUILD, "lfa_signal.o")
@@ -94,9 +100,9 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     if steps or _newer(LIB_LFA, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_LFA,
               *objs, "-Wl,-soname,liblfa.so"])
-    if _newer(LIB_TUNE, [tune_o]):
+    if _newer(LIB_TUNE, tune_objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TUNE,
-              tune_o, "-Wl,-soname,liblfa_tune.so"])
+              *tune_objs, "-Wl,-soname,liblfa_tune.so"])
     if verbose:
         print(f"built {LIB_LFA} ({len(steps)} objects recompiled)")
     return LIB_LFA

@@ -107,6 +107,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_domain_open_peer.argtypes = [c_int] + L.lfa_coll_domain_open_host.argtypes
     L.lfa_mc_group_id.restype = c_int
     L.lfa_mc_group_id.argtypes = [c_void_p]
+    L.lfa_mc_counters.restype = c_int
+    L.lfa_mc_counters.argtypes = [c_void_p, c_uint64, P(McCounters)]
     L.lfa_coll_domain_close.restype = c_int
     L.lfa_coll_domain_close.argtypes = [c_void_p]
     L.lfa_coll_ep_open.restype = c_int
@@ -270,6 +272,12 @@ def _ptr(x) -> int | None:
     return int(x)
 
 
+class McCounters(ctypes.Structure):
+    """struct lfa_mc_counters (include/lfa_coll.h)."""
+    _fields_ = [("p2p_ops", ctypes.c_uint64), ("oneshot", ctypes.c_uint64),
+                ("flag_barriers", ctypes.c_uint64), ("timed_out", ctypes.c_int)]
+
+
 class OneShot(ctypes.Structure):
     """struct lfa_oneshot (libfabric_amd/csrc/lfa_signal.h): one rank's
     one-shot reduction over the members' symmetric workspaces."""
@@ -278,7 +286,10 @@ class OneShot(ctypes.Structure):
                 ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
                 ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
                 ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
-                ("timeout_us", ctypes.c_uint64)]
+                ("ticket", ctypes.c_uint32), ("timeout_us", ctypes.c_uint64)]
+
+
+SIG_NONE = 0xFFFFFFFF   # lfa_signal.h LFA_SIG_NONE: no wait of the group timed out
 
 
 def oneshot_reduce(op: int, dt: int, a: OneShot, stream) -> None:
@@ -332,6 +343,13 @@ class Endpoint:
 
     def group_id(self, mc: int) -> int:
         return lib().lfa_mc_group_id(mc)
+
+    def counters(self, coll_addr: int | None = None) -> dict:
+        """lfa_mc_counters: which P2P paths the group's operations took."""
+        c = McCounters()
+        _chk(lib().lfa_mc_counters(self.ep, coll_addr or self.world, ctypes.byref(c)),
+             "lfa_mc_counters")
+        return {k: getattr(c, k) for k, _ in McCounters._fields_}
 
     def close(self) -> None:
         L = lib()

@@ -147,8 +147,6 @@ static void ep_release(struct lfa_coll_ep *ep)
 		hipFree(ep->ctl_dev);
 	if (ep->barrier_host)
 		hipHostFree(ep->barrier_host);
-	if (ep->sig_status)
-		hipHostFree(ep->sig_status);
 	if (ep->copy_stream)
 		hipStreamDestroy(ep->copy_stream);
 	if (ep->d2h_stream)
@@ -188,13 +186,10 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
 		    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess ||
 		    hipMalloc(&ep->ctl_dev, ctl) != hipSuccess ||
-		    hipHostMalloc((void **)&ep->sig_status, sizeof(uint32_t),
-				  hipHostMallocCoherent) != hipSuccess ||
 		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
-		*ep->sig_status = 0;
 		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	} else if (d->device >= 0) {
 		/* device buffers on a peer-transfer domain: the local items' kernels
@@ -202,13 +197,10 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		 * handshake records */
 		hipSetDevice(d->device);
 		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
-		    hipHostMalloc((void **)&ep->sig_status, sizeof(uint32_t),
-				  hipHostMallocCoherent) != hipSuccess ||
 		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
-		*ep->sig_status = 0;
 	}
 	memset(ep->cid_mask, 0xff, sizeof(ep->cid_mask));
 	ep->cid_mask[0] &= (uint8_t)~1u;            /* world group id 0 taken */
@@ -229,6 +221,61 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 
 static void hop_free(struct hop *h);
 
+static void sig_word_free(struct lfa_coll_mc *mc)
+{
+	if (mc->sig_word)
+		hipHostFree(mc->sig_word);
+	mc->sig_word = NULL;
+}
+
+/*
+ * Before a P2P operation of `mc`: its timed-out-wait word exists (allocated
+ * at the group's first P2P operation: host-mapped, LFA_SIG_NONE) and no wait
+ * of the group has timed out — after one the members' flag epochs disagree
+ * and a barrier could pass on stale posts, so the group refuses P2P
+ * operations (close and re-join it); other groups are unaffected.
+ */
+static int sig_ready(struct lfa_coll_mc *mc)
+{
+	if (mc->sig_failed)
+		return -LFA_EIO;
+	if (!mc->sig_word) {
+		hipSetDevice(mc->ep->dom->device);
+		if (hipHostMalloc((void **)&mc->sig_word, sizeof(uint32_t),
+				  hipHostMallocCoherent) != hipSuccess) {
+			mc->sig_word = NULL;
+			return -LFA_ENOMEM;
+		}
+		*(volatile uint32_t *)mc->sig_word = LFA_SIG_NONE;
+	}
+	if (*(volatile uint32_t *)mc->sig_word != LFA_SIG_NONE)
+		return -LFA_EIO;
+	return 0;
+}
+
+/* The operation just queued ran P2P kernels on `mc` if its ticket moved. */
+static void tag_p2p(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc, uint32_t t0)
+{
+	struct pending *p;
+
+	if (!ep->qlen || mc->p2p_ticket == t0)
+		return;
+	p = &ep->q[(ep->qhead + ep->qlen - 1) % ep->qcap];
+	p->pmc = mc;
+	p->ticket = mc->p2p_ticket;
+}
+
+/* Did a P2P wait of this operation, or of an earlier one of its group, time
+ * out?  (The group's kernels run in order; the word holds the lowest failing
+ * ticket.) */
+static int p2p_timed_out(const struct pending *p)
+{
+	if (p->timed_out)
+		return 1;
+	return p->pmc && p->ticket && p->pmc->sig_word &&
+	       *(volatile uint32_t *)p->pmc->sig_word <= p->ticket;
+}
+
 int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 {
 	if (!ep)
@@ -238,10 +285,9 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		for (size_t i = 0; i < ep->qlen; i++)
 			hop_free(ep->q[(ep->qhead + i) % ep->qcap].hop);
 		p2p_release(&ep->world);
+		sig_word_free(&ep->world);
 		if (ep->stream)
 			hipStreamDestroy(ep->stream);
-		if (ep->sig_status)
-			hipHostFree(ep->sig_status);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -251,6 +297,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	}
 	/* every P2P operation ended in a barrier: no peer touches it now */
 	p2p_release(&ep->world);
+	sig_word_free(&ep->world);
 	for (size_t i = 0; i < ep->qlen; i++)
 		hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
 	for (int i = 0; i < ep->nev; i++)
@@ -268,7 +315,6 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	hipFree(ep->ctl_dev);
 	free(ep->ctl_host);
 	hipHostFree(ep->barrier_host);
-	hipHostFree(ep->sig_status);
 	hipStreamDestroy(ep->stream);
 	hipStreamDestroy(ep->copy_stream);
 	hipStreamDestroy(ep->d2h_stream);
@@ -323,6 +369,26 @@ static struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a)
 	if (a == LFA_ADDR_NOTAVAIL || a == 0)
 		return &ep->world;
 	return (struct lfa_coll_mc *)(uintptr_t)a;
+}
+
+int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
+		    struct lfa_mc_counters *out)
+{
+	struct lfa_coll_mc *mc;
+
+	if (!ep || !out)
+		return -LFA_EINVAL;
+	mc = mc_of(ep, coll_addr);
+	if (!mc)
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	out->p2p_ops = mc->p2p_ticket;
+	out->oneshot = mc->n_oneshot;
+	out->flag_barriers = mc->n_barrier;
+	out->timed_out = mc->sig_failed ||
+			 (mc->sig_word && *(volatile uint32_t *)mc->sig_word != LFA_SIG_NONE);
+	pthread_mutex_unlock(&ep->lock);
+	return 0;
 }
 
 /* Grow-only device buffer, stream-ordered so in-flight users stay valid. */
@@ -631,11 +697,13 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 
 		if (st > 0)
 			break;
-		if (st == 0 && ep->sig_status && *(volatile uint32_t *)ep->sig_status) {
-			/* a flag barrier of this or an earlier operation gave up
-			 * waiting for a member (lfa_signal.hip) */
-			*ep->sig_status = 0;
-			ep->sig_failed = 1;
+		if (st == 0 && p2p_timed_out(p)) {
+			/* a flag barrier or one-shot wait of this operation, or of
+			 * an earlier one of its group, gave up waiting for a member
+			 * (lfa_signal.h): this one and every later P2P operation of
+			 * the group fail; the earlier ones completed normally */
+			if (p->pmc)
+				p->pmc->sig_failed = 1;
 			st = -1;
 			perr = ETIMEDOUT;
 		}
@@ -856,6 +924,11 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 				"P2P flag area memset") == hipSuccess &&
 	     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
 			  "P2P flag area memset sync") == hipSuccess;
+	/* every member grows at the same operation: the epochs restart with the
+	 * zeroed flags, so a count past 2^31 never meets a zero word that reads
+	 * as "ahead"  */
+	mc->bar_epoch = 0;
+	mc->os_epoch = 0;
 	if (ok && n > 1)
 		ok = lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
 				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
@@ -1164,10 +1237,10 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		return ret;
 	memset(&x, 0, sizeof(x));
 	if (plan_uses_sym(pl->steps, pl->nsteps)) {
-		/* after a timed-out wait the members' flag epochs disagree: a
-		 * P2P operation could pass a barrier on stale posts */
-		if (ep->sig_failed)
-			return -LFA_EIO;
+		ret = sig_ready(mc);
+		if (ret)
+			return ret;
+		x.ticket = ++mc->p2p_ticket;
 		ret = p2p_ensure(mc, plan_sym_need(pl->steps, pl->nsteps, mc->size,
 						   count, esz));
 		if (ret)
@@ -1371,9 +1444,13 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	if (ret)
 		return ret;
 	sym = plan_uses_sym(raw.steps, raw.nsteps);
-	if (sym && ep->sig_failed) {
-		plan_free(&raw);
-		return -LFA_EIO;        /* epochs disagree since a timed-out wait */
+	if (sym && dev) {
+		ret = sig_ready(mc);
+		if (ret) {
+			plan_free(&raw);
+			return ret;     /* epochs disagree since a timed-out wait */
+		}
+		h->r.x.ticket = ++mc->p2p_ticket;
 	}
 	/* a device hop's BARRIER stays: the flag kernel (sig_barrier) */
 	ret = lower_plan(&raw, mc->rank, mc->size, esz, &h->pl, sym && !dev, !dev);
@@ -1435,6 +1512,7 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		       int kind, struct lfa_coll_mc *jmc, int dev)
 {
 	struct hop *h = calloc(1, sizeof(*h));
+	const uint32_t t0 = mc->p2p_ticket;
 	int ret;
 
 	if (!h)
@@ -1445,6 +1523,8 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		ret = enqueue_host(ep, h, context, kind, jmc);
 	if (ret)
 		hop_free(h);
+	else
+		tag_p2p(ep, mc, t0);
 	return ret;
 }
 
@@ -1455,6 +1535,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 {
 	struct lfa_coll_mc *mc;
 	size_t esz;
+	uint32_t t0;
 	int root = -1, ret, host;
 
 	if (!ep)
@@ -1503,6 +1584,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	pthread_mutex_lock(&ep->lock);
 	hipSetDevice(ep->dom->device);
 	mc->seq++;                              /* coll_get_next_id :48-52 */
+	t0 = mc->p2p_ticket;
 	host = (buf && count && !is_device_ptr(buf)) ||
 	       (result && count && !is_device_ptr(result));
 	if (!count) {
@@ -1536,6 +1618,8 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	}
 	if (!ret)
 		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+	if (!ret)
+		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
 	return ret;
 }
@@ -1620,6 +1704,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	/* coll_ep_barrier2 (coll_coll.c:997-1033): an allreduce of ~rank with
 	 * FI_BAND over one uint64. */
 	struct lfa_coll_mc *mc;
+	uint32_t t0;
 	int ret;
 
 	if (!ep)
@@ -1646,6 +1731,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 		return ret;
 	}
 	hipSetDevice(ep->dom->device);
+	t0 = mc->p2p_ticket;
 	ep->barrier_host[0] = ~(uint64_t)mc->rank;
 	ret = hipMemcpyAsync(ep->barrier_dev, ep->barrier_host, sizeof(uint64_t),
 			     hipMemcpyHostToDevice, ep->stream) == hipSuccess ?
@@ -1656,6 +1742,8 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 				 LFA_BAND, ep->stream);
 	if (!ret)
 		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+	if (!ret)
+		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
 	return ret;
 }
@@ -1748,15 +1836,30 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	if (members_only && !ranks)
 		return -LFA_EINVAL;
 	if (ranks) {
+		/* ranks[i] is the parent rank of group rank i, in any order: the
+		 * group numbers its members by their position in the joined set,
+		 * as prov/coll does (coll_find_local_rank, coll_coll.c:669-689:
+		 * local_rank = index in the av_set's fi_addr_array) */
+		uint8_t *seen;
+
+		if (!nmembers || nmembers > (size_t)parent->size)
+			return -LFA_EINVAL;
+		seen = calloc((size_t)parent->size / 8 + 1, 1);
+		if (!seen)
+			return -LFA_ENOMEM;
 		for (size_t i = 0; i < nmembers; i++) {
 			if (ranks[i] < 0 || ranks[i] >= parent->size ||
-			    (i && ranks[i] <= ranks[i - 1]))
-				return -LFA_EINVAL;
+			    (seen[ranks[i] / 8] & (1u << (ranks[i] % 8)))) {
+				free(seen);
+				return -LFA_EINVAL;     /* out of range or listed twice */
+			}
+			seen[ranks[i] / 8] |= (uint8_t)(1u << (ranks[i] % 8));
 			if (ranks[i] == parent->rank) {
 				member = 1;
 				pos = (int)i;
 			}
 		}
+		free(seen);
 	} else {
 		member = 1;
 		pos = parent->rank;
@@ -1816,8 +1919,10 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 
 		pthread_mutex_lock(&ep->comm_lock);
 		hipSetDevice(ep->dom->device);
+		/* key = the position in the set: RCCL numbers the new
+		 * communicator by key, so its rank is the group rank */
 		if (ncclCommSplit(parent->comm, member ? 0 : NCCL_SPLIT_NOCOLOR,
-				  parent->rank, &mc->comm, &cfg) != ncclSuccess)
+				  member ? pos : parent->rank, &mc->comm, &cfg) != ncclSuccess)
 			ret = -LFA_EIO;
 		pthread_mutex_unlock(&ep->comm_lock);
 		mc->owns_comm = !ret;
@@ -1852,6 +1957,9 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 					  context, 1, mc, 0);
 		}
 	} else if (!ret) {
+		struct lfa_coll_mc *over = members_only ? mc : parent;
+		const uint32_t t0 = over->p2p_ticket;
+
 		hipSetDevice(ep->dom->device);
 		ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) ==
 		      hipSuccess ? 0 : -LFA_ENOMEM;
@@ -1862,7 +1970,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
 			hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
 				       hipMemcpyHostToDevice, ep->stream);
-			ret = run_device(ep, members_only ? mc : parent, LFA_ALLREDUCE, dmask,
+			ret = run_device(ep, over, LFA_ALLREDUCE, dmask,
 					 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
 					 LFA_UINT8, LFA_BAND, ep->stream);
 			if (!ret)
@@ -1871,6 +1979,8 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		}
 		if (!ret)
 			ret = enqueue_completion(ep, ep->stream, context, 1, mc);
+		if (!ret)
+			tag_p2p(ep, over, t0);
 	}
 	if (ret)
 		free_mask(ep, mc);
@@ -1922,6 +2032,11 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 			p->kind = 2;
 			p->mc = NULL;
 		}
+		if (p->pmc == mc) {
+			/* the stream has drained (flush above): the word is final */
+			p->timed_out = p2p_timed_out(p);
+			p->pmc = NULL;
+		}
 	}
 	free_mask(ep, mc);
 	/* release the group id only if the join assigned one (a
@@ -1938,6 +2053,7 @@ int lfa_mc_close(struct lfa_coll_mc *mc)
 	} else {
 		p2p_release(mc);        /* a peer domain's device workspace */
 	}
+	sig_word_free(mc);
 	free(mc->members);
 	free(mc);
 	return 0;

@@ -170,16 +170,18 @@ LFA_INTERNAL int sig_barrier(struct xrun *r)
 	uint32_t *post[LFA_SIG_MAX];
 	int ret;
 
-	if (!r->x.sym || mc->size > LFA_SIG_MAX || !mc->ep->sig_status)
+	if (!r->x.sym || mc->size > LFA_SIG_MAX || !mc->sig_word)
 		return -LFA_EINVAL;
 	for (int k = 0; k < mc->size; k++)
 		post[k] = k == mc->rank ? NULL :
 			  (uint32_t *)(r->x.sym[k] + row) + mc->rank;
 	ret = lfa_flag_barrier_async(post, (const uint32_t *)(r->x.sym[mc->rank] + row),
 				     mc->size, mc->rank, mc->bar_epoch + 1,
-				     mc->ep->sig_status, sig_timeout_us(), r->stream);
-	if (!ret)
+				     mc->sig_word, r->x.ticket, sig_timeout_us(), r->stream);
+	if (!ret) {
 		mc->bar_epoch++;
+		mc->n_barrier++;
+	}
 	return ret;
 }
 
@@ -190,7 +192,7 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	struct lfa_oneshot a;
 	int ret;
 
-	if (!r->x.sym || !mc->ep->sig_status || !esz || (int)st->nsrc != mc->size ||
+	if (!r->x.sym || !mc->sig_word || !esz || (int)st->nsrc != mc->size ||
 	    2 * (size_t)mc->size * os_slot(st, mc->size, esz) > r->x.region)
 		return -LFA_EINVAL;
 	memset(&a, 0, sizeof(a));
@@ -205,11 +207,14 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	a.n = mc->size;
 	a.rank = mc->rank;
 	a.epoch = mc->os_epoch + 1;
-	a.status = mc->ep->sig_status;
+	a.status = mc->sig_word;
+	a.ticket = r->x.ticket;
 	a.timeout_us = sig_timeout_us();
 	ret = lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
-	if (!ret)
+	if (!ret) {
 		mc->os_epoch++;
+		mc->n_oneshot++;
+	}
 	return ret;
 }
 

@@ -30,6 +30,7 @@ struct xctx {
 	void *base[3];          /* SEND, RESULT, TMP */
 	char *const *sym;       /* [group rank] */
 	size_t region;
+	uint32_t ticket;        /* the group's P2P operation number (timeouts) */
 };
 
 /* ====================================================================== */
@@ -60,6 +61,15 @@ struct lfa_coll_mc {
 	 * is one more; equal on every member, collectives being ordered) */
 	uint32_t bar_epoch;
 	uint32_t os_epoch;      /* one-shot operations, likewise */
+	/* timed-out P2P waits of this group (lfa_signal.h): the host-mapped
+	 * status word (lowest failing ticket, LFA_SIG_NONE), the last ticket
+	 * handed out, and whether a failure was reaped — the members' epochs
+	 * then disagree, so the group refuses P2P operations (other groups of
+	 * the endpoint are unaffected) */
+	uint32_t *sig_word;
+	uint32_t p2p_ticket;
+	int sig_failed;
+	uint64_t n_oneshot, n_barrier;  /* lfa_mc_counters */
 };
 
 struct lfa_coll_domain {
@@ -78,6 +88,11 @@ struct pending {
 	void *context;
 	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
 	struct lfa_coll_mc *mc;
+	/* the group the operation's P2P kernels ran on and its highest ticket
+	 * (0: none); timed_out: found failed when that group was closed */
+	struct lfa_coll_mc *pmc;
+	uint32_t ticket;
+	int timed_out;
 };
 
 struct lfa_coll_ep {
@@ -99,9 +114,6 @@ struct lfa_coll_ep {
 	void *barrier_dev;          /* 2 x uint64 */
 	void *ctl_dev;              /* P2P handle exchange, nranks records */
 	void *ctl_host;
-	uint32_t *sig_status;       /* host-mapped: a flag barrier timed out */
-	int sig_failed;             /* one did: the groups' flag epochs are no
-				     * longer agreed, P2P operations refused */
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
 	hipEvent_t evpool[64];      /* recycled completion events */

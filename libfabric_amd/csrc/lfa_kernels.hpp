@@ -36,6 +36,20 @@ __device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
   else *p = v;
 }
 
+// The wave's index in its workgroup, as a SCALAR.  threadIdx.x / 64 is the
+// same on every lane of a wave, but the compiler cannot prove it: a buffer
+// descriptor built from it counts as divergent, so every buffer load / store
+// through it was wrapped in a readfirstlane loop (4 v_readfirstlane, a
+// compare, an exec save and a branch per access) and the 64-bit tile base was
+// kept per lane in VGPRs.  readfirstlane makes it uniform: the descriptors
+// live in SGPRs and each access is one instruction.  UW = false keeps the
+// round-2 (divergent) form for the A/B in liblfa_tune.so.
+template <bool UW = true>
+__device__ __forceinline__ unsigned wave_id() {
+  if constexpr (UW) return __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  else return threadIdx.x / 64;
+}
+
 // OP applied lane-wise to the 16/sizeof(T) elements packed in a 16-B vector.
 template <int OP, typename T>
 __device__ __forceinline__ u32x4 apply_vec(u32x4 d, u32x4 s) {
@@ -100,11 +114,11 @@ constexpr int kLdsWaves = 4;
 constexpr int kStoreNt = 2, kStoreSc1 = 16;
 constexpr size_t kSc1Bytes = (size_t)192 << 20;
 
-template <int OP, typename T, int U, int SAUX>
+template <int OP, typename T, int U, int SAUX, bool UW = true>
 __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
     u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
   __shared__ u32x4 lds[2][kLdsWaves][U][64];
-  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const unsigned w = wave_id<UW>(), l = threadIdx.x % 64;
   const size_t base =
       (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
   if (base + 64 * U <= nvec) {
@@ -288,7 +302,9 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
       if constexpr (SAUX == kStoreNt) {
         st<true>(dst + i, v);
       } else {
-        const size_t wb = i - threadIdx.x % 64;  // the wave's first vector
+        // the wave's first vector, as a scalar (wave_id)
+        const size_t wb = (size_t)blockIdx.x * (kBlock * U) + (size_t)u * kBlock +
+                          (size_t)wave_id() * 64;
         __builtin_amdgcn_raw_buffer_store_b128(
             v, __builtin_amdgcn_make_buffer_rsrc(dst + wb, 0, 64 * 16, 0x00020000),
             (threadIdx.x % 64) * 16, 0, SAUX);
@@ -306,7 +322,7 @@ __global__ __launch_bounds__(W * 64) void reduce_tree_lds(TreeArgs a, int nin,
                                                           u32x4 *dst,
                                                           size_t nvec) {
   extern __shared__ u32x4 tlds[];  // [nin][W][U][64]
-  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const unsigned w = wave_id(), l = threadIdx.x % 64;
   const size_t base = (size_t)blockIdx.x * (W * 64 * U) + (size_t)w * 64 * U;
   auto slot = [&](int k, int u) { return ((k * W + w) * U + u) * 64; };
   if (base + 64 * U <= nvec) {
@@ -397,9 +413,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void *base,
 // input; its loads and stores go through buffer descriptors sized to the
 // wave's tile, so the last, partial tile needs no guards (out-of-range lanes
 // load 0 and their stores are dropped by the hardware).
-template <int OP, typename T, int NLEAF, int U>
-__global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec) {
-  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+template <int OP, typename T, int NLEAF, int U, bool UW>
+__device__ __forceinline__ void tree_put_body(const PutArgs &a, size_t nvec) {
+  const unsigned w = wave_id<UW>(), l = threadIdx.x % 64;
   const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
   if (wbase >= nvec) return;
   const size_t left = nvec - wbase;
@@ -423,6 +439,11 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec
                                              (unsigned)(u * 64 + l) * 16, 0,
                                              kSysAux);
   }
+}
+
+template <int OP, typename T, int NLEAF, int U, bool UW = true>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put(PutArgs a, size_t nvec) {
+  tree_put_body<OP, T, NLEAF, U, UW>(a, nvec);
 }
 
 // One element at system scope (relaxed atomics of the element's width; a
@@ -504,7 +525,7 @@ struct OsArgs {
   uint32_t *status;
   uint64_t timeout;            // wall-clock ticks
   size_t chunk;                // a multiple of 16
-  uint32_t epoch;
+  uint32_t epoch, ticket;
   int n, rank;
   int vec;                     // every range start and result 16-B aligned
 };
@@ -544,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
     while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
                      a.epoch) < 0) {
       if (wall_clock64() - t0 > a.timeout) {
-        __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        lfa_sig_note_timeout(a.status, a.ticket);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -709,7 +730,7 @@ __global__ __launch_bounds__(kBlock) void fetch_elem(F f, size_t n0, size_t off1
 template <int U, int SAUX, typename F>
 __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds(F f, size_t nvec) {
   __shared__ u32x4 lds[F::kIn][kLdsWaves][U][64];
-  const unsigned w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const unsigned w = wave_id(), l = threadIdx.x % 64;
   const size_t base =
       (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
   if (base + 64 * U <= nvec) {
@@ -938,7 +959,7 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
   }
 }
 
-template <int OP, typename T, int NLEAF>
+template <int OP, typename T, int NLEAF, int UF = 0>
 static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
                              hipStream_t s) {
   constexpr size_t E = sizeof(T);
@@ -946,7 +967,7 @@ static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head
   // 8 inputs) where the registers allow it: up to 8 leaves of 4-16 B
   // elements.  Wider fan-in or byte/short lanes keep 2 KiB (U = 4 there
   // needs > 256 VGPRs and gave wrong uint8 results at 16 leaves).
-  constexpr int U = (NLEAF <= 8 && E >= 4) ? 4 : 2;
+  constexpr int U = UF ? UF : (NLEAF <= 8 && E >= 4) ? 4 : 2;
   size_t nvec = vec ? (cnt - head) * E / 16 : 0;
   if (nvec) {
     PutArgs b = a;
@@ -967,7 +988,8 @@ static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
 
-template <int OP, typename T>
+// UF != 0 forces the vector body's tile (KiB per wave) — liblfa_tune.so only.
+template <int OP, typename T, int UF = 0>
 static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
                            int nsrc, size_t cnt, hipStream_t s) {
   if constexpr (!supported<OP, T>()) {
@@ -996,12 +1018,12 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
     size_t head = vec ? ((16 - p0 % 16) % 16) / E : 0;
     if (head > cnt) head = cnt;
     switch (pof2) {
-      case 1: return launch_tree_put_n<OP, T, 1>(a, cnt, vec, head, s);
-      case 2: return launch_tree_put_n<OP, T, 2>(a, cnt, vec, head, s);
-      case 4: return launch_tree_put_n<OP, T, 4>(a, cnt, vec, head, s);
-      case 8: return launch_tree_put_n<OP, T, 8>(a, cnt, vec, head, s);
-      case 16: return launch_tree_put_n<OP, T, 16>(a, cnt, vec, head, s);
-      case 32: return launch_tree_put_n<OP, T, 32>(a, cnt, vec, head, s);
+      case 1: return launch_tree_put_n<OP, T, 1, UF>(a, cnt, vec, head, s);
+      case 2: return launch_tree_put_n<OP, T, 2, UF>(a, cnt, vec, head, s);
+      case 4: return launch_tree_put_n<OP, T, 4, UF>(a, cnt, vec, head, s);
+      case 8: return launch_tree_put_n<OP, T, 8, UF>(a, cnt, vec, head, s);
+      case 16: return launch_tree_put_n<OP, T, 16, UF>(a, cnt, vec, head, s);
+      case 32: return launch_tree_put_n<OP, T, 32, UF>(a, cnt, vec, head, s);
       default: return -LFA_EINVAL;
     }
   }
@@ -1060,6 +1082,7 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     chunk = (chunk + 15) & ~(size_t)15;
     a.chunk = chunk < 4096 ? 4096 : chunk;
     a.epoch = h.epoch;
+    a.ticket = h.ticket;
     a.n = n;
     a.rank = r;
     a.vec = mis == 0 && E <= 16;

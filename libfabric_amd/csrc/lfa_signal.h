@@ -30,14 +30,24 @@ extern "C" {
 #define LFA_OS_MAX_RANKS 8              /* one-shot groups: 2..8 members */
 
 /*
+ * Timed-out waits.  *status is one host-mapped word per group holding the
+ * lowest `ticket` (the group's P2P operation number, from 1) whose wait gave
+ * up, LFA_SIG_NONE while none has.  A kernel that times out lowers it to its
+ * own ticket — the group's kernels run in stream order, so no two race on it
+ * — and the host fails that operation and every later P2P operation of the
+ * group, while the earlier ones complete normally.
+ */
+#define LFA_SIG_NONE 0xffffffffu
+
+/*
  * Enqueue a barrier on `stream`: after the steps before it on every member's
  * stream, before the steps after it.  post[k] (k != rank) = this rank's word
  * in peer k's barrier row (IPC-mapped); wait = this rank's own barrier row.
- * A peer that has not posted `epoch` within timeout_us makes the kernel store
- * 1 into *status (host-mapped memory) and return.  0 or -LFA_E*.
+ * A peer that has not posted `epoch` within timeout_us makes the kernel lower
+ * *status to `ticket` and return.  0 or -LFA_E*.
  */
 int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
-			   int rank, uint32_t epoch, uint32_t *status,
+			   int rank, uint32_t epoch, uint32_t *status, uint32_t ticket,
 			   uint64_t timeout_us, void *stream);
 
 /*
@@ -70,11 +80,25 @@ struct lfa_oneshot {
 	size_t flag_off;        /* the flag area's offset in a workspace */
 	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
 	uint32_t epoch;         /* this group's one-shot operations so far + 1 */
-	uint32_t *status;       /* host-mapped; 1 after a timed-out wait */
+	uint32_t *status;       /* host-mapped; lowered to ticket on a timeout */
+	uint32_t ticket;        /* this P2P operation's number in the group */
 	uint64_t timeout_us;
 };
 int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 				void *stream);
+
+#ifdef __HIPCC__
+/* A wait of operation `ticket` gave up: lower the group's status word to it
+ * (plain system-scope load and store: the group's kernels are stream-ordered,
+ * and every lane of one kernel that times out stores the same ticket). */
+static __device__ __forceinline__ void lfa_sig_note_timeout(uint32_t *status,
+							     uint32_t ticket)
+{
+	if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) > ticket)
+		__hip_atomic_store(status, ticket, __ATOMIC_RELAXED,
+				   __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#endif
 
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
 uint64_t lfa__wallclock_ticks_per_us(void);

@@ -21,7 +21,7 @@ struct BarArgs {
   const uint32_t *wait;
   uint32_t *status;
   uint64_t timeout;  // wall-clock ticks
-  uint32_t epoch;
+  uint32_t epoch, ticket;
   int n, rank;
 };
 
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(64) void flag_barrier(BarArgs a) {
   while ((int32_t)(__hip_atomic_load(a.wait + k, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
     if (wall_clock64() - t0 > a.timeout) {
-      __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      lfa_sig_note_timeout(a.status, a.ticket);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -63,7 +63,7 @@ extern "C" uint64_t lfa__wallclock_ticks_per_us(void) {
 
 extern "C" int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
                                       int rank, uint32_t epoch, uint32_t *status,
-                                      uint64_t timeout_us, void *stream) {
+                                      uint32_t ticket, uint64_t timeout_us, void *stream) {
   if (n < 1 || n > LFA_SIG_MAX || rank < 0 || rank >= n || !wait || !status || !post)
     return -LFA_EINVAL;
   if (n == 1) return 0;
@@ -77,6 +77,7 @@ extern "C" int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wai
   a.status = status;
   a.timeout = timeout_us * lfa__wallclock_ticks_per_us();
   a.epoch = epoch;
+  a.ticket = ticket;
   a.n = n;
   a.rank = rank;
   hipLaunchKernelGGL(flag_barrier, dim3(1), dim3(64), 0, (hipStream_t)stream, a);

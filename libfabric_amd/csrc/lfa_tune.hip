@@ -740,3 +740,151 @@ extern "C" int lfa__tune_stream(int kind, void *dst, const void *a, const void *
   }
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
+
+// ---------------------------------------------------------------------------
+// reduce_tree_put with a forced tile: the product picks
+// U = 4 KiB per wave only up to 8 leaves of >= 4-byte lanes; this entry
+// builds the other tiles for the narrow lanes so tools/probe_treeput_narrow.py
+// can check them lane by lane against the oracle.  u in {1, 2, 4}.
+// ---------------------------------------------------------------------------
+extern "C" int lfa__tune_treeput_u(int u, int op, int dt, void *const *dsts, int ndst,
+                                   const void *const *srcs, int nsrc, size_t cnt,
+                                   void *stream) {
+  using namespace lfa;
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto opc, auto *tag) -> int {
+    constexpr int O = decltype(opc)::value;
+    typedef typename std::remove_pointer<decltype(tag)>::type T;
+    switch (u) {
+      case 1: return launch_tree_put<O, T, 1>(dsts, ndst, srcs, nsrc, cnt, s);
+      case 2: return launch_tree_put<O, T, 2>(dsts, ndst, srcs, nsrc, cnt, s);
+      case 4: return launch_tree_put<O, T, 4>(dsts, ndst, srcs, nsrc, cnt, s);
+      default: return -LFA_EINVAL;
+    }
+  };
+  using SUM = std::integral_constant<int, OP_SUM>;
+  using MIN = std::integral_constant<int, OP_MIN>;
+  using PROD = std::integral_constant<int, OP_PROD>;
+  using BXOR = std::integral_constant<int, OP_BXOR>;
+  if (op == OP_SUM && dt == LFA_UINT8) return go(SUM(), (uint8_t *)0);
+  if (op == OP_SUM && dt == LFA_INT8) return go(SUM(), (int8_t *)0);
+  if (op == OP_SUM && dt == LFA_UINT16) return go(SUM(), (uint16_t *)0);
+  if (op == OP_SUM && dt == LFA_INT16) return go(SUM(), (int16_t *)0);
+  if (op == OP_MIN && dt == LFA_INT8) return go(MIN(), (int8_t *)0);
+  if (op == OP_PROD && dt == LFA_UINT8) return go(PROD(), (uint8_t *)0);
+  if (op == OP_BXOR && dt == LFA_UINT8) return go(BXOR(), (uint8_t *)0);
+  if (op == OP_SUM && dt == LFA_FLOAT) return go(SUM(), (float *)0);
+  return -LFA_EOPNOTSUPP;
+}
+
+// ---------------------------------------------------------------------------
+// combine_lds with the wave's tile drained in steps: the
+// loads of vector u of dst and src issue back to back (d0 s0 d1 s1 ...), and
+// step u waits only until its own pair has landed — vmcnt counts loads,
+// LDS-DMA and stores together in issue order, so before step u the
+// 2(U-1-u) younger loads and the u stores already issued may stay in
+// flight — then stores vector u while the later loads are still arriving.
+// The product waits vmcnt(0) for the whole 2·U KiB before its first store.
+// ---------------------------------------------------------------------------
+namespace lfa_pipe {
+using lfa::u32x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+  // gfx9 simm16: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] (15) | vmcnt[5:4] << 14
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int U, int W, int SAUX, int u>
+__device__ __forceinline__ void drain_step(u32x4 (*lds)[W][U][64], unsigned w, unsigned l,
+                                           u32x4 *dst, __amdgpu_buffer_rsrc_t r) {
+  if constexpr (u < U) {
+    wait_vm<2 * (U - 1 - u) + u>();
+    const u32x4 v = lfa::apply_vec<lfa::OP_SUM, float>(lds[0][w][u][l], lds[1][w][u][l]);
+    if constexpr (SAUX == lfa::kStoreNt)
+      __builtin_nontemporal_store(v, dst + u * 64 + l);
+    else
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    drain_step<U, W, SAUX, u + 1>(lds, w, l, dst, r);
+  }
+}
+
+template <int U, int W, int SAUX>
+__global__ __launch_bounds__(W * 64) void sum_lds_drain(u32x4 *__restrict__ dst,
+                                                        const u32x4 *__restrict__ src,
+                                                        size_t nvec) {
+  __shared__ u32x4 lds[2][W][U][64];
+  const unsigned w = lfa::wave_id(), l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (W * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    }
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+    drain_step<U, W, SAUX, 0>(lds, w, l, dst + base, r);
+  } else {
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        __builtin_nontemporal_store(
+            lfa::apply_vec<lfa::OP_SUM, float>(__builtin_nontemporal_load(dst + i),
+                                               __builtin_nontemporal_load(src + i)),
+            dst + i);
+    }
+  }
+}
+
+// the product's store policy for the size: write-through below kSc1Bytes
+template <int U, int W>
+static void drain_auto(u32x4 *d, const u32x4 *v, size_t nvec, hipStream_t s) {
+  const dim3 grid((unsigned)((nvec + W * 64 * U - 1) / (W * 64 * U))), block(W * 64);
+  if (nvec * 16 < lfa::kSc1Bytes)
+    hipLaunchKernelGGL((sum_lds_drain<U, W, lfa::kStoreSc1>), grid, block, 0, s, d, v, nvec);
+  else
+    hipLaunchKernelGGL((sum_lds_drain<U, W, lfa::kStoreNt>), grid, block, 0, s, d, v, nvec);
+}
+}  // namespace lfa_pipe
+
+// 70.. : the drained-in-steps forms.  70 U=4 W=4 (the product's tile), 71
+// U=8 W=4, 72 U=4 W=8, 73 U=2 W=8, 74 U=8 W=2, 75/76 U=4 with the store
+// policy forced nt / sc1.  77: the round-2 product (combine_lds with the wave
+// index divergent to the compiler, so its sc1 buffer stores ran in
+// readfirstlane loops), with the product's store policy for the size.
+extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_t nvec,
+                                  void *stream) {
+  using namespace lfa_pipe;
+  hipStream_t s = (hipStream_t)stream;
+  u32x4 *d = (u32x4 *)dst;
+  const u32x4 *v = (const u32x4 *)src;
+  const dim3 g4((unsigned)((nvec + 1023) / 1024)), b4(256);
+  switch (variant) {
+    case 70: drain_auto<4, 4>(d, v, nvec, s); break;
+    case 71: drain_auto<8, 4>(d, v, nvec, s); break;
+    case 72: drain_auto<4, 8>(d, v, nvec, s); break;
+    case 73: drain_auto<2, 8>(d, v, nvec, s); break;
+    case 74: drain_auto<8, 2>(d, v, nvec, s); break;
+    case 75:
+      hipLaunchKernelGGL((sum_lds_drain<4, 4, lfa::kStoreNt>), g4, b4, 0, s, d, v, nvec);
+      break;
+    case 76:
+      hipLaunchKernelGGL((sum_lds_drain<4, 4, lfa::kStoreSc1>), g4, b4, 0, s, d, v, nvec);
+      break;
+    case 77:
+      if (nvec * 16 < lfa::kSc1Bytes)
+        hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreSc1, false>), g4,
+                           b4, 0, s, d, v, nvec);
+      else
+        hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreNt, false>), g4,
+                           b4, 0, s, d, v, nvec);
+      break;
+    default: return -LFA_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}

@@ -712,13 +712,10 @@ static long olfa_index(const fi_addr_t *list, size_t n, fi_addr_t addr)
 	return -1;
 }
 
-static int olfa_cmp_int(const void *a, const void *b)
-{
-	return *(const int *)a - *(const int *)b;
-}
-
 /* A join whose parent is the set itself: its members, as world ranks, form
- * the group through lfa_join_members; the other world ranks call nothing. */
+ * the group through lfa_join_members; the other world ranks call nothing.
+ * Group rank i is the set's i-th address (coll_find_local_rank,
+ * coll_coll.c:669-689), whatever order insert / remove left it in. */
 static int olfa_join_self(struct olfa_ep *ep, struct olfa_av_set *set,
 			  struct olfa_mc *m, uint64_t flags, void *context)
 {
@@ -742,14 +739,8 @@ static int olfa_join_self(struct olfa_ep *ep, struct olfa_av_set *set,
 	pthread_mutex_unlock(&ep->lock);
 	if (ret)
 		goto out;
-	qsort(ranks, n, sizeof(int), olfa_cmp_int);
-	for (size_t i = 0; i < n; i++) {
-		if (i && ranks[i] == ranks[i - 1]) {
-			ret = -FI_EINVAL;       /* an address listed twice */
-			goto out;
-		}
-		m->members[i] = ep->waddr[ranks[i]];
-	}
+	for (size_t i = 0; i < n; i++)
+		m->members[i] = set->addr[i];   /* lfa_join_members rejects repeats */
 	m->nmembers = n;
 	ret = lfa_join_members(ep->le, lfa_coll_world_addr(ep->le), ranks, n, flags,
 			       &m->lmc, context);
@@ -886,10 +877,8 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 			goto err;
 		}
 		ranks[i] = (int)r;
+		m->members[i] = set->addr[i];   /* group rank i: the set's order */
 	}
-	qsort(ranks, n, sizeof(int), olfa_cmp_int);
-	for (size_t i = 0; i < n; i++)
-		m->members[i] = parent->members[ranks[i]];
 	m->nmembers = n;
 	pthread_mutex_unlock(&ep->lock);
 	ret = lfa_join_collective(ep->le, paddr, ranks, n, flags, &m->lmc, context);
@@ -1605,8 +1594,18 @@ static int olfa_set_grow(struct olfa_av_set *s, size_t need)
 	return 0;
 }
 
-/* util_av_set_insert / _remove / _union / _intersect / _diff
- * (prov/util/src/util_coll.c semantics via coll_av_set.c) */
+/* coll_av_set_insert / _remove / _union / _intersect / _diff
+ * (coll_av_set.c:35-164).  The ORDER they leave matters: it numbers the
+ * members of a group joined over the set (olfa_join).  insert and union
+ * append, remove moves the last address into the hole (:149-164).
+ * intersect keeps dst's order; diff removes src's addresses one by one, in
+ * src's order, exactly as remove would.  The reference's own intersect and
+ * diff lose members in some cases — intersect drops a common address whose
+ * order in src differs from dst's ({a,b,c,d} ∩ {c,a} = {c}), diff writes the
+ * found address over the last one instead of moving the last into the hole
+ * ({a,b,c,d} \ {b} = {a,b,c}) — so these follow the evident intent; they
+ * give the reference's result wherever the reference keeps every member
+ * (tests/test_off_lfa.py::test_av_set_order). */
 static int olfa_set_insert(struct fid_av_set *set, fi_addr_t addr)
 {
 	struct olfa_av_set *s = olfa_container_of(set, struct olfa_av_set, set_fid);
@@ -1626,8 +1625,7 @@ static int olfa_set_remove(struct fid_av_set *set, fi_addr_t addr)
 
 	if (i < 0)
 		return -FI_EINVAL;
-	memmove(&s->addr[i], &s->addr[i + 1], (s->count - i - 1) * sizeof(fi_addr_t));
-	s->count--;
+	s->addr[i] = s->addr[--s->count];       /* coll_av_set.c:156-160 */
 	return 0;
 }
 
@@ -1666,12 +1664,13 @@ static int olfa_set_diff(struct fid_av_set *dst, const struct fid_av_set *src)
 	struct olfa_av_set *d = olfa_container_of(dst, struct olfa_av_set, set_fid);
 	const struct olfa_av_set *s =
 		olfa_container_of(src, struct olfa_av_set, set_fid);
-	size_t k = 0;
 
-	for (size_t i = 0; i < d->count; i++)
-		if (olfa_index(s->addr, s->count, d->addr[i]) < 0)
-			d->addr[k++] = d->addr[i];
-	d->count = k;
+	for (size_t i = 0; i < s->count; i++) {
+		long j = olfa_index(d->addr, d->count, s->addr[i]);
+
+		if (j >= 0)
+			d->addr[j] = d->addr[--d->count];
+	}
 	return 0;
 }
 

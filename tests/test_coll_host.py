@@ -198,6 +198,68 @@ def _joins_members(ep, rank, world):
     ep.wait(ep.barrier())
 
 
+def _set_order(world):
+    """An av_set's address order as prov/coll leaves it (coll_av_set.c:
+    insert appends, remove moves the last address into the hole): stride
+    {0, 2, ..} + insert 1 (+ insert 3, remove 2 from N = 4) — N = 3 gives
+    [0, 2, 1], N = 5 [0, 3, 4, 1]."""
+    a = list(range(0, world, 2))
+    if world > 1:
+        a.append(1)
+    if world > 3:
+        a.append(3)
+        i = a.index(2)
+        a[i] = a[-1]
+        a.pop()
+    return a
+
+
+def _joins_set_order(ep, rank, world, oracle, coll):
+    """group rank r = the r-th address of the joined set
+    (coll_find_local_rank, coll_coll.c:669-689), not the r-th smallest, for
+    every algorithm; through lfa_join_collective (every rank calls) and
+    lfa_join_members (members only)."""
+    order = _set_order(world)
+    sends = _inputs(oracle, 8, 4099, world, 99)      # float, indexed by parent rank
+    mine = [sends[m] for m in order]
+    want = oracle.allreduce(2, 8, mine)[0]
+    if order != sorted(order) and len(order) > 2:
+        srt = oracle.allreduce(2, 8, [sends[m] for m in sorted(order)])[0]
+        assert srt.tobytes() != want.tobytes()        # the order is observable
+    for members_only in (False, True):
+        if members_only and rank not in order:
+            continue
+        mc, _ = (ep.join_members(order) if members_only else ep.join(order))
+        ep.wait_join()
+        addr = ep.mc_addr(mc)
+        if rank in order:
+            pos = order.index(rank)
+            for algo in (coll.ALGO_TREE, coll.ALGO_RD, coll.ALGO_TREE_COLL, coll.ALGO_P2P):
+                ep.set_algo(algo)
+                res = np.zeros(4099, np.float32)
+                ep.wait(ep.allreduce(sends[rank], res, 4099, 8, 2, coll_addr=addr))
+                assert res.tobytes() == want.tobytes(), (algo, members_only)
+                off, ln = coll.block(4099, len(order), pos)
+                res = np.zeros(max(ln, 1), np.float32)
+                ep.wait(ep.reduce_scatter(sends[rank], res, 4099, 8, 2, coll_addr=addr))
+                assert res[:ln].tobytes() == want[off:off + ln].tobytes(), ("rs", algo)
+                root = len(order) - 1               # a group rank
+                res = np.zeros(4099, np.float32)
+                ep.wait(ep.reduce(sends[rank], res, 4099, root, 8, 2, coll_addr=addr))
+                if pos == root:
+                    assert res.tobytes() == want.tobytes(), ("reduce", algo)
+            ep.set_algo(coll.ALGO_TREE)
+            x = np.array([rank, 7 * rank], np.int64)
+            res = np.zeros(2 * len(order), np.int64)
+            ep.wait(ep.allgather(x, res, 2, 6, coll_addr=addr))
+            assert res.tolist() == [v for m in order for v in (m, 7 * m)]
+            b = (np.arange(3, dtype=np.float64) + rank if pos == 0 else np.zeros(3))
+            ep.wait(ep.broadcast(b, 3, 0, 9, coll_addr=addr))
+            assert b.tolist() == (np.arange(3) + order[0]).tolist()
+        assert coll.lib().lfa_mc_close(mc) == 0
+    ep.wait(ep.barrier())
+
+
 def _reference_known_answers(ep, rank, world, coll):
     """The reference's own acceptance checks for fi_allreduce / fi_broadcast /
     fi_barrier, from prov/cxi/test/multinode/test_coll.c (a provider's test of
@@ -240,6 +302,7 @@ def _worker(rank, world, port, q):
             _overlap(ep, rank, world, oracle)
             _joins(ep, rank, world, oracle)
             _joins_members(ep, rank, world)
+            _joins_set_order(ep, rank, world, oracle, coll)
             if world > 1:
                 assert xfer.sent > 0 and xfer.received > 0
             assert not xfer.reqs, "transfers left behind"

@@ -173,7 +173,7 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 def test_c_executor_gpu_kernels_across_processes(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -342,6 +342,105 @@ def test_flag_barrier_timeout_is_an_error_completion():
         assert results.get(r) == "ok", results.get(r)
 
 
+def _timeout_queue_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                          LFA_SIG_TIMEOUT_MS="300")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        msg = "ok"
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            sends = _inputs(oracle, 8, 4096, world, 6)
+            want = oracle.allreduce(2, 8, sends)[0]
+            ra = torch.zeros(4096, dtype=torch.float32, device="cuda")
+            rb = torch.zeros(4096, dtype=torch.float32, device="cuda")
+            xs = _dev(sends[rank])
+            _ready()
+            ctx_a = ep.allreduce(xs, ra, 4096, 8, 2)      # every member
+            if rank == 0:
+                ep.wait(ctx_a)
+            else:
+                # B: rank 0 never calls it.  Both are queued before either
+                # is reaped; A must complete normally and only B fail.
+                ctx_b = ep.allreduce(xs, rb, 4096, 8, 2)
+                import time
+                time.sleep(1.0)                         # B's wait has timed out by now
+                done, err = [], None
+                t0 = time.time()
+                while err is None and time.time() - t0 < 30:
+                    try:
+                        done += ep.cq_read()
+                    except coll.CollError as e:
+                        err = str(e)
+                if done != [ctx_a]:
+                    msg = f"completions {done} (A={ctx_a}, B={ctx_b})"
+                elif err is None or "prov_errno 110" not in err:
+                    msg = f"B: {err}"
+                elif ra.cpu().numpy().tobytes() != want.tobytes():
+                    msg = "A's result is wrong"
+                else:
+                    try:                                # the group refuses P2P now
+                        ep.allreduce(xs, rb, 4096, 8, 2)
+                        msg = "P2P accepted on the timed-out group"
+                    except coll.CollError:
+                        pass
+            dist.barrier()
+            # another group of the same endpoint is unaffected (ADVICE r2:
+            # the timeout state is per group).  Formed by its members alone:
+            # the world group's tag sequence now differs between the ranks
+            # (rank 1 issued B), as it would under prov/coll
+            mc, _ = ep.join_members(list(range(world)))
+            ep.wait_join()
+            rc = torch.zeros(4096, dtype=torch.float32, device="cuda")
+            _ready()
+            ep.wait(ep.allreduce(xs, rc, 4096, 8, 2, coll_addr=ep.mc_addr(mc)))
+            if msg == "ok" and rc.cpu().numpy().tobytes() != want.tobytes():
+                msg = "new group's P2P result is wrong"
+            coll.lib().lfa_mc_close(mc)
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_timeout_fails_that_operation_not_the_one_before():
+    """two P2P operations queued, the second one's wait times out
+    (a member skips it), both reaped only afterwards: the first completes
+    normally with its result, the second fails with ETIMEDOUT — the kernel
+    records WHICH operation timed out (its ticket), not a bare flag — and the
+    timed-out group refuses P2P operations while a new group of the same
+    endpoint runs them."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_queue_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=100)
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert results.get(r) == "ok", results.get(r)
+
+
 def _oneshot_stream_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
@@ -354,7 +453,7 @@ def _oneshot_stream_worker(rank, world, port, q):
         try:
             ep.set_algo(coll.ALGO_P2P)
             rng = np.random.default_rng(77)         # the same sequence on every rank
-            ops, ctxs = [], []
+            ops, ctxs, n_os = [], [], 0
             for i in range(48):
                 kind = rng.choice(["allreduce", "reduce_scatter", "reduce", "big"])
                 dt, op = [(8, 2), (9, 3), (6, 1), (2, 0), (4, 7), (1, 9)][rng.integers(6)]
@@ -380,10 +479,17 @@ def _oneshot_stream_worker(rank, world, port, q):
                     _ready()
                     ctxs.append(ep.reduce(xs, r, count, root, dt, op))
                 ops.append((kind, r, exp, xs))
+                # the planner's one-shot rule (lfa_coll_plan.c plan_p2p)
+                nb = count * oracle.datatype_size(dt)
+                n_os += (nb <= (1 << 20) if kind == "reduce_scatter"
+                         else nb * world <= (256 << 10))
             done = []
             while len(done) < len(ctxs):
                 done += ep.cq_read()
             assert done == ctxs
+            # the one-shot kernel ran (not the four items it replaces)
+            c = ep.counters()
+            assert n_os > 0 and c["oneshot"] == n_os and not c["timed_out"], (c, n_os)
             for i, (kind, r, exp, _) in enumerate(ops):
                 if exp is not None:
                     got = r[:exp.size].cpu().numpy()
@@ -399,7 +505,7 @@ def _oneshot_stream_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 def test_oneshot_ops_in_flight_mixed(world):
     """48 LFA_ALGO_P2P operations queued at once across processes: one-shot
     allreduce / reduce_scatter / reduce (every root) of ragged small counts
@@ -469,6 +575,10 @@ def _every_entry_worker(rank, world, port, q):
                 ep.wait(ep.reduce(x, rr if rank == root else None, n, root, c["dt"], c["op"]))
                 if rank == root:
                     assert_parity(c["dt"], rr.cpu().numpy(), want, f"reduce {c['file']}")
+            # every one of them ran as the one-shot kernel (world <= 8 and
+            # <= 4 KiB per input: under the planner's thresholds)
+            cnt = ep.counters()
+            assert cnt["oneshot"] == 3 * len(cases) and not cnt["timed_out"], cnt
         finally:
             ep.close()
         dist.barrier()
@@ -479,7 +589,7 @@ def _every_entry_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 def test_oneshot_every_reducing_entry(world):
     """Every (op, datatype) of the write table with a reducing op (MIN..BXOR,
     int8..uint64, float, double, float complex, int128) through LFA_ALGO_P2P's

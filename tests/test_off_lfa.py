@@ -91,11 +91,77 @@ def _load(tmp_path, r, name, io, dt):
     return np.fromfile(tmp_path / f"r{r}_{name}_{io}.bin", dtype=dt)
 
 
-@pytest.mark.parametrize("n", [2, 3])
-@pytest.mark.parametrize("mode", [[], ["manual"]])
+@pytest.mark.parametrize("n,mode", [(2, []), (2, ["manual"]), (3, []), (3, ["manual"]),
+                                    (4, []), (5, ["manual"])])
 def test_peer_transport_collectives(tmp_path, n, mode):
     _peer_run(n, tmp_path, mode)
     _check_peer_outputs(tmp_path, n, ("", "_rd"))   # TREE and the reference's RD
+    _check_ordered_sets(tmp_path, n)
+
+
+class RefAvSet:
+    """The address order prov/coll's av_set calls leave (coll_av_set.c):
+    insert appends (:127-147), remove moves the last address into the hole
+    (:149-164), diff removes src's addresses in src's order the way remove
+    does — the reference's own diff overwrites the last address instead
+    (the build follows the evident intent)."""
+
+    def __init__(self, start, end, stride):
+        self.a = list(range(start, end + 1, stride))
+
+    def insert(self, x):
+        assert x not in self.a
+        self.a.append(x)
+
+    def remove(self, x):
+        i = self.a.index(x)
+        self.a[i] = self.a[-1]
+        self.a.pop()
+
+    def diff(self, other):
+        for x in other.a:
+            if x in self.a:
+                self.remove(x)
+
+
+def _check_ordered_sets(tmp_path, n):
+    """a group's rank r is the r-th address of the joined
+    set, not the r-th smallest.  Set A = stride {0,2,..} + insert 1 (+3,
+    -2 from N = 4), joined over the world; set B = all diff {0}, joined over
+    its own address.  The allgather blocks come in set order, the float SUM
+    allreduce equals the oracle fed in set order (its association order is
+    the set's), and the reduce root / broadcast root are group ranks."""
+    import numpy as np
+    import oracle
+    a = RefAvSet(0, n - 1, 2)
+    if n > 1:
+        a.insert(1)
+    if n > 3:
+        a.insert(3)
+        a.remove(2)
+    b = RefAvSet(0, n - 1, 1)
+    b.diff(RefAvSet(0, 0, 1))
+    for tag, ref in (("setA", a.a), ("setB", b.a)):
+        order = _load(tmp_path, 0, tag, "order", np.uint64).tolist()
+        assert order == ref, (tag, order, ref)
+        if not order:
+            continue
+        for r in order:
+            ag = _load(tmp_path, r, tag + "_allgather", "out", np.int32).reshape(-1, 3)
+            assert ag.tolist() == [[m, 10 * m, k] for k, m in enumerate(order)], (tag, r)
+        ins = [_load(tmp_path, r, tag + "_sum_f32", "in", np.float32) for r in order]
+        want = oracle.allreduce(2, 8, ins)[0]
+        for r in order:
+            got = _load(tmp_path, r, tag + "_sum_f32", "out", np.float32)
+            assert got.tobytes() == want.tobytes(), (tag, r)
+        if order != sorted(order) and len(order) > 2:
+            # the association order is visible: ascending numbering differs
+            srt = oracle.allreduce(2, 8, [ins[order.index(r)] for r in sorted(order)])[0]
+            assert srt.tobytes() != want.tobytes()
+        root = order[1] if len(order) > 1 else order[0]
+        ins = [_load(tmp_path, r, tag + "_reduce_f64", "in", np.float64) for r in order]
+        got = _load(tmp_path, root, tag + "_reduce_f64", "out", np.float64)
+        assert got.tobytes() == oracle.allreduce(2, 9, ins)[0].tobytes(), tag
 
 
 @pytest.mark.gpu

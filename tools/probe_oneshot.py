@@ -35,7 +35,7 @@ class OneShot(ctypes.Structure):
                 ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
                 ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
                 ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
-                ("timeout_us", ctypes.c_uint64)]
+                ("ticket", ctypes.c_uint32), ("timeout_us", ctypes.c_uint64)]
 
 
 def main() -> None:
@@ -46,7 +46,8 @@ def main() -> None:
                                            ctypes.POINTER(OneShot), ctypes.c_void_p]
     L.lfa_flag_barrier_async.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
-                                         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_void_p]
     hip = ctypes.CDLL("libamdhip64.so")
     torch.cuda.set_device(0)
     n, k_iters = 2, 200
@@ -57,7 +58,7 @@ def main() -> None:
     sym = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws])
     status = ctypes.c_void_p()
     assert hip.hipHostMalloc(ctypes.byref(status), ctypes.c_size_t(4), 0x40000000) == 0
-    ctypes.c_uint32.from_address(status.value).value = 0
+    ctypes.c_uint32.from_address(status.value).value = 0xFFFFFFFF   # LFA_SIG_NONE
     streams = [torch.cuda.Stream() for _ in range(n)]
     torch.cuda.synchronize()
     out = {}
@@ -67,7 +68,7 @@ def main() -> None:
     def oneshot(r, x, y, count):
         a = OneShot(x[r].data_ptr(), y[r].data_ptr(), count, -1,
                     ctypes.cast(sym, ctypes.c_void_p), (count * 4 + 255) // 256 * 256,
-                    flag_off, n, r, epoch[0], status.value, 2_000_000)
+                    flag_off, n, r, epoch[0], status.value, 1, 2_000_000)
         assert L.lfa_oneshot_reduce_async(2, 8, ctypes.byref(a),
                                           ctypes.c_void_p(streams[r].cuda_stream)) == 0
 
@@ -75,7 +76,7 @@ def main() -> None:
         post = (ctypes.c_void_p * n)(*[0 if k == r else ws[k].data_ptr() + flag_off + 4 * r
                                        for k in range(n)])
         assert L.lfa_flag_barrier_async(post, ctypes.c_void_p(ws[r].data_ptr() + flag_off), n,
-                                        r, bar[0], status.value, 2_000_000,
+                                        r, bar[0], status.value, 1, 2_000_000,
                                         ctypes.c_void_p(streams[r].cuda_stream)) == 0
 
     def four_step(r, x, y, count):
@@ -102,7 +103,7 @@ def main() -> None:
             for it in range(k_iters + 20):
                 if it == 20:
                     torch.cuda.synchronize()
-                    if ctypes.c_uint32.from_address(status.value).value:
+                    if ctypes.c_uint32.from_address(status.value).value != 0xFFFFFFFF:
                         # a wait timed out: the streams did not run together
                         print(json.dumps({"error": f"{form} {nbytes}: wait timed out"}))
                         sys.exit(1)
@@ -134,7 +135,7 @@ def main() -> None:
                 y[r].zero_()
             torch.cuda.synchronize()
         out[str(nbytes)] = row
-    out["timeouts"] = ctypes.c_uint32.from_address(status.value).value
+    out["timeouts"] = int(ctypes.c_uint32.from_address(status.value).value != 0xFFFFFFFF)
     print(json.dumps({"ranks_in_one_process": n, "per_op_gpu_time": out}), flush=True)
 
 
