@@ -854,6 +854,33 @@ def extra_host_allreduce(ep, world, reps=3, sweep=False):
                    "three streams"}
     if by_chunk:
         row["ms_by_chunk_mib"] = by_chunk
+    if world > 1:
+        # a GROUP chunk (every rank sets the same value) lets a
+        # group of N > 1 pipeline host buffers; device-buffer members then
+        # split into the same chunks — both sides of that trade measured
+        def timed(x, y):
+            ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
+            tt = []
+            for _ in range(reps):
+                barrier(world)
+                t0 = time.perf_counter()
+                ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
+                tt.append(max_over_ranks(time.perf_counter() - t0, world))
+            return round(statistics.median(tt) * 1e3, 3)
+        dx, dy = hx.to("cuda"), torch.empty(COUNT, device="cuda")
+        torch.cuda.synchronize()
+        row["device_whole_ms"] = timed(dx, dy)
+        want = dy.cpu()
+        for mib in (32, 64):
+            ep.set_group_chunk(mib << 20)
+            row[f"group_chunk_{mib}mib_host_ms"] = timed(hx, hy)
+            row[f"group_chunk_{mib}mib_device_ms"] = timed(dx, dy)
+            row[f"group_chunk_{mib}mib_bitwise_equal"] = bool(torch.equal(hy, want) and
+                                                             torch.equal(dy.cpu(), want))
+        ep.set_group_chunk(0)
+        row["group_chunk_note"] = ("lfa_coll_ep_set_group_chunk on every rank: host members "
+                                   "pipeline H2D/collective/D2H per chunk, device members "
+                                   "run the same chunks in place")
     return row
 
 

@@ -12,8 +12,12 @@
  *   lfa_atomic_write_handlers    replaces ofi_atomic_write_handlers[op][dt]
  *                                  prov/util/src/util_atomic.c:907-922,
  *                                  include/ofi_atomic.h:73-82
- *                                (same signature; dst/src are DEVICE
- *                                 pointers; synchronous on the null stream)
+ *                                (same signature; synchronous; dst/src are
+ *                                 device OR host pointers, classified per
+ *                                 call — see "The synchronous tables" below:
+ *                                 device operands run the gfx950 kernels
+ *                                 on the null stream, host operands the
+ *                                 host loop or the staged HBM stream)
  *   lfa_atomic_write_async()     the GPU form: same semantics, enqueued on a
  *                                  HIP stream, returns 0 / negative errno
  *   lfa_atomic_readwrite_handlers / lfa_atomic_readwrite_async

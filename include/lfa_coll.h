@@ -83,7 +83,24 @@ enum lfa_coll_algo {
 	 * flags, tree.  No intermediate transport copies, xGMI in and out
 	 * directions busy at once. */
 	LFA_ALGO_P2P = 4,
+	/* the default on device domains: per operation, LFA_ALGO_P2P's
+	 * one-kernel path for small buckets (allreduce / reduce of <= 256 KiB
+	 * summed over the members, reduce_scatter of <= 1 MiB, 2..8 members)
+	 * and LFA_ALGO_TREE above.  The choice depends only on (collective,
+	 * count, members, datatype size) — lfa_coll_auto_algo — and on the
+	 * group's P2P state, itself agreed by every member: the first small
+	 * bucket sets up the IPC workspaces with a MIN agreement over the
+	 * members, and if any member cannot map a peer's workspace every member
+	 * runs TREE from then on.  Same bits either way.  Peer domains run
+	 * LFA_ALGO_TREE. */
+	LFA_ALGO_AUTO = 5,
 };
+
+/* LFA_ALGO_AUTO's choice for one operation: LFA_ALGO_P2P or LFA_ALGO_TREE.
+ * p2p_ok: the group's agreed P2P state (0 once the workspace agreement
+ * failed).  Pure; every member computes the same. */
+int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
+		       size_t esz, int p2p_ok);
 
 /* ---- bootstrap (replaces fi_getinfo/fi_fabric/fi_domain/fi_endpoint
  *      and AV insertion for this path) ---------------------------------- */
@@ -158,8 +175,30 @@ void *lfa_coll_ep_stream(struct lfa_coll_ep *ep);
  * member's domain on a GPU (lfa_coll_domain_open_peer with a device): a
  * domain without one runs it as LFA_ALGO_TREE, a different schedule. */
 int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo);
-/* Host-staging chunk size in bytes (0 = default 32 MiB). */
+/* Host-staging chunk size in bytes (0 = default 32 MiB) of a ONE-member
+ * group: H2D, collective and D2H of consecutive chunks overlap. */
 int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
+/* The GROUP chunk, in bytes (0 = off, the default; also read from
+ * LFA_GROUP_CHUNK_BYTES at endpoint open).  A chunked member issues one
+ * device collective per chunk, so in a group of N > 1 chunking must be a
+ * group-wide choice: with a group chunk set — the SAME value on every
+ * member, like the collectives themselves — every member, whatever memory
+ * its buffers are in, splits allreduce / reduce / broadcast / equal-block
+ * reduce_scatter of more than one chunk into the same chunks
+ * (lfa_coll_member_chunk): host members pipeline H2D / collective / D2H
+ * across them, device members run the chunks back to back on their buffers
+ * (reduce_scatter's 2-D chunks staged on the device).  Every element meets
+ * the same schedule as unchunked, so results are bit-identical.  Off, a
+ * group of N > 1 stages host buffers whole (one chunk).  The result the
+ * reference defines stays the same: prov/coll copies host buffers whole
+ * (coll_coll.c:364, 1058). */
+int lfa_coll_ep_set_group_chunk(struct lfa_coll_ep *ep, size_t bytes);
+/* The chunk, in bytes, a member stages an operation with (0 = one chunk,
+ * the whole buffer): the group chunk when set (every member), otherwise the
+ * local chunk for a host member of a one-member group, otherwise 0.  Pure:
+ * what tests/test_coll_plan.py replays for mixed members. */
+size_t lfa_coll_member_chunk(int nranks, int host, size_t group_chunk,
+			     size_t local_chunk);
 
 /* ---- groups (fi_join_collective) -------------------------------------- */
 
@@ -376,6 +415,12 @@ void lfa_coll_block(size_t count, int nranks, int r, size_t *off, size_t *len);
  * pipeline does not chunk (ragged reduce_scatter, allgather, scatter).
  * Host-only, no GPU needed.
  */
+/* Staging geometry: chunk idx of an operation staged `chunk_bytes` at a time
+ * (0 = one chunk), for allreduce / reduce / broadcast (contiguous chunks) and
+ * reduce_scatter with count % nranks == 0 (chunk j gathers elements
+ * [j, j+w) of every rank's block: height nranks, pitch = one block).
+ * Returns 1 and fills *c, 0 past the last chunk, -LFA_EINVAL for other
+ * collectives and ragged reduce_scatter (staged whole). */
 struct lfa_host_chunk {
 	size_t src_off, src_pitch, width, height, dev_count, dst_off;
 };

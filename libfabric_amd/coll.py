@@ -30,7 +30,7 @@ c_int, c_size_t, c_void_p, c_uint64, c_uint32, c_int32 = (
     ctypes.c_uint32, ctypes.c_int32)
 c_ssize_t = ctypes.c_ssize_t
 
-ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL, ALGO_P2P = 0, 1, 2, 3, 4
+ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL, ALGO_P2P, ALGO_AUTO = 0, 1, 2, 3, 4, 5
 (STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY,
  STEP_ALLTOALL, STEP_ALLGATHER, STEP_BARRIER, STEP_TREE_PUT, STEP_ONESHOT) = range(11)
 BUF_SEND, BUF_RESULT, BUF_TMP, BUF_SYM_IN, BUF_SYM_OUT = 0, 1, 2, 3, 4
@@ -121,6 +121,12 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_ep_set_algo.argtypes = [c_void_p, c_int]
     L.lfa_coll_ep_set_chunk.restype = c_int
     L.lfa_coll_ep_set_chunk.argtypes = [c_void_p, c_size_t]
+    L.lfa_coll_ep_set_group_chunk.restype = c_int
+    L.lfa_coll_ep_set_group_chunk.argtypes = [c_void_p, c_size_t]
+    L.lfa_coll_auto_algo.restype = c_int
+    L.lfa_coll_auto_algo.argtypes = [c_int, c_size_t, c_int, c_size_t, c_int]
+    L.lfa_coll_member_chunk.restype = c_size_t
+    L.lfa_coll_member_chunk.argtypes = [c_int, c_int, c_size_t, c_size_t]
     L.lfa_coll_ep_flush.restype = c_int
     L.lfa_coll_ep_flush.argtypes = [c_void_p]
     L.lfa_coll_world_addr.restype = c_uint64
@@ -224,6 +230,16 @@ def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
                     "dst": tup(s.dst), "src": tup(s.src),
                     "first": s.first, "nsrc": s.nsrc})
     return Plan(out, [tup(r) for r in refs[:nr.value]], tmp.value)
+
+
+def auto_algo(coll: int, count: int, nranks: int, esz: int, p2p_ok: bool = True) -> int:
+    """lfa_coll_auto_algo: LFA_ALGO_AUTO's choice for one operation."""
+    return lib().lfa_coll_auto_algo(coll, count, nranks, esz, int(p2p_ok))
+
+
+def member_chunk(nranks: int, host: bool, group_chunk: int, local_chunk: int) -> int:
+    """lfa_coll_member_chunk: the chunk a member stages an operation with."""
+    return lib().lfa_coll_member_chunk(nranks, int(host), group_chunk, local_chunk)
 
 
 def host_chunks(coll: int, count: int, nranks: int, esz: int,
@@ -366,6 +382,10 @@ class Endpoint:
 
     def set_chunk(self, nbytes: int) -> None:
         _chk(lib().lfa_coll_ep_set_chunk(self.ep, nbytes), "set_chunk")
+
+    def set_group_chunk(self, nbytes: int) -> None:
+        """lfa_coll_ep_set_group_chunk: the same value on every member."""
+        _chk(lib().lfa_coll_ep_set_group_chunk(self.ep, nbytes), "set_group_chunk")
 
     @property
     def stream_handle(self) -> int:
@@ -573,6 +593,7 @@ def esz(dt: int) -> int:
     return SIZES[DT(dt)]
 
 
-__all__ = ["plan", "block", "host_chunks", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
-           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "esz",
+__all__ = ["plan", "block", "host_chunks", "member_chunk", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
+           "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "ALGO_AUTO",
+           "auto_algo", "esz",
            "HostEndpoint", "PeerXferOps", "TransportAgain"]

@@ -173,8 +173,14 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	ep->dom = d;
 	pthread_mutex_init(&ep->lock, NULL);
 	pthread_mutex_init(&ep->comm_lock, NULL);
-	ep->algo = LFA_ALGO_TREE;
+	/* device domains choose per bucket; peer domains run the tree */
+	ep->algo = d->host ? LFA_ALGO_TREE : LFA_ALGO_AUTO;
 	ep->chunk = LFA_DEFAULT_CHUNK;
+	{
+		const char *e = getenv("LFA_GROUP_CHUNK_BYTES");
+
+		ep->group_chunk = e ? (size_t)strtoull(e, NULL, 0) : 0;
+	}
 	/* the P2P workspace exchange needs these on every member even when a
 	 * local allocation fails later, so they exist up front */
 	ctl = (size_t)d->nranks * LFA_SYM_REC_BYTES;
@@ -333,7 +339,7 @@ int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo)
 {
 	if (!ep || (algo != LFA_ALGO_TREE && algo != LFA_ALGO_RD &&
 		    algo != LFA_ALGO_RCCL && algo != LFA_ALGO_TREE_COLL &&
-		    algo != LFA_ALGO_P2P))
+		    algo != LFA_ALGO_P2P && algo != LFA_ALGO_AUTO))
 		return -LFA_EINVAL;
 	ep->algo = algo;
 	return 0;
@@ -345,6 +351,22 @@ int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes)
 		return -LFA_EINVAL;
 	ep->chunk = bytes ? bytes : LFA_DEFAULT_CHUNK;
 	return 0;
+}
+
+int lfa_coll_ep_set_group_chunk(struct lfa_coll_ep *ep, size_t bytes)
+{
+	if (!ep)
+		return -LFA_EINVAL;
+	ep->group_chunk = bytes;
+	return 0;
+}
+
+size_t lfa_coll_member_chunk(int nranks, int host, size_t group_chunk,
+			     size_t local_chunk)
+{
+	if (group_chunk)
+		return group_chunk;
+	return host && nranks == 1 ? local_chunk : 0;
 }
 
 lfa_addr_t lfa_coll_world_addr(struct lfa_coll_ep *ep)
@@ -1141,6 +1163,26 @@ static int rccl_op(enum lfa_op op, ncclRedOp_t *o)
 	}
 }
 
+int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
+		       size_t esz, int p2p_ok)
+{
+	const size_t bytes = count * esz;
+
+	if (!p2p_ok || nranks < 2 || nranks > LFA_OS_MAX_RANKS || !count)
+		return LFA_ALGO_TREE;
+	switch (coll) {
+	case LFA_ALLREDUCE:
+	case LFA_REDUCE:
+		/* the planner's one-shot rule (plan_p2p): one kernel */
+		return bytes * (size_t)nranks <= LFA_SMALL_AG_BYTES ? LFA_ALGO_P2P :
+								     LFA_ALGO_TREE;
+	case LFA_REDUCE_SCATTER:
+		return bytes <= LFA_OS_RS_BYTES ? LFA_ALGO_P2P : LFA_ALGO_TREE;
+	default:
+		return LFA_ALGO_TREE;
+	}
+}
+
 /* LFA_ALGO_RCCL for one device-resident operation; 1 = handled. */
 static int try_rccl(struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 		    const void *buf, void *result, size_t count, int root,
@@ -1225,13 +1267,18 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 {
 	const struct plan *pl;
 	size_t esz = lfa_datatype_size(dt);
+	enum lfa_coll_algo algo = ep->algo;
 	struct xctx x;
 	int ret;
 
-	if (ep->algo == LFA_ALGO_RCCL && mc->size > 1 &&
+	if (algo == LFA_ALGO_RCCL && mc->size > 1 &&
 	    try_rccl(mc, coll, buf, result, count, root, dt, op, s, &ret))
 		return ret;
-	ret = cached_plan(ep, &pl, coll, ep->algo, mc->rank, mc->size, root,
+	if (algo == LFA_ALGO_AUTO)
+		algo = (enum lfa_coll_algo)lfa_coll_auto_algo(coll, count, mc->size, esz,
+							       mc->p2p_state >= 0);
+replan:
+	ret = cached_plan(ep, &pl, coll, algo, mc->rank, mc->size, root,
 			  count, esz);
 	if (ret)
 		return ret;
@@ -1240,11 +1287,20 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		ret = sig_ready(mc);
 		if (ret)
 			return ret;
-		x.ticket = ++mc->p2p_ticket;
 		ret = p2p_ensure(mc, plan_sym_need(pl->steps, pl->nsteps, mc->size,
 						   count, esz));
+		if (ret && ep->algo == LFA_ALGO_AUTO && mc->p2p_state == 0) {
+			/* the members agreed (MIN over their flags, p2p_ensure)
+			 * that some member cannot map a peer's workspace: every
+			 * one of them runs the tree from now on */
+			mc->p2p_state = -1;
+			algo = LFA_ALGO_TREE;
+			goto replan;
+		}
 		if (ret)
 			return ret;
+		mc->p2p_state = 1;
+		x.ticket = ++mc->p2p_ticket;
 		x.sym = mc->sym;
 		x.region = mc->sym_region;
 	}
@@ -1272,15 +1328,15 @@ int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
 		return -LFA_EINVAL;
 	nb = rs ? (size_t)nranks : 1;       /* blocks gathered per chunk */
 	span = count / nb;                  /* elements per block */
-	per = chunk_bytes / esz / nb;
+	/* chunk_bytes 0: one chunk, the whole buffer.  Which chunk a member
+	 * uses is lfa_coll_member_chunk's rule: in a group of N > 1 only a
+	 * group-wide chunk, so every member issues the same device schedule
+	 * whatever its memory type (chunking is otherwise a local
+	 * choice the peers cannot see) */
+	per = chunk_bytes ? chunk_bytes / esz / nb : span;
 	if (!per)
 		per = 1;
-	/* N > 1: one chunk, the whole buffer.  Every member then issues the
-	 * same device schedule as for device buffers, whatever its memory type
-	 * or chunk setting — chunking is a local choice the peers cannot see
-	 * (mixed host/device ranks would issue different RCCL
-	 * schedules and hang). */
-	if (per > span || nranks > 1)
+	if (per > span)
 		per = span;
 	if (!per || idx >= (span + per - 1) / per)
 		return 0;
@@ -1309,7 +1365,7 @@ int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
 static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			    enum lfa_collective_op coll, const void *buf,
 			    void *result, size_t count, int root,
-			    enum lfa_datatype dt, enum lfa_op op)
+			    enum lfa_datatype dt, enum lfa_op op, size_t chunk)
 {
 	size_t esz = lfa_datatype_size(dt), in_slot, idx;
 	struct lfa_host_chunk c0, c;
@@ -1317,7 +1373,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	int ret, slot = 0;
 	const int out = coll != LFA_REDUCE || mc->rank == root;
 
-	ret = lfa_coll_host_chunk(coll, count, mc->size, esz, ep->chunk, 0, &c0);
+	ret = lfa_coll_host_chunk(coll, count, mc->size, esz, chunk, 0, &c0);
 	if (ret <= 0)
 		return ret < 0 ? ret : 0;
 	/* chunk 0 is the widest; the output half starts 256-byte aligned
@@ -1333,7 +1389,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		hipEventRecord(done[i], ep->stream);
 	}
 	for (idx = 0; !ret &&
-	     lfa_coll_host_chunk(coll, count, mc->size, esz, ep->chunk, idx, &c) == 1;
+	     lfa_coll_host_chunk(coll, count, mc->size, esz, chunk, idx, &c) == 1;
 	     idx++) {
 		char *din = ep->hs[slot], *dout = din + in_slot;
 
@@ -1367,6 +1423,32 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		hipEventDestroy(comp[i]);
 		hipEventDestroy(done[i]);
 	}
+	return ret;
+}
+
+/*
+ * Device buffers under a group chunk: the chunks lfa_coll_host_chunk gives
+ * the host members, run back to back on the caller's buffers — contiguous
+ * chunks in place, reduce_scatter's 2-D chunks (elements [j, j+w) of every
+ * block) through the staging pipeline, which moves them device to device.
+ */
+static int run_device_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			      enum lfa_collective_op coll, const void *buf,
+			      void *result, size_t count, int root,
+			      enum lfa_datatype dt, enum lfa_op op, size_t chunk)
+{
+	struct lfa_host_chunk c;
+	int ret = 0;
+
+	if (coll == LFA_REDUCE_SCATTER)
+		return run_host_chunked(ep, mc, coll, buf, result, count, root, dt, op,
+					chunk);
+	for (size_t idx = 0; !ret &&
+	     lfa_coll_host_chunk(coll, count, mc->size, lfa_datatype_size(dt), chunk, idx,
+				 &c) == 1; idx++)
+		ret = run_device(ep, mc, coll, buf ? (const char *)buf + c.src_off : NULL,
+				 result ? (char *)result + c.dst_off : NULL, c.dev_count,
+				 root, dt, op, ep->stream);
 	return ret;
 }
 
@@ -1438,7 +1520,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	/* P2P keeps its schedule on device buffers (the peers' symmetric
 	 * workspaces are IPC-mapped device memory; its barriers become zero-byte
 	 * messages); host buffers and RCCL run as TREE */
-	if ((algo == LFA_ALGO_P2P && !dev) || algo == LFA_ALGO_RCCL)
+	if ((algo == LFA_ALGO_P2P && !dev) || algo == LFA_ALGO_RCCL ||
+	    algo == LFA_ALGO_AUTO)
 		algo = LFA_ALGO_TREE;
 	ret = plan_make(&raw, coll, algo, mc->rank, mc->size, root, count, esz);
 	if (ret)
@@ -1534,9 +1617,9 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		      enum lfa_datatype dt, enum lfa_op op, void *context)
 {
 	struct lfa_coll_mc *mc;
-	size_t esz;
+	size_t esz, chunk;
 	uint32_t t0;
-	int root = -1, ret, host;
+	int root = -1, ret, host, chunkable;
 
 	if (!ep)
 		return -LFA_EINVAL;
@@ -1587,20 +1670,26 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	t0 = mc->p2p_ticket;
 	host = (buf && count && !is_device_ptr(buf)) ||
 	       (result && count && !is_device_ptr(result));
+	chunkable = coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
+		    coll == LFA_REDUCE ||
+		    (coll == LFA_REDUCE_SCATTER && !(count % mc->size));
+	/* the chunk this member stages with: a group chunk applies to every
+	 * member alike, a local one only to a one-member group's host buffers
+	 * (lfa_coll_member_chunk), so every member issues the same device
+	 * collectives whatever memory its buffers are in */
+	chunk = lfa_coll_member_chunk(mc->size, host, ep->group_chunk, ep->chunk);
 	if (!count) {
 		ret = 0;
+	} else if (!host && chunk && chunkable &&
+		   count * esz > chunk) {
+		ret = run_device_chunked(ep, mc, coll, buf, result, count, root, dt, op,
+					 chunk);
 	} else if (!host) {
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
 				 ep->stream);
-	} else if ((coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
-		    coll == LFA_REDUCE ||
-		    (coll == LFA_REDUCE_SCATTER && !(count % mc->size)))) {
-		/* chunked at N = 1 only (lfa_coll_host_chunk): at N > 1 the one
-		 * chunk is the whole buffer, so the device schedule is the same
-		 * as for device buffers whatever memory type or chunk size the
-		 * other members use */
+	} else if (chunkable) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
-				       op);
+				       op, chunk);
 	} else {
 		size_t moff, mlen, in_b = count * esz, out_b = count * esz;
 

@@ -70,6 +70,9 @@ struct lfa_coll_mc {
 	uint32_t p2p_ticket;
 	int sig_failed;
 	uint64_t n_oneshot, n_barrier;  /* lfa_mc_counters */
+	/* LFA_ALGO_AUTO: 0 not tried, 1 the workspace agreement held, -1 it
+	 * failed on some member (every member then runs TREE) */
+	int p2p_state;
 };
 
 struct lfa_coll_domain {
@@ -105,7 +108,8 @@ struct lfa_coll_ep {
 	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
 				     * PCIe direction runs concurrently) */
 	enum lfa_coll_algo algo;
-	size_t chunk;
+	size_t chunk;               /* one-member groups: host staging chunk */
+	size_t group_chunk;         /* every member, any N (0 = off) */
 	void *ws;                   /* device workspace */
 	size_t ws_size;
 	void *hs[2];                /* device staging for host buffers */

@@ -39,21 +39,42 @@ namespace lfa {
 //   lfa__write_op<N>(dt, dst, src, cnt, stream)
 //   lfa__tree_op<N>(dt, dst, srcs, nsrc, cnt, stream)
 // which lfa_capi.cpp dispatches to.  Return 0 or a negative LFA_E* code.
+// Ops whose result bits do not depend on an integer's signedness: wrapping
+// SUM / PROD (the low bits of a two's-complement sum or product), the
+// bitwise and logical ops, READ / WRITE, CSWAP (bitwise compare), CSWAP_NE
+// (integer != is sign-blind) and MSWAP.  A signed integer type runs its
+// unsigned twin's kernels for them — the same bits, one kernel family
+// instead of two (liblfa.so size).  MIN / MAX and the
+// ordered compares keep their own.
+template <int OP>
+constexpr bool sign_blind() {
+  return !(OP == OP_MIN || OP == OP_MAX || OP == OP_CSWAP_LE || OP == OP_CSWAP_LT ||
+           OP == OP_CSWAP_GE || OP == OP_CSWAP_GT);
+}
+
+// the kernel type of a signed integer under OP: its unsigned twin when OP
+// is sign-blind (if constexpr: the signed family is never instantiated)
+template <int OP, typename S, typename U, typename F>
+static int signed_case(F &&f) {
+  if constexpr (sign_blind<OP>()) return f((U *)0);
+  else return f((S *)0);
+}
+
 template <int OP, typename F>
 static int by_type(int dt, F &&f) {
   switch (dt) {
-    case LFA_INT8: return f((int8_t *)0);
+    case LFA_INT8: return signed_case<OP, int8_t, uint8_t>(f);
     case LFA_UINT8: return f((uint8_t *)0);
-    case LFA_INT16: return f((int16_t *)0);
+    case LFA_INT16: return signed_case<OP, int16_t, uint16_t>(f);
     case LFA_UINT16: return f((uint16_t *)0);
-    case LFA_INT32: return f((int32_t *)0);
+    case LFA_INT32: return signed_case<OP, int32_t, uint32_t>(f);
     case LFA_UINT32: return f((uint32_t *)0);
-    case LFA_INT64: return f((int64_t *)0);
+    case LFA_INT64: return signed_case<OP, int64_t, uint64_t>(f);
     case LFA_UINT64: return f((uint64_t *)0);
     case LFA_FLOAT: return f((float *)0);
     case LFA_DOUBLE: return f((double *)0);
     case LFA_FLOAT_COMPLEX: return f((cf32 *)0);
-    case LFA_INT128: return f((i128 *)0);
+    case LFA_INT128: return signed_case<OP, i128, u128>(f);
     case LFA_UINT128: return f((u128 *)0);
     default: return -LFA_EOPNOTSUPP;
   }

@@ -841,7 +841,7 @@ static void launch_tree_lds(const TreeArgs &b, int nsrc, u32x4 *dst,
                      b, nsrc, dst, nvec);
 }
 
-template <int OP, typename T, int NLEAF>
+template <int OP, typename T, int NLEAF, bool ALL = false>
 static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                              size_t nvec, hipStream_t s, int variant = -1) {
   // Product choice (bench.py --tune-tree, profiles/r01_tune_tree_sc1.log):
@@ -850,23 +850,37 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
   // 63.2/58.2/53.9/51.7 for the nt-store forms, 256 MiB of inputs).
   if (variant < 0 && nvec * 16 < kSc1Bytes) variant = 11;
   if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
-  if (variant == 11) {
-    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
-                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
-                       dim3(kBlock), 0, s, b, dst, nvec);
-    return;
-  }
+  // nsrc lies in [NLEAF, 2·NLEAF): only these forms are reachable from the
+  // product choice, so only they are instantiated into liblfa.so (ALL: the
+  // tuning library, which times every form at every fan-in)
+  constexpr bool has3 = ALL || NLEAF == 2;   // nsrc <= 2
+  constexpr bool has2 = ALL || NLEAF >= 8;   // nsrc > 8
+  constexpr bool has1 = ALL || NLEAF <= 8;   // 3 <= nsrc <= 8
   if (variant == 2) {
-    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2>),
-                       dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
-                       dim3(kBlock), 0, s, b, dst, nvec);
+    if constexpr (has2) {
+      hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2>),
+                         dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                         dim3(kBlock), 0, s, b, dst, nvec);
+      return;
+    }
   } else if (variant == 3) {
-    launch_tree_lds<OP, T, NLEAF, kLdsWaves, 1>(b, nsrc, dst, nvec, s);
-  } else {
-    hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
-                       dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
-                       dim3(kBlock), 0, s, b, dst, nvec);
+    if constexpr (has3) {
+      launch_tree_lds<OP, T, NLEAF, kLdsWaves, 1>(b, nsrc, dst, nvec, s);
+      return;
+    }
+  } else if (variant == 1) {
+    if constexpr (has1) {
+      hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
+                         dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
+                         dim3(kBlock), 0, s, b, dst, nvec);
+      return;
+    }
   }
+  // variant 11, or a form this fan-in never selects: the write-through
+  // chunk form, correct at every size
+  hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                     dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                     dim3(kBlock), 0, s, b, dst, nvec);
 }
 
 // Leaf pairing of prov/coll's tree for nsrc ranks (see TreeArgs); returns

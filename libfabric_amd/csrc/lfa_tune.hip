@@ -446,7 +446,7 @@ struct TuneTreeBody {
                            dim3(kBlock), 0, s, b, dst, nvec);
         return;
       default:
-        launch_tree_body<OP, T, NLEAF>(b, nsrc, dst, nvec, s, variant);
+        launch_tree_body<OP, T, NLEAF, true>(b, nsrc, dst, nvec, s, variant);
     }
   }
 };

@@ -1194,7 +1194,7 @@ static int olfa_ep_setopt(fid_t fid, int level, int optname, const void *optval,
 			if (ret)
 				return ret;
 		} else if (*(const int *)optval < LFA_ALGO_TREE ||
-			   *(const int *)optval > LFA_ALGO_P2P) {
+			   *(const int *)optval > LFA_ALGO_AUTO) {
 			return -FI_EINVAL;
 		}
 		ep->algo = *(const int *)optval;

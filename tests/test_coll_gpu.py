@@ -361,6 +361,43 @@ def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
     ep.set_chunk(0)
 
 
+def test_group_chunk_device_and_host_members(coll, ep):
+    """under a group chunk a device-buffer member splits large
+    operations into the chunks the host members stage (lfa_coll_member_chunk)
+    — contiguous chunks run in place on its buffers, reduce_scatter's 2-D
+    chunks through device-to-device staging — and host members pipeline
+    with the group chunk instead of their local one.  At world size 1 every
+    chunk's collective is a copy, so the output must be the input at every
+    offset: odd chunk sizes, a ragged last chunk, mixed operands."""
+    count = (1 << 20) + 37
+    rng = np.random.default_rng(17)
+    hx = rng.uniform(0.9, 1.1, count)
+    dx = torch.from_numpy(hx).to(DEV)
+    try:
+        for group in (1 << 16, 3 * 8 * 1000 + 8, 1 << 30):
+            ep.set_group_chunk(group)
+            ep.set_chunk(1 << 12)          # a local chunk the group rule overrides
+            for fn, args in ((ep.allreduce, (9, 2)), (ep.reduce_scatter, (9, 3))):
+                d = torch.zeros_like(dx)
+                ep.wait(fn(dx, d, count, *args))
+                assert torch.equal(d, dx), (fn.__name__, group, "device")
+                h = np.zeros_like(hx)
+                ep.wait(fn(hx, h, count, *args))
+                assert np.array_equal(h, hx), (fn.__name__, group, "host")
+                h[:] = 0
+                ep.wait(fn(dx, h, count, *args))
+                assert np.array_equal(h, hx), (fn.__name__, group, "mixed")
+            d = torch.zeros_like(dx)
+            ep.wait(ep.reduce(dx, d, count, 0, 9, 1))
+            assert torch.equal(d, dx), ("reduce", group)
+            b = dx.clone()
+            ep.wait(ep.broadcast(b, count, 0, 9))
+            assert torch.equal(b, dx), ("broadcast", group)
+    finally:
+        ep.set_group_chunk(0)
+        ep.set_chunk(0)
+
+
 def test_rccl_other_collectives(coll, ep):
     count = 10_000
     x = torch.arange(count, dtype=torch.int64, device=DEV)

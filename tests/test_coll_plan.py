@@ -298,20 +298,74 @@ def test_host_chunked_elementwise_geometry(kind, count, chunk):
             assert not res[r].any()
 
 
+def _member_schedule(kind, count, n, esz, host, group_chunk, local_chunk):
+    """The device collectives a member issues for one operation: the
+    dev_count of each chunk (the shape of each device collective)."""
+    chunk = coll.member_chunk(n, host, group_chunk, local_chunk)
+    try:
+        cs = coll.host_chunks(kind, count, n, esz, chunk)
+    except coll.CollError:          # not chunkable: staged / run whole
+        return [count]
+    if not host and chunk and count * esz <= chunk:
+        return [count]              # a device member runs it in one piece
+    return [c.dev_count for c in cs]
+
+
 @pytest.mark.parametrize("n", range(2, 9))
-@pytest.mark.parametrize("chunk", [8, 4096, 1 << 20, 32 << 20])
-def test_host_staging_is_one_chunk_in_groups(n, chunk):
-    """chunking is a local choice a peer cannot see, so in a
-    group of N > 1 the host path stages ONE chunk, the whole buffer, and its
-    device collective has the shape a device-buffer member issues
-    (dev_count == count), whatever the chunk size."""
+@pytest.mark.parametrize("local", [8, 4096, 1 << 20, 32 << 20])
+def test_host_staging_is_one_chunk_in_groups(n, local):
+    """a member's LOCAL chunk is a choice its peers cannot
+    see, so without a group chunk a group of N > 1 stages host buffers
+    whole: one device collective of the full shape, the one a device-buffer
+    member issues, whatever the local chunk size."""
     for kind, count in ((ALLREDUCE, 70_001), (REDUCE, 70_001), (BROADCAST, 513),
                         (REDUCE_SCATTER, n * 9001)):
-        cs = coll.host_chunks(kind, count, n, 8, chunk)
-        assert len(cs) == 1, (kind, n, chunk)
+        assert coll.member_chunk(n, True, 0, local) == 0
+        cs = coll.host_chunks(kind, count, n, 8, coll.member_chunk(n, True, 0, local))
+        assert len(cs) == 1, (kind, n, local)
         assert cs[0].dev_count == count and cs[0].src_off == 0 and cs[0].dst_off == 0
-    # a one-member group still pipelines
-    assert len(coll.host_chunks(ALLREDUCE, 70_001, 1, 8, 4096)) > 1
+        assert _member_schedule(kind, count, n, 8, False, 0, local) == [count]
+    # a one-member group still pipelines with its local chunk
+    assert len(coll.host_chunks(ALLREDUCE, 70_001, 1, 8,
+                                coll.member_chunk(1, True, 0, 4096))) > 1
+
+
+@pytest.mark.parametrize("n", range(2, 9))
+@pytest.mark.parametrize("group", [8, 4096, 100_000, 1 << 20])
+def test_group_chunk_same_schedule_for_every_member(n, group):
+    """with a GROUP chunk (the same value on every member)
+    host and device members of N = 2..8 issue the identical sequence of
+    device collectives — whatever their local chunk — so mixed groups
+    stay matched; and the chunks still cover every element exactly once
+    (the staged replay below sums them)."""
+    for kind, count in ((ALLREDUCE, 70_001), (REDUCE, 70_001), (BROADCAST, 5_130),
+                        (REDUCE_SCATTER, n * 9001), (REDUCE_SCATTER, n * 9001 + 1),
+                        (ALLGATHER, 777), (ALLREDUCE, 3)):
+        scheds = {_member_schedule(kind, count, n, 8, host, group, local).__repr__()
+                  for host in (False, True) for local in (4096, 32 << 20)}
+        assert len(scheds) == 1, (kind, count, n, group, scheds)
+    # and the chunks are real when the buffer exceeds the chunk
+    assert len(_member_schedule(ALLREDUCE, 70_001, n, 8, False, group, 0)) == \
+        max(1, -(-70_001 * 8 // max(group, 8)))
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("group", [4096, 100_000])
+def test_group_chunked_results_equal_unchunked(n, group):
+    """The group-chunked staging, replayed on numpy for every member, gives
+    the unchunked result: allreduce, reduce and equal-block reduce_scatter."""
+    rng = np.random.default_rng(n * 13 + group)
+    for kind, count in ((ALLREDUCE, 70_001), (REDUCE, 70_001), (REDUCE_SCATTER, n * 9001)):
+        bufs = [rng.integers(-2**40, 2**40, count) for _ in range(n)]
+        res, covered = _stage_and_run(kind, bufs, count, n, 8,
+                                      coll.member_chunk(n, True, group, 0), root=n - 1)
+        total = np.sum(bufs, axis=0)
+        for r in range(n):
+            if kind == REDUCE_SCATTER:
+                off, ln = coll.block(count, n, r)
+                assert np.array_equal(res[r], total[off:off + ln])
+            elif kind == ALLREDUCE or r == n - 1:
+                assert np.array_equal(res[r], total)
 
 
 def test_host_chunk_rejects_unchunked_collectives():
@@ -401,3 +455,29 @@ def test_large_group_schedules_execute(algo, n):
     for r in range(n):
         off, ln = coll.block(count, n, r)
         assert res[r].tobytes() == full[off:off + ln].tobytes()
+
+
+# ----------------------------------- LFA_ALGO_AUTO --------
+
+@pytest.mark.parametrize("n", range(1, 11))
+def test_auto_algo_same_choice_on_every_member(n):
+    """LFA_ALGO_AUTO picks per operation from (collective, count, members,
+    datatype size) and the group's agreed P2P state only — no rank-local
+    input — so every member of N = 1..10 selects the same algorithm; and the
+    algorithm it picks for a small bucket is exactly the one-kernel path:
+    every member's P2P schedule is ONE one-shot step.  Above the thresholds,
+    outside 2..8 members, or once the P2P agreement failed: the tree."""
+    for kind, esz in ((ALLREDUCE, 4), (REDUCE, 8), (REDUCE_SCATTER, 8), (ALLGATHER, 4)):
+        for count in (1, 1000, (256 << 10) // (4 * max(n, 1)), (256 << 10) // (4 * max(n, 1)) + 1,
+                      (1 << 20) // 8, (1 << 20) // 8 + 1, 1 << 24):
+            a = coll.auto_algo(kind, count, n, esz)
+            nb = count * esz
+            small = (nb * n <= 256 << 10 if kind in (ALLREDUCE, REDUCE) else
+                     nb <= 1 << 20 if kind == REDUCE_SCATTER else False)
+            want = coll.ALGO_P2P if (2 <= n <= 8 and small) else coll.ALGO_TREE
+            assert a == want, (kind, count, n, esz)
+            assert coll.auto_algo(kind, count, n, esz, p2p_ok=False) == coll.ALGO_TREE
+            if a == coll.ALGO_P2P:
+                for r in range(n):
+                    p = coll.plan(kind, a, r, n, n - 1 if kind == REDUCE else -1, count, esz)
+                    assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT], (kind, n, r)
