@@ -114,7 +114,46 @@ constexpr int kLdsWaves = 4;
 constexpr int kStoreNt = 2, kStoreSc1 = 16;
 constexpr size_t kSc1Bytes = (size_t)192 << 20;
 
-template <int OP, typename T, int U, int SAUX, bool UW = true>
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt fields at their no-wait
+// maximum): every vector-memory operation of this wave but the N youngest
+// has completed — loads, LDS-DMA and stores count together, in issue order.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// Step u of a drained tile: wait until the pair of 1-KiB loads of vector u
+// has landed — in issue order the loads of u+1..U-1 (2 each, or 1 each for
+// ATOMIC_WRITE, which reads no dst) and the u stores already issued may stay
+// in flight — then combine and store vector u while the later loads arrive.
+template <int OP, typename T, int U, int SAUX, int u>
+__device__ __forceinline__ void combine_drain(u32x4 (*lds)[kLdsWaves][U][64], unsigned w,
+                                              unsigned l, u32x4 *dst,
+                                              __amdgpu_buffer_rsrc_t r) {
+  if constexpr (u < U) {
+    constexpr int per = OP == OP_WRITE ? 1 : 2;
+    wait_vmcnt<per * (U - 1 - u) + u>();
+    u32x4 v;
+    if constexpr (OP == OP_WRITE) v = lds[1][w][u][l];
+    else v = apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]);
+    if constexpr (SAUX == kStoreNt)
+      st<true>(dst + u * 64 + l, v);
+    else
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    combine_drain<OP, T, U, SAUX, u + 1>(lds, w, l, dst, r);
+  }
+}
+
+// DRAIN: the wave's loads issue pairwise (dst u, src u, dst u+1, ...) and
+// step u stores vector u as soon as its pair has landed (combine_drain),
+// instead of waiting vmcnt(0) for the whole 2·U KiB before the first store.
+// Back-to-back launches at 256 MiB per operand (tools/tune_combine.py,
+// profiles/r03_tune_combine_backtoback.log): 119.4 us against 120.7 us; no
+// change within noise at 32-128 MiB (write-through stores there), so the
+// product drains on the nt-store path only.
+template <int OP, typename T, int U, int SAUX, bool UW = true,
+          bool DRAIN = SAUX == kStoreNt>
 __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
     u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
   __shared__ u32x4 lds[2][kLdsWaves][U][64];
@@ -122,6 +161,21 @@ __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
   const size_t base =
       (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
   if (base + 64 * U <= nvec) {
+    if constexpr (DRAIN) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if constexpr (OP != OP_WRITE)  // ATOMIC_WRITE never reads dst
+          __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                           (lds_void *)&lds[0][w][u][0], 16, 0,
+                                           /*aux: nt*/ 2);
+        __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                         (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+      }
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+      combine_drain<OP, T, U, SAUX, 0>(lds, w, l, dst + base, r);
+      return;
+    }
     if constexpr (OP != OP_WRITE) {  // ATOMIC_WRITE never reads dst
 #pragma unroll
       for (int u = 0; u < U; u++)
@@ -513,6 +567,16 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t
 // ---------------------------------------------------------------------------
 constexpr int kOsMax = LFA_OS_MAX_RANKS;
 
+// One system-scope release / acquire per workgroup (0, the product) or per
+// wave (1, round 2's first form).  A workgroup's waves share a CU and so an
+// L2, which makes the single pair sufficient on one GPU — every
+// cross-process test runs on one MI355X — but its ordering across GPUs over
+// xGMI has not run anywhere yet, so the per-wave form stays
+// selectable: build with -DLFA_OS_WAVE_FENCES=1.
+#ifndef LFA_OS_WAVE_FENCES
+#define LFA_OS_WAVE_FENCES 0
+#endif
+
 struct OsArgs {
   TreeArgs t;                  // in[k]: own input range (k == rank) or own slot k
   char *push[kOsMax];          // peer k's slot of this rank (k != rank)
@@ -555,7 +619,8 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   //    share a CU and so an L2 — and one post per peer
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (t < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // wave 0: the posting lanes
+  if (LFA_OS_WAVE_FENCES || t < 64)  // wave 0: the posting lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if ((int)t < a.n && (int)t != a.rank) {
     __hip_atomic_store(a.post[t] + b * LFA_SIG_MAX, a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -573,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   }
   // the waiting wave acquires for the workgroup (same CU, same L2), then
   // every wave may read what the peers pushed
-  if (t < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (LFA_OS_WAVE_FENCES || t < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
   // 4. reduce chunk b of this rank's own range over every rank's input, rank
   //    order (system-scope loads: the slots were written by peers over xGMI)

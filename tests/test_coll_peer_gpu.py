@@ -14,6 +14,7 @@ prov/coll's (the oracle) bit for bit, including when one member hands in
 host buffers and the others device buffers.  The oracle is only the checker.
 """
 import os
+import queue
 import socket
 
 import numpy as np
@@ -141,10 +142,58 @@ def _body(ep, rank, world, oracle, coll):
     for r, want, _ in outs:
         assert r.cpu().numpy().tobytes() == want.tobytes(), "P2P in flight"
     ep.set_algo(coll.ALGO_TREE)
+    _set_order(ep, rank, world, oracle, coll)
     # a mixed pair on one member is refused
     from libfabric_amd.coll import CollError
     with pytest.raises(CollError):
         ep.allreduce(torch.zeros(4, device="cuda"), np.zeros(4, np.float32), 4, 8, 2)
+
+
+def _set_order(ep, rank, world, oracle, coll):
+    """VERDICT r2 #1 on the GPU: a group over a set whose order is not
+    ascending (prov/coll's av_set after stride + insert (+ remove): N = 3
+    gives [0, 2, 1], N = 5 [0, 3, 4, 1]) numbers its members by set position:
+    device-buffer allgather blocks in set order, a float SUM allreduce equal
+    to the oracle fed in set order (TREE on the kernels, and P2P's one-shot
+    and two-barrier paths), reduce and broadcast roots as group ranks."""
+    from test_coll_host import _set_order as order_of   # the reference's order rules
+    order = order_of(world)
+    mc, _ = ep.join(order)
+    ep.wait_join()
+    addr = ep.mc_addr(mc)
+    if rank in order:
+        pos = order.index(rank)
+        for algo in (coll.ALGO_TREE, coll.ALGO_P2P):
+            ep.set_algo(algo)
+            for count in (4099, 300_001):          # one-shot / copy + barriers + tree
+                sends = _inputs(oracle, 8, count, world, 555 + count)
+                want = oracle.allreduce(2, 8, [sends[m] for m in order])[0]
+                x = _dev(sends[rank])
+                r = torch.zeros(count, dtype=torch.float32, device="cuda")
+                _ready()
+                ep.wait(ep.allreduce(x, r, count, 8, 2, coll_addr=addr))
+                assert r.cpu().numpy().tobytes() == want.tobytes(), ("set order", algo, count)
+                root = len(order) - 1
+                r.zero_()
+                _ready()
+                ep.wait(ep.reduce(x, r, count, root, 8, 2, coll_addr=addr))
+                if pos == root:
+                    assert r.cpu().numpy().tobytes() == want.tobytes(), ("reduce", algo)
+        ep.set_algo(coll.ALGO_TREE)
+        g = torch.tensor([rank, 3 * rank], dtype=torch.int64, device="cuda")
+        out = torch.zeros(2 * len(order), dtype=torch.int64, device="cuda")
+        _ready()
+        ep.wait(ep.allgather(g, out, 2, 6, coll_addr=addr))
+        assert out.cpu().tolist() == [v for m in order for v in (m, 3 * m)]
+        b = (torch.arange(5, dtype=torch.float64, device="cuda") + rank if pos == 1
+             else torch.zeros(5, dtype=torch.float64, device="cuda"))
+        _ready()
+        ep.wait(ep.broadcast(b, 5, 1 if len(order) > 1 else 0, 9, coll_addr=addr))
+        src = order[1] if len(order) > 1 else order[0]
+        if len(order) > 1:
+            assert b.cpu().tolist() == (np.arange(5) + src).tolist()
+    coll.lib().lfa_mc_close(mc)
+    ep.wait(ep.barrier())
 
 
 def _worker(rank, world, port, q):
@@ -184,15 +233,18 @@ def test_c_executor_gpu_kernels_across_processes(world):
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=100)
+            try:
+                r, msg = q.get(timeout=100)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert results.get(r) == "ok", results.get(r)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
 def _growth_worker(rank, world, port, q):
@@ -252,15 +304,18 @@ def test_p2p_workspace_growth_in_flight():
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=110)
+            try:
+                r, msg = q.get(timeout=110)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert results.get(r) == "ok", results.get(r)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
 def _timeout_worker(rank, world, port, q):
@@ -331,15 +386,18 @@ def test_flag_barrier_timeout_is_an_error_completion():
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=100)
+            try:
+                r, msg = q.get(timeout=100)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert results.get(r) == "ok", results.get(r)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
 def _timeout_queue_worker(rank, world, port, q):
@@ -430,15 +488,18 @@ def test_timeout_fails_that_operation_not_the_one_before():
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=100)
+            try:
+                r, msg = q.get(timeout=100)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert results.get(r) == "ok", results.get(r)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
 def _oneshot_stream_worker(rank, world, port, q):
@@ -522,15 +583,18 @@ def test_oneshot_ops_in_flight_mixed(world):
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=110)
+            try:
+                r, msg = q.get(timeout=110)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert results.get(r) == "ok", results.get(r)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
 def _every_entry_worker(rank, world, port, q):
@@ -608,12 +672,15 @@ def test_oneshot_every_reducing_entry(world):
     results = {}
     try:
         for _ in range(world):
-            r, msg = q.get(timeout=140)
+            try:
+                r, msg = q.get(timeout=140)
+            except queue.Empty:         # a rank hung: report the others
+                break
             results[r] = msg
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert str(results.get(r)).startswith("ok"), results.get(r)
+    bad = {r: results.get(r) for r in range(world) if not str(results.get(r)).startswith("ok")}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))

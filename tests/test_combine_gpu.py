@@ -256,6 +256,98 @@ def test_tree_put_vs_oracle(lfa, nsrc, ndst, dt):
         assert not o[:esz].any() and not o[(n + 1) * esz:].any(), "wrote outside [0, n)"
 
 
+@pytest.mark.parametrize("dt", [0, 1, 2, 3])       # int8, uint8, int16, uint16
+def test_tree_put_narrow_lanes_16_32_leaves(lfa, dt):
+    """reduce_tree_put on 1- and 2-byte lanes at 16 and 32
+    leaves (16, 17, 31, 32 inputs), SUM and MIN, ragged and misaligned,
+    bit-exact against the oracle.  Round 2 found the 4-KiB-tile form wrong
+    for byte lanes at 16 leaves: the cause was the compiler's readfirstlane
+    loops around buffer accesses whose descriptor it thought divergent (the
+    wave index), not register spilling; the scalar wave index
+    removed them.  The U = 4 forms, which the product does not pick for these
+    lanes, are covered through liblfa_tune.so in the next test."""
+    esz = oracle.datatype_size(dt)
+    nd = oracle.DT_NP[dt]
+    info = np.iinfo(nd)
+    from libfabric_amd import _native
+    for op in (2, 0):
+        for nsrc in (16, 17, 31, 32):
+            n = 70_003
+            rng = np.random.default_rng(nsrc * 11 + dt + op)
+            sends = [rng.integers(info.min, info.max, n + 2, dtype=nd, endpoint=True)
+                     for _ in range(nsrc)]
+            want = oracle.allreduce(op, dt, [x[1:n + 1].copy() for x in sends])[0]
+            srcs = [torch.from_numpy(x.view(np.uint8).copy()).to(DEV) for x in sends]
+            outs = [torch.zeros((n + 2) * esz, dtype=torch.uint8, device=DEV) for _ in range(2)]
+            sa = (ctypes.c_void_p * nsrc)(*[t.data_ptr() + esz for t in srcs])
+            da = (ctypes.c_void_p * 2)(*[t.data_ptr() + esz for t in outs])
+            assert _native.lib().lfa_reduce_tree_put_async(op, dt, da, 2, sa, nsrc, n,
+                                                           None) == 0
+            torch.cuda.synchronize()
+            for o in outs:
+                got = o.cpu().numpy()[esz:(n + 1) * esz].view(nd)
+                assert np.array_equal(got, want), (op, dt, nsrc)
+
+
+def test_tree_put_u4_byte_lanes_16_leaves_regression(lfa):
+    """The exact round-2 failure — FI_SUM int8 / uint8, 16 and 17 inputs,
+    4 KiB tiles per wave (lfa__tune_treeput_u, liblfa_tune.so) — now
+    bit-exact; and the probe's round-2 kernel form still reproduces the
+    miscompile, so this test would see a regression of the fix."""
+    from libfabric_amd import _native
+    T = _native.lib("tune")
+    for dt, nd in ((0, np.int8), (1, np.uint8)):
+        for nsrc in (16, 17):
+            n = 1 << 18
+            rng = np.random.default_rng(nsrc + dt)
+            sends = [rng.integers(np.iinfo(nd).min, np.iinfo(nd).max, n, dtype=nd,
+                                  endpoint=True) for _ in range(nsrc)]
+            want = oracle.allreduce(2, dt, sends)[0]
+            srcs = [torch.from_numpy(x.copy()).to(DEV) for x in sends]
+            out = torch.zeros(n, dtype=torch.int8 if dt == 0 else torch.uint8, device=DEV)
+            sa = (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs])
+            da = (ctypes.c_void_p * 1)(out.data_ptr())
+            assert T.lfa__tune_treeput_u(4, 2, dt, da, 1, sa, nsrc, n, None) == 0
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), want), (dt, nsrc)
+            if dt == 0:
+                out.zero_()
+                assert T.lfa__tp_probe(0, da, 1, sa, nsrc, n, None) == 0   # round-2 form
+                torch.cuda.synchronize()
+                assert not np.array_equal(out.cpu().numpy(), want), "round-2 form now right?"
+
+
+@pytest.mark.parametrize("op,dt", [(0, 8), (1, 6), (3, 9), (6, 5), (11, 4), (8, 1), (9, 7)])
+def test_nt_store_path_every_op_family(lfa, op, dt):
+    """Buffers of >= 192 MiB take combine_lds's nt-store path, which issues
+    each wave's loads pairwise and stores step by step behind counted vmcnt
+    waits (the drained form).  One op of every family, ATOMIC_WRITE (one
+    load per step) included, at 200 MiB + a ragged tail, oracle-checked on
+    windows at both ends, in the middle and across the last full tile."""
+    nd = oracle.DT_NP[dt]
+    nbytes = (200 << 20) + 4 * 1000 + nd().itemsize * 3
+    n = nbytes // nd().itemsize
+    g = torch.Generator(device=DEV).manual_seed(op * 7 + dt)
+    d0 = torch.randint(0, 256, (n * nd().itemsize,), dtype=torch.uint8, device=DEV,
+                       generator=g)
+    sv = torch.randint(0, 256, (n * nd().itemsize,), dtype=torch.uint8, device=DEV,
+                       generator=g)
+    if nd in (np.float32, np.float64):     # finite values: a meaningful PROD / MIN
+        f = torch.float32 if nd == np.float32 else torch.float64
+        d0 = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
+        sv = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
+    d = d0.clone()
+    assert lfa.write_ptr(op, dt, d.data_ptr(), sv.data_ptr(), n) == 0
+    torch.cuda.synchronize()
+    e = nd().itemsize
+    tile = 16 * 1024 // e
+    for lo in (0, n // 2, (n // tile - 1) * tile - 777, n - 5000):
+        hi = min(n, lo + 5000)
+        want = d0[lo * e:hi * e].cpu().numpy().view(nd).copy()
+        oracle.write(op, dt, want, sv[lo * e:hi * e].cpu().numpy().view(nd).copy())
+        assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
+
+
 def test_tree_put_errors(lfa):
     import ctypes
     from libfabric_amd import _native
