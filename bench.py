@@ -705,7 +705,7 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
         for r in range(2):
             coll.oneshot_reduce(FI_SUM, FI_FLOAT, coll.OneShot(
                 sends[r].data_ptr(), results[r].data_ptr(), 1024, -1,
-                ctypes.cast(sym, ctypes.c_void_p), 4096, flag_off, 2, r, i + 1,
+                ctypes.cast(sym, ctypes.c_void_p), 4096, region // 2, flag_off, 2, r, i + 1,
                 status.data_ptr(), i + 1, 2_000_000), streams[r])
         for st in streams:
             st.synchronize()
@@ -986,6 +986,11 @@ def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
         t = max_over_ranks(time.perf_counter() - t0, world) / reps
         sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+        if algo == coll.ALGO_AUTO:
+            # the per-bucket choice (lfa_coll_auto_algo; the same on every rank)
+            chosen = coll.auto_algo(5, cnt, world, 8)
+            sweep[str(nbytes)]["algo"] = {coll.ALGO_P2P: "p2p_oneshot",
+                                          coll.ALGO_TREE: "tree"}.get(chosen, str(chosen))
         if egress_gbs and world > 1:
             # reduce_scatter moves (N-1)/N of the bucket out of every GPU
             floor = (world - 1) / world * nbytes / (egress_gbs * 1e9)
@@ -1078,6 +1083,9 @@ def extra_collectives(rank, world, stream, emit=None):
     out = {"xgmi_peer_copy_256mib": xgmi} if xgmi else {}
     emit(out)
     ep = coll.Endpoint.from_torch_dist()
+    # TREE unless a row selects another: the P2P forms (and LFA_ALGO_AUTO,
+    # the device-domain default, whose small buckets are P2P) run last
+    ep.set_algo(coll.ALGO_TREE)
     try:
         x = torch.rand(COUNT, device="cuda")
         y = torch.empty_like(x)
@@ -1202,6 +1210,26 @@ def extra_collectives(rank, world, stream, emit=None):
                                                                   coll.ALGO_P2P, egress)
             except Exception as e:  # noqa: BLE001
                 out["reduce_scatter_double_prod_p2p"] = {"error": f"{e}"[:200]}
+            ep.set_algo(coll.ALGO_TREE)
+            emit(out)
+            # the device-domain default (LFA_ALGO_AUTO): one-shot P2P for
+            # small buckets, TREE above — the chosen algorithm per bucket
+            try:
+                out["reduce_scatter_double_prod_auto"] = _rs_sweep(ep, rank, world,
+                                                                   coll.ALGO_AUTO, egress)
+                ep.set_algo(coll.ALGO_AUTO)
+                ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(200):
+                    ep.wait(ep.allreduce(a, b, 1024, 8, 2))
+                t = max_over_ranks(time.perf_counter() - t0, world) / 200
+                out["allreduce_4kib_float_sum_auto_us"] = round(t * 1e6, 1)
+                out["allreduce_4kib_auto_bitwise_equal_tree"] = \
+                    max_over_ranks(0.0 if torch.equal(b, ref4k) else 1.0, world) == 0.0
+                out["auto_counters"] = ep.counters()
+            except Exception as e:  # noqa: BLE001
+                out["reduce_scatter_double_prod_auto"] = {"error": f"{e}"[:200]}
             ep.set_algo(coll.ALGO_TREE)
             emit(out)
         if rank == 0:

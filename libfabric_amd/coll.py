@@ -300,7 +300,7 @@ class OneShot(ctypes.Structure):
     _fields_ = [("send", ctypes.c_void_p), ("result", ctypes.c_void_p),
                 ("count", ctypes.c_size_t), ("mode", ctypes.c_int),
                 ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
-                ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
+                ("parity_off", ctypes.c_size_t), ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
                 ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
                 ("ticket", ctypes.c_uint32), ("timeout_us", ctypes.c_uint64)]
 

@@ -73,10 +73,19 @@ LFA_INTERNAL int run_local(const struct lfa_step *s, const struct lfa_ref *refs,
 						 (int)s->nsrc, s->count, stream);
 	}
 	case LFA_STEP_COPY:
-		if (s->src.buf == LFA_BUF_SYM_IN || s->src.buf == LFA_BUF_SYM_OUT) {
-			/* bytes peers pushed over xGMI into this rank's workspace
-			 * (the P2P unstage): through the P2P kernel's system-scope
-			 * loads, which no cached copy of the line can satisfy */
+		if (s->src.buf == LFA_BUF_SYM_IN || s->src.buf == LFA_BUF_SYM_OUT ||
+		    s->dst.buf == LFA_BUF_SYM_IN || s->dst.buf == LFA_BUF_SYM_OUT) {
+			/* the symmetric workspace, either way, through the P2P
+			 * kernel: system-scope loads for bytes peers pushed into it
+			 * (the unstage), and WRITE-THROUGH stores for bytes this
+			 * rank stages into it.  A plain-store copy (hipMemcpyAsync's
+			 * blit, the nt body) leaves the lines valid in this GPU's L2
+			 * slices; peers later overwrite the same bytes — one-shot
+			 * slots share SYM_IN with the staging area — through their
+			 * IPC mappings, which do not invalidate them, and this rank's
+			 * next one-shot read them stale (DESIGN.md §6b, round 3:
+			 * the first one-shot after a two-barrier allreduce, 4+
+			 * members).  sc0 sc1 stores drop the line instead. */
 			void *d = resolve(x, s->dst);
 			const void *sp = resolve(x, s->src);
 
@@ -203,6 +212,7 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	a.mode = st->peer;
 	a.sym = r->x.sym;
 	a.slot_bytes = os_slot(st, mc->size, esz);
+	a.parity_off = (r->x.region / 2) & ~(size_t)255;   /* the same on every member */
 	a.flag_off = 2 * r->x.region;
 	a.n = mc->size;
 	a.rank = mc->rank;

@@ -792,12 +792,53 @@ __global__ __launch_bounds__(kBlock) void fetch_elem(F f, size_t n0, size_t off1
 // above interleaves its loads with stores that may alias them, so each lane
 // had only one or two loads in flight (75.7 % of HBM peak for a 256 MiB float
 // SUM readwrite, tools/probe_fetch.py).
-template <int U, int SAUX, typename F>
+// Step u of a drained fetch tile (combine_drain's scheme): the kIn loads of
+// vector u have landed once every op but the kIn·(U-1-u) younger loads and
+// the stores of steps 0..u-1 (res, and dst unless ATOMIC_READ) is done.
+template <int U, int SAUX, typename F, int u>
+__device__ __forceinline__ void fetch_drain(const F &f, u32x4 (*lds)[kLdsWaves][U][64],
+                                            unsigned w, unsigned l, size_t base,
+                                            __amdgpu_buffer_rsrc_t rr,
+                                            __amdgpu_buffer_rsrc_t rd) {
+  if constexpr (u < U) {
+    constexpr int nst = F::kWriteDst ? 2 : 1;
+    wait_vmcnt<F::kIn * (U - 1 - u) + nst * u>();
+    const u32x4 a = lds[0][w][u][l];
+    const u32x4 b = F::kIn > 1 ? lds[F::kIn > 1 ? 1 : 0][w][u][l] : a;
+    const u32x4 c = F::kIn > 2 ? lds[F::kIn > 2 ? 2 : 0][w][u][l] : a;
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    if constexpr (SAUX == kStoreNt) {
+      st<true>(f.rv + base + u * 64 + l, a);
+      if constexpr (F::kWriteDst) st<true>(f.dv + base + u * 64 + l, f.op(a, b, c));
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
+      if constexpr (F::kWriteDst)
+        __builtin_amdgcn_raw_buffer_store_b128(f.op(a, b, c), rd, off, 0, SAUX);
+    }
+    fetch_drain<U, SAUX, F, u + 1>(f, lds, w, l, base, rr, rd);
+  }
+}
+
+template <int U, int SAUX, typename F, bool DRAIN = false>
 __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds(F f, size_t nvec) {
   __shared__ u32x4 lds[F::kIn][kLdsWaves][U][64];
   const unsigned w = wave_id(), l = threadIdx.x % 64;
   const size_t base =
       (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (DRAIN && base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int k = 0; k < F::kIn; k++)
+        __builtin_amdgcn_global_load_lds((const void *)(f.in(k) + base + u * 64 + l),
+                                         (lds_void *)&lds[k][w][u][0], 16, 0,
+                                         /*aux: nt*/ 2);
+    fetch_drain<U, SAUX, F, 0>(
+        f, lds, w, l, base,
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000),
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000));
+    return;
+  }
   if (base + 64 * U <= nvec) {
 #pragma unroll
     for (int k = 0; k < F::kIn; k++)
@@ -1135,19 +1176,20 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     }
     if (!h.send || (!h.result && a.slen[r]) || (uintptr_t)h.send % E ||
         (uintptr_t)h.result % E ||
-        h.slot_bytes < most || h.slot_bytes % 256 || most > 0xffffffffu)
+        h.slot_bytes < most || h.slot_bytes % 256 || most > 0xffffffffu ||
+        h.parity_off % 256 || (size_t)n * h.slot_bytes > h.parity_off)
       return -LFA_EINVAL;
     for (int k = 0; k < n; k++)
       if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
     const void *srcs[kOsMax];
-    const size_t par = (size_t)(h.epoch & 1) * (size_t)n;
+    const size_t par = (size_t)(h.epoch & 1) * h.parity_off;
     uintptr_t mis = (uintptr_t)h.result % 16;
     for (int k = 0; k < n; k++) {
       mis |= ((uintptr_t)h.send + a.soff[k]) % 16;
       srcs[k] = k == r ? (const char *)h.send + a.soff[r]
-                       : h.sym[r] + (par + (size_t)k) * h.slot_bytes;
+                       : h.sym[r] + par + (size_t)k * h.slot_bytes;
       if (k != r) {
-        a.push[k] = h.sym[k] + (par + (size_t)r) * h.slot_bytes;
+        a.push[k] = h.sym[k] + par + (size_t)r * h.slot_bytes;
         a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
       }
     }

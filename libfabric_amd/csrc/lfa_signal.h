@@ -61,10 +61,14 @@ int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
  * whole vector (mode LFA_ONESHOT_ALL, allreduce), block k of
  * lfa_coll_block's partition (LFA_ONESHOT_SCATTER, reduce_scatter: result
  * receives this rank's block), or the whole vector for k == mode only
- * (reduce to root `mode`).  Slots are double-buffered by epoch parity:
- * member j holds rank k's part of epoch e at sym[j] + ((e & 1)·n + k)·
- * slot_bytes, so a peer one operation ahead never overwrites a slot still
- * being read.  Needs 2·n·slot_bytes of SYM_IN.
+ * (reduce to root `mode`).  Slots are double-buffered by epoch parity in two
+ * FIXED halves of SYM_IN: member j holds rank k's part of epoch e at
+ * sym[j] + (e & 1)·parity_off + k·slot_bytes, so a peer one operation ahead
+ * never overwrites a slot still being read.  The halves must not move with
+ * the slot size: with a parity-p base of p·n·slot_bytes, a small operation
+ * after a large one put its odd slots inside the large one's even slots,
+ * which the slower members were still reading (wrong results in the mixed
+ * in-flight test, round 3).  Needs n·slot_bytes <= parity_off.
  */
 #ifndef LFA_ONESHOT_ALL                 /* also in lfa_coll.h */
 #define LFA_ONESHOT_ALL (-1)
@@ -77,6 +81,7 @@ struct lfa_oneshot {
 	int mode;               /* LFA_ONESHOT_ALL / _SCATTER / root */
 	char *const *sym;       /* [n]: every member's workspace as mapped here */
 	size_t slot_bytes;      /* one slot: the largest part, rounded up to 256 */
+	size_t parity_off;      /* odd epochs' slots: this far above the even ones */
 	size_t flag_off;        /* the flag area's offset in a workspace */
 	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
 	uint32_t epoch;         /* this group's one-shot operations so far + 1 */

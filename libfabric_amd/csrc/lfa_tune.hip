@@ -621,7 +621,7 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
 // readwrite (swap = 0) or float CSWAP (swap = 1) over nvec co-aligned 16-B
 // vectors.  0 = the round-1 register form (fetch_vec, 2 vectors per lane),
 // 1..3 = fetch_lds U = 4 / 2 / 1 with nt stores, 4..5 = U = 4 / 2 with sc1
-// write-through stores.
+// write-through stores, 6 / 7 = U = 4 drained step by step (sc1 / nt).
 // ---------------------------------------------------------------------------
 extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void *src,
                                    const void *cmp, void *res, size_t nvec,
@@ -630,12 +630,15 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
   hipStream_t s = (hipStream_t)stream;
   auto go = [&](auto f) -> int {
     using FF = decltype(f);
-    auto lds = [&](auto u, auto aux) {
+    auto lds = [&](auto u, auto aux, auto drain) {
       constexpr int U = decltype(u)::value, A = decltype(aux)::value;
-      hipLaunchKernelGGL((fetch_lds<U, A, FF>),
+      constexpr bool D = decltype(drain)::value;
+      hipLaunchKernelGGL((fetch_lds<U, A, FF, D>),
                          dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu)),
                          dim3(kLdsWaves * 64), 0, s, f, nvec);
     };
+    using NO = std::false_type;
+    using YES = std::true_type;
     using I4 = std::integral_constant<int, 4>;
     using I2 = std::integral_constant<int, 2>;
     using I1 = std::integral_constant<int, 1>;
@@ -647,11 +650,13 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
                            dim3(grid_for(nvec, (size_t)kBlock * kFetchUnroll, 0x7fffffffu)),
                            dim3(kBlock), 0, s, f, nvec);
         break;
-      case 1: lds(I4(), NT()); break;
-      case 2: lds(I2(), NT()); break;
-      case 3: lds(I1(), NT()); break;
-      case 4: lds(I4(), SC1()); break;
-      case 5: lds(I2(), SC1()); break;
+      case 1: lds(I4(), NT(), NO()); break;
+      case 2: lds(I2(), NT(), NO()); break;
+      case 3: lds(I1(), NT(), NO()); break;
+      case 4: lds(I4(), SC1(), NO()); break;
+      case 5: lds(I2(), SC1(), NO()); break;
+      case 6: lds(I4(), SC1(), YES()); break;  // drained steps (combine_drain's scheme)
+      case 7: lds(I4(), NT(), YES()); break;
       default: return -LFA_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;

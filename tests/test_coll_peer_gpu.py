@@ -515,8 +515,14 @@ def _oneshot_stream_worker(rank, world, port, q):
             ep.set_algo(coll.ALGO_P2P)
             rng = np.random.default_rng(77)         # the same sequence on every rank
             ops, ctxs, n_os = [], [], 0
-            for i in range(48):
-                kind = rng.choice(["allreduce", "reduce_scatter", "reduce", "big"])
+            # ONESHOT_MIX (diagnosis): "small" = one-shot kinds only
+            kinds = (["allreduce", "reduce_scatter", "reduce"]
+                     if os.environ.get("ONESHOT_MIX") == "small" else
+                     ["allreduce", "reduce_scatter", "reduce", "big"])
+            nops = int(os.environ.get("ONESHOT_NOPS", "48"))
+            meta = []
+            for i in range(nops):
+                kind = rng.choice(kinds)
                 dt, op = [(8, 2), (9, 3), (6, 1), (2, 0), (4, 7), (1, 9)][rng.integers(6)]
                 count = int(rng.integers(1, 3000)) if kind != "big" else 300_001
                 sends = _inputs(oracle, dt, count, world, 1000 + i)
@@ -542,8 +548,10 @@ def _oneshot_stream_worker(rank, world, port, q):
                 ops.append((kind, r, exp, xs))
                 # the planner's one-shot rule (lfa_coll_plan.c plan_p2p)
                 nb = count * oracle.datatype_size(dt)
-                n_os += (nb <= (1 << 20) if kind == "reduce_scatter"
+                is_os = (nb <= (1 << 20) if kind == "reduce_scatter"
                          else nb * world <= (256 << 10))
+                meta.append((dt, op, count, n_os if is_os else None))
+                n_os += is_os
             done = []
             while len(done) < len(ctxs):
                 done += ep.cq_read()
@@ -551,10 +559,17 @@ def _oneshot_stream_worker(rank, world, port, q):
             # the one-shot kernel ran (not the four items it replaces)
             c = ep.counters()
             assert n_os > 0 and c["oneshot"] == n_os and not c["timed_out"], (c, n_os)
+            bad = []
             for i, (kind, r, exp, _) in enumerate(ops):
                 if exp is not None:
                     got = r[:exp.size].cpu().numpy()
-                    assert got.tobytes() == exp.tobytes(), f"op {i} {kind}"
+                    if got.tobytes() != exp.tobytes():
+                        w = np.nonzero(got.view(np.uint8) != exp.view(np.uint8))[0]
+                        dt, op, count, os_i = meta[i]
+                        bad.append(f"op {i} {kind} dt={dt} op={op} count={count} "
+                                   f"oneshot#={os_i} wrong_bytes={w.size} "
+                                   f"first={w[:4].tolist()} last={w[-2:].tolist()}")
+            assert not bad, "; ".join(bad)
             assert not ep.transport_errors, ep.transport_errors
         finally:
             ep.close()

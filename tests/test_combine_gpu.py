@@ -325,21 +325,21 @@ def test_nt_store_path_every_op_family(lfa, op, dt):
     load per step) included, at 200 MiB + a ragged tail, oracle-checked on
     windows at both ends, in the middle and across the last full tile."""
     nd = oracle.DT_NP[dt]
-    nbytes = (200 << 20) + 4 * 1000 + nd().itemsize * 3
-    n = nbytes // nd().itemsize
+    nbytes = (200 << 20) + 4 * 1000 + nd.itemsize * 3
+    n = nbytes // nd.itemsize
     g = torch.Generator(device=DEV).manual_seed(op * 7 + dt)
-    d0 = torch.randint(0, 256, (n * nd().itemsize,), dtype=torch.uint8, device=DEV,
+    d0 = torch.randint(0, 256, (n * nd.itemsize,), dtype=torch.uint8, device=DEV,
                        generator=g)
-    sv = torch.randint(0, 256, (n * nd().itemsize,), dtype=torch.uint8, device=DEV,
+    sv = torch.randint(0, 256, (n * nd.itemsize,), dtype=torch.uint8, device=DEV,
                        generator=g)
-    if nd in (np.float32, np.float64):     # finite values: a meaningful PROD / MIN
-        f = torch.float32 if nd == np.float32 else torch.float64
+    if nd.kind == "f":     # finite values: a meaningful PROD / MIN
+        f = torch.float32 if nd.itemsize == 4 else torch.float64
         d0 = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
         sv = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
     d = d0.clone()
     assert lfa.write_ptr(op, dt, d.data_ptr(), sv.data_ptr(), n) == 0
     torch.cuda.synchronize()
-    e = nd().itemsize
+    e = nd.itemsize
     tile = 16 * 1024 // e
     for lo in (0, n // 2, (n // tile - 1) * tile - 777, n - 5000):
         hi = min(n, lo + 5000)

@@ -68,7 +68,7 @@ def tune():
     h = torch.cuda.current_stream().cuda_stream
     n = S // 4
     nvec = n // 4
-    variants = [0, 1, 2, 3, 4, 5]
+    variants = [int(v) for v in os.environ.get("FETCH_VARIANTS", "0,1,2,3,4,5,6,7").split(",")]
     for swap, nbytes in ((0, 4 * S), (1, 5 * S)):
         g = torch.Generator(device="cuda").manual_seed(3)
         sets = [[torch.rand(n, device="cuda", generator=g) for _ in range(4)]

@@ -29,18 +29,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-class OneShot(ctypes.Structure):
-    _fields_ = [("send", ctypes.c_void_p), ("result", ctypes.c_void_p),
-                ("count", ctypes.c_size_t), ("mode", ctypes.c_int),
-                ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
-                ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
-                ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
-                ("ticket", ctypes.c_uint32), ("timeout_us", ctypes.c_uint64)]
-
-
 def main() -> None:
     import torch
     from libfabric_amd import lib
+    from libfabric_amd.coll import OneShot
     L = lib()
     L.lfa_oneshot_reduce_async.argtypes = [ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(OneShot), ctypes.c_void_p]
@@ -68,7 +60,7 @@ def main() -> None:
     def oneshot(r, x, y, count):
         a = OneShot(x[r].data_ptr(), y[r].data_ptr(), count, -1,
                     ctypes.cast(sym, ctypes.c_void_p), (count * 4 + 255) // 256 * 256,
-                    flag_off, n, r, epoch[0], status.value, 1, 2_000_000)
+                    region // 2, flag_off, n, r, epoch[0], status.value, 1, 2_000_000)
         assert L.lfa_oneshot_reduce_async(2, 8, ctypes.byref(a),
                                           ctypes.c_void_p(streams[r].cuda_stream)) == 0
 
