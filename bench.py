@@ -286,8 +286,8 @@ def read_traffic():
 def read_traffic_shard(shard_bytes: int):
     """Per-launch HBM bytes of the same kernel at the shard's operand size,
     from the committed PMC passes over `--only-extra sizes`
-    (profiles/r02_pmc_traffic_sizes.json, tools/pmc_sizes.py)."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic_sizes.json")
+    (profiles/r03_pmc_traffic_sizes.json, tools/pmc_sizes.py)."""
+    path = os.path.join(ROOT, "profiles", "r03_pmc_traffic_sizes.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:

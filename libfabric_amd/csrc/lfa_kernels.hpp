@@ -485,6 +485,11 @@ __device__ __forceinline__ void tree_put_body(const PutArgs &a, size_t nvec) {
                      kSysLoadAux));
     });
   }
+  // Output-major issue.  Pacing the outputs (a vmcnt wait or s_sleep between
+  // them) or u-major order (every output's u-th vector, then u + 1) gained
+  // 4.5 us at 8 -> 8 on one box and lost 2.5 us on the next (8 x 32 MiB,
+  // local HBM, bench.py --tune-treeput variants 18-22,
+  // profiles/r03_tune_treeput*.log): not a reproducible difference.
   for (int j = 0; j < a.nout; j++) {  // wave-uniform
     __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
 #pragma unroll
@@ -1255,12 +1260,26 @@ static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
     // round-1 register form and 174.6 / 201.1 us with nt stores
     // (tools/probe_fetch.py --tune, profiles/r02_tune_fetch.log).  Two
     // output streams make write-through win even where combine_lds (one
-    // output) keeps nt.
+    // output) keeps nt.  Round 3: two-input bodies (readwrite) store step by
+    // step as their loads land (fetch_drain), and from kSc1Bytes per operand
+    // with nt stores, as combine_lds does: 256 MiB float SUM 163.2 / 164.9 us
+    // nt-drained vs 166.7 / 166.8 sc1-drained vs 172.2 sc1 (two boxes, back
+    // to back, profiles/r03_tune_fetch*.log).  The three-input compare body
+    // gains nothing measurable either way (212.5 - 217.6 us over every form)
+    // and keeps round 2's.
     constexpr int U = 4;
-    if (nvec)
-      hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF>),
-                         dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu)),
-                         dim3(kLdsWaves * 64), 0, s, f, nvec);
+    constexpr bool D = FF::kIn == 2;
+    const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu));
+    bool nt = false;
+    if constexpr (D) {
+      nt = nvec * 16 >= kSc1Bytes;
+      if (nt)
+        hipLaunchKernelGGL((fetch_lds<U, kStoreNt, FF, true>), grid, dim3(kLdsWaves * 64), 0,
+                           s, f, nvec);
+    }
+    if (nvec && !nt)
+      hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF, D>), grid, dim3(kLdsWaves * 64), 0, s,
+                         f, nvec);
     if (head + tail)
       hipLaunchKernelGGL(fetch_elem<decltype(f)>,
                          dim3(grid_for(head + tail, kBlock, kElemGridCap)),

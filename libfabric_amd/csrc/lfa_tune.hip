@@ -566,6 +566,52 @@ __global__ __launch_bounds__(kBlock) void tp_tune_pre(PutArgs a, size_t nvec) {
   }
 }
 
+// Scalar wave index (the product's) with the outputs' stores paced: at 8
+// outputs the round-2 body, whose divergent wave index put every store in a
+// one-pass readfirstlane loop, ran 5 % faster than the product (round 3,
+// 91.5 vs 96.4 us).  MODE 1: before output j >= 1, wait until at most
+// output j-1's U stores are in flight; 2: until none are; 3: s_sleep 1
+// between outputs; 4: u-major order (every output's u-th vector, then u+1).
+template <int U, int LAUX, int SAUX, int MODE>
+__global__ __launch_bounds__(kBlock) void tp_pace(PutArgs a, size_t nvec) {
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, LAUX));
+    });
+  }
+  if constexpr (MODE == 4) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      for (int j = 0; j < a.nout; j++)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, v[u]), tile_rsrc((u32x4 *)a.out[j] + wbase, bytes),
+            (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  } else {
+    for (int j = 0; j < a.nout; j++) {
+      if (j) {
+        if constexpr (MODE == 1) wait_vmcnt<U>();
+        if constexpr (MODE == 2) wait_vmcnt<0>();
+        if constexpr (MODE == 3) __builtin_amdgcn_s_sleep(1);
+      }
+      __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                               (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    }
+  }
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
@@ -609,6 +655,16 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 15: TP(2, 19, 19); break;
     case 16: TPP(2, 19, 19); break;
     case 17: TP(1, 19, 17); break;
+#define TPM(M)                                                                       \
+  hipLaunchKernelGGL((tp_pace<4, 19, 17, M>),                                        \
+                     dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)), dim3(kBlock), \
+                     0, s, a, nvec)
+    case 18: TPM(0); break;   // the product body through this harness
+    case 19: TPM(1); break;
+    case 20: TPM(2); break;
+    case 21: TPM(3); break;
+    case 22: TPM(4); break;
+#undef TPM
     default: return -LFA_EINVAL;
   }
 #undef TP
