@@ -199,10 +199,13 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		ep->barrier_host[0] = ~(uint64_t)d->rank;   /* coll_ep_barrier2 :1011 */
 	} else if (d->device >= 0) {
 		/* device buffers on a peer-transfer domain: the local items' kernels
-		 * and the staging copies run on this stream; ctl_host holds the P2P
-		 * handshake records */
+		 * run on this stream, staged host buffers' H2D / D2H on the two copy
+		 * streams (so chunks pipeline); ctl_host holds the P2P handshake
+		 * records */
 		hipSetDevice(d->device);
 		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipStreamCreateWithFlags(&ep->d2h_stream, hipStreamNonBlocking) != hipSuccess ||
 		    !(ep->ctl_host = calloc(1, ctl))) {
 			ep_release(ep);
 			return -LFA_EIO;
@@ -294,6 +297,10 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		sig_word_free(&ep->world);
 		if (ep->stream)
 			hipStreamDestroy(ep->stream);
+		if (ep->copy_stream)
+			hipStreamDestroy(ep->copy_stream);
+		if (ep->d2h_stream)
+			hipStreamDestroy(ep->d2h_stream);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -520,9 +527,16 @@ struct hop {
 	int dev;                /* device buffers (xport_peer_dev) */
 	hipEvent_t fin;         /* device hop: the stream reached the end */
 	/* host buffers run as a device hop (LFA_ALGO_P2P on a GPU peer domain:
-	 * every member must follow the one schedule): staged copies */
+	 * every member must follow the one schedule): staged copies, H2D on the
+	 * endpoint's copy stream (in_ev: the run's first item waits for it), D2H
+	 * on its d2h stream after the run (out_ev ends the hop) */
 	void *st_in, *st_out, *user_out;
 	size_t out_bytes;
+	hipEvent_t in_ev, out_ev;
+	int in_waited;
+	/* a device hop whose every item is on the stream: a later P2P hop may
+	 * enqueue behind it (stream order) without waiting for it to finish */
+	int issued;
 	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
 	 * (they share the symmetric workspace), then grow it if needed through
 	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
@@ -542,8 +556,17 @@ static void hop_free(struct hop *h)
 	hop_free(h->sub);
 	plan_free(&h->pl);
 	if (h->dev) {
-		/* a failed run may have left items on the stream that use tmp */
+		/* a failed run may have left items on the stream that use tmp, and
+		 * staging copies in flight on the copy streams */
 		hipStreamSynchronize(h->r.stream);
+		if (h->in_ev) {
+			hipEventSynchronize(h->in_ev);
+			hipEventDestroy(h->in_ev);
+		}
+		if (h->out_ev) {
+			hipEventSynchronize(h->out_ev);
+			hipEventDestroy(h->out_ev);
+		}
 		if (h->tmp)
 			hipFree(h->tmp);
 		if (h->st_in)
@@ -582,30 +605,55 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 			if (h->phase != HOP_RUN || h->err)
 				continue;
 		}
-		ret = xrun_advance(&h->r);
-		if (ret < 0) {
-			h->err = ret;
-		} else if (ret && h->dev) {
-			/* done once the stream has run the last local items */
-			hipError_t e;
-
-			if (!h->fin &&
-			    (lfa_hip_note(&h->r.hip_err,
-					  hipEventCreateWithFlags(&h->fin, hipEventDisableTiming),
-					  "completion event create") != hipSuccess ||
-			     lfa_hip_note(&h->r.hip_err, hipEventRecord(h->fin, h->r.stream),
-					  "completion event record") != hipSuccess)) {
+		if (h->in_ev && !h->in_waited) {
+			/* the staged input's H2D (copy stream) before the first item */
+			if (lfa_hip_note(&h->r.hip_err, hipStreamWaitEvent(h->r.stream, h->in_ev, 0),
+					 "staged input wait") != hipSuccess) {
 				h->err = -LFA_EIO;
 				continue;
 			}
-			e = hipEventQuery(h->fin);
-			if (e == hipSuccess && h->out_bytes &&
-			    lfa_hip_note(&h->r.hip_err,
-					 hipMemcpy(h->user_out, h->st_out, h->out_bytes,
-						   hipMemcpyDeviceToHost),
-					 "staged result D2H") != hipSuccess)
-				h->err = -LFA_EIO;
-			else if (e == hipSuccess)
+			h->in_waited = 1;
+		}
+		ret = h->issued ? 1 : xrun_advance(&h->r);
+		if (ret < 0) {
+			h->err = ret;
+		} else if (ret && h->dev) {
+			/* done once the stream has run the last local items (and, for
+			 * staged host buffers, the D2H behind them) */
+			hipEvent_t last;
+			hipError_t e;
+
+			if (!h->issued) {
+				if (lfa_hip_note(&h->r.hip_err,
+						 hipEventCreateWithFlags(&h->fin, hipEventDisableTiming),
+						 "completion event create") != hipSuccess ||
+				    lfa_hip_note(&h->r.hip_err, hipEventRecord(h->fin, h->r.stream),
+						 "completion event record") != hipSuccess) {
+					h->err = -LFA_EIO;
+					continue;
+				}
+				if (h->out_bytes &&
+				    (lfa_hip_note(&h->r.hip_err,
+						  hipEventCreateWithFlags(&h->out_ev,
+									  hipEventDisableTiming),
+						  "staged result event create") != hipSuccess ||
+				     lfa_hip_note(&h->r.hip_err,
+						  hipStreamWaitEvent(ep->d2h_stream, h->fin, 0),
+						  "staged result wait") != hipSuccess ||
+				     lfa_hip_note(&h->r.hip_err,
+						  hipMemcpyAsync(h->user_out, h->st_out, h->out_bytes,
+								 hipMemcpyDeviceToHost, ep->d2h_stream),
+						  "staged result D2H") != hipSuccess ||
+				     lfa_hip_note(&h->r.hip_err, hipEventRecord(h->out_ev, ep->d2h_stream),
+						  "staged result event record") != hipSuccess)) {
+					h->err = -LFA_EIO;
+					continue;
+				}
+				h->issued = 1;
+			}
+			last = h->out_ev ? h->out_ev : h->fin;
+			e = hipEventQuery(last);
+			if (e == hipSuccess)
 				h->done = 1;
 			else if (e != hipErrorNotReady &&
 				 lfa_hip_note(&h->r.hip_err, e, "completion event query"))
@@ -741,6 +789,9 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			join_finish(ep, p->mc);
 		} else if (p->kind == 2) {
 			/* join of a handle closed before it completed */
+		} else if (p->kind == 3) {
+			/* a chunk of a larger operation (peer_chunked): its last
+			 * chunk completes it */
 		} else {
 			struct lfa_cq_entry *c = &out[(*nout)++];
 
@@ -1034,7 +1085,10 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 
 			if (p && p->err)
 				return p->err;
-			if (p && !p->done)
+			/* a device hop with every item on the stream is far enough:
+			 * this one's items queue behind it (a growth below first
+			 * synchronises the stream) */
+			if (p && !p->done && !p->issued)
 				return 0;
 		}
 		if (h->sym_need <= mc->sym_region)
@@ -1571,7 +1625,16 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		if (hipMalloc(&h->st_in, in_b ? in_b : 1) != hipSuccess ||
 		    hipMalloc(&h->st_out, h->out_bytes ? h->out_bytes : 1) != hipSuccess)
 			return -LFA_ENOMEM;     /* hop_free releases what was made */
-		if (hipMemcpy(h->st_in, buf, in_b, hipMemcpyHostToDevice) != hipSuccess)
+		/* H2D on the copy stream now: a chunked operation's later chunks
+		 * upload while the earlier ones reduce (host_progress_all makes
+		 * the run wait for in_ev) */
+		if (hipEventCreateWithFlags(&h->in_ev, hipEventDisableTiming) != hipSuccess) {
+			h->in_ev = NULL;
+			return -LFA_EIO;
+		}
+		if (hipMemcpyAsync(h->st_in, buf, in_b, hipMemcpyHostToDevice,
+				   ep->copy_stream) != hipSuccess ||
+		    hipEventRecord(h->in_ev, ep->copy_stream) != hipSuccess)
 			return -LFA_EIO;
 		buf = h->st_in;
 		result = h->st_out;
@@ -1609,6 +1672,49 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	else
 		tag_p2p(ep, mc, t0);
 	return ret;
+}
+
+/*
+ * The group chunk on a GPU peer domain.  Under LFA_ALGO_P2P
+ * every member — host buffers staged, device buffers in place — runs the
+ * one device schedule, so a group chunk splits an allreduce or reduce into
+ * the same ⌈count / chunk⌉ P2P operations on every member: a rule of
+ * (algorithm, collective, count, n, esz, chunk) only, never of the member's
+ * buffer type.  Host members' chunks then pipeline: chunk c+1's H2D (copy
+ * stream) and chunk c-1's D2H (d2h stream) overlap chunk c's kernels.
+ * reduce_scatter keeps one operation (its chunks are 2-D).
+ */
+static int peer_chunked(const struct lfa_coll_ep *ep, const struct lfa_coll_mc *mc,
+			enum lfa_collective_op coll, size_t count, size_t esz)
+{
+	return ep->algo == LFA_ALGO_P2P && ep->group_chunk && ep->dom->device >= 0 &&
+	       mc->size > 1 && mc->size <= LFA_TREE_MAX && mc->size <= LFA_PUT_MAX &&
+	       (coll == LFA_ALLREDUCE || coll == LFA_REDUCE) &&
+	       count * esz > ep->group_chunk;
+}
+
+static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			       enum lfa_collective_op coll, const void *buf,
+			       void *result, size_t count, int root,
+			       enum lfa_datatype dt, enum lfa_op op, void *context,
+			       int dev)
+{
+	const size_t esz = lfa_datatype_size(dt);
+	size_t per = ep->group_chunk / esz;
+
+	if (!per)
+		per = 1;
+	for (size_t off = 0; off < count; off += per) {
+		const size_t n = count - off < per ? count - off : per;
+		const int last = off + n == count;
+		void *r = result ? (char *)result + off * esz : NULL;
+		int ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
+				      dt, op, context, last ? 0 : 3, NULL, dev);
+
+		if (ret)
+			return ret;     /* the chunks already queued run and reap */
+	}
+	return 0;
 }
 
 static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
@@ -1659,8 +1765,12 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		     coll == LFA_REDUCE))
 			dev = 2;
 		pthread_mutex_lock(&ep->lock);
-		ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
-				  context, 0, NULL, dev);
+		if (dev && peer_chunked(ep, mc, coll, count, esz))
+			ret = peer_submit_chunked(ep, mc, coll, buf, result, count, root, dt,
+						  op, context, dev);
+		else
+			ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
+					  context, 0, NULL, dev);
 		pthread_mutex_unlock(&ep->lock);
 		return ret;
 	}

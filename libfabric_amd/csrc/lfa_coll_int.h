@@ -89,7 +89,8 @@ struct pending {
 	hipEvent_t ev;          /* device domains */
 	struct hop *hop;        /* host domains: the operation's state */
 	void *context;
-	int kind;               /* 0 collective, 1 join, 2 join of a closed mc */
+	int kind;               /* 0 collective, 1 join, 2 join of a closed mc,
+				 * 3 a non-final chunk of a collective (no entry) */
 	struct lfa_coll_mc *mc;
 	/* the group the operation's P2P kernels ran on and its highest ticket
 	 * (0: none); timed_out: found failed when that group was closed */
