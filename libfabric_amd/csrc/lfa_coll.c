@@ -301,6 +301,9 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 			hipStreamDestroy(ep->copy_stream);
 		if (ep->d2h_stream)
 			hipStreamDestroy(ep->d2h_stream);
+		for (int i = 0; i < LFA_STAGE_POOL; i++)
+			if (ep->stage[i].p)
+				hipFree(ep->stage[i].p);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -547,7 +550,61 @@ struct hop {
 	int32_t agree_in, agree_out;
 	unsigned char mine[LFA_SYM_REC_BYTES];
 	uint64_t scratch[2];    /* barrier word and its result */
+	struct lfa_coll_ep *ep;
 };
+
+/* A device buffer of at least `bytes` from the endpoint's staging pool (the
+ * smallest free one that fits, else a free slot (re)allocated to `bytes`),
+ * or a plain hipMalloc when every slot is busy; NULL on failure.  ep->lock
+ * held.  stage_put returns it. */
+static void *stage_get(struct lfa_coll_ep *ep, size_t bytes)
+{
+	struct stage_buf *fit = NULL, *spare = NULL;
+	void *p;
+
+	if (!bytes)
+		bytes = 1;
+	for (int i = 0; i < LFA_STAGE_POOL; i++) {
+		struct stage_buf *b = &ep->stage[i];
+
+		if (b->busy)
+			continue;
+		if (b->p && b->bytes >= bytes && (!fit || b->bytes < fit->bytes))
+			fit = b;
+		else if (!spare || (spare->p && !b->p))
+			spare = b;      /* prefer an empty slot */
+	}
+	if (fit) {
+		fit->busy = 1;
+		return fit->p;
+	}
+	if (spare) {
+		if (spare->p)
+			hipFree(spare->p);
+		spare->p = NULL;
+		spare->bytes = 0;
+		if (hipMalloc(&spare->p, bytes) != hipSuccess) {
+			spare->p = NULL;
+			return NULL;
+		}
+		spare->bytes = bytes;
+		spare->busy = 1;
+		return spare->p;
+	}
+	return hipMalloc(&p, bytes) == hipSuccess ? p : NULL;
+}
+
+static void stage_put(struct lfa_coll_ep *ep, void *p)
+{
+	if (!p)
+		return;
+	for (int i = 0; i < LFA_STAGE_POOL; i++)
+		if (ep->stage[i].p == p) {
+			ep->stage[i].busy = 0;
+			return;
+		}
+	hipFree(p);
+}
 
 static void hop_free(struct hop *h)
 {
@@ -557,22 +614,23 @@ static void hop_free(struct hop *h)
 	plan_free(&h->pl);
 	if (h->dev) {
 		/* a failed run may have left items on the stream that use tmp, and
-		 * staging copies in flight on the copy streams */
-		hipStreamSynchronize(h->r.stream);
+		 * staging copies in flight on the copy streams; a finished one
+		 * has passed its events already */
+		if (!h->done)
+			hipStreamSynchronize(h->r.stream);
 		if (h->in_ev) {
-			hipEventSynchronize(h->in_ev);
+			if (!h->done)
+				hipEventSynchronize(h->in_ev);
 			hipEventDestroy(h->in_ev);
 		}
 		if (h->out_ev) {
-			hipEventSynchronize(h->out_ev);
+			if (!h->done)
+				hipEventSynchronize(h->out_ev);
 			hipEventDestroy(h->out_ev);
 		}
-		if (h->tmp)
-			hipFree(h->tmp);
-		if (h->st_in)
-			hipFree(h->st_in);
-		if (h->st_out)
-			hipFree(h->st_out);
+		stage_put(h->ep, h->tmp);
+		stage_put(h->ep, h->st_in);
+		stage_put(h->ep, h->st_out);
 		if (h->fin)
 			hipEventDestroy(h->fin);
 	} else {
@@ -1571,6 +1629,7 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	struct plan raw;
 	int ret, sym;
 
+	h->ep = ep;
 	/* P2P keeps its schedule on device buffers (the peers' symmetric
 	 * workspaces are IPC-mapped device memory; its barriers become zero-byte
 	 * messages); host buffers and RCCL run as TREE */
@@ -1607,10 +1666,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	h->r.stream = ep->stream;
 	if (dev) {
 		hipSetDevice(ep->dom->device);
-		if (h->pl.tmp && hipMalloc(&h->tmp, h->pl.tmp) != hipSuccess) {
-			h->tmp = NULL;
+		if (h->pl.tmp && !(h->tmp = stage_get(ep, h->pl.tmp)))
 			return -LFA_ENOMEM;
-		}
 	} else if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp))) {
 		return -LFA_ENOMEM;
 	}
@@ -1622,8 +1679,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		h->out_bytes = coll == LFA_REDUCE_SCATTER ? mlen * esz :
 			       coll == LFA_REDUCE && mc->rank != root ? 0 : count * esz;
 		h->user_out = result;
-		if (hipMalloc(&h->st_in, in_b ? in_b : 1) != hipSuccess ||
-		    hipMalloc(&h->st_out, h->out_bytes ? h->out_bytes : 1) != hipSuccess)
+		if (!(h->st_in = stage_get(ep, in_b)) ||
+		    !(h->st_out = stage_get(ep, h->out_bytes)))
 			return -LFA_ENOMEM;     /* hop_free releases what was made */
 		/* H2D on the copy stream now: a chunked operation's later chunks
 		 * upload while the earlier ones reduce (host_progress_all makes

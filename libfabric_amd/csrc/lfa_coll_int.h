@@ -22,6 +22,7 @@
 #define LFA_CID_BYTES (LFA_MAX_GROUP_ID / 8)
 /* Bytes of one P2P handle-exchange record (struct sym_rec, lfa_coll.c). */
 #define LFA_SYM_REC_BYTES 80
+#define LFA_STAGE_POOL 128              /* peer-domain staging buffers kept */
 
 /* Where a plan's refs point for one execution: the operation's buffers and,
  * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
@@ -115,6 +116,14 @@ struct lfa_coll_ep {
 	size_t ws_size;
 	void *hs[2];                /* device staging for host buffers */
 	size_t hs_size;
+	/* peer domains: device staging of host buffers (LFA_ALGO_P2P) and the
+	 * device hops' TMP, kept across operations — a hipMalloc / hipFree pair
+	 * of 256 MiB per operation cost more than its PCIe copies */
+	struct stage_buf {
+		void *p;
+		size_t bytes;
+		int busy;
+	} stage[LFA_STAGE_POOL];
 	uint64_t *barrier_host;     /* pinned ~rank for barrier */
 	void *barrier_dev;          /* 2 x uint64 */
 	void *ctl_dev;              /* P2P handle exchange, nranks records */
