@@ -149,14 +149,15 @@ inline void note_error(int rc) {
 
 template <int OP, int DT>
 void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
+  if (!cnt) return;  // the reference's loop over zero elements: nothing, no GPU call
   const int k = ptr_kind(dst) | ptr_kind(res) | (OP == LFA_ATOMIC_READ ? 0 : ptr_kind(src));
-  if (cnt && k == kHost) {
+  if (k == kHost) {
     int rc = lfa_host_readwrite((lfa_op)OP, (lfa_datatype)DT, dst, src, res, cnt);
     if (rc) fprintf(stderr, "lfa: host fetch op=%d dt=%d failed (%d)\n", OP, DT, rc);
     note_error(rc);
     return;
   }
-  if (cnt && k != kDev) {
+  if (k != kDev) {
     fprintf(stderr, "lfa: fetch op=%d dt=%d: mixed host/device operands\n", OP, DT);
     note_error(-LFA_EINVAL);
     return;
@@ -172,14 +173,15 @@ void sync_rw_entry(void *dst, const void *src, void *res, size_t cnt) {
 template <int OP, int DT>
 void sync_swap_entry(void *dst, const void *src, const void *cmp, void *res,
                      size_t cnt) {
+  if (!cnt) return;
   const int k = ptr_kind(dst) | ptr_kind(src) | ptr_kind(cmp) | ptr_kind(res);
-  if (cnt && k == kHost) {
+  if (k == kHost) {
     int rc = lfa_host_swap((lfa_op)OP, (lfa_datatype)DT, dst, src, cmp, res, cnt);
     if (rc) fprintf(stderr, "lfa: host swap op=%d dt=%d failed (%d)\n", OP, DT, rc);
     note_error(rc);
     return;
   }
-  if (cnt && k != kDev) {
+  if (k != kDev) {
     fprintf(stderr, "lfa: swap op=%d dt=%d: mixed host/device operands\n", OP, DT);
     note_error(-LFA_EINVAL);
     return;
