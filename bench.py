@@ -695,7 +695,11 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device=dev) for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
     status = torch.full((1,), -1, dtype=torch.int32).pin_memory()   # LFA_SIG_NONE
-    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    # two priorities: HIP keeps a hardware-queue pool per priority, so the
+    # two ranks' kernels never share a queue (rank 0's wait would hold rank
+    # 1's launch behind it until the timeout)
+    streams = [torch.cuda.Stream(device=dev, priority=0),
+               torch.cuda.Stream(device=dev, priority=-1)]
     for r in results:
         r.zero_()
     torch.cuda.synchronize()

@@ -28,6 +28,7 @@
  * valid for every op including the bitwise/logical ones RCCL lacks.
  */
 #define _GNU_SOURCE
+#include <dirent.h>
 #include <errno.h>
 #include <pthread.h>
 #include <sched.h>
@@ -987,6 +988,21 @@ struct sym_rec {
 	hipIpcMemHandle_t h;
 };
 
+/* Open file descriptors of this process (LFA_DEBUG diagnostics: every
+ * exported or imported IPC workspace holds a dma-buf descriptor). */
+static int open_fds(void)
+{
+	DIR *d = opendir("/proc/self/fd");
+	int n = 0;
+
+	if (!d)
+		return -1;
+	while (readdir(d))
+		n++;
+	closedir(d);
+	return n - 3;   /* ".", ".." and the directory's own descriptor */
+}
+
 /* Unmap the peers' workspaces in `sym` and free this rank's `local`. */
 static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 {
@@ -1060,9 +1076,31 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	 * as "ahead"  */
 	mc->bar_epoch = 0;
 	mc->os_epoch = 0;
-	if (ok && n > 1)
-		ok = lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
+	if (ok && n > 1 && hipIpcGetMemHandle(&mine->h, mc->sym_local) != hipSuccess) {
+		/* seen once in a round-3 GPU run (2 of 8 processes on one GPU,
+		 * "invalid argument" at a workspace growth): export a fresh
+		 * allocation once more before failing the growth on every member */
+		(void)hipGetLastError();
+		if (getenv("LFA_DEBUG"))
+			fprintf(stderr, "lfa: P2P workspace export failed (%d fds open); "
+				"retrying on a new allocation\n", open_fds());
+		hipFree(mc->sym_local);
+		mc->sym_local = NULL;
+		ok = lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
+						 2 * region + LFA_SIG_AREA_BYTES),
+				  "P2P workspace hipMalloc (retry)") == hipSuccess &&
+		     lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
+						      LFA_SIG_AREA_BYTES, mc->ep->stream),
+				  "P2P flag area memset (retry)") == hipSuccess &&
+		     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
+				  "P2P flag area memset sync (retry)") == hipSuccess &&
+		     lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
 				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
+		if (!ok && mc->sym_local) {
+			hipFree(mc->sym_local);
+			mc->sym_local = NULL;
+		}
+	}
 	mine->ok = ok;
 	sym_free(mc, old_sym, old_local);
 }

@@ -18,6 +18,10 @@
 LFA_INTERNAL hipError_t lfa_hip_note(int *slot, hipError_t e, const char *what)
 {
 	if (e != hipSuccess) {
+		/* handled here: consume the thread's sticky HIP error, so the
+		 * caller's next framework call (a torch launch check, say) does
+		 * not report this failure as its own */
+		(void)hipGetLastError();
 		if (slot && !*slot)
 			*slot = (int)e;
 		if (getenv("LFA_DEBUG"))

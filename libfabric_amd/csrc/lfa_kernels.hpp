@@ -434,6 +434,54 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_elem(TreeArgs a, T *dst,
   }
 }
 
+// Operands not aligned to sizeof(T) — a caller's byte offset into a buffer,
+// which the reference's host loops take as they come (coll_coll.c:763 hands
+// the table whatever the caller passed).  Element i of such an operand is
+// moved byte-wise, and the tree is walked with a runtime leaf count: one
+// kernel per (OP, T) for a path only odd caller buffers take.
+template <typename T>
+__device__ __forceinline__ T ld_bytes(const void *p, size_t i) {
+  T v;
+  __builtin_memcpy(&v, (const char *)p + i * sizeof(T), sizeof(T));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void st_bytes(void *p, size_t i, T v) {
+  __builtin_memcpy((char *)p + i * sizeof(T), &v, sizeof(T));
+}
+
+// tree_eval_with's order (same leaves, same merges) for a runtime nleaf.
+template <int OP, typename T, typename L>
+__device__ __forceinline__ T tree_eval_rt(const TreeArgs &a, int nleaf, L &&load) {
+  T stack[6];
+  int depth = 0;
+  for (int k = 0; k < nleaf; k++) {
+    T v = load(a.hi[k]);
+    if (a.lo[k] >= 0) v = apply<OP, T>(v, load(a.lo[k]));
+    stack[depth++] = v;
+    for (int m = 1; m < nleaf; m <<= 1) {
+      if (((k + 1) & (2 * m - 1)) == 0) {
+        T hi = stack[--depth];
+        T lo = stack[--depth];
+        stack[depth++] = apply<OP, T>(hi, lo);
+      }
+    }
+  }
+  return stack[0];
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void reduce_tree_unaligned(TreeArgs a, int nleaf,
+                                                                void *dst, size_t n) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n; i += stride)
+    st_bytes<T>(dst, i, tree_eval_rt<OP, T>(a, nleaf, [&](int k) {
+                  return ld_bytes<T>(a.in[k], i);
+                }));
+}
+
 // ---------------------------------------------------------------------------
 // N-input tree with fan-out, across GPUs (LFA_ALGO_P2P)
 // ---------------------------------------------------------------------------
@@ -562,6 +610,30 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_put_elem(PutArgs a, size_t
   }
 }
 
+// Some operand not aligned to sizeof(T).  In the P2P schedules that is only
+// ever the caller's own buffer (its block read in place, its result written
+// in place: local memory), never a peer's workspace slot (256-B aligned), so
+// element-aligned operands keep their system-scope element accesses (bit k
+// of `in_sys` / `out_sys`) and the others are moved byte-wise.
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void reduce_tree_put_unaligned(PutArgs a, int nleaf,
+                                                                    uint32_t in_sys,
+                                                                    uint32_t out_sys,
+                                                                    size_t n) {
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * kBlock;
+  for (; i < n; i += stride) {
+    T v = tree_eval_rt<OP, T>(a.t, nleaf, [&](int k) {
+      return (in_sys >> k) & 1 ? sys_load<T>((const T *)a.t.in[k] + i)
+                               : ld_bytes<T>(a.t.in[k], i);
+    });
+    for (int j = 0; j < a.nout; j++) {
+      if ((out_sys >> j) & 1) sys_store<T>((T *)a.out[j] + i, v);
+      else st_bytes<T>(a.out[j], i, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // one-shot reduction (LFA_STEP_ONESHOT, lfa_signal.h): push, post, wait,
 // reduce — one launch for a small bucket instead of copy + barrier + tree +
@@ -597,6 +669,7 @@ struct OsArgs {
   uint32_t epoch, ticket;
   int n, rank;
   int vec;                     // every range start and result 16-B aligned
+  int unal;                    // send or result not aligned to the element
 };
 
 template <int OP, typename T, int NLEAF>
@@ -658,6 +731,16 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
                                                        (unsigned)o, 0, kSysLoadAux));
     });
     *(u32x4 *)(a.result + o) = v;
+  }
+  if (a.unal) {
+    // the caller's own input and result, byte-wise (local memory); the
+    // peers' slots (256-B aligned) keep their system-scope loads
+    for (size_t e = lo / E + t; e < hi / E; e += kBlock)
+      st_bytes<T>(a.result, e, tree_eval_with<OP, T, T, NLEAF>(a.t, [&](int k) {
+                    return k == a.rank ? ld_bytes<T>(a.t.in[k], e)
+                                       : sys_load<T>((const T *)a.t.in[k] + e);
+                  }));
+    return;
   }
   for (size_t e = vhi / E + t; e < hi / E; e += kBlock) {
     T v = tree_eval_with<OP, T, T, NLEAF>(
@@ -1068,7 +1151,12 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
       mis |= ((uintptr_t)srcs[k] % 16) ^ ((uintptr_t)dst % 16);
       anyelem |= (uintptr_t)srcs[k] % E;
     }
-    if (anyelem) return -LFA_EINVAL;  // element-misaligned inputs: unsupported
+    if (anyelem) {
+      hipLaunchKernelGGL((reduce_tree_unaligned<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock), 0, s,
+                         a, pof2, dst, cnt);
+      return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+    }
     bool vec = (mis == 0) && E <= 16;
     size_t head = vec ? ((16 - (uintptr_t)dst % 16) % 16) / E : 0;
     if (head > cnt) head = cnt;
@@ -1138,7 +1226,17 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
       mis |= ((uintptr_t)dsts[j] ^ p0) % 16;
       anyelem |= (uintptr_t)dsts[j] % E;
     }
-    if (anyelem) return -LFA_EINVAL;
+    if (anyelem) {
+      uint32_t in_sys = 0, out_sys = 0;
+      for (int k = 0; k < nsrc; k++)
+        if ((uintptr_t)srcs[k] % E == 0) in_sys |= 1u << k;
+      for (int j = 0; j < ndst; j++)
+        if ((uintptr_t)dsts[j] % E == 0) out_sys |= 1u << j;
+      hipLaunchKernelGGL((reduce_tree_put_unaligned<OP, T>),
+                         dim3(grid_for(cnt, kBlock, kElemGridCap)), dim3(kBlock), 0, s,
+                         a, pof2, in_sys, out_sys, cnt);
+      return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+    }
     const bool vec = mis == 0 && E <= 16;
     size_t head = vec ? ((16 - p0 % 16) % 16) / E : 0;
     if (head > cnt) head = cnt;
@@ -1179,8 +1277,7 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       }
       if (a.slen[k] > most) most = a.slen[k];
     }
-    if (!h.send || (!h.result && a.slen[r]) || (uintptr_t)h.send % E ||
-        (uintptr_t)h.result % E ||
+    if (!h.send || (!h.result && a.slen[r]) ||
         h.slot_bytes < most || h.slot_bytes % 256 || most > 0xffffffffu ||
         h.parity_off % 256 || (size_t)n * h.slot_bytes > h.parity_off)
       return -LFA_EINVAL;
@@ -1211,7 +1308,8 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     a.ticket = h.ticket;
     a.n = n;
     a.rank = r;
-    a.vec = mis == 0 && E <= 16;
+    a.unal = (uintptr_t)h.send % E || (uintptr_t)h.result % E;
+    a.vec = mis == 0 && E <= 16 && !a.unal;
     // the same grid on every member: `most` depends only on count and n
     const unsigned grid = (unsigned)((most + a.chunk - 1) / a.chunk);
     switch (pof2) {

@@ -348,3 +348,122 @@ def test_gpu_fetch_and_compare_any_shape(pair, n, off, edge, seed):
         torch.cuda.synchronize()
         assert np.array_equal(d.cpu().numpy(), want_d), f"swap op={op} dt={dt} n={n}"
         assert np.array_equal(r.cpu().numpy(), want_r), f"swap res op={op} dt={dt} n={n}"
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(pair=st.sampled_from(REDUCE_PAIRS), nsrc=st.integers(1, 16), ndst=st.integers(1, 4),
+       n=st.one_of(st.integers(0, 3000), st.integers(3000, 1 << 17)),
+       offs=st.lists(st.sampled_from([0, 0, 16, 1, 2, 3, 5, 8]), min_size=20, max_size=20),
+       seed=st.integers(0, 2**31))
+def test_gpu_tree_put_any_offsets(pair, nsrc, ndst, n, offs, seed):
+    """lfa_reduce_tree_put_async (the P2P kernel) with every operand at its
+    own drawn byte offset: co-aligned vector body, element path, and the
+    byte-wise path for operands not aligned to the element (a caller's own
+    block read or result written in place)."""
+    import torch
+    from libfabric_amd import atomic
+    op, dt = pair
+    esz = oracle.datatype_size(dt)
+    nd = oracle.DT_NP[dt]
+    rng = np.random.default_rng(seed)
+    sends = [_operand(dt, n, rng, 0.05) for _ in range(nsrc)]
+    srcs = [_dev(x, offs[k], n * esz, torch) for k, x in enumerate(sends)]
+    outs = [_dev(np.zeros(n * esz, np.uint8), offs[16 + j], n * esz, torch)
+            for j in range(ndst)]
+    atomic.reduce_tree_put(op, dt, outs, srcs, n)
+    torch.cuda.synchronize()
+    if n:
+        want = oracle.allreduce(op, dt, [x.view(nd) for x in sends])[0].view(np.uint8)
+        for j, o in enumerate(outs):
+            assert_parity(dt, o.cpu().numpy(), want,
+                          f"op={op} dt={dt} nsrc={nsrc} out={j} n={n} offs={offs}")
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(coll_op=st.sampled_from([ALLREDUCE, REDUCE_SCATTER, REDUCE]),
+       algo=st.sampled_from(ALGOS), n=st.integers(1, 8),
+       count=st.one_of(st.integers(0, 700), st.integers(700, 200_000)),
+       pair=st.sampled_from(SCHED_PAIRS), soff=st.integers(0, 15), roff=st.integers(0, 15),
+       root_pick=st.integers(0, 1 << 16), seed=st.integers(0, 2**31))
+def test_gpu_collectives_any_buffer_offset(coll_op, algo, n, count, pair, soff, roff,
+                                           root_pick, seed):
+    """Every rank's schedule on the GPU (lfa_coll_loopback: the executor, its
+    kernels and a device-copy transport) with the send and result buffers at
+    drawn byte offsets — including offsets that are not a multiple of the
+    element, which prov/coll's host loops accept as well."""
+    import torch
+    if coll_op == REDUCE and algo == coll.ALGO_TREE_COLL:
+        algo = coll.ALGO_TREE
+    op, dt = pair
+    nd = oracle.DT_NP[dt]
+    esz = oracle.datatype_size(dt)
+    rng = np.random.default_rng(seed)
+    sends = [_operand(dt, count, rng, 0.05) for _ in range(n)]
+    root = root_pick % n if coll_op == REDUCE else -1
+    full = oracle.allreduce(op, dt, [x.view(nd) for x in sends])[0] if count else \
+        np.zeros(0, nd)
+    lens = [coll.block(count, n, r)[1] if coll_op == REDUCE_SCATTER else count
+            for r in range(n)]
+    sd = [_dev(x, soff, count * esz, torch) for x in sends]
+    rd = [_dev(np.zeros(lens[r] * esz, np.uint8), roff, lens[r] * esz, torch)
+          for r in range(n)]
+    coll.loopback(coll_op, algo, n, root, dt, op, count, sd, rd)
+    torch.cuda.synchronize()
+    for r in range(n):
+        if coll_op == REDUCE and r != root:
+            continue
+        off = coll.block(count, n, r)[0] if coll_op == REDUCE_SCATTER else 0
+        assert_parity(dt, rd[r].cpu().numpy(), full[off:off + lens[r]].view(np.uint8),
+                      f"coll={coll_op} algo={algo} n={n} count={count} rank={r} "
+                      f"offs={soff},{roff}")
+    for x, d in zip(sends, sd):
+        assert np.array_equal(d.cpu().numpy(), x)      # inputs untouched
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [8, 2, 9, 6])
+@pytest.mark.parametrize("mode", [-1, -2, 0, 1])
+@pytest.mark.parametrize("offs", [(0, 0), (1, 3), (2, 0), (0, 5)])
+def test_gpu_oneshot_misaligned_buffers(dt, mode, offs):
+    """The one-shot kernel (LFA_STEP_ONESHOT) with the caller's send and
+    result at byte offsets that are not a multiple of the element: two ranks
+    on two streams of this process, each with its own workspace; every mode
+    (allreduce, reduce_scatter, reduce to either root) bit-exact against the
+    oracle, no wait timed out."""
+    import torch
+    op = 2 if dt in (8, 9) else 0                     # float/double SUM, ints MIN
+    esz = oracle.datatype_size(dt)
+    nd = oracle.DT_NP[dt]
+    count = 4000 // esz
+    rng = np.random.default_rng(dt * 100 + mode)
+    sends = [_operand(dt, count, rng, 0.05) for _ in range(2)]
+    full = oracle.allreduce(op, dt, [x.view(nd) for x in sends])[0].view(np.uint8)
+    region, flag_off = 1 << 20, 2 << 20
+    ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device="cuda")
+          for _ in range(2)]
+    sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
+    status = torch.full((1,), -1, dtype=torch.int32).pin_memory()
+    sd = [_dev(x, offs[0], count * esz, torch) for x in sends]
+    want, rd = [], []
+    for r in range(2):
+        off, ln = coll.block(count, 2, r) if mode == -2 else (0, count)
+        want.append(full[off * esz:(off + ln) * esz] if mode < 0 or mode == r else None)
+        rd.append(_dev(np.zeros(ln * esz, np.uint8), offs[1], ln * esz, torch))
+    torch.cuda.synchronize()
+    # two priorities: HIP keeps a hardware-queue pool per priority, so the
+    # ranks' kernels cannot land in one queue, where rank 0's wait would hold
+    # rank 1's launch behind it until the timeout
+    streams = [torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)]
+    for r in range(2):
+        coll.oneshot_reduce(op, dt, coll.OneShot(
+            sd[r].data_ptr(), rd[r].data_ptr(), count, mode,
+            ctypes.cast(sym, ctypes.c_void_p), 4096, region // 2, flag_off, 2, r, 1,
+            status.data_ptr(), 1, 5_000_000), streams[r])
+    for s in streams:
+        s.synchronize()
+    assert int(status.item()) == -1, "a one-shot wait timed out"
+    for r in range(2):
+        if want[r] is not None:
+            assert_parity(dt, rd[r].cpu().numpy(), want[r], f"rank {r} mode {mode} offs {offs}")
