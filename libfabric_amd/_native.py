@@ -84,6 +84,9 @@ def _bind_tune(L):
                                       c_size_t, c_void_p]
     L.lfa__tune_stream.restype = c_int
     L.lfa__tune_stream.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    L.lfa__tune_read_n.restype = c_int
+    L.lfa__tune_read_n.argtypes = [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t,
+                                   c_void_p]
 
 
 def lib(name: str = "lfa") -> ctypes.CDLL:

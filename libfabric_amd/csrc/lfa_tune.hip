@@ -769,7 +769,46 @@ __global__ __launch_bounds__(256) void write_only(u32x4 *dst, size_t nvec) {
   for (int u = 0; u < U; u++)
     __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
 }
+
+// NIN inputs read in the shape of the product tree below 192 MiB of output
+// (reduce_tree_chunk<U = 2>: each lane loads vectors t and t + 256 of every
+// input with nt loads), XOR-folded so nothing is stored but one vector per
+// workgroup that no real data reaches: the read side of the N -> 1 tree alone.
+template <int NIN>
+__global__ __launch_bounds__(256) void read_chunk(lfa::TreeArgs a, u32x4 *sink, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * 512 + threadIdx.x;
+  if (base + 256 >= nvec) return;
+  u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < NIN; k++)
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+      x ^= __builtin_nontemporal_load((const u32x4 *)a.in[k] + base + u * 256);
+  if (x.x == 0x9e3779b9u && x.y == 0x7f4a7c15u && x.z == 0x2545f491u && x.w == 1u)
+    sink[blockIdx.x] = x;
+}
 }  // namespace lfa_stream
+
+// The read side of the N-input tree (tools/probe_hbm.py --tree): nin in
+// {2, 4, 8, 16} inputs of nvec 16-B vectors each, at the caller's addresses.
+extern "C" int lfa__tune_read_n(const void *const *ins, int nin, void *sink, size_t nvec,
+                                void *stream) {
+  using namespace lfa_stream;
+  hipStream_t s = (hipStream_t)stream;
+  lfa::TreeArgs a;
+  memset(&a, 0, sizeof(a));
+  if (nin < 1 || nin > 16 || !nvec || nvec % 512) return -LFA_EINVAL;
+  for (int k = 0; k < nin; k++) a.in[k] = ins[k];
+  const dim3 grid((unsigned)(nvec / 512)), block(256);
+  switch (nin) {
+    case 2: hipLaunchKernelGGL((read_chunk<2>), grid, block, 0, s, a, (u32x4 *)sink, nvec); break;
+    case 4: hipLaunchKernelGGL((read_chunk<4>), grid, block, 0, s, a, (u32x4 *)sink, nvec); break;
+    case 8: hipLaunchKernelGGL((read_chunk<8>), grid, block, 0, s, a, (u32x4 *)sink, nvec); break;
+    case 16: hipLaunchKernelGGL((read_chunk<16>), grid, block, 0, s, a, (u32x4 *)sink, nvec); break;
+    default: return -LFA_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
 
 // kind 0: read a; 1: read a and b; 2: write dst, nt; 3: write dst, sc1.
 // nvec 16-B vectors per operand, a multiple of the 16 KiB workgroup tile.

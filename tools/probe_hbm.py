@@ -103,5 +103,85 @@ def main() -> None:
     print(json.dumps({"probe_hbm_256mib": out}), flush=True)
 
 
+def _timed(fn, stream, torch, reps=100):
+    t0 = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < 0.3:
+        fn(i)
+        i += 1
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(3):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(reps):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        best = us if best is None else min(best, us)
+    return best
+
+
+def tree(nin: int = 8, block: int = 32 << 20) -> None:
+    """--tree: the N -> 1 fused tree (atomic.reduce_tree, the product body)
+    against what HBM gives its access mix, in two input layouts: separate
+    allocations, and the collective's slots (round_up(B, 256) + 6 KiB apart in
+    one allocation).  Per layout: the read side alone (nin
+    streams in the product's load shape, lfa__tune_read_n), the write side
+    alone (sc1, the product's store policy at this size), and the tree; the
+    prediction is (nin + 1) / (nin / R + 1 / W)."""
+    import ctypes
+    import torch
+    from libfabric_amd import _native, atomic
+    T = _native.lib("tune")
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream()
+    h = stream.cuda_stream
+    n = block // 4
+    nsets = max(4, -(-(1 << 30) // (nin * block)))
+    sink = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    outs = [torch.empty(n, device="cuda") for _ in range(nsets)]
+    pitch = (block + 255) // 256 * 256 + (6 << 10)
+    layouts = {
+        "separate": [[torch.rand(n, device="cuda") for _ in range(nin)] for _ in range(nsets)],
+        "slots": [],
+    }
+    slabs = []
+    for _ in range(nsets):
+        slab = torch.rand(nin * pitch // 4, device="cuda")
+        slabs.append(slab)
+        layouts["slots"].append([slab[k * pitch // 4: k * pitch // 4 + n] for k in range(nin)])
+    res = {"nin": nin, "block_mib": block >> 20, "sets": nsets}
+    for name, sets in layouts.items():
+        ptrs = [(ctypes.c_void_p * nin)(*[x.data_ptr() for x in s]) for s in sets]
+
+        def rd(i):
+            assert T.lfa__tune_read_n(ptrs[i % nsets], nin, sink.data_ptr(), block // 16, h) == 0
+
+        def wr(i):
+            assert T.lfa__tune_stream(3, outs[i % nsets].data_ptr(), None, None, block // 16,
+                                      h) == 0
+
+        def tr(i):
+            atomic.reduce_tree(2, 8, outs[i % nsets], sets[i % nsets], n, stream)
+        r_us, w_us, t_us = (_timed(f, stream, torch) for f in (rd, wr, tr))
+        R, W = nin * block / r_us / 1e6, block / w_us / 1e6
+        pred = (nin + 1) / (nin / R + 1 / W)
+        got = (nin + 1) * block / t_us / 1e6
+        res[name] = {"read_us": round(r_us, 2), "read_tb_s": round(R, 3),
+                     "write_us": round(w_us, 2), "write_tb_s": round(W, 3),
+                     "tree_us": round(t_us, 2), "tree_tb_s": round(got, 3),
+                     "tree_frac_of_8tbs": round(got / 8, 4),
+                     "mix_prediction_tb_s": round(pred, 3),
+                     "tree_vs_prediction": round(got / pred, 4)}
+    print(json.dumps({"probe_hbm_tree": res}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--tree" in sys.argv:
+        for k in (8, 2):
+            tree(k)
+    else:
+        main()
