@@ -1,0 +1,245 @@
+"""Random programs of collectives across processes (CPU, the C executor over
+an owner's tagged transport).
+
+Every rank draws the same program from one seed: three groups (the world and
+two joined over random subsets in random set order, so group ranks are set
+positions — coll_coll.c:669-689), then a few hundred operations, each naming
+a group, a collective, an algorithm, a datatype / op, a count (ragged, empty,
+fewer elements than members) and a root.  A rank issues the operations of
+the groups it belongs to, in program order, with up to DEPTH of them in
+flight at once, so operations of different groups interleave differently on
+different ranks while every group's members agree on its sequence — the tag
+(group_id << 16 | seq, coll_coll.c:37-52) is what keeps them apart.  Each
+result is checked against the oracle fed in the group's set order.
+
+The transport is MpXfer below: non-blocking tagged messages over one inbound
+queue per process, matched per (sender, tag) in post order with an
+unexpected-message list — the way rxm's tagged receive queue serves
+prov/coll (coll_coll.c:770-814).  (tests/gloo_xfer.py's transfers complete
+only in a blocking wait, which is fine for one operation at a time but not
+for several groups' operations in flight.)
+"""
+import collections
+import ctypes
+import queue as queue_mod
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BROADCAST, SCATTER, BARRIER = \
+    3, 5, 6, 4, 1, 7, 0
+PAIRS = [(2, 8), (3, 9), (0, 6), (1, 8), (6, 7), (7, 1), (9, 4), (4, 8), (3, 10), (5, 2)]
+DEPTH = 6
+
+
+class MpXfer:
+    """Tagged send / recv / test over multiprocessing queues (host bytes)."""
+
+    def __init__(self, rank, queues):
+        self.rank, self.queues = rank, queues
+        self.unexpected = collections.defaultdict(collections.deque)
+        self.posted = collections.defaultdict(collections.deque)
+        self.reqs, self.next = {}, 1
+
+    def _new(self, state):
+        h = self.next
+        self.next += 1
+        self.reqs[h] = state
+        return h
+
+    def send(self, peer, ptr, nbytes, tag):
+        self.queues[peer].put((self.rank, tag, ctypes.string_at(ptr, nbytes) if nbytes else b""))
+        return self._new({"done": True})
+
+    def _deliver(self, st, data):
+        assert len(data) == st["n"], (len(data), st["n"])
+        if st["n"]:
+            ctypes.memmove(st["ptr"], data, st["n"])
+        st["done"] = True
+
+    def recv(self, peer, ptr, nbytes, tag):
+        st = {"done": False, "ptr": ptr, "n": nbytes}
+        key = (peer, tag)
+        if self.unexpected[key]:
+            self._deliver(st, self.unexpected[key].popleft())
+        else:
+            self.posted[key].append(st)
+        return self._new(st)
+
+    def _pump(self):
+        while True:
+            try:
+                src, tag, data = self.queues[self.rank].get_nowait()
+            except queue_mod.Empty:
+                return
+            key = (src, tag)
+            if self.posted[key]:
+                self._deliver(self.posted[key].popleft(), data)
+            else:
+                self.unexpected[key].append(data)
+
+    def test(self, h):
+        if not self.reqs[h]["done"]:
+            self._pump()
+        if self.reqs[h]["done"]:
+            del self.reqs[h]
+            return 1
+        return 0
+
+
+def _program(world, seed, nops):
+    rng = np.random.default_rng(seed)
+    groups = [list(range(world))]
+    for _ in range(2):
+        k = int(rng.integers(1, world + 1))
+        groups.append([int(x) for x in rng.permutation(world)[:k]])
+    ops = []
+    for i in range(nops):
+        g = int(rng.integers(0, len(groups)))
+        coll = int(rng.choice([ALLREDUCE, ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER,
+                               BROADCAST, SCATTER, BARRIER]))
+        op, dt = PAIRS[int(rng.integers(0, len(PAIRS)))]
+        count = int(rng.choice([0, 1, 2, 3, 7, int(rng.integers(1, 3000))]))
+        ops.append(dict(i=i, g=g, coll=coll, op=op, dt=dt, count=count,
+                        root=int(rng.integers(0, len(groups[g]))),
+                        algo=int(rng.choice([0, 1, 3, 4])), seed=seed * 1000 + i))
+    return groups, ops
+
+
+def _data(oracle, o, members):
+    """Every member's input for operation o, in group-rank order."""
+    nd = oracle.DT_NP[o["dt"]]
+    rng = np.random.default_rng(o["seed"])
+    n = len(members)
+    cnt = o["count"] * (n if o["coll"] == SCATTER else 1)
+    if nd.kind == "f":
+        return [rng.uniform(0.9, 1.1, cnt).astype(nd) for _ in range(n)]
+    if nd.kind == "c":
+        return [rng.uniform(0.9, 1.1, 2 * cnt).astype(np.float32).view(nd) for _ in range(n)]
+    ii = np.iinfo(nd)
+    return [rng.integers(ii.min, ii.max, cnt, dtype=nd, endpoint=True) for _ in range(n)]
+
+
+def _submit(ep, coll, oracle, o, members, addr, pos):
+    """Issue operation o on this rank; returns (ctx, check) where check()
+    verifies the result once the operation has completed.  The buffers stay
+    referenced by check until then: the caller owns them until completion
+    (fi_collective.3; prov/coll reads and writes them during progress)."""
+    ctx, check, bufs = _issue(ep, coll, oracle, o, members, addr, pos)
+    return ctx, lambda: (check(), bufs)
+
+
+def _issue(ep, coll, oracle, o, members, addr, pos):
+    ep.set_algo(o["algo"])
+    n, c, root = len(members), o["count"], o["root"]
+    nd = oracle.DT_NP[o["dt"]]
+    ins = _data(oracle, o, members)
+    mine = ins[pos].copy()
+    kind = o["coll"]
+    if kind == BARRIER:
+        return ep.barrier(coll_addr=addr), lambda: None, ()
+    if kind in (ALLREDUCE, REDUCE_SCATTER, REDUCE):
+        want = oracle.allreduce(o["op"], o["dt"], ins)[0] if c else np.zeros(0, nd)
+        if kind == REDUCE_SCATTER:
+            off, ln = coll.block(c, n, pos)
+            res = np.zeros(max(ln, 1), nd)
+            ctx = ep.reduce_scatter(mine, res, c, o["dt"], o["op"], coll_addr=addr)
+            return ctx, lambda: _eq(res[:ln], want[off:off + ln], o), (mine, res)
+        res = np.zeros(max(c, 1), nd)
+        if kind == ALLREDUCE:
+            ctx = ep.allreduce(mine, res, c, o["dt"], o["op"], coll_addr=addr)
+            return ctx, lambda: _eq(res[:c], want, o), (mine, res)
+        ctx = ep.reduce(mine, res, c, root, o["dt"], o["op"], coll_addr=addr)
+        return ctx, (lambda: _eq(res[:c], want, o)) if pos == root else (lambda: None), \
+            (mine, res)
+    if kind == ALLGATHER:
+        res = np.zeros(max(n * c, 1), nd)
+        ctx = ep.allgather(mine, res, c, o["dt"], coll_addr=addr)
+        return ctx, lambda: _eq(res[:n * c], np.concatenate(ins) if c else res[:0], o), \
+            (mine, res)
+    if kind == BROADCAST:
+        buf = mine if pos == root else np.zeros(max(c, 1), nd)
+        ctx = ep.broadcast(buf, c, root, o["dt"], coll_addr=addr)
+        return ctx, lambda: _eq(buf[:c], ins[root][:c], o), (buf,)
+    # SCATTER: the root's buffer holds n blocks of c elements
+    res = np.zeros(max(c, 1), nd)
+    src = mine if pos == root else None
+    ctx = ep.scatter(src, res, c, root, o["dt"], coll_addr=addr)
+    return ctx, lambda: _eq(res[:c], ins[root][pos * c:(pos + 1) * c], o), (src, res)
+
+
+def _eq(got, want, o):
+    assert got.tobytes() == np.ascontiguousarray(want).tobytes(), f"operation {o}"
+
+
+def _worker(rank, world, queues, seed, nops, q):
+    try:
+        import oracle
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, MpXfer(rank, queues))
+        try:
+            groups, ops = _program(world, seed, nops)
+            addrs = [ep.world]
+            handles = []
+            for members in groups[1:]:
+                mc, _ = ep.join(members)
+                ep.wait_join()
+                handles.append(mc)
+                addrs.append(ep.mc_addr(mc))
+            inflight, done = [], set()
+            for o in ops:
+                members = groups[o["g"]]
+                if rank not in members:
+                    continue
+                pos = members.index(rank)
+                inflight.append(_submit(ep, coll, oracle, o, members, addrs[o["g"]], pos))
+                while len(inflight) > DEPTH or (inflight and inflight[0][0] in done):
+                    ctx, check = inflight[0]
+                    while ctx not in done:
+                        done.update(ep.cq_read())
+                    check()
+                    inflight.pop(0)
+            while inflight:
+                ctx, check = inflight.pop(0)
+                while ctx not in done:
+                    done.update(ep.cq_read())
+                check()
+            for mc in handles:
+                coll.lib().lfa_mc_close(mc)
+            # the algorithm is endpoint state that every member must agree
+            # on; each rank's last set_algo was its own last operation's
+            ep.set_algo(coll.ALGO_TREE)
+            ep.wait(ep.barrier())
+        finally:
+            ep.close()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,seed", [(2, 11), (3, 12), (4, 13), (5, 14), (6, 15), (3, 16)])
+def test_random_programs_across_processes(world, seed):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    queues = [ctx.Queue() for _ in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, queues, seed, 400, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            try:
+                r, msg = q.get(timeout=200)
+            except Exception:  # noqa: BLE001 — a rank hung: report the others
+                break
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
