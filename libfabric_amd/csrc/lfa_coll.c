@@ -36,8 +36,12 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "lfa_coll_int.h"
+
+
 
 /* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
  * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
@@ -709,11 +713,14 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 					continue;
 				}
 				h->issued = 1;
+				LFA_TRACE("hop cid %#x issued", (unsigned)h->r.cid);
 			}
 			last = h->out_ev ? h->out_ev : h->fin;
 			e = hipEventQuery(last);
-			if (e == hipSuccess)
+			if (e == hipSuccess) {
 				h->done = 1;
+				LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
+			}
 			else if (e != hipErrorNotReady &&
 				 lfa_hip_note(&h->r.hip_err, e, "completion event query"))
 				h->err = -LFA_EIO;
@@ -1129,7 +1136,8 @@ static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, int *why
 static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 		      const void *buf, void *result, size_t count, int root,
-		      enum lfa_datatype dt, enum lfa_op op, int dev);
+		      enum lfa_datatype dt, enum lfa_op op, int dev,
+		      enum lfa_coll_algo algo);
 
 /* A handshake collective of hop `h` on its reserved seq (host buffers). */
 static int sub_start(struct lfa_coll_ep *ep, struct hop *h, enum lfa_collective_op coll,
@@ -1142,8 +1150,15 @@ static int sub_start(struct lfa_coll_ep *ep, struct hop *h, enum lfa_collective_
 	h->sub = calloc(1, sizeof(*h->sub));
 	if (!h->sub)
 		return -LFA_ENOMEM;
-	ret = host_start(ep, h->sub, mc, coll, buf, result, count, -1, dt, op, 0);
+	/* a fixed schedule: the handshake starts from progress, at a different
+	 * point of each member's calls, so the endpoint's algorithm then (the
+	 * caller may have selected another for later operations) can differ
+	 * between members */
+	ret = host_start(ep, h->sub, mc, coll, buf, result, count, -1, dt, op, 0,
+			 LFA_ALGO_TREE);
 	h->sub->r.cid = (uint64_t)mc->group_id << 16 | seq;
+	LFA_TRACE("hop cid %#x handshake %d on cid %#x (mc seq now %u)", (unsigned)h->r.cid,
+		  (int)coll, (unsigned)h->sub->r.cid, (unsigned)mc->seq);
 	return ret;
 }
 
@@ -1187,6 +1202,8 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 			if (p && !p->done && !p->issued)
 				return 0;
 		}
+		LFA_TRACE("hop cid %#x prologue: prior hops done or issued, need %zu have %zu",
+			  (unsigned)h->r.cid, h->sym_need, mc->sym_region);
 		if (h->sym_need <= mc->sym_region)
 			break;
 		h->sym_size = sym_grow(mc, h->sym_need);
@@ -1205,6 +1222,8 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 		if (ret)
 			return ret;
 		h->phase = HOP_SYM_GATHER;
+		LFA_TRACE("hop cid %#x workspace gather started (seq %u)", (unsigned)h->r.cid,
+			  (unsigned)h->sub_seq);
 		return 0;
 	case HOP_SYM_GATHER:
 		ret = sub_advance(h);
@@ -1216,6 +1235,8 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 		if (ret)
 			return ret;
 		h->phase = HOP_SYM_AGREE;
+		LFA_TRACE("hop cid %#x workspace gathered, mapped=%d", (unsigned)h->r.cid,
+			  (int)h->agree_in);
 		return 0;
 	case HOP_SYM_AGREE:
 		ret = sub_advance(h);
@@ -1234,6 +1255,8 @@ agreed:
 	h->r.x.sym = mc->sym;
 	h->r.x.region = mc->sym_region;
 	h->phase = HOP_RUN;
+	LFA_TRACE("hop cid %#x runs on the workspace (%zu B)", (unsigned)h->r.cid,
+		  mc->sym_region);
 	return 0;
 }
 
@@ -1413,11 +1436,11 @@ static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
 static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		      enum lfa_collective_op coll, const void *buf, void *result,
 		      size_t count, int root, enum lfa_datatype dt,
-		      enum lfa_op op, hipStream_t s)
+		      enum lfa_op op, hipStream_t s, enum lfa_coll_algo algo)
 {
 	const struct plan *pl;
 	size_t esz = lfa_datatype_size(dt);
-	enum lfa_coll_algo algo = ep->algo;
+	const enum lfa_coll_algo asked = algo;
 	struct xctx x;
 	int ret;
 
@@ -1439,7 +1462,7 @@ replan:
 			return ret;
 		ret = p2p_ensure(mc, plan_sym_need(pl->steps, pl->nsteps, mc->size,
 						   count, esz));
-		if (ret && ep->algo == LFA_ALGO_AUTO && mc->p2p_state == 0) {
+		if (ret && asked == LFA_ALGO_AUTO && mc->p2p_state == 0) {
 			/* the members agreed (MIN over their flags, p2p_ensure)
 			 * that some member cannot map a peer's workspace: every
 			 * one of them runs the tree from now on */
@@ -1556,7 +1579,7 @@ static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		hipStreamWaitEvent(ep->stream, h2d[slot], 0);
 		ret = run_device(ep, mc, coll, din,
 				 coll == LFA_BROADCAST ? din : dout, c.dev_count,
-				 root, dt, op, ep->stream);
+				 root, dt, op, ep->stream, ep->algo);
 		hipEventRecord(comp[slot], ep->stream);
 		hipStreamWaitEvent(ep->d2h_stream, comp[slot], 0);
 		if (out)
@@ -1598,7 +1621,7 @@ static int run_device_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 				 &c) == 1; idx++)
 		ret = run_device(ep, mc, coll, buf ? (const char *)buf + c.src_off : NULL,
 				 result ? (char *)result + c.dst_off : NULL, c.dev_count,
-				 root, dt, op, ep->stream);
+				 root, dt, op, ep->stream, ep->algo);
 	return ret;
 }
 
@@ -1620,7 +1643,7 @@ static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	dout = din + ((in_bytes + 15) & ~(size_t)15);
 	if (buf && in_bytes)
 		hipMemcpyAsync(din, buf, in_bytes, hipMemcpyDefault, ep->stream);
-	ret = run_device(ep, mc, coll, din, dout, count, root, dt, op, ep->stream);
+	ret = run_device(ep, mc, coll, din, dout, count, root, dt, op, ep->stream, ep->algo);
 	if (!ret && result && out_bytes)
 		hipMemcpyAsync(result, dout, out_bytes, hipMemcpyDefault,
 			       ep->stream);
@@ -1657,9 +1680,9 @@ static int mc_member(const struct lfa_coll_mc *mc)
 static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
 		      const void *buf, void *result, size_t count, int root,
-		      enum lfa_datatype dt, enum lfa_op op, int dev)
+		      enum lfa_datatype dt, enum lfa_op op, int dev,
+		      enum lfa_coll_algo algo)
 {
-	enum lfa_coll_algo algo = ep->algo;
 	size_t esz = lfa_datatype_size(dt);
 	/* this operation's sequence number, taken before a P2P handshake below
 	 * draws the next ones */
@@ -1750,7 +1773,8 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		       enum lfa_collective_op coll, const void *buf,
 		       void *result, size_t count, int root,
 		       enum lfa_datatype dt, enum lfa_op op, void *context,
-		       int kind, struct lfa_coll_mc *jmc, int dev)
+		       int kind, struct lfa_coll_mc *jmc, int dev,
+		       enum lfa_coll_algo algo)
 {
 	struct hop *h = calloc(1, sizeof(*h));
 	const uint32_t t0 = mc->p2p_ticket;
@@ -1759,7 +1783,10 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	if (!h)
 		return -LFA_ENOMEM;
 	mc->seq++;                              /* coll_get_next_id :48-52 */
-	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op, dev);
+	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op, dev, algo);
+	LFA_TRACE("submit cid %#x coll %d count %zu dev %d algo %d phase %d sub_seq %u -> %d",
+		  (unsigned)h->r.cid, (int)coll, count, dev, (int)algo, h->phase,
+		  (unsigned)h->sub_seq, ret);
 	if (!ret)
 		ret = enqueue_host(ep, h, context, kind, jmc);
 	if (ret)
@@ -1804,7 +1831,7 @@ static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		const int last = off + n == count;
 		void *r = result ? (char *)result + off * esz : NULL;
 		int ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
-				      dt, op, context, last ? 0 : 3, NULL, dev);
+				      dt, op, context, last ? 0 : 3, NULL, dev, ep->algo);
 
 		if (ret)
 			return ret;     /* the chunks already queued run and reap */
@@ -1865,7 +1892,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 						  op, context, dev);
 		else
 			ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
-					  context, 0, NULL, dev);
+					  context, 0, NULL, dev, ep->algo);
 		pthread_mutex_unlock(&ep->lock);
 		return ret;
 	}
@@ -1891,7 +1918,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 					 chunk);
 	} else if (!host) {
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
-				 ep->stream);
+				 ep->stream, ep->algo);
 	} else if (chunkable) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op, chunk);
@@ -2015,7 +2042,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 			h->scratch[0] = ~(uint64_t)mc->rank;
 			mc->seq++;
 			ret = host_start(ep, h, mc, LFA_ALLREDUCE, &h->scratch[0],
-					 &h->scratch[1], 1, -1, LFA_UINT64, LFA_BAND, 0);
+					 &h->scratch[1], 1, -1, LFA_UINT64, LFA_BAND, 0, ep->algo);
 			if (!ret)
 				ret = enqueue_host(ep, h, context, 0, NULL);
 			if (ret)
@@ -2033,7 +2060,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	if (!ret)
 		ret = run_device(ep, mc, LFA_ALLREDUCE, ep->barrier_dev,
 				 (uint64_t *)ep->barrier_dev + 1, 1, -1, LFA_UINT64,
-				 LFA_BAND, ep->stream);
+				 LFA_BAND, ep->stream, ep->algo);
 	if (!ret)
 		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
 	if (!ret)
@@ -2248,7 +2275,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			ret = host_submit(ep, members_only ? mc : parent, LFA_ALLREDUCE,
 					  mc->mask_host + LFA_CID_BYTES, mc->mask_host,
 					  LFA_CID_BYTES, -1, LFA_UINT8, LFA_BAND,
-					  context, 1, mc, 0);
+					  context, 1, mc, 0, LFA_ALGO_TREE);
 		}
 	} else if (!ret) {
 		struct lfa_coll_mc *over = members_only ? mc : parent;
@@ -2264,9 +2291,11 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
 			hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
 				       hipMemcpyHostToDevice, ep->stream);
+			/* the join's own agreement: a fixed schedule, whatever
+			 * algorithm each member has selected for its collectives */
 			ret = run_device(ep, over, LFA_ALLREDUCE, dmask,
 					 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
-					 LFA_UINT8, LFA_BAND, ep->stream);
+					 LFA_UINT8, LFA_BAND, ep->stream, LFA_ALGO_TREE);
 			if (!ret)
 				hipMemcpyAsync(mc->mask_host, (char *)dmask + LFA_CID_BYTES,
 					       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);

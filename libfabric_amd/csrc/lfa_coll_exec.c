@@ -225,6 +225,7 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	a.ticket = r->x.ticket;
 	a.timeout_us = sig_timeout_us();
 	ret = lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
+	LFA_TRACE("cid %#x one-shot launched (epoch %u, rc %d)", (unsigned)r->cid, a.epoch, ret);
 	if (!ret) {
 		mc->os_epoch++;
 		mc->n_oneshot++;
@@ -420,6 +421,7 @@ static int pdev_post(struct xrun *r, const struct lfa_step *st, void **req)
 	if (st->type == LFA_STEP_SEND) {
 		/* the stream first: a zero-byte send is a barrier arrival and
 		 * must leave only after this rank's earlier items completed */
+		LFA_TRACE("cid %#x send to %d: stream sync", (unsigned)r->cid, st->peer);
 		if (lfa_hip_note(&r->hip_err, hipStreamSynchronize(r->stream),
 				 "send: stream sync") != hipSuccess ||
 		    (st->count &&

@@ -9,6 +9,10 @@
 
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -203,6 +207,23 @@ struct xrun {
  * completion's prov_errno, fi_cq_err_entry's provider-specific error) and,
  * with LFA_DEBUG set, name the call on stderr.  Returns the call's result.
  */
+/* LFA_TRACE=1: one stderr line per hop state change (diagnostics). */
+static int lfa_trace_on __attribute__((unused)) = -1;
+#define LFA_TRACE(...)                                                        \
+	do {                                                                  \
+		if (lfa_trace_on < 0)                                         \
+			lfa_trace_on = getenv("LFA_TRACE") != NULL;            \
+		if (lfa_trace_on) {                                           \
+			struct timespec ts_;                                  \
+			clock_gettime(CLOCK_MONOTONIC, &ts_);                 \
+			fprintf(stderr, "lfa-trace %ld.%06ld pid %d: ",      \
+				(long)ts_.tv_sec, ts_.tv_nsec / 1000,         \
+				(int)getpid());                               \
+			fprintf(stderr, __VA_ARGS__);                         \
+			fputc('\n', stderr);                                  \
+		}                                                             \
+	} while (0)
+
 LFA_INTERNAL hipError_t lfa_hip_note(int *slot, hipError_t e, const char *what);
 
 /* lfa_coll_exec.c */

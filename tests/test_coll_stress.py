@@ -21,7 +21,9 @@ for several groups' operations in flight.)
 """
 import collections
 import ctypes
+import os
 import queue as queue_mod
+import time
 
 import numpy as np
 import pytest
@@ -79,6 +81,15 @@ class MpXfer:
             else:
                 self.unexpected[key].append(data)
 
+    def pump(self):
+        self._pump()
+
+    def waiting(self):
+        return {(p, hex(t)): len(v) for (p, t), v in self.posted.items() if v}
+
+    def stray(self):
+        return {(p, hex(t)): len(v) for (p, t), v in self.unexpected.items() if v}
+
     def test(self, h):
         if not self.reqs[h]["done"]:
             self._pump()
@@ -103,7 +114,7 @@ def _program(world, seed, nops):
         count = int(rng.choice([0, 1, 2, 3, 7, int(rng.integers(1, 3000))]))
         ops.append(dict(i=i, g=g, coll=coll, op=op, dt=dt, count=count,
                         root=int(rng.integers(0, len(groups[g]))),
-                        algo=int(rng.choice([0, 1, 3, 4])), seed=seed * 1000 + i))
+                        algo=int(rng.choice([0, 1, 3, 4, 5])), seed=seed * 1000 + i))
     return groups, ops
 
 
@@ -121,21 +132,59 @@ def _data(oracle, o, members):
     return [rng.integers(ii.min, ii.max, cnt, dtype=nd, endpoint=True) for _ in range(n)]
 
 
-def _submit(ep, coll, oracle, o, members, addr, pos):
+class HostMem:
+    """Buffers in host memory (numpy)."""
+
+    @staticmethod
+    def put(a):
+        return np.ascontiguousarray(a).copy()
+
+    @staticmethod
+    def zeros(n, nd):
+        return np.zeros(max(n, 1), nd)
+
+    @staticmethod
+    def get(b, nd):
+        return b
+
+
+class DevMem:
+    """Buffers in HBM (torch byte tensors on cuda:0): the kernels' path."""
+
+    @staticmethod
+    def put(a):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to("cuda")
+        torch.cuda.synchronize()        # ready before the provider's stream reads it
+        return t
+
+    @staticmethod
+    def zeros(n, nd):
+        import torch
+        t = torch.zeros(max(n, 1) * nd.itemsize, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        return t
+
+    @staticmethod
+    def get(b, nd):
+        return b.cpu().numpy().view(nd)
+
+
+def _submit(ep, coll, oracle, o, members, addr, pos, mem=HostMem):
     """Issue operation o on this rank; returns (ctx, check) where check()
     verifies the result once the operation has completed.  The buffers stay
     referenced by check until then: the caller owns them until completion
     (fi_collective.3; prov/coll reads and writes them during progress)."""
-    ctx, check, bufs = _issue(ep, coll, oracle, o, members, addr, pos)
+    ctx, check, bufs = _issue(ep, coll, oracle, o, members, addr, pos, mem)
     return ctx, lambda: (check(), bufs)
 
 
-def _issue(ep, coll, oracle, o, members, addr, pos):
+def _issue(ep, coll, oracle, o, members, addr, pos, mem):
     ep.set_algo(o["algo"])
     n, c, root = len(members), o["count"], o["root"]
     nd = oracle.DT_NP[o["dt"]]
     ins = _data(oracle, o, members)
-    mine = ins[pos].copy()
+    mine = mem.put(ins[pos])
     kind = o["coll"]
     if kind == BARRIER:
         return ep.barrier(coll_addr=addr), lambda: None, ()
@@ -143,41 +192,59 @@ def _issue(ep, coll, oracle, o, members, addr, pos):
         want = oracle.allreduce(o["op"], o["dt"], ins)[0] if c else np.zeros(0, nd)
         if kind == REDUCE_SCATTER:
             off, ln = coll.block(c, n, pos)
-            res = np.zeros(max(ln, 1), nd)
+            res = mem.zeros(ln, nd)
             ctx = ep.reduce_scatter(mine, res, c, o["dt"], o["op"], coll_addr=addr)
-            return ctx, lambda: _eq(res[:ln], want[off:off + ln], o), (mine, res)
-        res = np.zeros(max(c, 1), nd)
+            return ctx, lambda: _eq(mem.get(res, nd)[:ln], want[off:off + ln], o), (mine, res)
+        res = mem.zeros(c, nd)
         if kind == ALLREDUCE:
             ctx = ep.allreduce(mine, res, c, o["dt"], o["op"], coll_addr=addr)
-            return ctx, lambda: _eq(res[:c], want, o), (mine, res)
+            return ctx, lambda: _eq(mem.get(res, nd)[:c], want, o), (mine, res)
         ctx = ep.reduce(mine, res, c, root, o["dt"], o["op"], coll_addr=addr)
-        return ctx, (lambda: _eq(res[:c], want, o)) if pos == root else (lambda: None), \
-            (mine, res)
+        return ctx, (lambda: _eq(mem.get(res, nd)[:c], want, o)) if pos == root else \
+            (lambda: None), (mine, res)
     if kind == ALLGATHER:
-        res = np.zeros(max(n * c, 1), nd)
+        res = mem.zeros(n * c, nd)
         ctx = ep.allgather(mine, res, c, o["dt"], coll_addr=addr)
-        return ctx, lambda: _eq(res[:n * c], np.concatenate(ins) if c else res[:0], o), \
-            (mine, res)
+        return ctx, lambda: _eq(mem.get(res, nd)[:n * c],
+                                np.concatenate(ins) if c else np.zeros(0, nd), o), (mine, res)
     if kind == BROADCAST:
-        buf = mine if pos == root else np.zeros(max(c, 1), nd)
+        buf = mine if pos == root else mem.zeros(c, nd)
         ctx = ep.broadcast(buf, c, root, o["dt"], coll_addr=addr)
-        return ctx, lambda: _eq(buf[:c], ins[root][:c], o), (buf,)
+        return ctx, lambda: _eq(mem.get(buf, nd)[:c], ins[root][:c], o), (buf,)
     # SCATTER: the root's buffer holds n blocks of c elements
-    res = np.zeros(max(c, 1), nd)
+    res = mem.zeros(c, nd)
     src = mine if pos == root else None
     ctx = ep.scatter(src, res, c, root, o["dt"], coll_addr=addr)
-    return ctx, lambda: _eq(res[:c], ins[root][pos * c:(pos + 1) * c], o), (src, res)
+    return ctx, lambda: _eq(mem.get(res, nd)[:c], ins[root][pos * c:(pos + 1) * c], o), \
+        (src, res)
 
 
 def _eq(got, want, o):
     assert got.tobytes() == np.ascontiguousarray(want).tobytes(), f"operation {o}"
 
 
-def _worker(rank, world, queues, seed, nops, q):
+def _worker(rank, world, queues, seed, nops, q, dev=False):
     try:
         import oracle
         from libfabric_amd import coll
-        ep = coll.HostEndpoint(rank, world, MpXfer(rank, queues))
+        mem = HostMem
+        if dev:
+            import torch
+            torch.cuda.set_device(0)
+            mem = DevMem
+        xf = MpXfer(rank, queues)
+        stall_s = float(os.environ.get("STRESS_STALL_S", "60"))
+        logdir = os.environ.get("STRESS_LOG_DIR")
+        logf = open(os.path.join(logdir, f"{'dev' if dev else 'host'}_w{world}_s{seed}_r{rank}.log"),
+                    "w", buffering=1) if logdir else None
+        if logf:
+            # the provider's LFA_TRACE lines (stderr) into the same file
+            os.dup2(logf.fileno(), 2)
+
+        def trace(*a):
+            if logf:
+                logf.write(f"{time.time():.3f} " + " ".join(str(x) for x in a) + "\n")
+        ep = coll.HostEndpoint(rank, world, xf, device=0 if dev else -1)
         try:
             groups, ops = _program(world, seed, nops)
             addrs = [ep.world]
@@ -188,23 +255,48 @@ def _worker(rank, world, queues, seed, nops, q):
                 handles.append(mc)
                 addrs.append(ep.mc_addr(mc))
             inflight, done = [], set()
+
+            def reap(ctx):
+                t0 = time.time()
+                trace("reap", ctx)
+                while ctx not in done:
+                    try:
+                        got = ep.cq_read()
+                    except Exception as e:  # noqa: BLE001
+                        trace("cq error", e)
+                        raise
+                    if got:
+                        trace("done", got)
+                    done.update(got)
+                    if time.time() - t0 > stall_s:
+                        xf.pump()
+                        if dev:
+                            trace("counters", [ep.counters(a) for a in addrs])
+                        raise TimeoutError(
+                            f"rank {rank}: op {ids[ctx]} stalled; in flight "
+                            f"{[ids[c] for c, _ in inflight]}; waiting recvs "
+                            f"{xf.waiting()}; unexpected {xf.stray()}")
+
+            ids = {}
             for o in ops:
                 members = groups[o["g"]]
                 if rank not in members:
                     continue
                 pos = members.index(rank)
-                inflight.append(_submit(ep, coll, oracle, o, members, addrs[o["g"]], pos))
+                ctx, check = _submit(ep, coll, oracle, o, members, addrs[o["g"]], pos, mem)
+                ids[ctx] = (o["i"], o["g"], o["coll"], o["algo"], o["count"])
+                trace("submit", ctx, ids[ctx])
+                inflight.append((ctx, check))
                 while len(inflight) > DEPTH or (inflight and inflight[0][0] in done):
                     ctx, check = inflight[0]
-                    while ctx not in done:
-                        done.update(ep.cq_read())
+                    reap(ctx)
                     check()
                     inflight.pop(0)
             while inflight:
-                ctx, check = inflight.pop(0)
-                while ctx not in done:
-                    done.update(ep.cq_read())
+                ctx, check = inflight[0]
+                reap(ctx)
                 check()
+                inflight.pop(0)
             for mc in handles:
                 coll.lib().lfa_mc_close(mc)
             # the algorithm is endpoint state that every member must agree
@@ -219,12 +311,11 @@ def _worker(rank, world, queues, seed, nops, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,seed", [(2, 11), (3, 12), (4, 13), (5, 14), (6, 15), (3, 16)])
-def test_random_programs_across_processes(world, seed):
+def _run(world, seed, nops, dev=False, timeout=200):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     queues = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_worker, args=(r, world, queues, seed, 400, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, queues, seed, nops, q, dev))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -232,13 +323,91 @@ def test_random_programs_across_processes(world, seed):
     try:
         for _ in range(world):
             try:
-                r, msg = q.get(timeout=200)
+                r, msg = q.get(timeout=timeout)
             except Exception:  # noqa: BLE001 — a rank hung: report the others
                 break
             results[r] = msg
     finally:
+        t_end = time.time() + 20
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=max(0.1, t_end - time.time()))
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=5)
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
+
+
+@pytest.mark.parametrize("world,seed", [(2, 11), (3, 12), (4, 13), (5, 14), (6, 15), (3, 16)])
+def test_random_programs_across_processes(world, seed):
+    _run(world, seed, 400)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,seed", [(2, 21), (3, 22), (4, 23), (5, 24)])
+def test_random_programs_gpu_peer_domains(world, seed):
+    """The same programs with DEVICE buffers on GPU peer domains (processes
+    sharing the GPU): every algorithm's kernels, transfers staged through
+    the owner's transport, and under P2P / AUTO the IPC workspaces, flag
+    barriers and one-shot kernels of three groups at once."""
+    _run(world, seed, 160, dev=True, timeout=100)
+
+
+def _join_worker(rank, world, queues, q):
+    try:
+        import oracle
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, MpXfer(rank, queues))
+        try:
+            # every member a different algorithm at join time: the join's own
+            # agreement (a BAND allreduce over the parent) must not follow it
+            ep.set_algo([coll.ALGO_RD, coll.ALGO_TREE, coll.ALGO_TREE_COLL][rank % 3])
+            members = [world - 1] + list(range(world - 1))
+            mc, _ = ep.join(members)
+            ep.wait_join()
+            ep.set_algo(coll.ALGO_RD)
+            rng = np.random.default_rng(3)
+            ins = [rng.uniform(0.9, 1.1, 1001).astype(np.float32) for _ in range(world)]
+            res = np.zeros(1001, np.float32)
+            pos = members.index(rank)
+            ep.wait(ep.allreduce(ins[pos], res, 1001, 8, 2, coll_addr=ep.mc_addr(mc)))
+            want = oracle.allreduce(2, 8, ins)[0]
+            assert res.tobytes() == want.tobytes()
+            coll.lib().lfa_mc_close(mc)
+        finally:
+            ep.close()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [3, 5])
+def test_join_agreement_ignores_selected_algorithm(world):
+    """The join's group-id agreement runs one fixed schedule (TREE) whatever
+    algorithm each member has selected for its own collectives; round 3 found
+    internal collectives — the join agreement and the P2P workspace
+    handshake, which starts from progress at a different point of each
+    member's calls — following the endpoint's current setting, which members
+    may hold differently at that moment (a hang when the schedules differ)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    queues = [ctx.Queue() for _ in range(world)]
+    procs = [ctx.Process(target=_join_worker, args=(r, world, queues, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            try:
+                r, msg = q.get(timeout=60)
+            except Exception:  # noqa: BLE001
+                break
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=10)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
