@@ -243,7 +243,17 @@ def _set_order(ep, rank, world, oracle, coll):
     ep.wait(ep.barrier())
 
 
+
+def _log_stderr(tag, rank, world):
+    """PEER_LOG_DIR set: this rank's stderr (LFA_DEBUG / LFA_TRACE lines) goes
+    to a file there, so a hung multi-process test leaves per-rank traces."""
+    d = os.environ.get("PEER_LOG_DIR")
+    if d:
+        f = open(os.path.join(d, f"{tag}_w{world}_r{rank}.log"), "w", buffering=1)
+        os.dup2(f.fileno(), 2)
+
 def _worker(rank, world, port, q):
+    _log_stderr("exec", rank, world)
     try:
         # LFA_DEBUG: a failing HIP call is named on stderr (and its code is
         # the completion's prov_errno)
@@ -287,7 +297,7 @@ def test_c_executor_gpu_kernels_across_processes(world):
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
@@ -358,7 +368,7 @@ def test_p2p_workspace_growth_in_flight():
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
@@ -440,7 +450,7 @@ def test_flag_barrier_timeout_is_an_error_completion():
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
@@ -542,7 +552,7 @@ def test_timeout_fails_that_operation_not_the_one_before():
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
@@ -657,7 +667,7 @@ def test_oneshot_ops_in_flight_mixed(world, seed, nops):
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
@@ -746,7 +756,7 @@ def test_oneshot_every_reducing_entry(world):
             results[r] = msg
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=5)
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if not str(results.get(r)).startswith("ok")}
