@@ -14,6 +14,7 @@ prov/coll's (the oracle) bit for bit, including when one member hands in
 host buffers and the others device buffers.  The oracle is only the checker.
 """
 import os
+import sys
 import queue
 import socket
 
@@ -270,7 +271,11 @@ def _worker(rank, world, port, q):
             if world > 1:
                 assert xfer.sent > 0 and xfer.received > 0
         finally:
+            if os.environ.get("PEER_LOG_DIR"):
+                sys.stderr.write(f"open fds before close: {len(os.listdir('/proc/self/fd'))}\n")
             ep.close()
+            if os.environ.get("PEER_LOG_DIR"):
+                sys.stderr.write(f"open fds after close: {len(os.listdir('/proc/self/fd'))}\n")
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok"))
