@@ -41,8 +41,6 @@
 
 #include "lfa_coll_int.h"
 
-
-
 /* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
  * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
 #define LFA_DEFAULT_CHUNK (32u << 20)
@@ -720,8 +718,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 			if (e == hipSuccess) {
 				h->done = 1;
 				LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
-			}
-			else if (e != hipErrorNotReady &&
+			} else if (e != hipErrorNotReady &&
 				 lfa_hip_note(&h->r.hip_err, e, "completion event query"))
 				h->err = -LFA_EIO;
 		} else if (ret) {

@@ -223,7 +223,7 @@ def _eq(got, want, o):
     assert got.tobytes() == np.ascontiguousarray(want).tobytes(), f"operation {o}"
 
 
-def _worker(rank, world, queues, seed, nops, q, dev=False):
+def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=0):
     try:
         import oracle
         from libfabric_amd import coll
@@ -231,7 +231,9 @@ def _worker(rank, world, queues, seed, nops, q, dev=False):
         if dev:
             import torch
             torch.cuda.set_device(0)
-            mem = DevMem
+            # host_rank: that member hands in host buffers on its GPU peer
+            # domain (staged), the others device buffers — one schedule
+            mem = HostMem if rank == host_rank else DevMem
         xf = MpXfer(rank, queues)
         stall_s = float(os.environ.get("STRESS_STALL_S", "60"))
         logdir = os.environ.get("STRESS_LOG_DIR")
@@ -245,6 +247,8 @@ def _worker(rank, world, queues, seed, nops, q, dev=False):
             if logf:
                 logf.write(f"{time.time():.3f} " + " ".join(str(x) for x in a) + "\n")
         ep = coll.HostEndpoint(rank, world, xf, device=0 if dev else -1)
+        if gchunk:
+            ep.set_group_chunk(gchunk)      # the same value on every member
         try:
             groups, ops = _program(world, seed, nops)
             addrs = [ep.world]
@@ -311,11 +315,12 @@ def _worker(rank, world, queues, seed, nops, q, dev=False):
         q.put((rank, traceback.format_exc()))
 
 
-def _run(world, seed, nops, dev=False, timeout=200):
+def _run(world, seed, nops, dev=False, timeout=200, host_rank=-1, gchunk=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     queues = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_worker, args=(r, world, queues, seed, nops, q, dev))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, queues, seed, nops, q, dev, host_rank, gchunk))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -351,6 +356,17 @@ def test_random_programs_gpu_peer_domains(world, seed):
     the owner's transport, and under P2P / AUTO the IPC workspaces, flag
     barriers and one-shot kernels of three groups at once."""
     _run(world, seed, 160, dev=True, timeout=100)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,seed,gchunk", [(3, 31, 0), (4, 32, 4000)])
+def test_random_programs_gpu_mixed_members(world, seed, gchunk):
+    """The same with rank 0 handing in HOST buffers on its GPU peer domain
+    while the others hand in device buffers (staged through device copies
+    under P2P, the host form of the schedule otherwise), and with a group
+    chunk on every member (P2P allreduce / reduce split into the same chunks
+    everywhere)."""
+    _run(world, seed, 160, dev=True, timeout=100, host_rank=0, gchunk=gchunk)
 
 
 def _join_worker(rank, world, queues, q):
