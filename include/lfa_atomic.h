@@ -88,6 +88,7 @@ int lfa_atomic_write_async(enum lfa_op op, enum lfa_datatype datatype,
  * recursive-doubling association for nsrc ranks (every pairwise step is
  * `higher-rank partial OP lower-rank partial`).  `srcs` is a HOST array of
  * DEVICE pointers; dst may alias any srcs[k].  1 <= nsrc <= LFA_TREE_MAX.
+ * Any byte offset: operands not aligned to the element are moved byte-wise.
  */
 #define LFA_TREE_MAX 32
 int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype datatype,
@@ -100,7 +101,10 @@ int lfa_reduce_tree_async(enum lfa_op op, enum lfa_datatype datatype,
  * store is system scope (sc0 sc1), so a peer ordered after this kernel (e.g.
  * by a stream-ordered barrier) reads the stored bytes.  `dsts`/`srcs` are
  * HOST arrays of device pointers; outputs must not alias inputs.
- * 1 <= nsrc <= LFA_TREE_MAX, 1 <= ndst <= LFA_PUT_MAX.
+ * 1 <= nsrc <= LFA_TREE_MAX, 1 <= ndst <= LFA_PUT_MAX.  An operand not aligned
+ * to the element is moved byte-wise with ordinary (device-scope) accesses, so
+ * it must be this GPU's own memory — in the P2P schedules only the caller's
+ * buffers can be; the peers' workspace slots are 256-B aligned.
  */
 #define LFA_PUT_MAX 32
 int lfa_reduce_tree_put_async(enum lfa_op op, enum lfa_datatype datatype,
