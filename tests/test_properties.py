@@ -248,6 +248,46 @@ def test_schedule_any_group(coll_op, algo, n, count, root_pick, pair, seed):
                       f"coll={coll_op} algo={algo} n={n} count={count} rank={r}")
 
 
+ALLGATHER, BROADCAST, SCATTER = 4, 1, 7
+
+
+@settings(max_examples=200, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(coll_op=st.sampled_from([ALLGATHER, BROADCAST, SCATTER]), n=st.integers(1, 9),
+       count=st.integers(0, 300), esz=st.sampled_from([1, 2, 4, 8, 16]),
+       root_pick=st.integers(0, 1 << 16), seed=st.integers(0, 2**31))
+def test_data_movement_schedules_any_group(coll_op, n, count, esz, root_pick, seed):
+    """allgather (rank blocks in group-rank order), broadcast (the root's
+    buffer everywhere) and scatter (block r of the root's buffer to rank r)
+    at drawn group sizes, counts, element sizes and roots, every rank's
+    schedule run by the host simulator (coll_do_allgather coll_coll.c:452,
+    coll_do_scatter :510, coll_ep_broadcast :1158)."""
+    dt = {1: 1, 2: 3, 4: 5, 8: 7, 16: 15}[esz]
+    rng = np.random.default_rng(seed)
+    root = root_pick % n
+    nb = count * esz
+    if coll_op == ALLGATHER:
+        sends = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(n)]
+        res = [np.zeros(n * nb, np.uint8) for _ in range(n)]
+        _plansim.run(coll_op, 0, n, -1, dt, 2, count, sends, res)
+        want = np.concatenate(sends) if nb else np.zeros(0, np.uint8)
+        for r in range(n):
+            assert res[r].tobytes() == want.tobytes(), (n, count, esz, r)
+    elif coll_op == BROADCAST:
+        bufs = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(n)]
+        want = bufs[root].copy()
+        _plansim.run(coll_op, 0, n, root, dt, 2, count, [None] * n, bufs)
+        for r in range(n):
+            assert bufs[r].tobytes() == want.tobytes(), (n, count, esz, r, root)
+    else:
+        big = rng.integers(0, 256, n * nb, dtype=np.uint8)
+        res = [np.zeros(nb, np.uint8) for _ in range(n)]
+        _plansim.run(coll_op, 0, n, root, dt, 2, count,
+                     [big if r == root else np.zeros(0, np.uint8) for r in range(n)], res)
+        for r in range(n):
+            assert res[r].tobytes() == big[r * nb:(r + 1) * nb].tobytes(), (n, count, r, root)
+
+
 # ---------------------------------------------------------------- GPU ----
 
 def _dev(buf, off, nbytes, torch):
