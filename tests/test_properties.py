@@ -507,3 +507,46 @@ def test_gpu_oneshot_misaligned_buffers(dt, mode, offs):
     for r in range(2):
         if want[r] is not None:
             assert_parity(dt, rd[r].cpu().numpy(), want[r], f"rank {r} mode {mode} offs {offs}")
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(coll_op=st.sampled_from([ALLGATHER, BROADCAST, SCATTER]), n=st.integers(1, 8),
+       count=st.one_of(st.integers(0, 500), st.integers(500, 100_000)),
+       esz=st.sampled_from([1, 2, 4, 8, 16]), soff=st.integers(0, 15), roff=st.integers(0, 15),
+       root_pick=st.integers(0, 1 << 16), seed=st.integers(0, 2**31))
+def test_gpu_data_movement_any_buffer_offset(coll_op, n, count, esz, soff, roff, root_pick,
+                                             seed):
+    """allgather / broadcast / scatter through the executor on the GPU
+    (lfa_coll_loopback) with the buffers at drawn byte offsets."""
+    import torch
+    dt = {1: 1, 2: 3, 4: 5, 8: 7, 16: 15}[esz]
+    rng = np.random.default_rng(seed)
+    root = root_pick % n
+    nb = count * esz
+    if coll_op == ALLGATHER:
+        sends = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(n)]
+        sd = [_dev(x, soff, nb, torch) for x in sends]
+        rd = [_dev(np.zeros(n * nb, np.uint8), roff, n * nb, torch) for _ in range(n)]
+        coll.loopback(coll_op, 0, n, -1, dt, 2, count, sd, rd)
+        torch.cuda.synchronize()
+        want = np.concatenate(sends) if nb else np.zeros(0, np.uint8)
+        for r in range(n):
+            assert np.array_equal(rd[r].cpu().numpy(), want), (n, count, esz, r)
+    elif coll_op == BROADCAST:
+        bufs = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(n)]
+        want = bufs[root].copy()
+        bd = [_dev(x, roff, nb, torch) for x in bufs]
+        coll.loopback(coll_op, 0, n, root, dt, 2, count, [None] * n, bd)
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert np.array_equal(bd[r].cpu().numpy(), want), (n, count, esz, r, root)
+    else:
+        big = rng.integers(0, 256, n * nb, dtype=np.uint8)
+        sd = [_dev(big if r == root else np.zeros(0, np.uint8), soff,
+                   n * nb if r == root else 0, torch) for r in range(n)]
+        rd = [_dev(np.zeros(nb, np.uint8), roff, nb, torch) for _ in range(n)]
+        coll.loopback(coll_op, 0, n, root, dt, 2, count, sd, rd)
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert np.array_equal(rd[r].cpu().numpy(), big[r * nb:(r + 1) * nb]), (n, count, r)
