@@ -550,3 +550,33 @@ def test_gpu_data_movement_any_buffer_offset(coll_op, n, count, esz, soff, roff,
         torch.cuda.synchronize()
         for r in range(n):
             assert np.array_equal(rd[r].cpu().numpy(), big[r * nb:(r + 1) * nb]), (n, count, r)
+
+
+@settings(max_examples=300, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(kind=st.sampled_from([ALLREDUCE, REDUCE, REDUCE_SCATTER]), n=st.integers(1, 9),
+       per=st.integers(1, 3000), chunk=st.integers(8, 1 << 16), root_pick=st.integers(0, 99),
+       seed=st.integers(0, 2**31))
+def test_host_chunk_geometry_any_shape(kind, n, per, chunk, root_pick, seed):
+    """lfa_coll_host_chunk's staging geometry (the host-buffer pipeline and
+    the group chunk) at drawn collective, group size, count and chunk bytes:
+    replayed on numpy (tests/test_coll_plan.py::_stage_and_run) every element
+    is covered once and every rank ends with exactly its part of the sum."""
+    from tests.test_coll_plan import _stage_and_run
+    esz = 8
+    count = n * per if kind == REDUCE_SCATTER else per
+    root = root_pick % n
+    rng = np.random.default_rng(seed)
+    bufs = [rng.integers(-2**40, 2**40, count) for _ in range(n)]
+    res, covered = _stage_and_run(kind, bufs, count, n, esz, chunk, root=root)
+    total = np.sum(bufs, axis=0)
+    if kind == REDUCE_SCATTER:
+        assert covered == per
+        for r in range(n):
+            off, ln = coll.block(count, n, r)
+            assert np.array_equal(res[r], total[off:off + ln])
+    else:
+        assert covered == count
+        for r in range(n):
+            if kind == ALLREDUCE or r == root:
+                assert np.array_equal(res[r], total)
