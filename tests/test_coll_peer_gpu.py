@@ -245,6 +245,19 @@ def _set_order(ep, rank, world, oracle, coll):
 
 
 
+
+def _share_gpu(world):
+    """Before this process's first HIP call: with more than 4 processes on
+    the one GPU, 2 hardware queues each instead of the default 4.  Past the
+    scheduler's queue slots the GPU time-slices the processes' queues, and a
+    one-shot kernel waiting for a peer whose queue is not mapped waits out a
+    quantum: 8 processes took 10-26 ms per 4 KiB allreduce with 4 queues each
+    and 0.1-0.2 ms with 2 (tools/probe_p2p_latency.py) —
+    slow enough to time tests out.  One process per GPU (the product's
+    layout) never meets this."""
+    if world > 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"
+
 def _log_stderr(tag, rank, world):
     """PEER_LOG_DIR set: this rank's stderr (LFA_DEBUG / LFA_TRACE lines) goes
     to a file there, so a hung multi-process test leaves per-rank traces."""
@@ -259,6 +272,7 @@ def _worker(rank, world, port, q):
         # LFA_DEBUG: a failing HIP call is named on stderr (and its code is
         # the completion's prov_errno)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
@@ -312,6 +326,7 @@ def test_c_executor_gpu_kernels_across_processes(world):
 def _growth_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
@@ -384,6 +399,7 @@ def _timeout_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                           LFA_SIG_TIMEOUT_MS="300")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
@@ -466,6 +482,7 @@ def _timeout_queue_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                           LFA_SIG_TIMEOUT_MS="300")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
@@ -567,6 +584,7 @@ def test_timeout_fails_that_operation_not_the_one_before():
 def _oneshot_stream_worker(rank, world, port, q, seed=77, nops=48):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import oracle
@@ -682,6 +700,7 @@ def test_oneshot_ops_in_flight_mixed(world, seed, nops):
 def _every_entry_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import json as _json

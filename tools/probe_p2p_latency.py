@@ -37,6 +37,8 @@ def _worker(rank, world, port, reps, q):
         import torch
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if world > 4 and "GPU_MAX_HW_QUEUES" not in os.environ:
+            os.environ["GPU_MAX_HW_QUEUES"] = "2"   # queue slots
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from gloo_xfer import GlooXfer
