@@ -256,7 +256,7 @@ def _share_gpu(world):
     slow enough to time tests out.  One process per GPU (the product's
     layout) never meets this."""
     if world > 4:
-        os.environ["GPU_MAX_HW_QUEUES"] = "2"
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LFA_TEST_HW_QUEUES", "2")
 
 def _log_stderr(tag, rank, world):
     """PEER_LOG_DIR set: this rank's stderr (LFA_DEBUG / LFA_TRACE lines) goes
