@@ -1195,6 +1195,12 @@ def extra_collectives(rank, world, stream, emit=None):
                     ep.wait(ep.allreduce(a, b, 1024, 8, 2))
                 t = max_over_ranks(time.perf_counter() - t0, world) / 200
                 out[name] = round(t * 1e6, 1)
+                # the same loop timed in C (liblfa_bench.so): what a C caller
+                # of fi_allreduce + fi_cq_read sees, without the Python
+                # wrapper's ~10 us per call
+                barrier(world)
+                c_us = max_over_ranks(ep.bench_loop(3, a, b, 1024, 8, 2, reps=200), world)
+                out[name.replace("_us", "_c_loop_us")] = round(c_us, 1)
                 if algo == coll.ALGO_TREE:
                     ref4k = b.clone()
                 elif algo == coll.ALGO_P2P and world > 1:

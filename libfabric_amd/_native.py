@@ -12,7 +12,8 @@ import torch  # noqa: F401  (must precede the CDLL loads below)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 _LIBS = {"lfa": "liblfa.so", "coll": "liblfa_coll.so",
-         "tune": "liblfa_tune.so"}   # tuning forms: bench.py --tune* only
+         "tune": "liblfa_tune.so",    # tuning forms: bench.py --tune* only
+         "bench": "liblfa_bench.so"}  # C latency loop: bench.py only
 _loaded = {}
 
 
@@ -100,10 +101,18 @@ def lib(name: str = "lfa") -> ctypes.CDLL:
             "(there is no CPU fallback for the combine path)")
     if name == "coll":
         lib("lfa")
+    if name == "bench":
+        lib("coll")
     L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     if name == "lfa":
         _bind_lfa(L)
     elif name == "tune":
         _bind_tune(L)
+    elif name == "bench":
+        c = ctypes
+        L.lfa_bench_loop.restype = c.c_int
+        L.lfa_bench_loop.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_size_t,
+                                     c.c_int, c.c_int, c.c_int, c.c_uint64, c.c_int, c.c_int,
+                                     c.POINTER(c.c_double)]
     _loaded[name] = L
     return L

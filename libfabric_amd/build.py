@@ -132,6 +132,25 @@ def build_coll(verbose: bool = False) -> str | None:
     return LIB_COLL
 
 
+LIB_BENCH = os.path.join(PKG, "liblfa_bench.so")
+
+
+def build_bench(verbose: bool = False) -> str | None:
+    """liblfa_bench.so: bench-only C helpers (lfa_bench_loop), linked to the
+    provider; never loaded by the product path."""
+    src = os.path.join(CSRC, "lfa_bench.c")
+    if not os.path.exists(src):
+        return None
+    if _newer(LIB_BENCH, [src, os.path.join(INC, "lfa_coll.h"), LIB_COLL]):
+        _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
+              "-Wno-unused-parameter", "-I" + INC, "-shared", "-o", LIB_BENCH, src,
+              "-L" + PKG, "-llfa_coll", "-Wl,-rpath,$ORIGIN",
+              "-Wl,-soname,liblfa_bench.so"])
+        if verbose:
+            print(f"built {LIB_BENCH}")
+    return LIB_BENCH
+
+
 EXAMPLE = os.path.join(ROOT, "examples", "c_drop_in")
 
 
@@ -201,6 +220,7 @@ def build_off_lfa(verbose: bool = False) -> str | None:
 def build_all(verbose: bool = False) -> None:
     build_lfa(verbose=verbose)
     build_coll(verbose=verbose)
+    build_bench(verbose=verbose)
     build_example(verbose=verbose)
     build_off_lfa(verbose=verbose)
 

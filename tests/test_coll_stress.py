@@ -432,3 +432,62 @@ def test_join_agreement_ignores_selected_algorithm(world):
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
     assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
+
+
+def _bench_loop_worker(rank, world, queues, q):
+    try:
+        import oracle
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, MpXfer(rank, queues))
+        try:
+            rng = np.random.default_rng(9)
+            ins = [rng.uniform(0.9, 1.1, 1024).astype(np.float32) for _ in range(world)]
+            want = oracle.allreduce(2, 8, ins)[0]
+            res = np.zeros(1024, np.float32)
+            for algo in (coll.ALGO_TREE, coll.ALGO_RD):
+                ep.set_algo(algo)
+                us = ep.bench_loop(3, ins[rank], res, 1024, 8, 2, reps=50)
+                assert us > 0 and res.tobytes() == want.tobytes(), (algo, us)
+                off, ln = coll.block(1024, world, rank)
+                rs = np.zeros(ln, np.float32)
+                ep.bench_loop(5, ins[rank], rs, 1024, 8, 2, reps=20)
+                assert rs.tobytes() == want[off:off + ln].tobytes()
+                rr = np.zeros(1024, np.float32)
+                ep.bench_loop(6, ins[rank], rr, 1024, 8, 2, root=world - 1, reps=20)
+                if rank == world - 1:
+                    assert rr.tobytes() == want.tobytes()
+        finally:
+            ep.close()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_bench_c_loop_across_processes():
+    """bench.py's C-timed latency loop (liblfa_bench.so lfa_bench_loop):
+    allreduce / reduce_scatter / reduce submitted and reaped in C across 3
+    processes, results equal to the oracle."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    queues = [ctx.Queue() for _ in range(world)]
+    procs = [ctx.Process(target=_bench_loop_worker, args=(r, world, queues, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            try:
+                r, msg = q.get(timeout=60)
+            except Exception:  # noqa: BLE001
+                break
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
