@@ -10,7 +10,8 @@ the same domain, whose transfers go through the owner's (gloo) transport.
 Not xGMI: the peers' workspaces are this GPU's own HBM.
 
   python tools/probe_p2p_latency.py [--world 2] [--reps 300]
-prints one JSON line (median / p10 / p90 us per allreduce, per size).
+prints one JSON line (median / p10 / p90 us per allreduce, per size, Python-timed;
+c_loop_mean_us: the same operations submitted and reaped in C).
 """
 import argparse
 import json
@@ -80,6 +81,13 @@ def _worker(rank, world, port, reps, q):
                         "median_us": round(statistics.median(ts) * 1e6, 1),
                         "p10_us": round(ts[len(ts) // 10] * 1e6, 1),
                         "p90_us": round(ts[9 * len(ts) // 10] * 1e6, 1), "reps": n}
+                    # the same operation submitted and reaped in C
+                    # (liblfa_bench.so): the provider path without Python
+                    dist.barrier()
+                    kind = 5 if name == "p2p_rs" else 3
+                    dt_, op_ = (9, 3) if name == "p2p_rs" else (8, 2)
+                    out[f"{name}_{nbytes}"]["c_loop_mean_us"] = round(
+                        ep.bench_loop(kind, x, r, cnt, dt_, op_, reps=n), 1)
         finally:
             ep.close()
         dist.barrier()
