@@ -580,3 +580,65 @@ def test_host_chunk_geometry_any_shape(kind, n, per, chunk, root_pick, seed):
         for r in range(n):
             if kind == ALLREDUCE or r == root:
                 assert np.array_equal(res[r], total)
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(kind=st.sampled_from([ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BROADCAST, SCATTER]),
+       algo=st.sampled_from([0, 1, 2, 3, 4, 5]), pair=st.sampled_from(SCHED_PAIRS),
+       count=st.one_of(st.integers(0, 3000), st.integers(3000, 300_000)),
+       host=st.booleans(), gchunk=st.sampled_from([0, 0, 4096, 1 << 20]),
+       off=st.sampled_from([0, 0, 16, 4, 1]), seed=st.integers(0, 2**31))
+def test_gpu_rccl_domain_world1_any_call(ep1, kind, algo, pair, count, host, gchunk, off,
+                                         seed):
+    """The RCCL device domain at world size 1 (every collective is a copy of
+    the caller's data): each submit path — device buffers in place, host
+    buffers staged whole or in chunks, a group chunk, every algorithm, byte
+    offsets — returns the input where the reference's one-rank collective
+    does."""
+    import torch
+    ep = ep1
+    op, dt = pair
+    esz = oracle.datatype_size(dt)
+    rng = np.random.default_rng(seed)
+    nb = count * esz
+    data = _operand(dt, count * (1 if kind != SCATTER else 1), rng, 0.05)
+    ep.set_algo(algo)
+    ep.set_group_chunk(gchunk)
+    try:
+        if host:
+            src = _at(data, off, nb)
+            dst = _at(np.zeros(nb, np.uint8), (off + 3) % 16, nb)
+            get = lambda b: b.copy()                                     # noqa: E731
+        else:
+            src = _dev(data, off, nb, torch)
+            dst = _dev(np.zeros(nb, np.uint8), (off + 3) % 16, nb, torch)
+            get = lambda b: b.cpu().numpy()                              # noqa: E731
+            torch.cuda.synchronize()
+        if kind == ALLREDUCE:
+            ctx = ep.allreduce(src, dst, count, dt, op)
+        elif kind == REDUCE_SCATTER:
+            ctx = ep.reduce_scatter(src, dst, count, dt, op)
+        elif kind == REDUCE:
+            ctx = ep.reduce(src, dst, count, 0, dt, op)
+        elif kind == ALLGATHER:
+            ctx = ep.allgather(src, dst, count, dt)
+        elif kind == SCATTER:
+            ctx = ep.scatter(src, dst, count, 0, dt)
+        else:
+            ctx = ep.broadcast(src, count, 0, dt)
+            dst = src
+        ep.wait(ctx, timeout_s=60)
+        got = get(dst)
+        assert got.tobytes() == data.tobytes(), (kind, algo, count, host, gchunk, off)
+    finally:
+        ep.set_group_chunk(0)
+
+
+@pytest.fixture(scope="module")
+def ep1():
+    """One RCCL device-domain endpoint at world size 1 for the module."""
+    from libfabric_amd import coll as c
+    ep = c.Endpoint(0, 1, 0, c.Endpoint.unique_id())
+    yield ep
+    ep.close()
