@@ -36,13 +36,25 @@ DEPTH = 6
 
 
 class MpXfer:
-    """Tagged send / recv / test over multiprocessing queues (host bytes)."""
+    """Tagged send / recv / test over multiprocessing queues (host bytes).
+    refuse_every = k: every k-th post is refused with TransportAgain (the
+    owner's queue full, -FI_EAGAIN), which the provider must retry later
+    (coll_coll.c:845-852)."""
 
-    def __init__(self, rank, queues):
+    def __init__(self, rank, queues, refuse_every=0):
         self.rank, self.queues = rank, queues
         self.unexpected = collections.defaultdict(collections.deque)
         self.posted = collections.defaultdict(collections.deque)
         self.reqs, self.next = {}, 1
+        self.refuse_every, self.posts, self.refused = refuse_every, 0, 0
+
+    def _gate(self):
+        if self.refuse_every:
+            self.posts += 1
+            if self.posts % self.refuse_every == 0:
+                from libfabric_amd.coll import TransportAgain
+                self.refused += 1
+                raise TransportAgain()
 
     def _new(self, state):
         h = self.next
@@ -51,6 +63,7 @@ class MpXfer:
         return h
 
     def send(self, peer, ptr, nbytes, tag):
+        self._gate()
         self.queues[peer].put((self.rank, tag, ctypes.string_at(ptr, nbytes) if nbytes else b""))
         return self._new({"done": True})
 
@@ -61,6 +74,7 @@ class MpXfer:
         st["done"] = True
 
     def recv(self, peer, ptr, nbytes, tag):
+        self._gate()
         st = {"done": False, "ptr": ptr, "n": nbytes}
         key = (peer, tag)
         if self.unexpected[key]:
@@ -223,7 +237,8 @@ def _eq(got, want, o):
     assert got.tobytes() == np.ascontiguousarray(want).tobytes(), f"operation {o}"
 
 
-def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=0):
+def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=0,
+            refuse_every=0):
     try:
         import oracle
         from libfabric_amd import coll
@@ -238,7 +253,7 @@ def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=
             # host_rank: that member hands in host buffers on its GPU peer
             # domain (staged), the others device buffers — one schedule
             mem = HostMem if rank == host_rank else DevMem
-        xf = MpXfer(rank, queues)
+        xf = MpXfer(rank, queues, refuse_every)
         stall_s = float(os.environ.get("STRESS_STALL_S", "60"))
         logdir = os.environ.get("STRESS_LOG_DIR")
         logf = open(os.path.join(logdir, f"{'dev' if dev else 'host'}_w{world}_s{seed}_r{rank}.log"),
@@ -305,6 +320,8 @@ def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=
                 reap(ctx)
                 check()
                 inflight.pop(0)
+            if refuse_every and world > 1:
+                assert xf.refused > 0, "no post was refused"
             for mc in handles:
                 coll.lib().lfa_mc_close(mc)
             # the algorithm is endpoint state that every member must agree
@@ -319,12 +336,14 @@ def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=
         q.put((rank, traceback.format_exc()))
 
 
-def _run(world, seed, nops, dev=False, timeout=200, host_rank=-1, gchunk=0):
+def _run(world, seed, nops, dev=False, timeout=200, host_rank=-1, gchunk=0,
+         refuse_every=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     queues = [ctx.Queue() for _ in range(world)]
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, queues, seed, nops, q, dev, host_rank, gchunk))
+                         args=(r, world, queues, seed, nops, q, dev, host_rank, gchunk,
+                               refuse_every))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -350,6 +369,14 @@ def _run(world, seed, nops, dev=False, timeout=200, host_rank=-1, gchunk=0):
 @pytest.mark.parametrize("world,seed", [(2, 11), (3, 12), (4, 13), (5, 14), (6, 15), (3, 16)])
 def test_random_programs_across_processes(world, seed):
     _run(world, seed, 400)
+
+
+@pytest.mark.parametrize("world,seed,every", [(3, 41, 3), (4, 42, 7)])
+def test_random_programs_with_transport_pushback(world, seed, every):
+    """The same programs while the owner refuses every k-th send / receive
+    post with -FI_EAGAIN: the provider re-posts it on a later progress call
+    (coll_coll.c:845-852) and every result stays exact."""
+    _run(world, seed, 300, refuse_every=every)
 
 
 @pytest.mark.gpu
