@@ -400,6 +400,13 @@ def test_random_programs_gpu_mixed_members(world, seed, gchunk):
     _run(world, seed, 160, dev=True, timeout=100, host_rank=0, gchunk=gchunk)
 
 
+@pytest.mark.gpu
+def test_random_programs_gpu_with_transport_pushback():
+    """GPU peer domains (device buffers, staged transfers, P2P workspaces)
+    while the owner refuses every 5th post with -FI_EAGAIN."""
+    _run(3, 51, 160, dev=True, timeout=100, refuse_every=5)
+
+
 def _join_worker(rank, world, queues, q):
     try:
         import oracle
