@@ -12,6 +12,9 @@
  *                                             on device and host buffers,
  *                                             completions through the owner,
  *                                             subset join (world size 1)
+ *   off_lfa_host <provider.so> avset          av_set union / intersect /
+ *                                             diff on sets read from stdin,
+ *                                             result order printed (CPU)
  *
  * Sequence mirrored from rxm: rxm_fabric.c:85-121 (getinfo with
  * FI_PEER_TRANSFER, fi_fabric), rxm_domain.c:944-953 (fi_domain2 FI_PEER),
@@ -258,6 +261,82 @@ static int wait_join(struct fid_ep *ep, struct fid_mc *mc, void *ctx)
 typedef struct fi_provider *(*ini_fn)(void);
 typedef void (*freeinfo_fn)(struct fi_info *);
 
+/* An av_set holding exactly `a[0..n)` in that order: an empty set (start =
+ * end = FI_ADDR_NOTAVAIL, coll_av_set.c:255-262), then inserts. */
+static struct fid_av_set *ordered_set(struct fid_av *av, const fi_addr_t *a, int n)
+{
+	struct fi_av_set_attr sattr = { 0 };
+	struct fid_av_set *s = NULL;
+
+	sattr.count = 64;
+	sattr.start_addr = FI_ADDR_NOTAVAIL;
+	sattr.end_addr = FI_ADDR_NOTAVAIL;
+	CHECK_RC(fi_av_set(av, &sattr, &s, NULL), 0);
+	for (int i = 0; s && i < n; i++)
+		CHECK_RC(fi_av_set_insert(s, a[i]), 0);
+	return s;
+}
+
+/*
+ * avset mode: a batch of set operations read from stdin, one per line,
+ *   <op> <nd> d0 .. d(nd-1) <ns> s0 .. s(ns-1)      op: u | i | d
+ * builds dst and src in those orders, applies union / intersect / diff
+ * (dst op= src) and prints "<rc> <count> <addresses in dst's order>".  The
+ * fi_av_set API has no call that lists a set, so the order is read through
+ * the provider's exported test accessor off_lfa_test_set_order (the order a
+ * join would number the members by).
+ */
+typedef long (*set_order_fn)(struct fid_av_set *, fi_addr_t *, size_t);
+
+static int avset_batch(void *dl, struct fid_av *av)
+{
+	set_order_fn order = (set_order_fn)dlsym(dl, "off_lfa_test_set_order");
+	char op;
+	int nd, ns, lines = 0;
+
+	if (!order) {
+		fprintf(stderr, "off_lfa_test_set_order missing\n");
+		return 1;
+	}
+	while (scanf(" %c %d", &op, &nd) == 2) {
+		fi_addr_t d[64], s[64], out[64];
+		struct fid_av_set *ds, *ss;
+		long n;
+		int rc = -1;
+
+		if (nd < 0 || nd > 64)
+			return 1;
+		for (int i = 0; i < nd; i++)
+			if (scanf("%lu", (unsigned long *)&d[i]) != 1)
+				return 1;
+		if (scanf("%d", &ns) != 1 || ns < 0 || ns > 64)
+			return 1;
+		for (int i = 0; i < ns; i++)
+			if (scanf("%lu", (unsigned long *)&s[i]) != 1)
+				return 1;
+		ds = ordered_set(av, d, nd);
+		ss = ordered_set(av, s, ns);
+		if (!ds || !ss)
+			return 1;
+		if (op == 'u')
+			rc = fi_av_set_union(ds, ss);
+		else if (op == 'i')
+			rc = fi_av_set_intersect(ds, ss);
+		else if (op == 'd')
+			rc = fi_av_set_diff(ds, ss);
+		n = order(ds, out, 64);
+		printf("%d %ld", rc, n);
+		for (long i = 0; i < n; i++)
+			printf(" %lu", (unsigned long)out[i]);
+		printf("\n");
+		fi_close(&ss->fid);
+		fi_close(&ds->fid);
+		lines++;
+	}
+	fflush(stdout);
+	return failures ? 1 : 0;
+}
+
 int main(int argc, char **argv)
 {
 	void *dl;
@@ -286,7 +365,7 @@ int main(int argc, char **argv)
 	size_t len;
 
 	if (argc < 3) {
-		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> cpu|gpu [manual]\n", argv[0]);
+		fprintf(stderr, "usage: %s <liboff_lfa-fi.so> cpu|gpu|avset [manual]\n", argv[0]);
 		return 2;
 	}
 	gpu = !strcmp(argv[2], "gpu");
@@ -372,6 +451,10 @@ int main(int argc, char **argv)
 	ectx.eq = &own.eq;
 	eq_attr.flags = FI_PEER;
 	CHECK_RC(fi_eq_open(fabric, &eq_attr, &eq, &ectx), 0);
+	if (!strcmp(argv[2], "avset")) {
+		own.nranks = 64;
+		return failures ? 1 : avset_batch(dl, av);
+	}
 
 	/* endpoint with a peer transfer context (coll_ep.c:116-170) */
 	memset(&tctx, 0, sizeof(tctx));

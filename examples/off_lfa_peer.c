@@ -871,6 +871,40 @@ static void ordered_sets(struct fid_av *av, struct fid_ep *ep, struct fid_mc *wo
 	fi_close(&zero->fid);
 	fi_close(&b->fid);
 	fi_close(&a->fid);
+
+	/* C = the world in descending order (empty set + inserts) intersected
+	 * with [0, 2, 1] (N >= 5), [0, 1] (N = 3, 4) or [0]: coll_av_set.c:71-96
+	 * leaves the
+	 * common addresses in SRC's order, so group rank k is src[k], not the
+	 * k-th address of dst's order */
+	{
+		struct fid_av_set *c, *csrc;
+		struct fid_mc *gc;
+		fi_addr_t src[3] = { 0, 2, 1 };
+		size_t ns = nranks >= 5 ? 3 : (nranks >= 3 ? 2 : 1);
+
+		if (ns == 2)
+			src[1] = 1;
+		sattr.start_addr = FI_ADDR_NOTAVAIL;
+		sattr.end_addr = FI_ADDR_NOTAVAIL;
+		CHECK(fi_av_set(av, &sattr, &c, NULL) == 0, "set C");
+		CHECK(fi_av_set(av, &sattr, &csrc, NULL) == 0, "set C src");
+		for (int r = nranks - 1; r >= 0; r--)
+			CHECK(fi_av_set_insert(c, (fi_addr_t)r) == 0, "C insert %d", r);
+		for (size_t k = 0; k < ns; k++)
+			CHECK(fi_av_set_insert(csrc, src[k]) == 0, "C src insert");
+		CHECK(fi_av_set_intersect(c, csrc) == 0, "intersect");
+		for (n = 0; n < ns; n++)
+			order[n] = src[n];
+		dump("setC", "order", order, n * sizeof(fi_addr_t));
+		CHECK(fi_join_collective(ep, fi_mc_addr(world_mc), c, 0, &gc, &req[0]) == 0,
+		      "join C");
+		wait_join(gc);
+		ordered_group(ep, gc, "setC", order, n);
+		fi_close(&gc->fid);
+		fi_close(&csrc->fid);
+		fi_close(&c->fid);
+	}
 }
 
 static int run_rank(const char *prov_path)

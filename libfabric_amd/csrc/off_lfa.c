@@ -1598,14 +1598,26 @@ static int olfa_set_grow(struct olfa_av_set *s, size_t need)
  * (coll_av_set.c:35-164).  The ORDER they leave matters: it numbers the
  * members of a group joined over the set (olfa_join).  insert and union
  * append, remove moves the last address into the hole (:149-164).
- * intersect keeps dst's order; diff removes src's addresses one by one, in
- * src's order, exactly as remove would.  The reference's own intersect and
- * diff lose members in some cases — intersect drops a common address whose
- * order in src differs from dst's ({a,b,c,d} ∩ {c,a} = {c}), diff writes the
- * found address over the last one instead of moving the last into the hole
- * ({a,b,c,d} \ {b} = {a,b,c}) — so these follow the evident intent; they
- * give the reference's result wherever the reference keeps every member
- * (tests/test_off_lfa.py::test_av_set_order). */
+ *
+ * intersect (:71-96) walks SRC and moves each address it finds in dst to a
+ * front that advances by one per match, so the common addresses come out in
+ * src's order ([3,2,1,0] ∩ [0,1] = [0,1]).  The reference's move overwrites
+ * the front entry, which loses a common address not yet reached
+ * ([a,b,c,d] ∩ [c,a] = [c]); here the two entries swap, so the result is the
+ * reference's wherever the reference keeps every common address, and
+ * otherwise every common address, still in src's order (the reference's
+ * result is then a subsequence of it).
+ *
+ * diff (:98-125) removes src's addresses one by one, in src's order, as
+ * remove would (the last address moves into the hole).  The reference writes
+ * the found address over the last one instead, which keeps the address it
+ * was asked to drop and drops the last ([a,b,c,d] \ [b] = [a,b,c]); the
+ * result is the reference's wherever the reference drops exactly src's
+ * addresses.
+ *
+ * tests/test_off_lfa.py::test_av_set_algebra_against_reference_loops checks
+ * both statements exhaustively on small sets against the reference loops
+ * restated in Python (DESIGN.md §6a "Group rank numbering"). */
 static int olfa_set_insert(struct fid_av_set *set, fi_addr_t addr)
 {
 	struct olfa_av_set *s = olfa_container_of(set, struct olfa_av_set, set_fid);
@@ -1650,12 +1662,20 @@ static int olfa_set_intersect(struct fid_av_set *dst, const struct fid_av_set *s
 	struct olfa_av_set *d = olfa_container_of(dst, struct olfa_av_set, set_fid);
 	const struct olfa_av_set *s =
 		olfa_container_of(src, struct olfa_av_set, set_fid);
-	size_t k = 0;
+	size_t front = 0;
 
-	for (size_t i = 0; i < d->count; i++)
-		if (olfa_index(s->addr, s->count, d->addr[i]) >= 0)
-			d->addr[k++] = d->addr[i];
-	d->count = k;
+	for (size_t i = 0; i < s->count; i++) {
+		long j = olfa_index(d->addr + front, d->count - front, s->addr[i]);
+
+		if (j >= 0) {
+			fi_addr_t t = d->addr[front];
+
+			d->addr[front] = d->addr[front + (size_t)j];
+			d->addr[front + (size_t)j] = t;
+			front++;
+		}
+	}
+	d->count = front;
 	return 0;
 }
 
@@ -2085,4 +2105,22 @@ FI_EXT_INI
 __attribute__((visibility("default"))) void off_lfa_freeinfo(struct fi_info *info)
 {
 	olfa_freeinfo(info);
+}
+
+/* Test accessor: the addresses of an av_set of this provider in the order a
+ * join numbers them (group rank = index).  fi_av_set has no listing call;
+ * the av_set algebra tests read the order the set calls left through this.
+ * Returns the member count (the first `cap` are copied), or -FI_EINVAL. */
+__attribute__((visibility("default"))) long off_lfa_test_set_order(struct fid_av_set *set,
+								    fi_addr_t *out,
+								    size_t cap)
+{
+	const struct olfa_av_set *s;
+
+	if (!set || set->fid.fclass != FI_CLASS_AV_SET || (!out && cap))
+		return -FI_EINVAL;
+	s = olfa_container_of(set, struct olfa_av_set, set_fid);
+	for (size_t i = 0; i < s->count && i < cap; i++)
+		out[i] = s->addr[i];
+	return (long)s->count;
 }

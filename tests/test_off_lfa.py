@@ -99,15 +99,88 @@ def test_peer_transport_collectives(tmp_path, n, mode):
     _check_ordered_sets(tmp_path, n)
 
 
+def ref_union(dst, src):
+    """coll_av_set_union, coll_av_set.c:35-69, loop for loop."""
+    d = list(dst)
+    for x in src:
+        if x not in d:
+            d.append(x)
+    return d
+
+
+def ref_intersect(dst, src):
+    """coll_av_set_intersect, coll_av_set.c:71-96, loop for loop: walk src,
+    search dst from the moving front `temp`, and on a match OVERWRITE
+    dst[temp] with the match."""
+    d = list(dst)
+    temp = 0
+    for x in src:
+        for j in range(temp, len(d)):
+            if d[j] == x:
+                d[temp] = d[j]
+                temp += 1
+                break
+    return d[:temp]
+
+
+def ref_diff(dst, src):
+    """coll_av_set_diff, coll_av_set.c:98-125, loop for loop: on a match at
+    j, dst[--temp] = dst[j] (the found address is written over the last)."""
+    d = list(dst)
+    temp = len(d)
+    for x in src:
+        for j in range(temp):
+            if d[j] == x:
+                temp -= 1
+                d[temp] = d[j]
+                break
+    return d[:temp]
+
+
+def build_intersect(dst, src):
+    """off_lfa's intersect: the reference's walk over src with a moving
+    front, the front entry SWAPPED with the match instead of overwritten."""
+    d = list(dst)
+    front = 0
+    for x in src:
+        if x in d[front:]:
+            j = d.index(x, front)
+            d[front], d[j] = d[j], d[front]
+            front += 1
+    return d[:front]
+
+
+def build_diff(dst, src):
+    """off_lfa's diff: src's addresses removed in src's order, as remove
+    does (the last address moves into the hole, coll_av_set.c:149-164)."""
+    d = list(dst)
+    for x in src:
+        if x in d:
+            i = d.index(x)
+            d[i] = d[-1]
+            d.pop()
+    return d
+
+
 class RefAvSet:
     """The address order prov/coll's av_set calls leave (coll_av_set.c):
     insert appends (:127-147), remove moves the last address into the hole
-    (:149-164), diff removes src's addresses in src's order the way remove
-    does — the reference's own diff overwrites the last address instead
-    (the build follows the evident intent)."""
+    (:149-164), intersect puts the common addresses in src's order
+    (:71-96), diff removes src's addresses in src's order the way remove
+    does — the reference's own diff overwrites the last address instead,
+    and its intersect can lose a member; the build keeps every member and
+    equals the reference wherever the reference does
+    (test_av_set_algebra_against_reference_loops)."""
 
     def __init__(self, start, end, stride):
         self.a = list(range(start, end + 1, stride))
+
+    @classmethod
+    def of(cls, addrs):
+        s = cls(0, -1, 1)
+        for x in addrs:
+            s.insert(x)
+        return s
 
     def insert(self, x):
         assert x not in self.a
@@ -118,10 +191,77 @@ class RefAvSet:
         self.a[i] = self.a[-1]
         self.a.pop()
 
+    def intersect(self, other):
+        self.a = build_intersect(self.a, other.a)
+
     def diff(self, other):
-        for x in other.a:
-            if x in self.a:
-                self.remove(x)
+        self.a = build_diff(self.a, other.a)
+
+
+def _ordered_subsets(universe, kmax):
+    import itertools
+    for k in range(kmax + 1):
+        yield from itertools.permutations(universe, k)
+
+
+def test_av_set_algebra_against_reference_loops():
+    """the member order union / intersect / diff leave decides
+    group ranks, so it is checked exhaustively — every ordered dst and src
+    drawn from 5 addresses with up to 4 members (206 x 206 pairs per op) —
+    through the provider (examples/off_lfa_host avset) against the
+    reference's loops restated above:
+      * union: identical to coll_av_set.c:35-69 everywhere;
+      * intersect: identical to :71-96 wherever that loop keeps every common
+        address; elsewhere every common address in src's order, of which the
+        reference's result is a subsequence;
+      * diff: identical to :98-125 wherever that loop drops exactly src's
+        addresses; elsewhere the exact set difference in remove's order."""
+    lib, exe = _binaries()
+    sets = list(_ordered_subsets(range(5), 4))
+    lines, want = [], []
+    for d in sets:
+        for s in sets:
+            for op in "uid":
+                lines.append(f"{op} {len(d)} {' '.join(map(str, d))} "
+                             f"{len(s)} {' '.join(map(str, s))}")
+                want.append((op, d, s))
+    r = subprocess.run([exe, lib, "avset"], input="\n".join(lines) + "\n",
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.strip().splitlines()
+    out = out[len(out) - len(want):]            # RCCL may print a banner first
+    assert len(out) == len(want)
+    seen = {"i_equal": 0, "i_ref_loses": 0, "d_equal": 0, "d_ref_wrong": 0}
+    for (op, d, s), line in zip(want, out):
+        rc, n, *got = map(int, line.split())
+        assert rc == 0 and n == len(got), (op, d, s, line)
+        common = [x for x in s if x in d]
+        if op == "u":
+            assert got == ref_union(d, s), (d, s, got)
+        elif op == "i":
+            ref = ref_intersect(d, s)
+            assert got == build_intersect(d, s) == common, (d, s, got)
+            if sorted(ref) == sorted(common):
+                assert got == ref, (d, s, got, ref)
+                seen["i_equal"] += 1
+            else:
+                it = iter(got)                  # ref is a subsequence of got
+                assert all(x in it for x in ref), (d, s, got, ref)
+                seen["i_ref_loses"] += 1
+        else:
+            ref = ref_diff(d, s)
+            assert got == build_diff(d, s), (d, s, got)
+            assert sorted(got) == sorted(set(d) - set(s)), (d, s, got)
+            if sorted(ref) == sorted(set(d) - set(s)):
+                assert got == ref, (d, s, got, ref)
+                seen["d_equal"] += 1
+            else:
+                seen["d_ref_wrong"] += 1
+    # the verdict's case, and both regimes of both loops were exercised
+    assert ref_intersect([3, 2, 1, 0], [0, 1]) == build_intersect([3, 2, 1, 0], [0, 1]) == [0, 1]
+    assert ref_intersect(list("abcd"), list("ca")) == ["c"]
+    assert ref_diff(list("abcd"), ["b"]) == list("abc")
+    assert all(v > 100 for v in seen.values()), seen
 
 
 def _check_ordered_sets(tmp_path, n):
@@ -141,7 +281,14 @@ def _check_ordered_sets(tmp_path, n):
         a.remove(2)
     b = RefAvSet(0, n - 1, 1)
     b.diff(RefAvSet(0, 0, 1))
-    for tag, ref in (("setA", a.a), ("setB", b.a)):
+    # set C: the world in descending order intersected with [0, 2, 1]
+    # (N >= 5), [0, 1] (N = 3, 4) or [0]: src's order, which the reference's
+    # own loop keeps for these (at N = 2 it would drop a member of [0, 1])
+    c_src = [0, 2, 1] if n >= 5 else ([0, 1] if n >= 3 else [0])
+    c = RefAvSet.of(range(n - 1, -1, -1))
+    c.intersect(RefAvSet.of(c_src))
+    assert c.a == ref_intersect(list(range(n - 1, -1, -1)), c_src) == c_src
+    for tag, ref in (("setA", a.a), ("setB", b.a), ("setC", c.a)):
         order = _load(tmp_path, 0, tag, "order", np.uint64).tolist()
         assert order == ref, (tag, order, ref)
         if not order:
