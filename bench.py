@@ -694,7 +694,7 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     region, flag_off = 1 << 20, 2 << 20
     ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device=dev) for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
-    status = torch.full((1,), -1, dtype=torch.int32).pin_memory()   # LFA_SIG_NONE
+    status = torch.full((1,), -1, dtype=torch.int64).pin_memory()   # LFA_SIG_NONE
     # two priorities: HIP keeps a hardware-queue pool per priority, so the
     # two ranks' kernels never share a queue (rank 0's wait would hold rank
     # 1's launch behind it until the timeout)
@@ -1373,17 +1373,32 @@ def tune_treeput(args) -> None:
     nsrc, blk = 8, 32 * 1024 * 1024 // 4
     variants = ([int(x) for x in args.variants.split(",")] if args.variants
                 else [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+    # --treeput-layout skew: every input and output block in one allocation,
+    # block k at k * (B + 6 KiB) (the collective's slot skew);
+    # sep: separate allocations (adjacent 32 MiB blocks, the same HBM
+    # channels at the same offset)
+    skew = args.treeput_layout == "skew"
     rows = []
     for ndst in (1, 8):
         sets = []
         for _ in range(2):
-            srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
-            dsts = [torch.empty(blk, device="cuda") for _ in range(ndst)]
+            if skew:
+                pitch = blk * 4 + 6144
+                pool = torch.empty((nsrc + ndst) * pitch, dtype=torch.uint8, device="cuda")
+                blocks = [pool[k * pitch:k * pitch + blk * 4].view(torch.float32)
+                          for k in range(nsrc + ndst)]
+                for b in blocks[:nsrc]:
+                    b.uniform_()
+                srcs, dsts = blocks[:nsrc], blocks[nsrc:]
+            else:
+                pool = None
+                srcs = [torch.rand(blk, device="cuda") for _ in range(nsrc)]
+                dsts = [torch.empty(blk, device="cuda") for _ in range(ndst)]
             sets.append((srcs, dsts, (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs]),
-                         (ctypes.c_void_p * ndst)(*[t.data_ptr() for t in dsts])))
+                         (ctypes.c_void_p * ndst)(*[t.data_ptr() for t in dsts]), pool))
         ref = None
         for v in variants:
-            srcs, dsts, sa, da = sets[0]
+            srcs, dsts, sa, da, _ = sets[0]
             assert L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h) == 0
             torch.cuda.synchronize()
             if ref is None:
@@ -1396,7 +1411,7 @@ def tune_treeput(args) -> None:
                 evs = [(torch.cuda.Event(enable_timing=True),
                         torch.cuda.Event(enable_timing=True)) for _ in range(10)]
                 for i, (a, b) in enumerate(evs):
-                    srcs, dsts, sa, da = sets[i % 2]
+                    srcs, dsts, sa, da, _ = sets[i % 2]
                     a.record()
                     L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h)
                     b.record()
@@ -1405,7 +1420,8 @@ def tune_treeput(args) -> None:
         for v in variants:
             ms = statistics.median(times[v])
             gbps = (nsrc + ndst) * blk * 4 / (ms * 1e-3) / 1e9
-            rows.append({"ndst": ndst, "variant": v, "median_us": round(ms * 1e3, 2),
+            rows.append({"ndst": ndst, "variant": v, "layout": args.treeput_layout,
+                         "median_us": round(ms * 1e3, 2),
                          "gbs": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)})
         del sets
         torch.cuda.empty_cache()
@@ -1508,6 +1524,8 @@ def main() -> None:
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--tune-tree-layout", action="store_true")
     ap.add_argument("--tune-treeput", action="store_true")
+    ap.add_argument("--treeput-layout", choices=("sep", "skew"), default="sep",
+                    help="--tune-treeput: separate allocations or one skewed pool")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
     ap.add_argument("--only-extra", default="", help="run one extra: tree_put, host_rs, config3, sizes (dev); "

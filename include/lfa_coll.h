@@ -255,6 +255,12 @@ struct lfa_mc_counters {
 };
 int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		    struct lfa_mc_counters *out);
+/* Test entry: the group's P2P ticket count continues from `ticket` (every
+ * member must seed the same value before the group's next P2P operation).
+ * Tickets and the timed-out status word are 64-bit; this lets a test run
+ * operations across 2^32 without issuing 4 billion of them.  0 or
+ * -LFA_EINVAL (unknown group, or operations of the group in flight). */
+int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ticket);
 
 /* ---- fi_ops_collective ------------------------------------------------ */
 

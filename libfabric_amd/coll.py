@@ -110,6 +110,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_mc_group_id.argtypes = [c_void_p]
     L.lfa_mc_counters.restype = c_int
     L.lfa_mc_counters.argtypes = [c_void_p, c_uint64, P(McCounters)]
+    L.lfa_mc_seed_ticket.restype = c_int
+    L.lfa_mc_seed_ticket.argtypes = [c_void_p, c_uint64, c_uint64]
     L.lfa_coll_domain_close.restype = c_int
     L.lfa_coll_domain_close.argtypes = [c_void_p]
     L.lfa_coll_ep_open.restype = c_int
@@ -309,10 +311,10 @@ class OneShot(ctypes.Structure):
                 ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
                 ("parity_off", ctypes.c_size_t), ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
                 ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
-                ("ticket", ctypes.c_uint32), ("timeout_us", ctypes.c_uint64)]
+                ("ticket", ctypes.c_uint64), ("timeout_us", ctypes.c_uint64)]
 
 
-SIG_NONE = 0xFFFFFFFF   # lfa_signal.h LFA_SIG_NONE: no wait of the group timed out
+SIG_NONE = 0xFFFFFFFFFFFFFFFF   # lfa_signal.h LFA_SIG_NONE: no wait of the group timed out
 
 
 def oneshot_reduce(op: int, dt: int, a: OneShot, stream) -> None:
@@ -381,6 +383,12 @@ class Endpoint:
         _chk(lib().lfa_mc_counters(self.ep, coll_addr or self.world, ctypes.byref(c)),
              "lfa_mc_counters")
         return {k: getattr(c, k) for k, _ in McCounters._fields_}
+
+    def seed_ticket(self, ticket: int, coll_addr: int | None = None) -> None:
+        """lfa_mc_seed_ticket (test entry): the group's P2P tickets continue
+        from `ticket`; every member seeds the same value."""
+        _chk(lib().lfa_mc_seed_ticket(self.ep, coll_addr or self.world, ticket),
+             "lfa_mc_seed_ticket")
 
     def close(self) -> None:
         L = lib()

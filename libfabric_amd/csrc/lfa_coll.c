@@ -253,20 +253,20 @@ static int sig_ready(struct lfa_coll_mc *mc)
 		return -LFA_EIO;
 	if (!mc->sig_word) {
 		hipSetDevice(mc->ep->dom->device);
-		if (hipHostMalloc((void **)&mc->sig_word, sizeof(uint32_t),
+		if (hipHostMalloc((void **)&mc->sig_word, sizeof(uint64_t),
 				  hipHostMallocCoherent) != hipSuccess) {
 			mc->sig_word = NULL;
 			return -LFA_ENOMEM;
 		}
-		*(volatile uint32_t *)mc->sig_word = LFA_SIG_NONE;
+		*(volatile uint64_t *)mc->sig_word = LFA_SIG_NONE;
 	}
-	if (*(volatile uint32_t *)mc->sig_word != LFA_SIG_NONE)
+	if (*(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE)
 		return -LFA_EIO;
 	return 0;
 }
 
 /* The operation just queued ran P2P kernels on `mc` if its ticket moved. */
-static void tag_p2p(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc, uint32_t t0)
+static void tag_p2p(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc, uint64_t t0)
 {
 	struct pending *p;
 
@@ -285,7 +285,7 @@ static int p2p_timed_out(const struct pending *p)
 	if (p->timed_out)
 		return 1;
 	return p->pmc && p->ticket && p->pmc->sig_word &&
-	       *(volatile uint32_t *)p->pmc->sig_word <= p->ticket;
+	       *(volatile uint64_t *)p->pmc->sig_word <= p->ticket;
 }
 
 int lfa_coll_ep_close(struct lfa_coll_ep *ep)
@@ -421,9 +421,28 @@ int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	out->oneshot = mc->n_oneshot;
 	out->flag_barriers = mc->n_barrier;
 	out->timed_out = mc->sig_failed ||
-			 (mc->sig_word && *(volatile uint32_t *)mc->sig_word != LFA_SIG_NONE);
+			 (mc->sig_word && *(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE);
 	pthread_mutex_unlock(&ep->lock);
 	return 0;
+}
+
+int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ticket)
+{
+	struct lfa_coll_mc *mc;
+	int ret = 0;
+
+	if (!ep)
+		return -LFA_EINVAL;
+	mc = mc_of(ep, coll_addr);
+	if (!mc)
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	if (ep->qlen)
+		ret = -LFA_EINVAL;
+	else
+		mc->p2p_ticket = ticket;
+	pthread_mutex_unlock(&ep->lock);
+	return ret;
 }
 
 /* Grow-only device buffer, stream-ordered so in-flight users stay valid. */
@@ -840,14 +859,19 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			st = -1;
 			perr = ETIMEDOUT;
 		}
-		if (p->kind == 0 && st == 0 && *nout >= count)
+		if (p->chain && p->chain == ep->failed_chain) {
+			/* a chunk of an operation whose error was already
+			 * reported: its outcome is that error, no second entry */
+		} else if (p->kind == 0 && st == 0 && *nout >= count) {
 			break;
-		if (st < 0) {
+		} else if (st < 0) {
 			ep->err.op_context = p->context;
 			ep->err.flags = LFA_COLLECTIVE;
 			ep->err.err = p->hop ? perr : LFA_EIO;
 			ep->err.prov_errno = perr;
 			ep->have_err = 1;
+			if (p->chain)
+				ep->failed_chain = p->chain;
 		} else if (p->kind == 1) {
 			join_finish(ep, p->mc);
 		} else if (p->kind == 2) {
@@ -1007,17 +1031,97 @@ static int open_fds(void)
 	return n - 3;   /* ".", ".." and the directory's own descriptor */
 }
 
+/*
+ * LFA_DEBUG: a history of the P2P workspaces' virtual address ranges in this
+ * process — 'A'llocated and 'F'reed local workspaces, 'I'mported and 'C'losed
+ * peer mappings — so a failed export can be matched against the ranges the
+ * same addresses held before (the hipIpcGetMemHandle
+ * "invalid argument" seen at a workspace growth).
+ */
+#define VA_HIST 256
+static struct va_ev {
+	char kind;
+	const void *p;
+	size_t bytes;
+	unsigned long long seq;
+} va_hist[VA_HIST];
+static unsigned long long va_n;
+static pthread_mutex_t va_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static int va_debug(void)
+{
+	static int on = -1;
+
+	if (on < 0)
+		on = getenv("LFA_DEBUG") != NULL;
+	return on;
+}
+
+static void va_note(char kind, const void *p, size_t bytes)
+{
+	if (!va_debug() || !p)
+		return;
+	if (!bytes) {
+		void *base = NULL;
+		size_t sz = 0;
+
+		if (hipMemGetAddressRange(&base, &sz, (void *)p) == hipSuccess)
+			bytes = sz;
+		else
+			(void)hipGetLastError();
+	}
+	pthread_mutex_lock(&va_lock);
+	va_hist[va_n % VA_HIST] = (struct va_ev){ kind, p, bytes, va_n };
+	va_n++;
+	pthread_mutex_unlock(&va_lock);
+}
+
+/* Everything the history knows about [p, p + bytes), and what HIP says of p. */
+static void va_explain(const char *what, const void *p, size_t bytes)
+{
+	hipPointerAttribute_t at;
+	void *base = NULL;
+	size_t sz = 0;
+	hipError_t e1, e2;
+
+	if (!va_debug())
+		return;
+	memset(&at, 0, sizeof(at));
+	e1 = hipPointerGetAttributes(&at, p);
+	e2 = hipMemGetAddressRange(&base, &sz, (void *)p);
+	(void)hipGetLastError();
+	fprintf(stderr, "lfa: %s: %p + %zu B; attributes rc %d type %d device %d "
+		"devptr %p hostptr %p; range rc %d base %p size %zu; %d fds open\n",
+		what, p, bytes, (int)e1, (int)at.type, at.device, at.devicePointer,
+		at.hostPointer, (int)e2, base, sz, open_fds());
+	pthread_mutex_lock(&va_lock);
+	for (unsigned long long i = va_n > VA_HIST ? va_n - VA_HIST : 0; i < va_n; i++) {
+		const struct va_ev *v = &va_hist[i % VA_HIST];
+		const char *a = v->p, *b = p;
+
+		if (a < b + bytes && b < a + v->bytes)
+			fprintf(stderr, "lfa:   overlaps event #%llu %c %p + %zu B%s\n", v->seq,
+				v->kind, v->p, v->bytes, v->p == p ? " (same base)" : "");
+	}
+	fprintf(stderr, "lfa:   (%llu workspace events so far)\n", va_n);
+	pthread_mutex_unlock(&va_lock);
+}
+
 /* Unmap the peers' workspaces in `sym` and free this rank's `local`. */
 static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 {
 	if (sym) {
 		for (int k = 0; k < mc->size; k++)
-			if (k != mc->rank && sym[k])
+			if (k != mc->rank && sym[k]) {
+				va_note('C', sym[k], 0);
 				hipIpcCloseMemHandle(sym[k]);
+			}
 		free(sym);
 	}
-	if (local)
+	if (local) {
+		va_note('F', local, 0);
 		hipFree(local);
+	}
 }
 
 static void p2p_release(struct lfa_coll_mc *mc)
@@ -1080,14 +1184,21 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	 * as "ahead"  */
 	mc->bar_epoch = 0;
 	mc->os_epoch = 0;
+	if (ok)
+		va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
 	if (ok && n > 1 && hipIpcGetMemHandle(&mine->h, mc->sym_local) != hipSuccess) {
 		/* seen once in a round-3 GPU run (2 of 8 processes on one GPU,
 		 * "invalid argument" at a workspace growth): export a fresh
 		 * allocation once more before failing the growth on every member */
-		(void)hipGetLastError();
-		if (getenv("LFA_DEBUG"))
-			fprintf(stderr, "lfa: P2P workspace export failed (%d fds open); "
-				"retrying on a new allocation\n", open_fds());
+		hipError_t e = hipGetLastError();
+
+		if (va_debug()) {
+			fprintf(stderr, "lfa: P2P workspace export failed (%s); retrying on a "
+				"new allocation\n", hipGetErrorString(e));
+			va_explain("failed export", mc->sym_local,
+				   2 * region + LFA_SIG_AREA_BYTES);
+		}
+		va_note('F', mc->sym_local, 0);
 		hipFree(mc->sym_local);
 		mc->sym_local = NULL;
 		ok = lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
@@ -1100,6 +1211,11 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 				  "P2P flag area memset sync (retry)") == hipSuccess &&
 		     lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
 				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
+		if (va_debug() && mc->sym_local) {
+			va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
+			va_explain(ok ? "retry exported" : "retry failed", mc->sym_local,
+				   2 * region + LFA_SIG_AREA_BYTES);
+		}
 		if (!ok && mc->sym_local) {
 			hipFree(mc->sym_local);
 			mc->sym_local = NULL;
@@ -1125,6 +1241,8 @@ static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, int *why
 					"P2P hipIpcOpenMemHandle") != hipSuccess) {
 			mc->sym[k] = NULL;
 			ret = -LFA_EIO;
+		} else {
+			va_note('I', mc->sym[k], 0);
 		}
 	}
 	return ret;
@@ -1774,7 +1892,7 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		       enum lfa_coll_algo algo)
 {
 	struct hop *h = calloc(1, sizeof(*h));
-	const uint32_t t0 = mc->p2p_ticket;
+	const uint64_t t0 = mc->p2p_ticket;
 	int ret;
 
 	if (!h)
@@ -1819,6 +1937,7 @@ static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			       int dev)
 {
 	const size_t esz = lfa_datatype_size(dt);
+	const uint64_t chain = ++ep->next_chain;
 	size_t per = ep->group_chunk / esz;
 
 	if (!per)
@@ -1830,8 +1949,18 @@ static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		int ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
 				      dt, op, context, last ? 0 : 3, NULL, dev, ep->algo);
 
-		if (ret)
-			return ret;     /* the chunks already queued run and reap */
+		if (ret) {
+			/* the caller is told the operation never started: the
+			 * chunks already queued still run (their peers wait for
+			 * them) but reap silently.  The members have now issued
+			 * different operations on the group, so its later
+			 * collectives fail (P2P waits time out): close and
+			 * re-join it (lfa_coll.h) */
+			if (off)
+				ep->failed_chain = chain;
+			return ret;
+		}
+		ep->q[(ep->qhead + ep->qlen - 1) % ep->qcap].chain = chain;
 	}
 	return 0;
 }
@@ -1843,7 +1972,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 {
 	struct lfa_coll_mc *mc;
 	size_t esz, chunk;
-	uint32_t t0;
+	uint64_t t0;
 	int root = -1, ret, host, chunkable;
 
 	if (!ep)
@@ -2022,7 +2151,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	/* coll_ep_barrier2 (coll_coll.c:997-1033): an allreduce of ~rank with
 	 * FI_BAND over one uint64. */
 	struct lfa_coll_mc *mc;
-	uint32_t t0;
+	uint64_t t0;
 	int ret;
 
 	if (!ep)
@@ -2276,7 +2405,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 		}
 	} else if (!ret) {
 		struct lfa_coll_mc *over = members_only ? mc : parent;
-		const uint32_t t0 = over->p2p_ticket;
+		const uint64_t t0 = over->p2p_ticket;
 
 		hipSetDevice(ep->dom->device);
 		ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) ==

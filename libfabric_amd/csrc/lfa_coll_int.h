@@ -35,7 +35,7 @@ struct xctx {
 	void *base[3];          /* SEND, RESULT, TMP */
 	char *const *sym;       /* [group rank] */
 	size_t region;
-	uint32_t ticket;        /* the group's P2P operation number (timeouts) */
+	uint64_t ticket;        /* the group's P2P operation number (timeouts) */
 };
 
 /* ====================================================================== */
@@ -71,8 +71,8 @@ struct lfa_coll_mc {
 	 * handed out, and whether a failure was reaped — the members' epochs
 	 * then disagree, so the group refuses P2P operations (other groups of
 	 * the endpoint are unaffected) */
-	uint32_t *sig_word;
-	uint32_t p2p_ticket;
+	uint64_t *sig_word;
+	uint64_t p2p_ticket;
 	int sig_failed;
 	uint64_t n_oneshot, n_barrier;  /* lfa_mc_counters */
 	/* LFA_ALGO_AUTO: 0 not tried, 1 the workspace agreement held, -1 it
@@ -100,8 +100,12 @@ struct pending {
 	/* the group the operation's P2P kernels ran on and its highest ticket
 	 * (0: none); timed_out: found failed when that group was closed */
 	struct lfa_coll_mc *pmc;
-	uint32_t ticket;
+	uint64_t ticket;
 	int timed_out;
+	/* the chunks of one chunked operation (peer_submit_chunked) share a
+	 * nonzero chain id: the operation posts ONE completion — the first
+	 * chunk's error, or the last chunk's success */
+	uint64_t chain;
 };
 
 struct lfa_coll_ep {
@@ -114,6 +118,9 @@ struct lfa_coll_ep {
 	hipStream_t d2h_stream;     /* host staging copies, D2H (the other
 				     * PCIe direction runs concurrently) */
 	enum lfa_coll_algo algo;
+	uint64_t next_chain;        /* chain ids of chunked operations */
+	uint64_t failed_chain;      /* the chain whose error was reported: its
+				     * remaining chunks reap silently */
 	size_t chunk;               /* one-member groups: host staging chunk */
 	size_t group_chunk;         /* every member, any N (0 = off) */
 	void *ws;                   /* device workspace */

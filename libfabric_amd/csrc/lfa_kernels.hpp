@@ -663,10 +663,11 @@ struct OsArgs {
   const uint32_t *wait;        // own one-shot rows
   const char *send;
   char *result;
-  uint32_t *status;
+  uint64_t *status;
   uint64_t timeout;            // wall-clock ticks
   size_t chunk;                // a multiple of 16
-  uint32_t epoch, ticket;
+  uint64_t ticket;
+  uint32_t epoch;
   int n, rank;
   int vec;                     // every range start and result 16-B aligned
   int unal;                    // send or result not aligned to the element

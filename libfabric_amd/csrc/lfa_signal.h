@@ -32,12 +32,14 @@ extern "C" {
 /*
  * Timed-out waits.  *status is one host-mapped word per group holding the
  * lowest `ticket` (the group's P2P operation number, from 1) whose wait gave
- * up, LFA_SIG_NONE while none has.  A kernel that times out lowers it to its
+ * up, LFA_SIG_NONE while none has.  Both are 64-bit, so no group ever hands
+ * out a ticket equal to LFA_SIG_NONE or wraps to 0 (a 32-bit
+ * ticket met 0xffffffff after 2^32 P2P operations and failed that one).  A kernel that times out lowers it to its
  * own ticket — the group's kernels run in stream order, so no two race on it
  * — and the host fails that operation and every later P2P operation of the
  * group, while the earlier ones complete normally.
  */
-#define LFA_SIG_NONE 0xffffffffu
+#define LFA_SIG_NONE 0xffffffffffffffffull	/* 64-bit: never reached by a ticket */
 
 /*
  * Enqueue a barrier on `stream`: after the steps before it on every member's
@@ -47,7 +49,7 @@ extern "C" {
  * *status to `ticket` and return.  0 or -LFA_E*.
  */
 int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
-			   int rank, uint32_t epoch, uint32_t *status, uint32_t ticket,
+			   int rank, uint32_t epoch, uint64_t *status, uint64_t ticket,
 			   uint64_t timeout_us, void *stream);
 
 /*
@@ -85,8 +87,8 @@ struct lfa_oneshot {
 	size_t flag_off;        /* the flag area's offset in a workspace */
 	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
 	uint32_t epoch;         /* this group's one-shot operations so far + 1 */
-	uint32_t *status;       /* host-mapped; lowered to ticket on a timeout */
-	uint32_t ticket;        /* this P2P operation's number in the group */
+	uint64_t *status;       /* host-mapped; lowered to ticket on a timeout */
+	uint64_t ticket;        /* this P2P operation's number in the group */
 	uint64_t timeout_us;
 };
 int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
@@ -96,8 +98,8 @@ int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 /* A wait of operation `ticket` gave up: lower the group's status word to it
  * (plain system-scope load and store: the group's kernels are stream-ordered,
  * and every lane of one kernel that times out stores the same ticket). */
-static __device__ __forceinline__ void lfa_sig_note_timeout(uint32_t *status,
-							     uint32_t ticket)
+static __device__ __forceinline__ void lfa_sig_note_timeout(uint64_t *status,
+							     uint64_t ticket)
 {
 	if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) > ticket)
 		__hip_atomic_store(status, ticket, __ATOMIC_RELAXED,

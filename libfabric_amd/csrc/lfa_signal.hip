@@ -19,9 +19,10 @@ namespace {
 struct BarArgs {
   uint32_t *post[LFA_SIG_MAX];
   const uint32_t *wait;
-  uint32_t *status;
+  uint64_t *status;
   uint64_t timeout;  // wall-clock ticks
-  uint32_t epoch, ticket;
+  uint64_t ticket;
+  uint32_t epoch;
   int n, rank;
 };
 
@@ -62,8 +63,8 @@ extern "C" uint64_t lfa__wallclock_ticks_per_us(void) {
 }
 
 extern "C" int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
-                                      int rank, uint32_t epoch, uint32_t *status,
-                                      uint32_t ticket, uint64_t timeout_us, void *stream) {
+                                      int rank, uint32_t epoch, uint64_t *status,
+                                      uint64_t ticket, uint64_t timeout_us, void *stream) {
   if (n < 1 || n > LFA_SIG_MAX || rank < 0 || rank >= n || !wait || !status || !post)
     return -LFA_EINVAL;
   if (n == 1) return 0;

@@ -612,6 +612,121 @@ __global__ __launch_bounds__(kBlock) void tp_pace(PutArgs a, size_t nvec) {
   }
 }
 
+// Round 4 forms of the 8 -> M push, product scope bits:
+// STAGGER: wave g = 4·b + w writes the outputs starting at g mod M, so at
+// any moment the waves' stores spread over every output stream instead of
+// sweeping them in the same order.
+template <int U, int LAUX, int SAUX, bool STAGGER>
+__global__ __launch_bounds__(kBlock) void tp_r4(PutArgs a, size_t nvec) {
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, LAUX));
+    });
+  }
+  const int j0 = STAGGER ? (int)((blockIdx.x * (kBlock / 64) + w) % (unsigned)a.nout) : 0;
+  for (int jj = 0; jj < a.nout; jj++) {
+    int j = j0 + jj;
+    if (j >= a.nout) j -= a.nout;
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
+// Inputs through LDS-DMA (global_load_lds_dwordx4 with the loads' cache
+// bits): the 8·U KiB of a wave's tile occupy no VGPRs while in flight, so
+// more waves fit per SIMD; then the tree from LDS and the product's stores.
+template <int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void tp_lds(PutArgs a, size_t nvec) {
+  __shared__ u32x4 tl[8 * (kBlock / 64) * U * 64];  // [k][w][u][64]
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t wbase = (size_t)blockIdx.x * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  auto slot = [&](int k, int u) { return ((k * (kBlock / 64) + (int)w) * U + u) * 64; };
+  u32x4 v[U];
+  if (wbase + 64 * U <= nvec) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)((const u32x4 *)a.t.in[k] + wbase + u * 64 + l),
+            (lds_void *)&tl[slot(k, u)], 16, 0, LAUX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(
+          a.t, [&](int k) { return tl[slot(k, u) + l]; });
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = wbase + (size_t)u * 64 + l;
+      v[u] = i < nvec ? tree_eval_with<OP_SUM, float, u32x4, 8>(
+                            a.t, [&](int k) { return ((const u32x4 *)a.t.in[k])[i]; })
+                      : u32x4{0, 0, 0, 0};
+    }
+  }
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  for (int j = 0; j < a.nout; j++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
+// Outputs split over the workgroup's waves: each wave reduces its own U-KiB
+// tile as in the product and parks the result in LDS; after one barrier,
+// wave w writes the WHOLE workgroup tile (4·U KiB, contiguous) to outputs
+// w, w + 4, ...  Same bytes; each wave then has 2 output streams of
+// 4·U KiB at 8 outputs instead of 8 streams of U KiB.
+template <int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void tp_split(PutArgs a, size_t nvec) {
+  constexpr int W = kBlock / 64;
+  __shared__ u32x4 res[W * U * 64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t gbase = (size_t)blockIdx.x * (kBlock * U);
+  const size_t wbase = gbase + (size_t)w * 64 * U;
+  if (wbase < nvec) {
+    const size_t left = nvec - wbase;
+    const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const unsigned off = (unsigned)(u * 64 + l) * 16;
+      res[(w * U + u) * 64 + l] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int k) {
+        return __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, LAUX));
+      });
+    }
+  }
+  __syncthreads();
+  if (gbase >= nvec) return;
+  const size_t gleft = nvec - gbase;
+  const unsigned gbytes = (unsigned)((gleft < (size_t)W * 64 * U ? gleft : (size_t)W * 64 * U) * 16);
+  for (int j = (int)w; j < a.nout; j += W) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + gbase, gbytes);
+#pragma unroll
+    for (int t = 0; t < W * U; t++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res[t * 64 + l]), r,
+                                             (unsigned)(t * 64 + l) * 16, 0, SAUX);
+  }
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
@@ -665,6 +780,19 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 21: TPM(3); break;
     case 22: TPM(4); break;
 #undef TPM
+#define TPG(K, U, ...)                                                              \
+  hipLaunchKernelGGL((K<U, 19, 17, ##__VA_ARGS__>),                                  \
+                     dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)), dim3(kBlock), \
+                     0, s, a, nvec)
+    case 23: TPG(tp_r4, 4, false); break;   // the product body, this harness
+    case 24: TPG(tp_r4, 4, true); break;    // staggered output order
+    case 25: TPG(tp_r4, 2, true); break;
+    case 26: TPG(tp_lds, 2); break;         // LDS-DMA inputs, 64 KiB LDS / WG
+    case 27: TPG(tp_lds, 1); break;
+    case 28: TPG(tp_split, 4); break;       // outputs split over the waves
+    case 29: TPG(tp_split, 2); break;
+    case 30: TPG(tp_split, 1); break;
+#undef TPG
     default: return -LFA_EINVAL;
   }
 #undef TP

@@ -395,6 +395,148 @@ def test_p2p_workspace_growth_in_flight():
     assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
+def _spawn(target, world, timeout=110, args=()):
+    """Run `target(rank, world, port, q, *args)` in `world` spawned processes
+    and fail with every rank's message unless all put "ok"."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *args))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            try:
+                r, msg = q.get(timeout=timeout)
+            except queue.Empty:         # a rank hung: report the others
+                break
+            results[r] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=5)
+            if p.is_alive():
+                p.kill()
+    bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
+
+
+def _ticket_wrap_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            base = (1 << 32) - 3
+            ep.seed_ticket(base)
+            # one-shot buckets and two-barrier ones, in flight together,
+            # with tickets 2^32-2 ... 2^32+5: 0xffffffff is one of them
+            sizes = (1000, 3 << 18, 5, 4096, 70_001, 1 << 20, 33, 2048)
+            outs, ctxs = [], []
+            for k, n in enumerate(sizes):
+                sends = _inputs(oracle, 8, n, world, 500 + k)
+                want = oracle.allreduce(2, 8, sends)[0]
+                r = torch.zeros(n, dtype=torch.float32, device="cuda")
+                xs = _dev(sends[rank])
+                _ready()
+                ctxs.append(ep.allreduce(xs, r, n, 8, 2))
+                outs.append((r, want, xs))
+            done = []
+            while len(done) < len(ctxs):
+                done += ep.cq_read()
+            assert done == ctxs
+            for (r, want, _), n in zip(outs, sizes):
+                assert r.cpu().numpy().tobytes() == want.tobytes(), f"P2P n={n}"
+            c = ep.counters()
+            assert c["p2p_ops"] == base + len(sizes) and c["timed_out"] == 0, c
+            assert c["oneshot"] > 0 and c["flag_barriers"] > 0, c
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_p2p_tickets_cross_2_pow_32():
+    """the per-group P2P ticket and the timed-out status word are
+    64-bit.  With 32-bit ones, ticket 0xffffffff equalled the 'no timeout'
+    value, so that operation failed with ETIMEDOUT and the group refused P2P
+    from then on.  Tickets seeded just below 2^32 on both members, eight
+    one-shot and two-barrier allreduces in flight across the boundary: all
+    complete, bit-exact, with no timeout recorded."""
+    _spawn(_ticket_wrap_worker, 2)
+
+
+def _chunk_error_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                          LFA_SIG_TIMEOUT_MS="300")
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import ctypes
+        import time
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        msg = "ok"
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            # members disagree on the group chunk (a caller error): rank 0
+            # splits 4 MiB into 4 chunks, rank 1 into 2, so rank 0's third
+            # chunk waits for a peer that never arrives and fails — a middle
+            # chunk — and its fourth fails behind it
+            ep.set_group_chunk((1 << 20) * (rank + 1))
+            n = 1 << 20
+            xs = torch.ones(n, dtype=torch.float32, device="cuda")
+            rs = torch.zeros(n, dtype=torch.float32, device="cuda")
+            _ready()
+            ctx = ep.allreduce(xs, rs, n, 8, 2)
+            L = coll.lib()
+            ok, errs = [], []
+            t0 = time.time()
+            while time.time() - t0 < 3.0:
+                got = L.lfa_cq_read(ep.ep, ep._ents, 16)
+                if got > 0:
+                    ok += [ep._ents[i].op_context for i in range(got)]
+                elif got == -coll.EIO:
+                    e = coll.CqErrEntry()
+                    assert L.lfa_cq_readerr(ep.ep, ctypes.byref(e)) == 1
+                    errs.append((e.op_context, e.prov_errno))
+            if rank == 0 and (ok or [c for c, _ in errs] != [ctx] or errs[0][1] != 110):
+                msg = f"rank 0: successes {ok}, errors {errs} (ctx {ctx}): want one ETIMEDOUT"
+            if rank == 1 and (ok != [ctx] or errs):
+                msg = f"rank 1: successes {ok}, errors {errs} (ctx {ctx}): want one success"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_chunked_operation_posts_one_completion():
+    """a group-chunked operation is ONE operation to the caller.
+    Before, every chunk that failed posted its own error entry under the
+    caller's context (and the last chunk a further one), so one fi_allreduce
+    produced several completions.  Now the first failing chunk's error is the
+    operation's only entry; a member whose chunks all succeed posts one
+    success."""
+    _spawn(_chunk_error_worker, 2)
+
+
 def _timeout_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),

@@ -484,7 +484,7 @@ def test_gpu_oneshot_misaligned_buffers(dt, mode, offs):
     ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device="cuda")
           for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
-    status = torch.full((1,), -1, dtype=torch.int32).pin_memory()
+    status = torch.full((1,), -1, dtype=torch.int64).pin_memory()
     sd = [_dev(x, offs[0], count * esz, torch) for x in sends]
     want, rd = [], []
     for r in range(2):

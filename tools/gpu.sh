@@ -1,0 +1,73 @@
+#!/bin/bash
+# GPU stages for one gpurun call:   tools/gpu.sh <stage> [<stage> ...]
+# Each stage is one or more tools/gpu_step.sh steps (own time limit, log in
+# gpurun_out/<name>.log); stages run in order and the call stops at the first
+# fault (gpu_step.sh exits 99 on anything but pass / ordinary test failure).
+#
+#   smoke        __graft_entry__.smoke()
+#   suite        pytest -m gpu (the whole GPU suite)
+#   tests:<k>    pytest -m gpu -k <k>
+#   peer8        the 8-process executor test once at the default 4 hardware
+#                queues per process, per-rank LFA_TRACE / LFA_DEBUG logs under
+#                gpurun_out/peer_logs, HIP runtime errors (AMD_LOG_LEVEL=1)
+#   bench        driver-shaped bench (--gpus 1 --steps 20 --warmup 5) under
+#                rocprofv3 --kernel-trace --stats
+#   benchplain   the same without the profiler
+#   pmc          the headline kernel's FETCH_SIZE / WRITE_SIZE in separate passes
+#   treeput      bench.py --tune-treeput A/B (TREEPUT_VARIANTS, default 0), in
+#                separate allocations and in one skewed pool
+#   treeput_pmc  counters of the 8->8 tree_put (TREEPUT_PMC_VARIANT)
+#   clat         small-collective latency: world-1 RCCL domain and 2-process
+#                P2P, C-timed loop (liblfa_bench.so) and its breakdown
+#   sizes        combine kernel durations vs size under --kernel-trace
+#   host2        2-process host-buffer allreduce, default vs group chunks
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+S=tools/gpu_step.sh
+P="rocprofv3 --kernel-trace --stats --output-format csv"
+PT="python3 -u -m pytest -x -v --timeout 200 --timeout-method thread"
+for stage in "$@"; do
+  case "$stage" in
+    smoke)
+      $S smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" || exit 99 ;;
+    suite)
+      $S gpu_tests 1100 $PT -m gpu -q tests || exit 99 ;;
+    tests:*)
+      k="${stage#tests:}"
+      $S "tests_$(echo "$k" | tr -c 'A-Za-z0-9_\n' '_')" 600 $PT -m gpu tests -k "$k" || exit 99 ;;
+    peer8)
+      mkdir -p gpurun_out/peer_logs
+      PEER_LOG_DIR=gpurun_out/peer_logs LFA_TRACE=1 AMD_LOG_LEVEL=1 LFA_TEST_HW_QUEUES=4 \
+        $S peer8 300 $PT -m gpu tests/test_coll_peer_gpu.py \
+        -k "test_c_executor_gpu_kernels_across_processes and 8" || exit 99 ;;
+    bench)
+      $S prof_bench 500 $P -d gpurun_out/prof_bench -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 || exit 99 ;;
+    benchplain)
+      $S bench 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 || exit 99 ;;
+    pmc)
+      $S pmc_fetch 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extras && \
+      $S pmc_write 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extras || exit 99 ;;
+    treeput)
+      for lay in sep skew; do
+        $S "tune_treeput_$lay" 400 python3 -u bench.py --tune-treeput --treeput-layout $lay \
+          --variants "${TREEPUT_VARIANTS:-0}" --tune-rounds "${TREEPUT_ROUNDS:-10}" || exit 99
+      done ;;
+    treeput_pmc)
+      for c in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES" \
+               "TA_BUSY_avr GRBM_GUI_ACTIVE" "WRITE_SIZE" "FETCH_SIZE"; do
+        tag=$(echo "$c" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+        $S "treeput_pmc_$tag" 150 timeout -s KILL 140 rocprofv3 --pmc $c --output-format csv \
+          -d "gpurun_out/treeput_pmc_$tag" -o run -- python3 bench.py --tune-treeput \
+          --variants "${TREEPUT_PMC_VARIANT:-0}" --tune-rounds 2 || exit 99
+      done ;;
+    clat)
+      $S clat 300 python3 -u tools/probe_latency.py || exit 99 ;;
+    sizes)
+      $S ksizes 300 $P -d gpurun_out/ksizes -o run -- python3 bench.py --only-extra sizes || exit 99 ;;
+    host2)
+      $S host2 300 python3 -u tools/probe_host_group_chunk.py || exit 99 ;;
+    *)
+      echo "unknown stage $stage"; exit 2 ;;
+  esac
+done

@@ -38,7 +38,7 @@ def main() -> None:
                                            ctypes.POINTER(OneShot), ctypes.c_void_p]
     L.lfa_flag_barrier_async.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
-                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_void_p]
     hip = ctypes.CDLL("libamdhip64.so")
     torch.cuda.set_device(0)
@@ -49,8 +49,8 @@ def main() -> None:
           for _ in range(n)]
     sym = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws])
     status = ctypes.c_void_p()
-    assert hip.hipHostMalloc(ctypes.byref(status), ctypes.c_size_t(4), 0x40000000) == 0
-    ctypes.c_uint32.from_address(status.value).value = 0xFFFFFFFF   # LFA_SIG_NONE
+    assert hip.hipHostMalloc(ctypes.byref(status), ctypes.c_size_t(8), 0x40000000) == 0
+    ctypes.c_uint64.from_address(status.value).value = 0xFFFFFFFFFFFFFFFF   # LFA_SIG_NONE
     streams = [torch.cuda.Stream() for _ in range(n)]
     torch.cuda.synchronize()
     out = {}
@@ -95,7 +95,7 @@ def main() -> None:
             for it in range(k_iters + 20):
                 if it == 20:
                     torch.cuda.synchronize()
-                    if ctypes.c_uint32.from_address(status.value).value != 0xFFFFFFFF:
+                    if ctypes.c_uint64.from_address(status.value).value != 0xFFFFFFFFFFFFFFFF:
                         # a wait timed out: the streams did not run together
                         print(json.dumps({"error": f"{form} {nbytes}: wait timed out"}))
                         sys.exit(1)
@@ -127,7 +127,7 @@ def main() -> None:
                 y[r].zero_()
             torch.cuda.synchronize()
         out[str(nbytes)] = row
-    out["timeouts"] = int(ctypes.c_uint32.from_address(status.value).value != 0xFFFFFFFF)
+    out["timeouts"] = int(ctypes.c_uint64.from_address(status.value).value != 0xFFFFFFFFFFFFFFFF)
     print(json.dumps({"ranks_in_one_process": n, "per_op_gpu_time": out}), flush=True)
 
 
