@@ -873,15 +873,20 @@ def extra_host_allreduce(ep, world, reps=3, sweep=False):
             return round(statistics.median(tt) * 1e3, 3)
         dx, dy = hx.to("cuda"), torch.empty(COUNT, device="cuda")
         torch.cuda.synchronize()
-        row["device_whole_ms"] = timed(dx, dy)
+        # the default (LFA_GROUP_CHUNK_AUTO: 32 MiB chunks from 64 MiB on,
+        # every member) — row["ms"] above is the host side of it
+        row["device_default_ms"] = timed(dx, dy)
         want = dy.cpu()
+        ep.set_group_chunk(0)
+        row["device_whole_ms"] = timed(dx, dy)
+        row["host_whole_ms"] = timed(hx, hy)
         for mib in (32, 64):
             ep.set_group_chunk(mib << 20)
             row[f"group_chunk_{mib}mib_host_ms"] = timed(hx, hy)
             row[f"group_chunk_{mib}mib_device_ms"] = timed(dx, dy)
             row[f"group_chunk_{mib}mib_bitwise_equal"] = bool(torch.equal(hy, want) and
                                                              torch.equal(dy.cpu(), want))
-        ep.set_group_chunk(0)
+        ep.set_group_chunk(coll.GROUP_CHUNK_AUTO)
         row["group_chunk_note"] = ("lfa_coll_ep_set_group_chunk on every rank: host members "
                                    "pipeline H2D/collective/D2H per chunk, device members "
                                    "run the same chunks in place")

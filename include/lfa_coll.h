@@ -178,8 +178,10 @@ int lfa_coll_ep_set_algo(struct lfa_coll_ep *ep, enum lfa_coll_algo algo);
 /* Host-staging chunk size in bytes (0 = default 32 MiB) of a ONE-member
  * group: H2D, collective and D2H of consecutive chunks overlap. */
 int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
-/* The GROUP chunk, in bytes (0 = off, the default; also read from
- * LFA_GROUP_CHUNK_BYTES at endpoint open).  A chunked member issues one
+/* The GROUP chunk, in bytes: LFA_GROUP_CHUNK_AUTO (the default), 0 = off,
+ * or a size (also read from LFA_GROUP_CHUNK_BYTES at endpoint open).  AUTO
+ * is lfa_coll_group_chunk's rule, a function of the operation's byte count
+ * alone, so every member derives the same chunk.  A chunked member issues one
  * device collective per chunk, so in a group of N > 1 chunking must be a
  * group-wide choice: with a group chunk set — the SAME value on every
  * member, like the collectives themselves — every member, whatever memory
@@ -193,10 +195,19 @@ int lfa_coll_ep_set_chunk(struct lfa_coll_ep *ep, size_t bytes);
  * reference defines stays the same: prov/coll copies host buffers whole
  * (coll_coll.c:364, 1058). */
 int lfa_coll_ep_set_group_chunk(struct lfa_coll_ep *ep, size_t bytes);
+#define LFA_GROUP_CHUNK_AUTO ((size_t)-1)
+/* The group chunk an operation of `bytes` (count × datatype size, the
+ * per-member input) runs with in a group of `nranks` under the setting
+ * `group_chunk` (0 = none): AUTO gives LFA_AUTO_CHUNK_BYTES (32 MiB) to
+ * operations of at least twice that in groups of N > 1, none otherwise; a
+ * size is used as it is.  Pure: the same on every member. */
+#define LFA_AUTO_CHUNK_BYTES ((size_t)32 << 20)
+size_t lfa_coll_group_chunk(size_t group_chunk, int nranks, size_t bytes);
 /* The chunk, in bytes, a member stages an operation with (0 = one chunk,
- * the whole buffer): the group chunk when set (every member), otherwise the
- * local chunk for a host member of a one-member group, otherwise 0.  Pure:
- * what tests/test_coll_plan.py replays for mixed members. */
+ * the whole buffer): the group chunk when there is one (every member; pass
+ * lfa_coll_group_chunk's result), otherwise the local chunk for a host
+ * member of a one-member group, otherwise 0.  Pure: what
+ * tests/test_coll_plan.py replays for mixed members. */
 size_t lfa_coll_member_chunk(int nranks, int host, size_t group_chunk,
 			     size_t local_chunk);
 

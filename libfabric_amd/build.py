@@ -141,11 +141,12 @@ def build_bench(verbose: bool = False) -> str | None:
     src = os.path.join(CSRC, "lfa_bench.c")
     if not os.path.exists(src):
         return None
-    if _newer(LIB_BENCH, [src, os.path.join(INC, "lfa_coll.h"), LIB_COLL]):
+    if _newer(LIB_BENCH, [src, os.path.join(INC, "lfa_coll.h"), LIB_COLL, LIB_LFA]):
         _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
-              "-Wno-unused-parameter", "-I" + INC, "-shared", "-o", LIB_BENCH, src,
-              "-L" + PKG, "-llfa_coll", "-Wl,-rpath,$ORIGIN",
-              "-Wl,-soname,liblfa_bench.so"])
+              "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__", "-I" + INC,
+              "-I" + os.path.join(ROCM, "include"), "-shared", "-o", LIB_BENCH, src,
+              "-L" + PKG, "-llfa_coll", "-llfa", "-L" + os.path.join(ROCM, "lib"),
+              "-lamdhip64", "-Wl,-rpath,$ORIGIN", "-Wl,-soname,liblfa_bench.so"])
         if verbose:
             print(f"built {LIB_BENCH}")
     return LIB_BENCH

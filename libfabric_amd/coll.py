@@ -32,6 +32,8 @@ c_int, c_size_t, c_void_p, c_uint64, c_uint32, c_int32 = (
 c_ssize_t = ctypes.c_ssize_t
 
 ALGO_TREE, ALGO_RD, ALGO_RCCL, ALGO_TREE_COLL, ALGO_P2P, ALGO_AUTO = 0, 1, 2, 3, 4, 5
+GROUP_CHUNK_AUTO = (1 << 64) - 1   # lfa_coll.h LFA_GROUP_CHUNK_AUTO, the default
+AUTO_CHUNK_BYTES = 32 << 20        # lfa_coll.h LFA_AUTO_CHUNK_BYTES
 (STEP_SEND, STEP_RECV, STEP_GROUP_END, STEP_REDUCE, STEP_TREE, STEP_COPY,
  STEP_ALLTOALL, STEP_ALLGATHER, STEP_BARRIER, STEP_TREE_PUT, STEP_ONESHOT) = range(11)
 BUF_SEND, BUF_RESULT, BUF_TMP, BUF_SYM_IN, BUF_SYM_OUT = 0, 1, 2, 3, 4
@@ -130,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_auto_algo.argtypes = [c_int, c_size_t, c_int, c_size_t, c_int]
     L.lfa_coll_member_chunk.restype = c_size_t
     L.lfa_coll_member_chunk.argtypes = [c_int, c_int, c_size_t, c_size_t]
+    L.lfa_coll_group_chunk.restype = c_size_t
+    L.lfa_coll_group_chunk.argtypes = [c_size_t, c_int, c_size_t]
     L.lfa_coll_ep_flush.restype = c_int
     L.lfa_coll_ep_flush.argtypes = [c_void_p]
     L.lfa_coll_world_addr.restype = c_uint64
@@ -238,6 +242,12 @@ def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
 def auto_algo(coll: int, count: int, nranks: int, esz: int, p2p_ok: bool = True) -> int:
     """lfa_coll_auto_algo: LFA_ALGO_AUTO's choice for one operation."""
     return lib().lfa_coll_auto_algo(coll, count, nranks, esz, int(p2p_ok))
+
+
+def group_chunk(setting: int, nranks: int, nbytes: int) -> int:
+    """lfa_coll_group_chunk: the group chunk an operation of `nbytes` runs
+    with under `setting` (GROUP_CHUNK_AUTO, 0 or a size)."""
+    return lib().lfa_coll_group_chunk(setting, nranks, nbytes)
 
 
 def member_chunk(nranks: int, host: bool, group_chunk: int, local_chunk: int) -> int:
@@ -637,7 +647,7 @@ def esz(dt: int) -> int:
     return SIZES[DT(dt)]
 
 
-__all__ = ["plan", "block", "host_chunks", "member_chunk", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
+__all__ = ["plan", "block", "host_chunks", "group_chunk", "member_chunk", "HostChunk", "loopback", "Endpoint", "Plan", "COLL", "DT", "OP",
            "ALGO_TREE", "ALGO_RD", "ALGO_RCCL", "ALGO_TREE_COLL", "ALGO_P2P", "ALGO_AUTO",
            "auto_algo", "esz",
            "HostEndpoint", "PeerXferOps", "TransportAgain"]

@@ -182,7 +182,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	{
 		const char *e = getenv("LFA_GROUP_CHUNK_BYTES");
 
-		ep->group_chunk = e ? (size_t)strtoull(e, NULL, 0) : 0;
+		ep->group_chunk = e ? (size_t)strtoull(e, NULL, 0) : LFA_GROUP_CHUNK_AUTO;
 	}
 	/* the P2P workspace exchange needs these on every member even when a
 	 * local allocation fails later, so they exist up front */
@@ -372,6 +372,16 @@ int lfa_coll_ep_set_group_chunk(struct lfa_coll_ep *ep, size_t bytes)
 		return -LFA_EINVAL;
 	ep->group_chunk = bytes;
 	return 0;
+}
+
+size_t lfa_coll_group_chunk(size_t group_chunk, int nranks, size_t bytes)
+{
+	if (group_chunk != LFA_GROUP_CHUNK_AUTO)
+		return group_chunk;
+	/* host members of a group pipeline H2D / collective / D2H per chunk
+	 * (2 processes, 256 MiB: 20.4 ms whole, 13.1 ms in 32 MiB chunks,
+	 * DESIGN.md §3); below two chunks there is nothing to overlap */
+	return nranks > 1 && bytes >= 2 * LFA_AUTO_CHUNK_BYTES ? LFA_AUTO_CHUNK_BYTES : 0;
 }
 
 size_t lfa_coll_member_chunk(int nranks, int host, size_t group_chunk,
@@ -1921,24 +1931,26 @@ static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
  * stream) and chunk c-1's D2H (d2h stream) overlap chunk c's kernels.
  * reduce_scatter keeps one operation (its chunks are 2-D).
  */
-static int peer_chunked(const struct lfa_coll_ep *ep, const struct lfa_coll_mc *mc,
-			enum lfa_collective_op coll, size_t count, size_t esz)
+static size_t peer_chunked(const struct lfa_coll_ep *ep, const struct lfa_coll_mc *mc,
+			   enum lfa_collective_op coll, size_t count, size_t esz)
 {
-	return ep->algo == LFA_ALGO_P2P && ep->group_chunk && ep->dom->device >= 0 &&
+	const size_t g = lfa_coll_group_chunk(ep->group_chunk, mc->size, count * esz);
+
+	return ep->algo == LFA_ALGO_P2P && g && ep->dom->device >= 0 &&
 	       mc->size > 1 && mc->size <= LFA_TREE_MAX && mc->size <= LFA_PUT_MAX &&
 	       (coll == LFA_ALLREDUCE || coll == LFA_REDUCE) &&
-	       count * esz > ep->group_chunk;
+	       count * esz > g ? g : 0;
 }
 
 static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 			       enum lfa_collective_op coll, const void *buf,
 			       void *result, size_t count, int root,
 			       enum lfa_datatype dt, enum lfa_op op, void *context,
-			       int dev)
+			       int dev, size_t chunk)
 {
 	const size_t esz = lfa_datatype_size(dt);
 	const uint64_t chain = ++ep->next_chain;
-	size_t per = ep->group_chunk / esz;
+	size_t per = chunk / esz;
 
 	if (!per)
 		per = 1;
@@ -2013,9 +2025,9 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		     coll == LFA_REDUCE))
 			dev = 2;
 		pthread_mutex_lock(&ep->lock);
-		if (dev && peer_chunked(ep, mc, coll, count, esz))
+		if (dev && (chunk = peer_chunked(ep, mc, coll, count, esz)))
 			ret = peer_submit_chunked(ep, mc, coll, buf, result, count, root, dt,
-						  op, context, dev);
+						  op, context, dev, chunk);
 		else
 			ret = host_submit(ep, mc, coll, buf, result, count, root, dt, op,
 					  context, 0, NULL, dev, ep->algo);
@@ -2035,7 +2047,10 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	 * member alike, a local one only to a one-member group's host buffers
 	 * (lfa_coll_member_chunk), so every member issues the same device
 	 * collectives whatever memory its buffers are in */
-	chunk = lfa_coll_member_chunk(mc->size, host, ep->group_chunk, ep->chunk);
+	chunk = lfa_coll_member_chunk(mc->size, host,
+				      lfa_coll_group_chunk(ep->group_chunk, mc->size,
+							   count * esz),
+				      ep->chunk);
 	if (!count) {
 		ret = 0;
 	} else if (!host && chunk && chunkable &&

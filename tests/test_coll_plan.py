@@ -349,6 +349,37 @@ def test_group_chunk_same_schedule_for_every_member(n, group):
         max(1, -(-70_001 * 8 // max(group, 8)))
 
 
+@pytest.mark.parametrize("n", range(1, 9))
+def test_default_group_chunk_same_schedule_for_every_member(n):
+    """the group chunk is ON by default (GROUP_CHUNK_AUTO).
+    Its size is a function of the operation's byte count (and N) alone —
+    32 MiB chunks from 64 MiB on in groups of N > 1, none below — so host
+    and device members of N = 2..8, whatever their local chunk, issue the
+    identical sequence of device collectives without any setter call; a
+    one-member group keeps its local chunk."""
+    auto, ch = coll.GROUP_CHUNK_AUTO, coll.AUTO_CHUNK_BYTES
+    for nbytes in (4096, ch, 2 * ch - 8, 2 * ch, 256 << 20, (256 << 20) + 24, 1 << 30):
+        g = coll.group_chunk(auto, n, nbytes)
+        assert g == (ch if n > 1 and nbytes >= 2 * ch else 0), (n, nbytes, g)
+        for kind, esz in ((ALLREDUCE, 4), (REDUCE, 8), (BROADCAST, 4), (REDUCE_SCATTER, 8)):
+            count = nbytes // esz
+            if kind == REDUCE_SCATTER:
+                count -= count % n
+            g = coll.group_chunk(auto, n, count * esz)
+            scheds = {repr(_member_schedule(kind, count, n, esz, host, g, local))
+                      for host in (False, True) for local in (4096, 32 << 20)}
+            if n > 1:
+                assert len(scheds) == 1, (kind, count, n, scheds)
+            sched = _member_schedule(kind, count, n, esz, False, g, 0)
+            assert sum(sched) == count
+            if g:                       # chunked: at least two device collectives
+                assert len(sched) >= count * esz // g, (kind, count, n, sched)
+    # explicit settings are used as they are, AUTO never reaches a one-member group
+    assert coll.group_chunk(0, 8, 1 << 30) == 0
+    assert coll.group_chunk(1 << 20, 8, 4096) == 1 << 20
+    assert coll.group_chunk(auto, 1, 1 << 30) == 0
+
+
 @pytest.mark.parametrize("n", [2, 3, 8])
 @pytest.mark.parametrize("group", [4096, 100_000])
 def test_group_chunked_results_equal_unchunked(n, group):

@@ -78,10 +78,17 @@ def _worker(rank, world, port, reps, q):
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 tl.append(t.item())
             row = {"torch_h2d_then_d2h_ms": round(statistics.median(tl) * 1e3, 2)}
-            row["device_whole_ms"] = timed(dx, dy)
+            # no setter call: the default group chunk (LFA_GROUP_CHUNK_AUTO,
+            # 32 MiB chunks from 64 MiB on)
+            row["device_default_ms"] = timed(dx, dy)
             want = dy.cpu()
-            row["host_whole_ms"] = timed(hx, hy)
+            row["host_default_ms"] = timed(hx, hy)
             ok = torch.equal(hy, want)
+            ep.set_group_chunk(0)
+            row["device_whole_ms"] = timed(dx, dy)
+            ok = ok and torch.equal(dy.cpu(), want)
+            row["host_whole_ms"] = timed(hx, hy)
+            ok = ok and torch.equal(hy, want)
             for mib in (64, 32, 16, 8):
                 ep.set_group_chunk(mib << 20)
                 row[f"host_group_chunk_{mib}mib_ms"] = timed(hx, hy)
@@ -90,6 +97,8 @@ def _worker(rank, world, port, reps, q):
                 ok = ok and torch.equal(dy.cpu(), want)
             ep.set_group_chunk(0)
             row["host_whole_again_ms"] = timed(hx, hy)     # order / warm-up check
+            ep.set_group_chunk(coll.GROUP_CHUNK_AUTO)
+            row["host_default_again_ms"] = timed(hx, hy)
             row["bitwise_equal"] = bool(ok)
         finally:
             ep.close()
