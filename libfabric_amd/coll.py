@@ -321,7 +321,9 @@ class OneShot(ctypes.Structure):
                 ("sym", ctypes.c_void_p), ("slot_bytes", ctypes.c_size_t),
                 ("parity_off", ctypes.c_size_t), ("flag_off", ctypes.c_size_t), ("n", ctypes.c_int), ("rank", ctypes.c_int),
                 ("epoch", ctypes.c_uint32), ("status", ctypes.c_void_p),
-                ("ticket", ctypes.c_uint64), ("timeout_us", ctypes.c_uint64)]
+                ("ticket", ctypes.c_uint64), ("timeout_us", ctypes.c_uint64),
+                ("done_ctr", ctypes.c_void_p), ("done_word", ctypes.c_void_p),
+                ("done_val", ctypes.c_uint64)]
 
 
 SIG_NONE = 0xFFFFFFFFFFFFFFFF   # lfa_signal.h LFA_SIG_NONE: no wait of the group timed out

@@ -141,9 +141,36 @@ int lfa_coll_domain_close(struct lfa_coll_domain *d)
 	return 0;
 }
 
+/* The completion word and its counter (device endpoints), zeroed. */
+static int done_word_init(struct lfa_coll_ep *ep)
+{
+	if (hipMalloc((void **)&ep->done_ctr, sizeof(uint32_t)) != hipSuccess) {
+		ep->done_ctr = NULL;
+		return -1;
+	}
+	if (hipHostMalloc((void **)&ep->done_word, sizeof(uint64_t),
+			  hipHostMallocCoherent) != hipSuccess) {
+		ep->done_word = NULL;
+		return -1;
+	}
+	*(volatile uint64_t *)ep->done_word = 0;
+	return hipMemset(ep->done_ctr, 0, sizeof(uint32_t)) == hipSuccess ? 0 : -1;
+}
+
+static void done_word_free(struct lfa_coll_ep *ep)
+{
+	if (ep->done_ctr)
+		hipFree(ep->done_ctr);
+	if (ep->done_word)
+		hipHostFree(ep->done_word);
+	ep->done_ctr = NULL;
+	ep->done_word = NULL;
+}
+
 /* Frees whatever lfa_coll_ep_open managed to create (open's error path). */
 static void ep_release(struct lfa_coll_ep *ep)
 {
+	done_word_free(ep);
 	if (ep->barrier_dev)
 		hipFree(ep->barrier_dev);
 	if (ep->ctl_dev)
@@ -195,7 +222,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		    hipHostMalloc((void **)&ep->barrier_host, 2 * sizeof(uint64_t), 0) != hipSuccess ||
 		    hipMalloc(&ep->barrier_dev, 4 * sizeof(uint64_t)) != hipSuccess ||
 		    hipMalloc(&ep->ctl_dev, ctl) != hipSuccess ||
-		    !(ep->ctl_host = calloc(1, ctl))) {
+		    !(ep->ctl_host = calloc(1, ctl)) || done_word_init(ep)) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
@@ -209,7 +236,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		if (hipStreamCreateWithFlags(&ep->stream, hipStreamNonBlocking) != hipSuccess ||
 		    hipStreamCreateWithFlags(&ep->copy_stream, hipStreamNonBlocking) != hipSuccess ||
 		    hipStreamCreateWithFlags(&ep->d2h_stream, hipStreamNonBlocking) != hipSuccess ||
-		    !(ep->ctl_host = calloc(1, ctl))) {
+		    !(ep->ctl_host = calloc(1, ctl)) || done_word_init(ep)) {
 			ep_release(ep);
 			return -LFA_EIO;
 		}
@@ -307,6 +334,9 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		for (int i = 0; i < LFA_STAGE_POOL; i++)
 			if (ep->stage[i].p)
 				hipFree(ep->stage[i].p);
+		for (int i = 0; i < ep->nev; i++)
+			hipEventDestroy(ep->evpool[i]);
+		done_word_free(ep);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -318,9 +348,11 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	p2p_release(&ep->world);
 	sig_word_free(&ep->world);
 	for (size_t i = 0; i < ep->qlen; i++)
-		hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
+		if (ep->q[(ep->qhead + i) % ep->qcap].ev)
+			hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
 	for (int i = 0; i < ep->nev; i++)
 		hipEventDestroy(ep->evpool[i]);
+	done_word_free(ep);
 	for (int i = 0; i < 8; i++)
 		if (ep->pc[i].valid)
 			plan_free(&ep->pc[i].pl);
@@ -508,6 +540,17 @@ static void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
 		hipEventDestroy(ev);
 }
 
+/* A completion event from the endpoint's pool (ep->lock held): creating
+ * one costs a runtime call per operation otherwise.  NULL on failure. */
+static hipEvent_t event_get(struct lfa_coll_ep *ep)
+{
+	hipEvent_t ev;
+
+	if (ep->nev)
+		return ep->evpool[--ep->nev];
+	return hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess ? ev : NULL;
+}
+
 /* A free slot at the tail of the FIFO of in-flight operations. */
 static struct pending *queue_slot(struct lfa_coll_ep *ep)
 {
@@ -527,13 +570,24 @@ static struct pending *queue_slot(struct lfa_coll_ep *ep)
 }
 
 static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
-			      void *context, int kind, struct lfa_coll_mc *mc)
+			      void *context, int kind, struct lfa_coll_mc *mc,
+			      uint64_t done_val)
 {
 	struct pending *p = queue_slot(ep);
 
 	if (!p)
 		return -LFA_ENOMEM;
 	memset(p, 0, sizeof(*p));
+	if (done_val) {
+		/* the one-shot kernel stores done_val into the completion word:
+		 * no event to record or query */
+		p->done_val = done_val;
+		p->context = context;
+		p->kind = kind;
+		p->mc = mc;
+		ep->qlen++;
+		return 0;
+	}
 	if (ep->nev)
 		p->ev = ep->evpool[--ep->nev];
 	else if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess)
@@ -653,18 +707,18 @@ static void hop_free(struct hop *h)
 		if (h->in_ev) {
 			if (!h->done)
 				hipEventSynchronize(h->in_ev);
-			hipEventDestroy(h->in_ev);
+			release_event(h->ep, h->in_ev);
 		}
 		if (h->out_ev) {
 			if (!h->done)
 				hipEventSynchronize(h->out_ev);
-			hipEventDestroy(h->out_ev);
+			release_event(h->ep, h->out_ev);
 		}
 		stage_put(h->ep, h->tmp);
 		stage_put(h->ep, h->st_in);
 		stage_put(h->ep, h->st_out);
 		if (h->fin)
-			hipEventDestroy(h->fin);
+			release_event(h->ep, h->fin);
 	} else {
 		free(h->tmp);
 	}
@@ -713,20 +767,20 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 			hipEvent_t last;
 			hipError_t e;
 
+			if (!h->issued && h->r.x.done_val) {
+				h->issued = 1;
+				LFA_TRACE("hop cid %#x issued (completion word %llu)",
+					  (unsigned)h->r.cid, (unsigned long long)h->r.x.done_val);
+			}
 			if (!h->issued) {
-				if (lfa_hip_note(&h->r.hip_err,
-						 hipEventCreateWithFlags(&h->fin, hipEventDisableTiming),
-						 "completion event create") != hipSuccess ||
+				if (!(h->fin = event_get(ep)) ||
 				    lfa_hip_note(&h->r.hip_err, hipEventRecord(h->fin, h->r.stream),
 						 "completion event record") != hipSuccess) {
 					h->err = -LFA_EIO;
 					continue;
 				}
 				if (h->out_bytes &&
-				    (lfa_hip_note(&h->r.hip_err,
-						  hipEventCreateWithFlags(&h->out_ev,
-									  hipEventDisableTiming),
-						  "staged result event create") != hipSuccess ||
+				    (!(h->out_ev = event_get(ep)) ||
 				     lfa_hip_note(&h->r.hip_err,
 						  hipStreamWaitEvent(ep->d2h_stream, h->fin, 0),
 						  "staged result wait") != hipSuccess ||
@@ -741,6 +795,13 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 				}
 				h->issued = 1;
 				LFA_TRACE("hop cid %#x issued", (unsigned)h->r.cid);
+			}
+			if (h->r.x.done_val) {
+				if (*(volatile uint64_t *)ep->done_word >= h->r.x.done_val) {
+					h->done = 1;
+					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
+				}
+				continue;
 			}
 			last = h->out_ev ? h->out_ev : h->fin;
 			e = hipEventQuery(last);
@@ -816,7 +877,8 @@ static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
 
 /* Completion state of a queued operation: 0 done, 1 pending, <0 / hip error
  * code (>0 in *perr) failed. */
-static int pending_state(const struct pending *p, int *perr)
+static int pending_state(const struct lfa_coll_ep *ep, const struct pending *p,
+			 int *perr)
 {
 	if (p->hop) {
 		if (p->hop->err) {
@@ -826,6 +888,8 @@ static int pending_state(const struct pending *p, int *perr)
 		}
 		return p->hop->done ? 0 : 1;
 	}
+	if (p->done_val)
+		return *(volatile uint64_t *)ep->done_word >= p->done_val ? 0 : 1;
 	hipError_t e = hipEventQuery(p->ev);
 
 	if (e == hipErrorNotReady)
@@ -841,9 +905,10 @@ static void pending_release(struct lfa_coll_ep *ep, struct pending *p)
 {
 	if (p->hop)
 		hop_free(p->hop);
-	else
+	else if (p->ev)
 		release_event(ep, p->ev);
 	p->hop = NULL;
+	p->ev = NULL;
 }
 
 /* Reap completed operations in issue order. */
@@ -855,7 +920,7 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 		host_progress_all(ep);
 	while (ep->qlen && !ep->have_err) {
 		struct pending *p = &ep->q[ep->qhead];
-		int perr = 0, st = pending_state(p, &perr);
+		int perr = 0, st = pending_state(ep, p, &perr);
 
 		if (st > 0)
 			break;
@@ -961,7 +1026,7 @@ ssize_t lfa_eq_read(struct lfa_coll_ep *ep, uint32_t *event,
 
 		progress(ep, tmp, 0, &n);
 		if (ep->qlen && ep->q[ep->qhead].kind == 1 &&
-		    pending_state(&ep->q[ep->qhead], &perr) > 0)
+		    pending_state(ep, &ep->q[ep->qhead], &perr) > 0)
 			break;
 	}
 	if (ep->dom->host && !(ep->qlen && ep->q[ep->qhead].kind == 1))
@@ -1556,6 +1621,36 @@ static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
 }
 
 /*
+ * A small reducing collective of a one-member group (allreduce, reduce,
+ * reduce_scatter: each a copy of the input) as the one-shot kernel with
+ * n = 1: one launch that ends in the completion word, so the operation
+ * completes without an event (the plan would be one COPY
+ * item plus an event record and query).
+ */
+static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
+		    enum lfa_datatype dt, enum lfa_op op)
+{
+	struct lfa_oneshot a;
+	int ret;
+
+	memset(&a, 0, sizeof(a));
+	a.send = buf;
+	a.result = result;
+	a.count = count;
+	a.mode = LFA_ONESHOT_ALL;
+	a.n = 1;
+	a.rank = 0;
+	a.done_ctr = ep->done_ctr;
+	a.done_word = ep->done_word;
+	a.done_val = ep->done_seq + 1;
+	ret = lfa_oneshot_reduce_async(op, dt, &a, ep->stream);
+	if (ret)
+		return ret;
+	ep->op_done_val = ++ep->done_seq;
+	return 0;
+}
+
+/*
  * One operation on device buffers, enqueued on ep->stream.
  */
 static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
@@ -1569,9 +1664,14 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	struct xctx x;
 	int ret;
 
+	ep->op_done_val = 0;
 	if (algo == LFA_ALGO_RCCL && mc->size > 1 &&
 	    try_rccl(mc, coll, buf, result, count, root, dt, op, s, &ret))
 		return ret;
+	if (mc->size == 1 && s == ep->stream && ep->done_word &&
+	    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE || coll == LFA_REDUCE_SCATTER) &&
+	    count * esz <= LFA_ONESHOT_SOLO_BYTES)
+		return run_solo(ep, buf, result, count, dt, op);
 	if (algo == LFA_ALGO_AUTO)
 		algo = (enum lfa_coll_algo)lfa_coll_auto_algo(coll, count, mc->size, esz,
 							       mc->p2p_state >= 0);
@@ -1601,6 +1701,14 @@ replan:
 		x.ticket = ++mc->p2p_ticket;
 		x.sym = mc->sym;
 		x.region = mc->sym_region;
+		if (pl->nsteps == 1 && pl->steps[0].type == LFA_STEP_ONESHOT &&
+		    s == ep->stream && ep->done_word) {
+			/* the small bucket is one kernel: it ends in the
+			 * completion word, no event */
+			x.done_ctr = ep->done_ctr;
+			x.done_word = ep->done_word;
+			x.done_seq = &ep->done_seq;
+		}
 	}
 	ret = grow(&ep->ws, &ep->ws_size, pl->tmp, s);
 	if (!ret) {
@@ -1609,6 +1717,8 @@ replan:
 		x.base[LFA_BUF_TMP] = ep->ws;
 		ret = exec_plan(mc, pl, &x, op, dt, s);
 	}
+	if (!ret)
+		ep->op_done_val = x.done_val;
 	return ret;
 }
 
@@ -1850,6 +1960,14 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	}
 	h->dev = dev != 0;
 	h->r.stream = ep->stream;
+	if (dev == 1 && sym && h->pl.nsteps == 1 && h->pl.steps[0].type == LFA_STEP_ONESHOT &&
+	    ep->done_word) {
+		/* one kernel in place on device buffers: it ends in the
+		 * completion word, no event */
+		h->r.x.done_ctr = ep->done_ctr;
+		h->r.x.done_word = ep->done_word;
+		h->r.x.done_seq = &ep->done_seq;
+	}
 	if (dev) {
 		hipSetDevice(ep->dom->device);
 		if (h->pl.tmp && !(h->tmp = stage_get(ep, h->pl.tmp)))
@@ -1871,10 +1989,8 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		/* H2D on the copy stream now: a chunked operation's later chunks
 		 * upload while the earlier ones reduce (host_progress_all makes
 		 * the run wait for in_ev) */
-		if (hipEventCreateWithFlags(&h->in_ev, hipEventDisableTiming) != hipSuccess) {
-			h->in_ev = NULL;
+		if (!(h->in_ev = event_get(ep)))
 			return -LFA_EIO;
-		}
 		if (hipMemcpyAsync(h->st_in, buf, in_b, hipMemcpyHostToDevice,
 				   ep->copy_stream) != hipSuccess ||
 		    hipEventRecord(h->in_ev, ep->copy_stream) != hipSuccess)
@@ -1984,7 +2100,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 {
 	struct lfa_coll_mc *mc;
 	size_t esz, chunk;
-	uint64_t t0;
+	uint64_t t0, done_val = 0;
 	int root = -1, ret, host, chunkable;
 
 	if (!ep)
@@ -2058,8 +2174,11 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		ret = run_device_chunked(ep, mc, coll, buf, result, count, root, dt, op,
 					 chunk);
 	} else if (!host) {
+		/* a small bucket's one-shot kernel ends in the completion word */
+		ep->op_done_val = 0;
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
 				 ep->stream, ep->algo);
+		done_val = ep->op_done_val;
 	} else if (chunkable) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op, chunk);
@@ -2079,7 +2198,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 				     root, dt, op);
 	}
 	if (!ret)
-		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, done_val);
 	if (!ret)
 		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
@@ -2194,6 +2313,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 	}
 	hipSetDevice(ep->dom->device);
 	t0 = mc->p2p_ticket;
+	ep->op_done_val = 0;
 	ep->barrier_host[0] = ~(uint64_t)mc->rank;
 	ret = hipMemcpyAsync(ep->barrier_dev, ep->barrier_host, sizeof(uint64_t),
 			     hipMemcpyHostToDevice, ep->stream) == hipSuccess ?
@@ -2203,7 +2323,7 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 				 (uint64_t *)ep->barrier_dev + 1, 1, -1, LFA_UINT64,
 				 LFA_BAND, ep->stream, ep->algo);
 	if (!ret)
-		ret = enqueue_completion(ep, ep->stream, context, 0, NULL);
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, ep->op_done_val);
 	if (!ret)
 		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
@@ -2442,7 +2562,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 					       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
 		}
 		if (!ret)
-			ret = enqueue_completion(ep, ep->stream, context, 1, mc);
+			ret = enqueue_completion(ep, ep->stream, context, 1, mc, 0);
 		if (!ret)
 			tag_p2p(ep, over, t0);
 	}

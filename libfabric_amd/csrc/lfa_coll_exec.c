@@ -224,7 +224,14 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 	a.status = mc->sig_word;
 	a.ticket = r->x.ticket;
 	a.timeout_us = sig_timeout_us();
+	if (r->x.done_word && r->x.done_seq) {
+		a.done_ctr = r->x.done_ctr;
+		a.done_word = r->x.done_word;
+		a.done_val = *r->x.done_seq + 1;
+	}
 	ret = lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
+	if (!ret && a.done_word)
+		r->x.done_val = ++*r->x.done_seq;
 	LFA_TRACE("cid %#x one-shot launched (epoch %u, rc %d)", (unsigned)r->cid, a.epoch, ret);
 	if (!ret) {
 		mc->os_epoch++;

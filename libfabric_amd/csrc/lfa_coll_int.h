@@ -36,6 +36,13 @@ struct xctx {
 	char *const *sym;       /* [group rank] */
 	size_t region;
 	uint64_t ticket;        /* the group's P2P operation number (timeouts) */
+	/* completion word (lfa_signal.h struct lfa_oneshot): set by the caller
+	 * when the plan's one step is the one-shot kernel; the launch takes
+	 * its value from *done_seq (stream order) and reports it in done_val */
+	uint32_t *done_ctr;
+	uint64_t *done_word;
+	uint64_t *done_seq;
+	uint64_t done_val;
 };
 
 /* ====================================================================== */
@@ -102,6 +109,9 @@ struct pending {
 	struct lfa_coll_mc *pmc;
 	uint64_t ticket;
 	int timed_out;
+	/* device domains: completes when the endpoint's completion word reaches
+	 * done_val (the one-shot kernel wrote it; no event), 0: the event */
+	uint64_t done_val;
 	/* the chunks of one chunked operation (peer_submit_chunked) share a
 	 * nonzero chain id: the operation posts ONE completion — the first
 	 * chunk's error, or the last chunk's success */
@@ -142,6 +152,14 @@ struct lfa_coll_ep {
 	uint8_t cid_mask[LFA_CID_BYTES];
 	struct lfa_coll_mc world;
 	hipEvent_t evpool[64];      /* recycled completion events */
+	/* the completion word of small operations: the last
+	 * workgroup of a one-shot kernel on ep->stream counts in done_ctr and
+	 * stores the launch's value (done_seq, in stream order) into done_word,
+	 * which the host reads instead of querying an event */
+	uint32_t *done_ctr;         /* device, 0 at rest */
+	uint64_t *done_word;        /* host-mapped */
+	uint64_t done_seq;
+	uint64_t op_done_val;       /* run_device's last launch's value, or 0 */
 	int nev;
 	struct plan_cache {         /* last schedules built, keyed by shape */
 		int valid, coll, algo, rank, n, root;

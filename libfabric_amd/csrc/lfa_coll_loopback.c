@@ -79,7 +79,8 @@ int lfa_coll_loopback(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 		done = 1;
 		progressed = 0;
 		for (int r = 0; r < n && !ret; r++) {
-			struct xctx xc = {{send[r], result[r], tmp[r]}, sym, region};
+			struct xctx xc = { .base = { send[r], result[r], tmp[r] }, .sym = sym,
+					   .region = region };
 
 			if (coll == LFA_BROADCAST)
 				xc.base[LFA_BUF_SEND] = result[r];

@@ -13,6 +13,9 @@
 
 #define LFA_INTERNAL __attribute__((visibility("hidden")))
 #define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
+/* a one-member group's reducing collective of at most this many bytes runs
+ * as the n = 1 one-shot kernel with the completion word (run_solo) */
+#define LFA_ONESHOT_SOLO_BYTES (256u << 10)
 #define LFA_OS_RS_BYTES (1u << 20)      /* P2P reduce_scatter: one-shot */
 
 /* A heap-allocated plan. */

@@ -671,6 +671,9 @@ struct OsArgs {
   int n, rank;
   int vec;                     // every range start and result 16-B aligned
   int unal;                    // send or result not aligned to the element
+  uint32_t *done_ctr;          // completion word (lfa_signal.h), optional
+  uint64_t *done_word;
+  uint64_t done_val;
 };
 
 template <int OP, typename T, int NLEAF>
@@ -698,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   //    share a CU and so an L2 — and one post per peer
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (LFA_OS_WAVE_FENCES || t < 64)  // wave 0: the posting lanes
+  if (a.n > 1 && (LFA_OS_WAVE_FENCES || t < 64))  // wave 0: the posting lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if ((int)t < a.n && (int)t != a.rank) {
     __hip_atomic_store(a.post[t] + b * LFA_SIG_MAX, a.epoch, __ATOMIC_RELAXED,
@@ -717,36 +720,56 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   }
   // the waiting wave acquires for the workgroup (same CU, same L2), then
   // every wave may read what the peers pushed
-  if (LFA_OS_WAVE_FENCES || t < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (a.n > 1 && (LFA_OS_WAVE_FENCES || t < 64)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
   // 4. reduce chunk b of this rank's own range over every rank's input, rank
   //    order (system-scope loads: the slots were written by peers over xGMI)
   const size_t own = a.slen[a.rank];
-  if (lo >= own) return;
-  const size_t hi = lo + a.chunk < own ? lo + a.chunk : own;
-  const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;
-  for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16) {
-    u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
-      return __builtin_bit_cast(
-          u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)own),
-                                                       (unsigned)o, 0, kSysLoadAux));
-    });
-    *(u32x4 *)(a.result + o) = v;
+  if (lo < own) {
+    const size_t hi = lo + a.chunk < own ? lo + a.chunk : own;
+    const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;
+    for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16) {
+      u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
+        return __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)own),
+                                                         (unsigned)o, 0, kSysLoadAux));
+      });
+      *(u32x4 *)(a.result + o) = v;
+    }
+    if (a.unal) {
+      // the caller's own input and result, byte-wise (local memory); the
+      // peers' slots (256-B aligned) keep their system-scope loads
+      for (size_t e = lo / E + t; e < hi / E; e += kBlock)
+        st_bytes<T>(a.result, e, tree_eval_with<OP, T, T, NLEAF>(a.t, [&](int k) {
+                      return k == a.rank ? ld_bytes<T>(a.t.in[k], e)
+                                         : sys_load<T>((const T *)a.t.in[k] + e);
+                    }));
+    } else {
+      for (size_t e = vhi / E + t; e < hi / E; e += kBlock) {
+        T v = tree_eval_with<OP, T, T, NLEAF>(
+            a.t, [&](int k) { return sys_load<T>((const T *)a.t.in[k] + e); });
+        ((T *)a.result)[e] = v;
+      }
+    }
   }
-  if (a.unal) {
-    // the caller's own input and result, byte-wise (local memory); the
-    // peers' slots (256-B aligned) keep their system-scope loads
-    for (size_t e = lo / E + t; e < hi / E; e += kBlock)
-      st_bytes<T>(a.result, e, tree_eval_with<OP, T, T, NLEAF>(a.t, [&](int k) {
-                    return k == a.rank ? ld_bytes<T>(a.t.in[k], e)
-                                       : sys_load<T>((const T *)a.t.in[k] + e);
-                  }));
-    return;
-  }
-  for (size_t e = vhi / E + t; e < hi / E; e += kBlock) {
-    T v = tree_eval_with<OP, T, T, NLEAF>(
-        a.t, [&](int k) { return sys_load<T>((const T *)a.t.in[k] + e); });
-    ((T *)a.result)[e] = v;
+  // 5. completion word: this workgroup's result stores acknowledged, then
+  //    one system-scope release (its waves share a CU and an L2) before it
+  //    counts itself; the last workgroup resets the counter for the next
+  //    launch on the stream and publishes done_val to the host
+  if (a.done_word) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      if (seen + 1 == gridDim.x) {
+        __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -1260,8 +1283,8 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
   } else {
     constexpr size_t E = sizeof(T);
     const int n = h.n, r = h.rank;
-    if (n < 2 || n > kOsMax || r < 0 || r >= n || !h.sym || !h.status ||
-        h.mode < LFA_ONESHOT_SCATTER || h.mode >= n)
+    if (n < 1 || n > kOsMax || r < 0 || r >= n || (n > 1 && (!h.sym || !h.status)) ||
+        h.mode < LFA_ONESHOT_SCATTER || h.mode >= n || (h.done_word && !h.done_ctr))
       return -LFA_EINVAL;
     if (h.count == 0) return 0;
     OsArgs a;
@@ -1278,11 +1301,11 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       }
       if (a.slen[k] > most) most = a.slen[k];
     }
-    if (!h.send || (!h.result && a.slen[r]) ||
-        h.slot_bytes < most || h.slot_bytes % 256 || most > 0xffffffffu ||
-        h.parity_off % 256 || (size_t)n * h.slot_bytes > h.parity_off)
+    if (!h.send || (!h.result && a.slen[r]) || most > 0xffffffffu ||
+        (n > 1 && (h.slot_bytes < most || h.slot_bytes % 256 || h.parity_off % 256 ||
+                   (size_t)n * h.slot_bytes > h.parity_off)))
       return -LFA_EINVAL;
-    for (int k = 0; k < n; k++)
+    for (int k = 0; k < n && n > 1; k++)
       if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
     const void *srcs[kOsMax];
     const size_t par = (size_t)(h.epoch & 1) * h.parity_off;
@@ -1297,7 +1320,10 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       }
     }
     const int pof2 = tree_leaves(a.t, srcs, n);
-    a.wait = (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF);
+    a.wait = n > 1 ? (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF) : nullptr;
+    a.done_ctr = h.done_ctr;
+    a.done_word = h.done_word;
+    a.done_val = h.done_val;
     a.send = (const char *)h.send;
     a.result = (char *)h.result;
     a.status = h.status;
@@ -1314,6 +1340,9 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     // the same grid on every member: `most` depends only on count and n
     const unsigned grid = (unsigned)((most + a.chunk - 1) / a.chunk);
     switch (pof2) {
+      case 1:
+        hipLaunchKernelGGL((oneshot_reduce<OP, T, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+        break;
       case 2:
         hipLaunchKernelGGL((oneshot_reduce<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, a);
         break;

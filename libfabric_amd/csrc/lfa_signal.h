@@ -27,7 +27,7 @@ extern "C" {
  * by rank k's workgroup b */
 #define LFA_SIG_OS_OFF 256
 #define LFA_SIG_OS_CHUNKS 128
-#define LFA_OS_MAX_RANKS 8              /* one-shot groups: 2..8 members */
+#define LFA_OS_MAX_RANKS 8              /* one-shot groups: 1..8 members */
 
 /*
  * Timed-out waits.  *status is one host-mapped word per group holding the
@@ -63,7 +63,10 @@ int lfa_flag_barrier_async(uint32_t *const *post, const uint32_t *wait, int n,
  * whole vector (mode LFA_ONESHOT_ALL, allreduce), block k of
  * lfa_coll_block's partition (LFA_ONESHOT_SCATTER, reduce_scatter: result
  * receives this rank's block), or the whole vector for k == mode only
- * (reduce to root `mode`).  Slots are double-buffered by epoch parity in two
+ * (reduce to root `mode`).  n = 1 is the degenerate group: no pushes, no
+ * flags, no workspace (sym and status may be NULL) — the part is copied into
+ * `result` in one launch, the small-bucket path of a one-member group.
+ * Slots are double-buffered by epoch parity in two
  * FIXED halves of SYM_IN: member j holds rank k's part of epoch e at
  * sym[j] + (e & 1)·parity_off + k·slot_bytes, so a peer one operation ahead
  * never overwrites a slot still being read.  The halves must not move with
@@ -85,11 +88,20 @@ struct lfa_oneshot {
 	size_t slot_bytes;      /* one slot: the largest part, rounded up to 256 */
 	size_t parity_off;      /* odd epochs' slots: this far above the even ones */
 	size_t flag_off;        /* the flag area's offset in a workspace */
-	int n, rank;            /* 2 <= n <= LFA_OS_MAX_RANKS */
+	int n, rank;            /* 1 <= n <= LFA_OS_MAX_RANKS */
 	uint32_t epoch;         /* this group's one-shot operations so far + 1 */
 	uint64_t *status;       /* host-mapped; lowered to ticket on a timeout */
 	uint64_t ticket;        /* this P2P operation's number in the group */
 	uint64_t timeout_us;
+	/* Completion word, optional (done_word NULL: none):
+	 * every workgroup, its result stores acknowledged and released at
+	 * system scope, counts itself in *done_ctr (device memory, 0 at rest);
+	 * the last one resets it and stores done_val into *done_word
+	 * (host-mapped), so the host sees the operation complete with one
+	 * memory read, without an event record / query per operation. */
+	uint32_t *done_ctr;
+	uint64_t *done_word;
+	uint64_t done_val;
 };
 int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 				void *stream);

@@ -1116,3 +1116,78 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
   }
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
+
+// ---------------------------------------------------------------------------
+// Where a launch's fixed cost goes: the product combine body
+// (float SUM, LDS-DMA staged, 4 KiB per operand per wave) with a timestamp
+// pair per WAVE — s_memrealtime (the constant 100 MHz clock) when the wave
+// starts and after its stores are acknowledged (vmcnt(0)) — and the XCC the
+// wave ran on.  stamps[4·(4·b + w) ...] = {start, end, xcc, 0}.  Diagnostic
+// build only: the stamps go to their own buffer, no output depends on them.
+// ---------------------------------------------------------------------------
+namespace lfa {
+
+template <int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_stamped(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec,
+    unsigned long long *stamps) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      u32x4 v = apply_vec<OP_SUM, float>(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == kStoreNt)
+        st<true>(dst + base + u * 64 + l, v);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (l == 0) {
+    // HW_REG_XCC_ID (gfx940+): bits [3:0] the XCC this wave runs on
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 0xf;
+    unsigned long long *s = stamps + 4 * ((size_t)blockIdx.x * kLdsWaves + w);
+    s[0] = t0;
+    s[1] = t1;
+    s[2] = xcc;
+    s[3] = 0;
+  }
+}
+
+}  // namespace lfa
+
+extern "C" int lfa__tune_combine_stamped(void *dst, const void *src, size_t nvec,
+                                         int sc1, void *stamps, void *stream) {
+  using namespace lfa;
+  const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll, 0x7fffffffu));
+  if (sc1)
+    hipLaunchKernelGGL((combine_stamped<kUnroll, kStoreSc1>), grid, dim3(kLdsWaves * 64), 0,
+                       (hipStream_t)stream, (u32x4 *)dst, (const u32x4 *)src, nvec,
+                       (unsigned long long *)stamps);
+  else
+    hipLaunchKernelGGL((combine_stamped<kUnroll, kStoreNt>), grid, dim3(kLdsWaves * 64), 0,
+                       (hipStream_t)stream, (u32x4 *)dst, (const u32x4 *)src, nvec,
+                       (unsigned long long *)stamps);
+  return hipGetLastError() == hipSuccess ? (int)grid.x : -LFA_EIO;
+}
