@@ -343,8 +343,13 @@ ssize_t lfa_cq_read(struct lfa_coll_ep *ep, struct lfa_cq_entry *buf,
 ssize_t lfa_cq_readerr(struct lfa_coll_ep *ep, struct lfa_cq_err_entry *buf);
 ssize_t lfa_eq_read(struct lfa_coll_ep *ep, uint32_t *event,
 		    struct lfa_eq_entry *entry);
-/* Blocks until every queued operation has completed (convenience). */
+/* Blocks until every queued operation has completed (convenience); on a GPU
+ * peer domain it also frees the idle staging buffers. */
 int lfa_coll_ep_flush(struct lfa_coll_ep *ep);
+/* Device bytes a GPU peer domain's staging pool holds (busy and idle):
+ * bounded by what operations in flight use plus 1 GiB kept idle, and 0 idle
+ * after lfa_coll_ep_flush (diagnostics, tests). */
+size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep);
 
 /* ---- schedules as data ------------------------------------------------ */
 

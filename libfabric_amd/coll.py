@@ -136,6 +136,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_group_chunk.argtypes = [c_size_t, c_int, c_size_t]
     L.lfa_coll_ep_flush.restype = c_int
     L.lfa_coll_ep_flush.argtypes = [c_void_p]
+    L.lfa_coll_ep_stage_bytes.restype = c_size_t
+    L.lfa_coll_ep_stage_bytes.argtypes = [c_void_p]
     L.lfa_coll_world_addr.restype = c_uint64
     L.lfa_coll_world_addr.argtypes = [c_void_p]
     L.lfa_join_collective.restype = c_int
@@ -395,6 +397,15 @@ class Endpoint:
         _chk(lib().lfa_mc_counters(self.ep, coll_addr or self.world, ctypes.byref(c)),
              "lfa_mc_counters")
         return {k: getattr(c, k) for k, _ in McCounters._fields_}
+
+    def flush(self) -> None:
+        """lfa_coll_ep_flush: every queued operation completed (peer domains:
+        idle staging buffers freed)."""
+        _chk(lib().lfa_coll_ep_flush(self.ep), "lfa_coll_ep_flush")
+
+    def stage_bytes(self) -> int:
+        """lfa_coll_ep_stage_bytes: device bytes in the staging pool."""
+        return lib().lfa_coll_ep_stage_bytes(self.ep)
 
     def seed_ticket(self, ticket: int, coll_addr: int | None = None) -> None:
         """lfa_mc_seed_ticket (test entry): the group's P2P tickets continue

@@ -210,6 +210,8 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 		const char *e = getenv("LFA_GROUP_CHUNK_BYTES");
 
 		ep->group_chunk = e ? (size_t)strtoull(e, NULL, 0) : LFA_GROUP_CHUNK_AUTO;
+		e = getenv("LFA_STAGE_POOL_BYTES");
+		ep->stage_cap = e ? (size_t)strtoull(e, NULL, 0) : LFA_STAGE_POOL_BYTES;
 	}
 	/* the P2P workspace exchange needs these on every member even when a
 	 * local allocation fails later, so they exist up front */
@@ -680,16 +682,60 @@ static void *stage_get(struct lfa_coll_ep *ep, size_t bytes)
 	return hipMalloc(&p, bytes) == hipSuccess ? p : NULL;
 }
 
+/* Idle bytes in the staging pool (ep->lock held). */
+static size_t stage_idle(const struct lfa_coll_ep *ep)
+{
+	size_t idle = 0;
+
+	for (int i = 0; i < LFA_STAGE_POOL; i++)
+		if (ep->stage[i].p && !ep->stage[i].busy)
+			idle += ep->stage[i].bytes;
+	return idle;
+}
+
+/* Back to the pool; freed instead when the pool's idle bytes would pass
+ * LFA_STAGE_POOL_BYTES (a sweep of sizes or many chunks in
+ * flight otherwise pinned the sum of every buffer until close). */
 static void stage_put(struct lfa_coll_ep *ep, void *p)
 {
 	if (!p)
 		return;
 	for (int i = 0; i < LFA_STAGE_POOL; i++)
 		if (ep->stage[i].p == p) {
+			if (stage_idle(ep) + ep->stage[i].bytes > ep->stage_cap) {
+				hipFree(p);
+				ep->stage[i].p = NULL;
+				ep->stage[i].bytes = 0;
+			}
 			ep->stage[i].busy = 0;
 			return;
 		}
 	hipFree(p);
+}
+
+/* Free every idle staging buffer (ep->lock held). */
+static void stage_trim(struct lfa_coll_ep *ep)
+{
+	for (int i = 0; i < LFA_STAGE_POOL; i++)
+		if (ep->stage[i].p && !ep->stage[i].busy) {
+			hipFree(ep->stage[i].p);
+			ep->stage[i].p = NULL;
+			ep->stage[i].bytes = 0;
+		}
+}
+
+size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep)
+{
+	size_t n = 0;
+
+	if (!ep)
+		return 0;
+	pthread_mutex_lock(&ep->lock);
+	for (int i = 0; i < LFA_STAGE_POOL; i++)
+		if (ep->stage[i].p)
+			n += ep->stage[i].bytes;
+	pthread_mutex_unlock(&ep->lock);
+	return n;
 }
 
 static void hop_free(struct hop *h)
@@ -1061,6 +1107,8 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 				else if (h && !h->done)
 					busy = 1;
 			}
+			if (!busy && !err)
+				stage_trim(ep);
 			pthread_mutex_unlock(&ep->lock);
 			if (err)
 				return err;

@@ -27,6 +27,10 @@
 /* Bytes of one P2P handle-exchange record (struct sym_rec, lfa_coll.c). */
 #define LFA_SYM_REC_BYTES 80
 #define LFA_STAGE_POOL 128              /* peer-domain staging buffers kept */
+/* idle staging bytes the pool keeps by default (the endpoint's
+ * stage_cap, LFA_STAGE_POOL_BYTES at open): a buffer returned above it is
+ * freed, and lfa_coll_ep_flush frees every idle one */
+#define LFA_STAGE_POOL_BYTES ((size_t)1 << 30)
 
 /* Where a plan's refs point for one execution: the operation's buffers and,
  * for LFA_ALGO_P2P, every group rank's symmetric workspace as mapped here
@@ -145,6 +149,7 @@ struct lfa_coll_ep {
 		size_t bytes;
 		int busy;
 	} stage[LFA_STAGE_POOL];
+	size_t stage_cap;           /* idle staging bytes kept */
 	uint64_t *barrier_host;     /* pinned ~rank for barrier */
 	void *barrier_dev;          /* 2 x uint64 */
 	void *ctl_dev;              /* P2P handle exchange, nranks records */

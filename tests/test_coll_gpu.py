@@ -394,7 +394,7 @@ def test_group_chunk_device_and_host_members(coll, ep):
             ep.wait(ep.broadcast(b, count, 0, 9))
             assert torch.equal(b, dx), ("broadcast", group)
     finally:
-        ep.set_group_chunk(0)
+        ep.set_group_chunk(coll.GROUP_CHUNK_AUTO)   # the default
         ep.set_chunk(0)
 
 

@@ -194,7 +194,7 @@ def _group_chunk(ep, rank, world, oracle, coll):
                         assert got.tobytes() == want.tobytes(), ("group chunk reduce", algo,
                                                                  group, rt)
     finally:
-        ep.set_group_chunk(0)
+        ep.set_group_chunk(coll.GROUP_CHUNK_AUTO)   # the default
 
 
 def _set_order(ep, rank, world, oracle, coll):
@@ -475,6 +475,59 @@ def test_p2p_tickets_cross_2_pow_32():
     one-shot and two-barrier allreduces in flight across the boundary: all
     complete, bit-exact, with no timeout recorded."""
     _spawn(_ticket_wrap_worker, 2)
+
+
+def _stage_pool_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1",
+                          LFA_STAGE_POOL_BYTES=str(8 << 20))
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        msg = "ok"
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            ep.set_group_chunk(0)
+            # rank 0 on host buffers: every operation stages its input and
+            # output through the pool; a sweep of sizes, each larger than the
+            # last, would have kept every one of them
+            for k, mib in enumerate((1, 2, 3, 5, 6)):
+                n = (mib << 20) // 4
+                sends = _inputs(oracle, 8, n, world, 900 + k)
+                want = oracle.allreduce(2, 8, sends)[0]
+                x = sends[rank] if rank == 0 else _dev(sends[rank])
+                r = np.zeros(n, np.float32) if rank == 0 else torch.zeros(n, device="cuda")
+                _ready()
+                ep.wait(ep.allreduce(x, r, n, 8, 2))
+                got = r if rank == 0 else r.cpu().numpy()
+                if got.tobytes() != want.tobytes():
+                    msg = f"allreduce of {mib} MiB wrong"
+            held = ep.stage_bytes()
+            if held > (8 << 20):
+                msg = f"idle staging {held} B after the sweep, cap 8 MiB"
+            ep.flush()
+            if ep.stage_bytes():
+                msg = f"{ep.stage_bytes()} B still staged after flush"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_staging_pool_is_bounded():
+    """the peer domain's staging pool keeps at most its cap of
+    idle bytes (LFA_STAGE_POOL_BYTES, 1 GiB by default; 8 MiB here) across
+    a sweep of sizes with a host-buffer member, results exact, and
+    lfa_coll_ep_flush frees every idle buffer."""
+    _spawn(_stage_pool_worker, 2)
 
 
 def _chunk_error_worker(rank, world, port, q):

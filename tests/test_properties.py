@@ -632,7 +632,7 @@ def test_gpu_rccl_domain_world1_any_call(ep1, kind, algo, pair, count, host, gch
         got = get(dst)
         assert got.tobytes() == data.tobytes(), (kind, algo, count, host, gchunk, off)
     finally:
-        ep.set_group_chunk(0)
+        ep.set_group_chunk(coll.GROUP_CHUNK_AUTO)   # the default
 
 
 @pytest.fixture(scope="module")
