@@ -995,6 +995,12 @@ def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
         t = max_over_ranks(time.perf_counter() - t0, world) / reps
         sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+        if nbytes <= (1 << 20):
+            # latency: one operation submitted and reaped at a time, in C
+            # (liblfa_bench.so), without the Python wrapper's ~10 us per call
+            barrier(world)
+            sweep[str(nbytes)]["latency_c_loop_us"] = round(max_over_ranks(
+                ep.bench_loop(5, a, b, cnt, 9, 3, reps=200), world), 1)
         if algo == coll.ALGO_AUTO:
             # the per-bucket choice (lfa_coll_auto_algo; the same on every rank)
             chosen = coll.auto_algo(5, cnt, world, 8)

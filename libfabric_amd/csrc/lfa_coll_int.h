@@ -150,6 +150,8 @@ struct lfa_coll_ep {
 		int busy;
 	} stage[LFA_STAGE_POOL];
 	size_t stage_cap;           /* idle staging bytes kept */
+	int stage_trim_due;         /* idle bytes passed the cap: trim when the
+				     * queue has drained */
 	uint64_t *barrier_host;     /* pinned ~rank for barrier */
 	void *barrier_dev;          /* 2 x uint64 */
 	void *ctl_dev;              /* P2P handle exchange, nranks records */

@@ -337,6 +337,50 @@ def test_rccl_allreduce_device_and_host(coll, ep):
     ep.set_chunk(0)
 
 
+def test_completion_word_interleaved_with_events(coll, ep):
+    """a one-member group runs small reducing collectives as
+    the n = 1 one-shot kernel, which completes through the endpoint's
+    completion word (no event); larger ones, allgather, broadcast and the
+    barrier keep events.  Sixty operations of both kinds in flight at once,
+    every op and datatype class, unaligned buffers among them: completions
+    in issue order, every result the copy the reference defines."""
+    rng = np.random.default_rng(11)
+    cases = []
+    for k in range(60):
+        dt, op = CASES[k % len(CASES)]
+        nd = oracle.DT_NP[dt]
+        count = int(rng.choice([1, 33, 1024, 65_536 // nd.itemsize,
+                                (256 << 10) // nd.itemsize, (300 << 10) // nd.itemsize]))
+        off = int(rng.integers(0, 3)) * nd.itemsize if k % 5 == 0 else 0
+        src = _inputs(dt, 1, count, 1000 + k)[0]
+        buf = torch.zeros(off + count * nd.itemsize + 64, dtype=torch.uint8, device=DEV)
+        buf[off:off + count * nd.itemsize] = torch.from_numpy(src.view(np.uint8).copy())
+        res = torch.zeros_like(buf)
+        cases.append((dt, op, count, off, src, buf, res, k % 3))
+    torch.cuda.synchronize()
+    e = ep._ep          # buffers are ready: submit without a sync in between
+    ctxs = []
+    for dt, op, count, off, src, buf, res, kind in cases:
+        x, y = buf[off:], res[off:]
+        if kind == 0:
+            ctxs.append(e.allreduce(x, y, count, dt, op))
+        elif kind == 1:
+            ctxs.append(e.reduce_scatter(x, y, count, dt, op))
+        else:
+            ctxs.append(e.reduce(x, y, count, 0, dt, op))
+        if len(ctxs) % 7 == 0:
+            ctxs.append(e.barrier())
+    done = []
+    while len(done) < len(ctxs):
+        done += e.cq_read()
+    assert done == ctxs
+    for dt, op, count, off, src, buf, res, kind in cases:
+        nb = count * oracle.DT_NP[dt].itemsize
+        got = res[off:off + nb].cpu().numpy().view(oracle.DT_NP[dt])
+        assert got.tobytes() == src.tobytes(), (dt, op, count, off, kind)
+        assert not res[:off].any() and not res[off + nb:].any(), "wrote outside"
+
+
 def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
     """reduce and reduce_scatter on host buffers go through the chunked
     H2D / collective / D2H pipeline (reduce_scatter: one 2-D H2D per chunk);

@@ -21,6 +21,9 @@
 #                P2P, C-timed loop (liblfa_bench.so) and its breakdown
 #   sizes        combine kernel durations vs size under --kernel-trace
 #   host2        2-process host-buffer allreduce, default vs group chunks
+#   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
+#   tplayout     8->8 tree_put per buffer set and per pool pitch
+#   ramp         per-wave timestamps of one combine launch (ramp / drain)
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -67,6 +70,12 @@ for stage in "$@"; do
       $S ksizes 300 $P -d gpurun_out/ksizes -o run -- python3 bench.py --only-extra sizes || exit 99 ;;
     host2)
       $S host2 300 python3 -u tools/probe_host_group_chunk.py || exit 99 ;;
+    ipc)
+      $S ipc_growth 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
+    tplayout)
+      $S treeput_layout 300 python3 -u tools/probe_treeput_layout.py || exit 99 ;;
+    ramp)
+      $S ramp 300 python3 -u tools/probe_ramp.py || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac

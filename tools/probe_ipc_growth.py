@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""The P2P workspace export path under repetition, GPU box.
+
+Round 3 saw hipIpcGetMemHandle return "invalid argument" twice, each time on
+one member of a 5- or 8-process group at the workspace's SECOND growth (the
+8 MiB region to 16 MiB, exported while the old workspace and the peers'
+mappings were still held).  This probe drives exactly that path — the
+provider's own sym_prepare / sym_open / sym_free through LFA_ALGO_P2P
+allreduces on GPU peer domains — many times: every cycle opens an endpoint,
+grows its workspace four times (regions 8, 16, 32, 64 MiB) with torch
+allocations churning between the steps, checks every result, and closes it.
+With LFA_DEBUG every failed export prints the failing pointer, what HIP says
+about it and every earlier workspace event of the process overlapping it
+(lfa_coll.c va_explain); the worker counts those lines.
+
+    python tools/probe_ipc_growth.py [--world 8] [--cycles 12]
+prints one JSON line: exports attempted, failures, and the diagnostics.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+SIZES = (1 << 20, 12 << 20, 24 << 20, 48 << 20)   # bytes: workspace regions 8, 16, 32, 64 MiB
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cycles, logdir, q):
+    try:
+        log = open(os.path.join(logdir, f"r{rank}.log"), "w", buffering=1)
+        os.dup2(log.fileno(), 2)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        bad = 0
+        churn = []
+        for c in range(cycles):
+            ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+            try:
+                ep.set_algo(coll.ALGO_P2P)
+                ep.set_group_chunk(0)
+                for k, nbytes in enumerate(SIZES):
+                    n = nbytes // 4
+                    x = torch.full((n,), float(rank + 1), device="cuda")
+                    r = torch.empty_like(x)
+                    # allocator churn between the growths, as a caller's
+                    # tensors come and go
+                    churn.append(torch.empty((1 + (c + k) % 5) << 20, dtype=torch.uint8,
+                                             device="cuda"))
+                    if len(churn) > 6:
+                        churn.pop(0)
+                    torch.cuda.synchronize()
+                    ep.wait(ep.allreduce(x, r, n, 8, 2))
+                    want = world * (world + 1) / 2
+                    if not bool((r == want).all()):
+                        bad += 1
+            finally:
+                ep.close()
+            dist.barrier()
+        dist.destroy_process_group()
+        log.flush()
+        q.put((rank, {"wrong_results": bad}))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--cycles", type=int, default=12)
+    a = ap.parse_args()
+    import torch.multiprocessing as mp
+    logdir = os.path.join(ROOT, "gpurun_out", "ipc_growth_logs")
+    os.makedirs(logdir, exist_ok=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.cycles, logdir, q))
+             for r in range(a.world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(a.world):
+            r, v = q.get(timeout=600)
+            res[r] = v
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    fails, notes = 0, []
+    for r in range(a.world):
+        with open(os.path.join(logdir, f"r{r}.log")) as f:
+            lines = [ln.rstrip() for ln in f if ln.startswith("lfa:")]
+        fails += sum("export failed" in ln for ln in lines)
+        notes += [f"r{r}: {ln}" for ln in lines][:40]
+    out = {"world": a.world, "cycles": a.cycles,
+           "exports": a.world * a.cycles * 4, "export_failures": fails,
+           "per_rank": res, "diagnostics": notes[:200]}
+    print(json.dumps({"probe_ipc_growth": out}), flush=True)
+    if not all(isinstance(v, dict) for v in res.values()):
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

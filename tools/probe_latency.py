@@ -115,6 +115,14 @@ def _worker(rank, world, port, reps, q):
             out["p2p_allreduce_4kib"] = _split(ep, 3, x, r, 1024, 8, 2, reps)
             dist.barrier()
             out["p2p_reduce_scatter_4kib_double_prod"] = _split(ep, 5, xd, rd, 512, 9, 3, reps)
+            # which part of the reduce_scatter's extra cost is the collective
+            # and which the (op, datatype)
+            dist.barrier()
+            rf = torch.empty(512, device="cuda")
+            out["p2p_reduce_scatter_4kib_float_sum"] = _split(ep, 5, x, rf, 1024, 8, 2, reps)
+            dist.barrier()
+            rdd = torch.empty(512, device="cuda", dtype=torch.float64)
+            out["p2p_allreduce_4kib_double_prod"] = _split(ep, 3, xd, rdd, 512, 9, 3, reps)
             out["counters"] = ep.counters()
         finally:
             ep.close()
