@@ -11,6 +11,8 @@
 //             round trip), then ds_read_b128 -> add -> global store
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+#include <time.h>
 
 #include "lfa_kernels.hpp"
 
@@ -1190,4 +1192,116 @@ extern "C" int lfa__tune_combine_stamped(void *dst, const void *src, size_t nvec
                        (hipStream_t)stream, (u32x4 *)dst, (const u32x4 *)src, nvec,
                        (unsigned long long *)stamps);
   return hipGetLastError() == hipSuccess ? (int)grid.x : -LFA_EIO;
+}
+
+// ---------------------------------------------------------------------------
+// Where a small operation's time goes after the launch: a
+// one-workgroup copy of `bytes` (<= 4 KiB) that ends in a host-mapped
+// completion word, timed from the host (launch call -> word seen) in a loop.
+//   mode 0  the product: the one-shot launcher with n = 1 (float FI_SUM over
+//           one rank: a copy) and the word
+//   mode 1  this file's copy of that body: stores, waitcnt, system release,
+//           agent counter, system release, word
+//   mode 2  the same without either system release (diagnostic only: the
+//           data are not ordered before the word)
+//   mode 3  write-through (sc0 sc1) data stores, then the releases
+//   mode 4  no data: the counter and the word only, with the releases
+//   mode 5  no data, no releases: the word alone
+// Returns the mean microseconds per operation in *us.
+// ---------------------------------------------------------------------------
+namespace lfa {
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void solo_diag(const u32x4 *src, u32x4 *dst,
+                                                    unsigned nvec, uint32_t *ctr,
+                                                    uint64_t *word, uint64_t val) {
+  const unsigned t = threadIdx.x;
+  if constexpr (MODE <= 3) {
+    if (t < nvec) {
+      u32x4 v = src[t];
+      if constexpr (MODE == 3)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(nvec * 16), 0x00020000), t * 16,
+            0, kSysAux);
+      else
+        dst[t] = v;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) {
+    if constexpr (MODE != 2 && MODE != 5) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const uint32_t seen =
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen + 1 == gridDim.x) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (MODE != 2 && MODE != 5) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+}  // namespace lfa
+
+extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size_t bytes,
+                                      int reps, double *us) {
+  using namespace lfa;
+  hipStream_t s;
+  uint32_t *ctr = nullptr;
+  uint64_t *word = nullptr;
+  if (bytes > 4096 || bytes % 16 || reps <= 0 || !us) return -LFA_EINVAL;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -LFA_EIO;
+  if (hipMalloc((void **)&ctr, 4) != hipSuccess ||
+      hipHostMalloc((void **)&word, 8, hipHostMallocCoherent) != hipSuccess ||
+      hipMemset(ctr, 0, 4) != hipSuccess) {
+    hipStreamDestroy(s);
+    return -LFA_EIO;
+  }
+  *(volatile uint64_t *)word = 0;
+  const unsigned nvec = (unsigned)(bytes / 16);
+  struct lfa_oneshot a;
+  memset(&a, 0, sizeof(a));
+  a.send = src;
+  a.result = dst;
+  a.count = bytes / 4;
+  a.mode = LFA_ONESHOT_ALL;
+  a.n = 1;
+  a.done_ctr = ctr;
+  a.done_word = word;
+  int rc = 0;
+  double t0 = 0;
+  for (int i = -50; i < reps && !rc; i++) {  // 50 untimed: code load, clocks
+    if (i == 0) {
+      struct timespec ts;
+      clock_gettime(CLOCK_MONOTONIC, &ts);
+      t0 = ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+    }
+    const uint64_t val = (uint64_t)(i + 51);
+    switch (mode) {
+      case 0:
+        a.done_val = val;
+        rc = launch_oneshot<OP_SUM, float>(a, s);
+        break;
+#define SD(M) \
+  hipLaunchKernelGGL((solo_diag<M>), dim3(1), dim3(kBlock), 0, s, (const u32x4 *)src, \
+                     (u32x4 *)dst, nvec, ctr, word, val)
+      case 1: SD(1); break;
+      case 2: SD(2); break;
+      case 3: SD(3); break;
+      case 4: SD(4); break;
+      case 5: SD(5); break;
+#undef SD
+      default: rc = -LFA_EINVAL;
+    }
+    while (!rc && *(volatile uint64_t *)word < val) {
+    }
+  }
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  *us = (ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3 - t0) / reps;
+  hipStreamSynchronize(s);
+  hipFree(ctr);
+  hipHostFree(word);
+  hipStreamDestroy(s);
+  return rc;
 }

@@ -24,6 +24,7 @@
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
+#   solo         launch -> completion word of one small kernel, by part
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -76,6 +77,8 @@ for stage in "$@"; do
       $S treeput_layout 300 python3 -u tools/probe_treeput_layout.py || exit 99 ;;
     ramp)
       $S ramp 300 python3 -u tools/probe_ramp.py || exit 99 ;;
+    solo)
+      $S solo 200 python3 -u tools/probe_solo_latency.py || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac
