@@ -100,9 +100,12 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     if steps or _newer(LIB_LFA, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_LFA,
               *objs, "-Wl,-soname,liblfa.so"])
-    if _newer(LIB_TUNE, tune_objs):
+    if _newer(LIB_TUNE, tune_objs + [LIB_LFA]):
+        # the tuning forms share the product's launchers, which call into
+        # liblfa.so (lfa__wallclock_ticks_per_us)
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TUNE,
-              *tune_objs, "-Wl,-soname,liblfa_tune.so"])
+              *tune_objs, "-L" + PKG, "-llfa", "-Wl,-rpath,$ORIGIN",
+              "-Wl,-soname,liblfa_tune.so"])
     if verbose:
         print(f"built {LIB_LFA} ({len(steps)} objects recompiled)")
     return LIB_LFA

@@ -148,7 +148,9 @@ struct lfa_coll_ep {
 		void *p;
 		size_t bytes;
 		int busy;
+		uint64_t used;      /* stage_clock at the last stage_get */
 	} stage[LFA_STAGE_POOL];
+	uint64_t stage_clock;
 	size_t stage_cap;           /* idle staging bytes kept */
 	int stage_trim_due;         /* idle bytes passed the cap: trim when the
 				     * queue has drained */

@@ -43,7 +43,10 @@ def _worker(rank, world, port, cycles, logdir, q):
     try:
         log = open(os.path.join(logdir, f"r{rank}.log"), "w", buffering=1)
         os.dup2(log.fileno(), 2)
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        # AMD_LOG_LEVEL=1: the HIP runtime names a failing export's cause
+        # (its hsa_status) on stderr too
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1",
+                          AMD_LOG_LEVEL="1")
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(0)
@@ -86,7 +89,7 @@ def _worker(rank, world, port, cycles, logdir, q):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
-    ap.add_argument("--cycles", type=int, default=12)
+    ap.add_argument("--cycles", type=int, default=24)
     a = ap.parse_args()
     import torch.multiprocessing as mp
     logdir = os.path.join(ROOT, "gpurun_out", "ipc_growth_logs")
@@ -111,9 +114,10 @@ def main():
     fails, notes = 0, []
     for r in range(a.world):
         with open(os.path.join(logdir, f"r{r}.log")) as f:
-            lines = [ln.rstrip() for ln in f if ln.startswith("lfa:")]
+            lines = [ln.rstrip() for ln in f
+                     if ln.startswith("lfa:") or ("IPC" in ln or "ipc" in ln)]
         fails += sum("export failed" in ln for ln in lines)
-        notes += [f"r{r}: {ln}" for ln in lines][:40]
+        notes += [f"r{r}: {ln}" for ln in lines if "overlaps event" not in ln][:40]
     out = {"world": a.world, "cycles": a.cycles,
            "exports": a.world * a.cycles * 4, "export_failures": fails,
            "per_rank": res, "diagnostics": notes[:200]}
