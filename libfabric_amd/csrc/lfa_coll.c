@@ -1330,14 +1330,25 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	if (ok)
 		va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
 	if (ok && n > 1 && hipIpcGetMemHandle(&mine->h, mc->sym_local) != hipSuccess) {
-		/* the runtime's export of a fresh allocation fails now and then
-		 * with "invalid argument" (round 3: 2 of 8 processes once; round 4,
-		 * tools/probe_ipc_growth.py: 2 of 384 exports).  The
-		 * allocation is ordinary — device memory, its own base and size —
-		 * so the same allocation is exported again after a pause first,
-		 * then a fresh one, before the growth fails on every member */
+		/*
+		 * The runtime refuses to export some fresh allocations: ROCr's IPC
+		 * create returns HSA_STATUS_ERROR (AMD_LOG_LEVEL=1: "Failed to
+		 * create memory for IPC, failed with hsa_status: 4096"), which
+		 * hipIpcGetMemHandle reports as "invalid argument".  Round 4 pinned
+		 * it down (tools/probe_ipc_growth.py): 2 to 8 of
+		 * 384 to 768 exports; the allocation is ordinary (device memory,
+		 * its own base and size), the SAME allocation fails on every retry,
+		 * and a replacement allocated after freeing it lands at the same
+		 * address and can fail again — the failure follows the address,
+		 * which earlier workspaces of this process held and exported.  So
+		 * the replacement is allocated while the refused allocation is
+		 * still held, which gives it another address, and the refused ones
+		 * are freed afterwards; after LFA_EXPORT_TRIES the growth fails on
+		 * every member (the agreement below).
+		 */
 		hipError_t e = hipGetLastError();
-		int again = 0;
+		char *refused[LFA_EXPORT_TRIES];
+		int nref = 0;
 
 		if (va_debug()) {
 			fprintf(stderr, "lfa: P2P workspace export failed (%s)\n",
@@ -1345,44 +1356,43 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 			va_explain("failed export", mc->sym_local,
 				   2 * region + LFA_SIG_AREA_BYTES);
 		}
-		for (int t = 1; t <= 3 && !again; t++) {
-			usleep(200u * (unsigned)t);
-			again = hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
-			if (!again)
+		ok = 0;
+		while (!ok && mc->sym_local && nref < LFA_EXPORT_TRIES) {
+			refused[nref++] = mc->sym_local;
+			mc->sym_local = NULL;
+			ok = lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
+							 2 * region + LFA_SIG_AREA_BYTES),
+					  "P2P workspace hipMalloc (replacement)") == hipSuccess;
+			if (!ok) {
+				mc->sym_local = NULL;
+				break;
+			}
+			va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
+			ok = lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
+							      LFA_SIG_AREA_BYTES, mc->ep->stream),
+					  "P2P flag area memset (replacement)") == hipSuccess &&
+			     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
+					  "P2P flag area memset sync (replacement)") == hipSuccess &&
+			     hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
+			if (!ok)
 				(void)hipGetLastError();
 			if (va_debug())
-				fprintf(stderr, "lfa: export of the same allocation, try %d after "
-					"%u us: %s\n", t, 200u * (unsigned)t,
-					again ? "exported" : "failed");
+				va_explain(ok ? "replacement exported" : "replacement refused",
+					   mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
 		}
-		if (again)
-			goto exported;
-		if (va_debug())
-			fprintf(stderr, "lfa: retrying on a new allocation\n");
-		va_note('F', mc->sym_local, 0);
-		hipFree(mc->sym_local);
-		mc->sym_local = NULL;
-		ok = lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
-						 2 * region + LFA_SIG_AREA_BYTES),
-				  "P2P workspace hipMalloc (retry)") == hipSuccess &&
-		     lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
-						      LFA_SIG_AREA_BYTES, mc->ep->stream),
-				  "P2P flag area memset (retry)") == hipSuccess &&
-		     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
-				  "P2P flag area memset sync (retry)") == hipSuccess &&
-		     lfa_hip_note(why, hipIpcGetMemHandle(&mine->h, mc->sym_local),
-				  "P2P workspace hipIpcGetMemHandle") == hipSuccess;
-		if (va_debug() && mc->sym_local) {
-			va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
-			va_explain(ok ? "retry exported" : "retry failed", mc->sym_local,
-				   2 * region + LFA_SIG_AREA_BYTES);
+		if (!ok) {
+			lfa_hip_note(why, hipErrorInvalidValue, "P2P workspace hipIpcGetMemHandle");
+			if (mc->sym_local) {
+				va_note('F', mc->sym_local, 0);
+				hipFree(mc->sym_local);
+				mc->sym_local = NULL;
+			}
 		}
-		if (!ok && mc->sym_local) {
-			hipFree(mc->sym_local);
-			mc->sym_local = NULL;
+		for (int i = 0; i < nref; i++) {
+			va_note('F', refused[i], 0);
+			hipFree(refused[i]);
 		}
 	}
-exported:
 	mine->ok = ok;
 	sym_free(mc, old_sym, old_local);
 }
@@ -1709,28 +1719,20 @@ static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
 
 /*
  * A small reducing collective of a one-member group (allreduce, reduce,
- * reduce_scatter: each a copy of the input) as the one-shot kernel with
- * n = 1: one launch that ends in the completion word, so the operation
- * completes without an event (the plan would be one COPY
- * item plus an event record and query).
+ * reduce_scatter: each a copy of the input) as one launch that ends in the
+ * completion word, so the operation completes without an event (VERDICT r3
+ * #4; the plan would be one COPY item plus an event record and query).
  */
 static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
-		    enum lfa_datatype dt, enum lfa_op op)
+		    enum lfa_datatype dt)
 {
-	struct lfa_oneshot a;
 	int ret;
 
-	memset(&a, 0, sizeof(a));
-	a.send = buf;
-	a.result = result;
-	a.count = count;
-	a.mode = LFA_ONESHOT_ALL;
-	a.n = 1;
-	a.rank = 0;
-	a.done_ctr = ep->done_ctr;
-	a.done_word = ep->done_word;
-	a.done_val = ep->done_seq + 1;
-	ret = lfa_oneshot_reduce_async(op, dt, &a, ep->stream);
+	/* the one-shot kernel with n = 1 gives the same bytes; this kernel's
+	 * arguments are 48 bytes instead of ~700, about 1 us less from launch
+	 * to the word (tools/probe_solo_latency.py) */
+	ret = lfa_solo_copy_async(result, buf, count * lfa_datatype_size(dt), ep->done_ctr,
+				  ep->done_word, ep->done_seq + 1, ep->stream);
 	if (ret)
 		return ret;
 	ep->op_done_val = ++ep->done_seq;
@@ -1758,7 +1760,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	if (mc->size == 1 && s == ep->stream && ep->done_word &&
 	    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE || coll == LFA_REDUCE_SCATTER) &&
 	    count * esz <= LFA_ONESHOT_SOLO_BYTES)
-		return run_solo(ep, buf, result, count, dt, op);
+		return run_solo(ep, buf, result, count, dt);
 	if (algo == LFA_ALGO_AUTO)
 		algo = (enum lfa_coll_algo)lfa_coll_auto_algo(coll, count, mc->size, esz,
 							       mc->p2p_state >= 0);

@@ -27,6 +27,8 @@
 /* Bytes of one P2P handle-exchange record (struct sym_rec, lfa_coll.c). */
 #define LFA_SYM_REC_BYTES 80
 #define LFA_STAGE_POOL 128              /* peer-domain staging buffers kept */
+#define LFA_EXPORT_TRIES 4              /* workspace allocations per growth
+					 * whose IPC export may be refused */
 /* idle staging bytes the pool keeps by default (the endpoint's
  * stage_cap, LFA_STAGE_POOL_BYTES at open): a buffer returned above it is
  * freed, and lfa_coll_ep_flush frees every idle one */

@@ -106,6 +106,18 @@ struct lfa_oneshot {
 int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 				void *stream);
 
+/*
+ * A one-member group's small reducing collective (allreduce, reduce and
+ * reduce_scatter of one rank are each a copy of the input): `bytes` from
+ * send to result in one launch of a few workgroups that ends in the
+ * completion word, as struct lfa_oneshot's done_* fields describe.  The
+ * same result as the one-shot kernel with n = 1 for every (op, datatype),
+ * with 48 bytes of kernel arguments instead of ~700 (about
+ * 1 us of launch-to-word latency).  Any alignment.  0 or -LFA_E*.
+ */
+int lfa_solo_copy_async(void *result, const void *send, size_t bytes, uint32_t *done_ctr,
+			uint64_t *done_word, uint64_t done_val, void *stream);
+
 #ifdef __HIPCC__
 /* A wait of operation `ticket` gave up: lower the group's status word to it
  * (plain system-scope load and store: the group's kernels are stream-ordered,

@@ -47,7 +47,51 @@ __global__ __launch_bounds__(64) void flag_barrier(BarArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+// One-member copy ending in the completion word (lfa_solo_copy_async).
+// Workgroup b copies bytes [b·4 KiB, (b+1)·4 KiB): 16 B per lane when both
+// pointers are 16-B aligned, byte-wise otherwise and for the tail.
+__global__ __launch_bounds__(256) void solo_copy(char *dst, const char *src, size_t bytes,
+                                                 uint32_t *ctr, uint64_t *word,
+                                                 uint64_t val) {
+  const unsigned t = threadIdx.x;
+  const size_t lo = (size_t)blockIdx.x * 4096;
+  const size_t hi = lo + 4096 < bytes ? lo + 4096 : bytes;
+  const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const size_t vhi = vec ? lo + ((hi - lo) & ~(size_t)15) : lo;
+  if (lo + (size_t)t * 16 < vhi) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    *(u32x4 *)(dst + lo + (size_t)t * 16) = *(const u32x4 *)(src + lo + (size_t)t * 16);
+  }
+  for (size_t o = vhi + t; o < hi; o += 256) dst[o] = src[o];
+  // the completion word: this workgroup's stores acknowledged and released
+  // at system scope, then the last workgroup publishes `val` (lfa_signal.h)
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const uint32_t seen =
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen + 1 == gridDim.x) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int lfa_solo_copy_async(void *result, const void *send, size_t bytes,
+                                   uint32_t *done_ctr, uint64_t *done_word, uint64_t done_val,
+                                   void *stream) {
+  if (!bytes) return 0;
+  if (!result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
+    return -LFA_EINVAL;
+  const unsigned grid = (unsigned)((bytes + 4095) / 4096);
+  hipLaunchKernelGGL(solo_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)result,
+                     (const char *)send, bytes, done_ctr, done_word, done_val);
+  return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+}
 
 extern "C" uint64_t lfa__wallclock_ticks_per_us(void) {
   static uint64_t t = 0;

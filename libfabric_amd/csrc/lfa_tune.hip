@@ -1087,6 +1087,98 @@ static void drain_auto(u32x4 *d, const u32x4 *v, size_t nvec, hipStream_t s) {
 // policy forced nt / sc1.  77: the round-2 product (combine_lds with the wave
 // index divergent to the compiler, so its sc1 buffer stores ran in
 // readfirstlane loops), with the product's store policy for the size.
+// Dynamically scheduled combine (the per-wave stamps of
+// tools/probe_ramp.py put one launch's fixed cost in its drain, with the
+// XCDs finishing up to 0.9 us apart at 32 MiB per operand and 2 us at 64):
+// a resident grid whose waves take 4 KiB-per-operand tiles from a global
+// counter, so a slower XCD takes fewer tiles instead of finishing last.  The
+// next tile's index is fetched while the current tile's loads are in flight
+// (PF).  The last wave to leave resets the counters for the next launch.
+namespace lfa {
+
+template <int U, int SAUX, bool PF>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_dyn(u32x4 *__restrict__ dst,
+                                                             const u32x4 *__restrict__ src,
+                                                             size_t nvec, unsigned *ctr) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  auto grab = [&]() -> unsigned {
+    unsigned v = 0;
+    if (l == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  unsigned t = grab();
+  while (t < ntiles) {
+    const size_t base = (size_t)t * 64 * U;
+    unsigned next = 0;
+    if (base + 64 * U <= nvec) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                         (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+      if constexpr (PF) next = grab();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        u32x4 v = apply_vec<OP_SUM, float>(lds[0][w][u][l], lds[1][w][u][l]);
+        if constexpr (SAUX == kStoreNt)
+          st<true>(dst + base + u * 64 + l, v);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+      }
+    } else {
+      if constexpr (PF) next = grab();
+      for (int u = 0; u < U; u++) {
+        size_t i = base + (size_t)u * 64 + l;
+        if (i < nvec)
+          st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+      }
+    }
+    t = PF ? next : grab();
+  }
+  // every wave's last grab is behind it: the last one out resets both
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (l == 0) {
+    const unsigned total = gridDim.x * kLdsWaves;
+    if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+        total) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int U, int SAUX, bool PF>
+static void launch_dyn(u32x4 *d, const u32x4 *v, size_t nvec, hipStream_t s) {
+  static unsigned *ctr = nullptr;
+  static int grid = 0;
+  if (!ctr) {
+    if (hipMalloc((void **)&ctr, 64) != hipSuccess || hipMemset(ctr, 0, 64) != hipSuccess)
+      return;
+  }
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_dyn<U, SAUX, PF>,
+                                                   kLdsWaves * 64, 0) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return;
+  grid = per_cu * cus;
+  const size_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  const size_t need = (ntiles + kLdsWaves - 1) / kLdsWaves;
+  const unsigned g = (unsigned)(need < (size_t)grid ? need : (size_t)grid);
+  hipLaunchKernelGGL((combine_dyn<U, SAUX, PF>), dim3(g), dim3(kLdsWaves * 64), 0, s, d, v,
+                     nvec, ctr);
+}
+
+}  // namespace lfa
+
 extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_t nvec,
                                   void *stream) {
   using namespace lfa_pipe;
@@ -1106,6 +1198,14 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 76:
       hipLaunchKernelGGL((sum_lds_drain<4, 4, lfa::kStoreSc1>), g4, b4, 0, s, d, v, nvec);
       break;
+    case 80: lfa::launch_dyn<4, lfa::kStoreSc1, true>(d, v, nvec, s); break;
+    case 81:
+      if (nvec * 16 < lfa::kSc1Bytes) lfa::launch_dyn<4, lfa::kStoreSc1, true>(d, v, nvec, s);
+      else lfa::launch_dyn<4, lfa::kStoreNt, true>(d, v, nvec, s);
+      break;
+    case 82: lfa::launch_dyn<2, lfa::kStoreSc1, true>(d, v, nvec, s); break;
+    case 83: lfa::launch_dyn<4, lfa::kStoreSc1, false>(d, v, nvec, s); break;
+    case 84: lfa::launch_dyn<8, lfa::kStoreSc1, true>(d, v, nvec, s); break;
     case 77:
       if (nvec * 16 < lfa::kSc1Bytes)
         hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreSc1, false>), g4,
@@ -1207,6 +1307,7 @@ extern "C" int lfa__tune_combine_stamped(void *dst, const void *src, size_t nvec
 //   mode 3  write-through (sc0 sc1) data stores, then the releases
 //   mode 4  no data: the counter and the word only, with the releases
 //   mode 5  no data, no releases: the word alone
+//   mode 6  lfa_solo_copy_async (liblfa.so): the product's world-1 path
 // Returns the mean microseconds per operation in *us.
 // ---------------------------------------------------------------------------
 namespace lfa {
@@ -1291,6 +1392,9 @@ extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size
       case 4: SD(4); break;
       case 5: SD(5); break;
 #undef SD
+      case 6:
+        rc = lfa_solo_copy_async(dst, src, bytes, ctr, word, val, s);
+        break;
       default: rc = -LFA_EINVAL;
     }
     while (!rc && *(volatile uint64_t *)word < val) {

@@ -25,6 +25,7 @@
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
 #   solo         launch -> completion word of one small kernel, by part
+#   tunecomb     back-to-back combine forms at 32/64/256 MiB (COMBINE_VARIANTS)
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -79,6 +80,9 @@ for stage in "$@"; do
       $S ramp 300 python3 -u tools/probe_ramp.py || exit 99 ;;
     solo)
       $S solo 200 python3 -u tools/probe_solo_latency.py || exit 99 ;;
+    tunecomb)
+      $S tune_combine 500 python3 -u tools/tune_combine.py --sizes 32,64,256 \
+        --variants "${COMBINE_VARIANTS:-30,80,81,82,83,84}" --rounds "${COMBINE_ROUNDS:-12}" || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 MODES = ("product_oneshot_n1", "body_copy_with_releases", "body_no_releases_diag",
-         "body_writethrough_stores", "word_only_with_releases", "word_only_no_releases")
+         "body_writethrough_stores", "word_only_with_releases", "word_only_no_releases",
+         "product_solo_copy")
 
 
 def main():

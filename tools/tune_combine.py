@@ -8,7 +8,7 @@ one form between ONE event pair, operands rotating over >= 1 GiB so the
 256 MB Infinity Cache cannot serve repeats; forms are interleaved round by
 round after a clock prewarm.  Variants are bench.py --tune's ids (30 = the
 product launch; 70.. drained forms and 77 = the round-2 product, through
-liblfa_tune.so).
+liblfa_tune.so; 80.. the dynamically scheduled forms).
 
     python tools/tune_combine.py --sizes 32,64,256 --variants 30,77,70 [--rounds 15]
 """
@@ -43,7 +43,7 @@ def main():
 
     def fn(v):
         return (L.lfa__tune_sum_f32 if v < 12 or v == 30 else
-                L.lfa__tune3_sum_f32 if 70 <= v < 80 else L.lfa__tune2_sum_f32)
+                L.lfa__tune3_sum_f32 if 70 <= v < 90 else L.lfa__tune2_sum_f32)
 
     # correctness first, odd size (partial last tile)
     n = (1 << 20) + 77
