@@ -1161,6 +1161,7 @@ struct sym_rec {
 	int32_t ok;
 	int32_t pad;
 	hipIpcMemHandle_t h;
+	uint64_t id;            /* the workspace's identity word (LFA_SIG_ID_OFF) */
 };
 
 /* Open file descriptors of this process (LFA_DEBUG diagnostics: every
@@ -1254,7 +1255,117 @@ static void va_explain(const char *what, const void *p, size_t bytes)
 	pthread_mutex_unlock(&va_lock);
 }
 
-/* Unmap the peers' workspaces in `sym` and free this rank's `local`. */
+/*
+ * Exported workspaces are kept, not freed (LFA_WS_CACHE_BYTES, default
+ * 4 GiB per process; 0 frees them as before).  The runtime remembers an
+ * exported address after hipFree: a later allocation at that address — the
+ * allocator hands freed ranges straight back — is refused an export
+ * (hsa_status 4096), or exported with a handle its peers map onto other
+ * memory, so the owner waits for posts that land elsewhere (round 4, DESIGN.md
+ * §12: tools/probe_ipc_growth.py).  A workspace released by a growth or an
+ * endpoint close goes to this cache; the next workspace of the same size on
+ * the same device takes it back and exports it again — the same memory
+ * under the same address — so no fresh allocation ever lands on an address
+ * that was exported.  Above the cap the least recently used go back to HIP.
+ */
+#define WS_CACHE_SLOTS 64
+static struct ws_slot {
+	char *p;
+	size_t bytes;
+	int dev;
+	unsigned long long used;
+} ws_cache[WS_CACHE_SLOTS];
+static size_t ws_held;
+static unsigned long long ws_clock;
+static pthread_mutex_t ws_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t ws_cap(void)
+{
+	static long long cap = -1;
+
+	if (cap < 0) {
+		const char *e = getenv("LFA_WS_CACHE_BYTES");
+
+		cap = e ? atoll(e) : (4ll << 30);
+		if (cap < 0)
+			cap = 0;
+	}
+	return (size_t)cap;
+}
+
+/* A kept workspace of exactly `bytes` on the current device, or NULL. */
+static char *ws_take(size_t bytes)
+{
+	int dev = -1;
+	char *p = NULL;
+
+	if (hipGetDevice(&dev) != hipSuccess)
+		return NULL;
+	pthread_mutex_lock(&ws_lock);
+	for (int i = 0; i < WS_CACHE_SLOTS && !p; i++)
+		if (ws_cache[i].p && ws_cache[i].bytes == bytes && ws_cache[i].dev == dev) {
+			p = ws_cache[i].p;
+			ws_cache[i].p = NULL;
+			ws_held -= bytes;
+		}
+	pthread_mutex_unlock(&ws_lock);
+	return p;
+}
+
+/* Keep workspace `p` (its whole allocation) for a later ws_take. */
+static void ws_give(char *p)
+{
+	void *base = NULL;
+	size_t bytes = 0;
+	int dev = -1, slot = -1;
+	char *evict[WS_CACHE_SLOTS];
+	int ne = 0;
+
+	hipPointerAttribute_t at;
+
+	memset(&at, 0, sizeof(at));
+	if (!ws_cap() || hipMemGetAddressRange(&base, &bytes, p) != hipSuccess ||
+	    base != (void *)p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+		(void)hipGetLastError();
+		hipFree(p);
+		return;
+	}
+	dev = at.device;
+	pthread_mutex_lock(&ws_lock);
+	for (int i = 0; i < WS_CACHE_SLOTS && slot < 0; i++)
+		if (!ws_cache[i].p)
+			slot = i;
+	if (slot < 0) {         /* every slot held: the least recently used goes */
+		slot = 0;
+		for (int i = 1; i < WS_CACHE_SLOTS; i++)
+			if (ws_cache[i].used < ws_cache[slot].used)
+				slot = i;
+		evict[ne++] = ws_cache[slot].p;
+		ws_held -= ws_cache[slot].bytes;
+	}
+	ws_cache[slot] = (struct ws_slot){ p, bytes, dev, ++ws_clock };
+	ws_held += bytes;
+	while (ws_held > ws_cap()) {
+		int lru = -1;
+
+		for (int i = 0; i < WS_CACHE_SLOTS; i++)
+			if (ws_cache[i].p && i != slot &&
+			    (lru < 0 || ws_cache[i].used < ws_cache[lru].used))
+				lru = i;
+		if (lru < 0)
+			lru = slot;
+		evict[ne++] = ws_cache[lru].p;
+		ws_held -= ws_cache[lru].bytes;
+		ws_cache[lru].p = NULL;
+		if (lru == slot)
+			break;
+	}
+	pthread_mutex_unlock(&ws_lock);
+	for (int i = 0; i < ne; i++)
+		hipFree(evict[i]);
+}
+
+/* Unmap the peers' workspaces in `sym` and release this rank's `local`. */
 static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 {
 	if (sym) {
@@ -1267,8 +1378,47 @@ static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 	}
 	if (local) {
 		va_note('F', local, 0);
-		hipFree(local);
+		ws_give(local);
 	}
+}
+
+/* A new identity word: this process, a count, the clock. */
+static uint64_t ws_identity(void)
+{
+	static uint64_t n;
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ((uint64_t)getpid() << 40) ^ ((uint64_t)__atomic_add_fetch(&n, 1, __ATOMIC_RELAXED) << 24) ^
+	       (uint64_t)ts.tv_nsec ^ ((uint64_t)ts.tv_sec << 30) ^ 1;
+}
+
+/* A workspace of 2·region + the flag area: a kept one of that size, else a
+ * new allocation (hipMalloc's result). */
+static hipError_t ws_alloc(char **p, size_t region)
+{
+	const size_t bytes = 2 * region + LFA_SIG_AREA_BYTES;
+
+	*p = ws_take(bytes);
+	if (*p)
+		return hipSuccess;
+	return hipMalloc((void **)p, bytes);
+}
+
+/* The flag area zeroed (epoch 0) and the identity word written, before any
+ * peer can learn the handle and post into it (the agreement follows). */
+static int ws_reset(struct lfa_coll_mc *mc, char *local, size_t region, uint64_t id,
+		    int *why)
+{
+	char *area = local + 2 * region;
+
+	return lfa_hip_note(why, hipMemsetAsync(area, 0, LFA_SIG_AREA_BYTES, mc->ep->stream),
+			    "P2P flag area memset") == hipSuccess &&
+	       lfa_hip_note(why, hipMemcpyAsync(area + LFA_SIG_ID_OFF, &id, sizeof(id),
+						hipMemcpyHostToDevice, mc->ep->stream),
+			    "P2P identity word") == hipSuccess &&
+	       lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
+			    "P2P flag area sync") == hipSuccess;
 }
 
 static void p2p_release(struct lfa_coll_mc *mc)
@@ -1314,18 +1464,12 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	memset(mine, 0, sizeof(*mine));
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
-	ok = ok && lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
-					      2 * region + LFA_SIG_AREA_BYTES),
+	ok = ok && lfa_hip_note(why, ws_alloc(&mc->sym_local, region),
 				"P2P workspace hipMalloc") == hipSuccess;
 	if (!ok)
 		mc->sym_local = NULL;
-	/* the flag area starts at epoch 0, and is zero before any peer can
-	 * learn the handle and post into it (the agreement follows) */
-	ok = ok && lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
-						    LFA_SIG_AREA_BYTES, mc->ep->stream),
-				"P2P flag area memset") == hipSuccess &&
-	     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
-			  "P2P flag area memset sync") == hipSuccess;
+	mine->id = ws_identity();
+	ok = ok && ws_reset(mc, mc->sym_local, region, mine->id, why);
 	/* every member grows at the same operation: the epochs restart with the
 	 * zeroed flags, so a count past 2^31 never meets a zero word that reads
 	 * as "ahead"  */
@@ -1372,11 +1516,7 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 				break;
 			}
 			va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
-			ok = lfa_hip_note(why, hipMemsetAsync(mc->sym_local + 2 * region, 0,
-							      LFA_SIG_AREA_BYTES, mc->ep->stream),
-					  "P2P flag area memset (replacement)") == hipSuccess &&
-			     lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
-					  "P2P flag area memset sync (replacement)") == hipSuccess &&
+			ok = ws_reset(mc, mc->sym_local, region, mine->id, why) &&
 			     hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
 			if (!ok)
 				(void)hipGetLastError();
@@ -1401,8 +1541,24 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	sym_free(mc, old_sym, old_local);
 }
 
-/* Every member's record in hand: map the peers' workspaces. */
-static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, int *why)
+/* FNV-1a of an IPC handle (LFA_DEBUG lines). */
+static uint64_t handle_digest(const hipIpcMemHandle_t *h)
+{
+	const unsigned char *b = (const unsigned char *)h;
+	uint64_t x = 0xcbf29ce484222325ull;
+
+	for (size_t i = 0; i < sizeof(*h); i++)
+		x = (x ^ b[i]) * 0x100000001b3ull;
+	return x;
+}
+
+/* Every member's record in hand: map the peers' workspaces of 2·region + the
+ * flag area, and read each one's identity word through the mapping — a
+ * mapping onto any other memory fails the handshake on every member (the
+ * agreement) instead of leaving its owner waiting for posts that land
+ * elsewhere. */
+static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, size_t region,
+		    int *why)
 {
 	int ret = 0;
 
@@ -1418,7 +1574,25 @@ static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, int *why
 			mc->sym[k] = NULL;
 			ret = -LFA_EIO;
 		} else {
+			uint64_t id = 0;
+
 			va_note('I', mc->sym[k], 0);
+			if (lfa_hip_note(why, hipMemcpy(&id, mc->sym[k] + 2 * region + LFA_SIG_ID_OFF,
+							sizeof(id), hipMemcpyDeviceToHost),
+					 "P2P identity read") != hipSuccess) {
+				ret = -LFA_EIO;
+			} else if (id != recs[k].id) {
+				lfa_hip_note(why, hipErrorInvalidValue, "P2P workspace identity");
+				if (va_debug()) {
+					fprintf(stderr, "lfa: peer %d workspace mapped onto other memory: "
+						"identity %#llx, read %#llx; handle digest %#llx\n", k,
+						(unsigned long long)recs[k].id, (unsigned long long)id,
+						(unsigned long long)handle_digest(&recs[k].h));
+					va_explain("mismatched mapping", mc->sym[k],
+						   2 * region + LFA_SIG_AREA_BYTES);
+				}
+				ret = -LFA_EIO;
+			}
 		}
 	}
 	return ret;
@@ -1505,7 +1679,8 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 		if (mc->size == 1) {
 			h->agree_in = h->agree_out = ((struct sym_rec *)h->mine)->ok;
 			recs[0] = *(struct sym_rec *)h->mine;
-			h->agree_out = h->agree_out && sym_open(mc, recs, &h->r.hip_err) == 0;
+			h->agree_out = h->agree_out &&
+				       sym_open(mc, recs, h->sym_size, &h->r.hip_err) == 0;
 			goto agreed;
 		}
 		ret = sub_start(ep, h, LFA_ALLGATHER, h->mine, recs, sizeof(struct sym_rec),
@@ -1520,7 +1695,7 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 		ret = sub_advance(h);
 		if (ret <= 0)
 			return ret;
-		h->agree_in = sym_open(mc, recs, &h->r.hip_err) == 0;
+		h->agree_in = sym_open(mc, recs, h->sym_size, &h->r.hip_err) == 0;
 		ret = sub_start(ep, h, LFA_ALLREDUCE, &h->agree_in, &h->agree_out, 1,
 				LFA_INT32, LFA_MIN, (uint16_t)(h->sub_seq + 1));
 		if (ret)
@@ -1579,7 +1754,7 @@ static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
 	     hipStreamSynchronize(ep->stream) != hipSuccess))
 		ret = -LFA_EIO;
 	if (!ret)
-		ret = sym_open(mc, recs, NULL);
+		ret = sym_open(mc, recs, region, NULL);
 	if (n > 1) {
 		/* agree that every member mapped every peer (MIN of the flags) */
 		int32_t all = ret == 0;

@@ -27,6 +27,10 @@ extern "C" {
  * by rank k's workgroup b */
 #define LFA_SIG_OS_OFF 256
 #define LFA_SIG_OS_CHUNKS 128
+/* identity word: a value the owner writes before exporting the workspace
+ * and sends with its handle, read back by every peer through its mapping
+ * (lfa_coll.c sym_open) */
+#define LFA_SIG_ID_OFF (LFA_SIG_AREA_BYTES - 64u)
 #define LFA_OS_MAX_RANKS 8              /* one-shot groups: 1..8 members */
 
 /*

@@ -1094,6 +1094,11 @@ static void drain_auto(u32x4 *d, const u32x4 *v, size_t nvec, hipStream_t s) {
 // counter, so a slower XCD takes fewer tiles instead of finishing last.  The
 // next tile's index is fetched while the current tile's loads are in flight
 // (PF).  The last wave to leave resets the counters for the next launch.
+// REJECTED (round 4, profiles/r04_tune_combine_dynamic.jsonl): 8-16x slower
+// than the product at every size — the launch's time is the tile count times
+// ~32 ns (32 MiB: 8,192 grabs 261 us, U=8's 4,096 grabs 132 us), i.e. one
+// device-scope atomic on one address completes every ~32 ns however many
+// waves ask.  Kept as the measured record.
 namespace lfa {
 
 template <int U, int SAUX, bool PF>

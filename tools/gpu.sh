@@ -22,6 +22,7 @@
 #   sizes        combine kernel durations vs size under --kernel-trace
 #   host2        2-process host-buffer allreduce, default vs group chunks
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
+#   ipcab        the same with exported workspaces freed (cache 0), then kept
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
 #   solo         launch -> completion word of one small kernel, by part
@@ -74,6 +75,13 @@ for stage in "$@"; do
       $S host2 300 python3 -u tools/probe_host_group_chunk.py || exit 99 ;;
     ipc)
       $S ipc_growth 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
+    ipcab)
+      # the same probe with exported workspaces freed (the old behaviour),
+      # then kept (the default)
+      $S ipc_growth_nocache 420 python3 -u tools/probe_ipc_growth.py --cache-bytes 0 && \
+      $S ipc_growth_cache 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
+    ipctrace)
+      $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)
       $S treeput_layout 300 python3 -u tools/probe_treeput_layout.py || exit 99 ;;
     ramp)

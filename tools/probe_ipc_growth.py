@@ -39,7 +39,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, cycles, logdir, q):
+def _worker(rank, world, port, cycles, logdir, trace, cache, q):
     try:
         log = open(os.path.join(logdir, f"r{rank}.log"), "w", buffering=1)
         os.dup2(log.fileno(), 2)
@@ -47,6 +47,10 @@ def _worker(rank, world, port, cycles, logdir, q):
         # (its hsa_status) on stderr too
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1",
                           AMD_LOG_LEVEL="1")
+        if trace:
+            os.environ["LFA_TRACE"] = "1"     # one stderr line per operation state
+        if cache is not None:
+            os.environ["LFA_WS_CACHE_BYTES"] = str(cache)
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(0)
@@ -54,6 +58,7 @@ def _worker(rank, world, port, cycles, logdir, q):
         from gloo_xfer import GlooXfer
         from libfabric_amd import coll
         bad = 0
+        failed = []
         churn = []
         for c in range(cycles):
             ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
@@ -71,7 +76,16 @@ def _worker(rank, world, port, cycles, logdir, q):
                     if len(churn) > 6:
                         churn.pop(0)
                     torch.cuda.synchronize()
-                    ep.wait(ep.allreduce(x, r, n, 8, 2))
+                    try:
+                        ep.wait(ep.allreduce(x, r, n, 8, 2))
+                    except coll.CollError as e:
+                        # a failed handshake fails on every member at once
+                        # (the agreement); a timed-out wait on one member
+                        # only, so that one ends the probe
+                        if "prov_errno 110" in str(e):
+                            raise
+                        failed.append((c, k, str(e)))
+                        break
                     want = world * (world + 1) / 2
                     if not bool((r == want).all()):
                         bad += 1
@@ -80,7 +94,7 @@ def _worker(rank, world, port, cycles, logdir, q):
             dist.barrier()
         dist.destroy_process_group()
         log.flush()
-        q.put((rank, {"wrong_results": bad}))
+        q.put((rank, {"wrong_results": bad, "failed_growths": failed}))
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, traceback.format_exc()))
@@ -90,14 +104,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--cycles", type=int, default=24)
+    ap.add_argument("--trace", action="store_true", help="LFA_TRACE=1 in every rank")
+    ap.add_argument("--cache-bytes", type=int, default=None,
+                    help="LFA_WS_CACHE_BYTES in every rank (0: workspaces freed)")
     a = ap.parse_args()
     import torch.multiprocessing as mp
-    logdir = os.path.join(ROOT, "gpurun_out", "ipc_growth_logs")
+    logdir = os.path.join(ROOT, "gpurun_out",
+                          "ipc_growth_logs" + ("" if a.cache_bytes is None else f"_c{a.cache_bytes}"))
     os.makedirs(logdir, exist_ok=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.cycles, logdir, q))
+    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.cycles, logdir, a.trace,
+                                                 a.cache_bytes, q))
              for r in range(a.world)]
     for p in procs:
         p.start()
@@ -111,14 +130,16 @@ def main():
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    fails, notes = 0, []
+    fails, ids, notes = 0, 0, []
     for r in range(a.world):
         with open(os.path.join(logdir, f"r{r}.log")) as f:
             lines = [ln.rstrip() for ln in f
                      if ln.startswith("lfa:") or ("IPC" in ln or "ipc" in ln)]
         fails += sum("export failed" in ln for ln in lines)
+        ids += sum("mapped onto other memory" in ln for ln in lines)
         notes += [f"r{r}: {ln}" for ln in lines if "overlaps event" not in ln][:40]
-    out = {"world": a.world, "cycles": a.cycles,
+    out = {"world": a.world, "cycles": a.cycles, "ws_cache_bytes": a.cache_bytes,
+           "identity_mismatches_logged": ids,
            "exports": a.world * a.cycles * 4, "export_failures": fails,
            "per_rank": res, "diagnostics": notes[:200]}
     print(json.dumps({"probe_ipc_growth": out}), flush=True)
