@@ -350,6 +350,12 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep);
  * bounded by what operations in flight use plus 1 GiB kept idle, and 0 idle
  * after lfa_coll_ep_flush (diagnostics, tests). */
 size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep);
+/* Device bytes of released P2P workspaces this process keeps for reuse
+ * (LFA_WS_CACHE_BYTES, default 4 GiB; 0 frees them).  An exported workspace
+ * is never handed back to the allocator below that cap: a fresh allocation at
+ * a once-exported address may be refused an export, or exported as the
+ * earlier memory.  Diagnostics, tests. */
+size_t lfa_coll_ws_cached_bytes(void);
 
 /* ---- schedules as data ------------------------------------------------ */
 

@@ -138,6 +138,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_ep_flush.argtypes = [c_void_p]
     L.lfa_coll_ep_stage_bytes.restype = c_size_t
     L.lfa_coll_ep_stage_bytes.argtypes = [c_void_p]
+    L.lfa_coll_ws_cached_bytes.restype = c_size_t
+    L.lfa_coll_ws_cached_bytes.argtypes = []
     L.lfa_coll_world_addr.restype = c_uint64
     L.lfa_coll_world_addr.argtypes = [c_void_p]
     L.lfa_join_collective.restype = c_int
@@ -250,6 +252,11 @@ def group_chunk(setting: int, nranks: int, nbytes: int) -> int:
     """lfa_coll_group_chunk: the group chunk an operation of `nbytes` runs
     with under `setting` (GROUP_CHUNK_AUTO, 0 or a size)."""
     return lib().lfa_coll_group_chunk(setting, nranks, nbytes)
+
+
+def ws_cached_bytes() -> int:
+    """lfa_coll_ws_cached_bytes: released P2P workspaces kept for reuse."""
+    return lib().lfa_coll_ws_cached_bytes()
 
 
 def member_chunk(nranks: int, host: bool, group_chunk: int, local_chunk: int) -> int:

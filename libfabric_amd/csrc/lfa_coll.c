@@ -1365,6 +1365,16 @@ static void ws_give(char *p)
 		hipFree(evict[i]);
 }
 
+size_t lfa_coll_ws_cached_bytes(void)
+{
+	size_t n;
+
+	pthread_mutex_lock(&ws_lock);
+	n = ws_held;
+	pthread_mutex_unlock(&ws_lock);
+	return n;
+}
+
 /* Unmap the peers' workspaces in `sym` and release this rank's `local`. */
 static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 {
@@ -1492,7 +1502,10 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 		 * the replacement is allocated while the refused allocation is
 		 * still held, which gives it another address, and the refused ones
 		 * are freed afterwards; after LFA_EXPORT_TRIES the growth fails on
-		 * every member (the agreement below).
+		 * every member (the agreement below).  With the workspace cache
+		 * (ws_give) no fresh allocation lands on a once-exported address,
+		 * and this path is the fallback for LFA_WS_CACHE_BYTES=0 and for
+		 * workspaces evicted above the cap.
 		 */
 		hipError_t e = hipGetLastError();
 		char *refused[LFA_EXPORT_TRIES];

@@ -530,6 +530,64 @@ def test_staging_pool_is_bounded():
     _spawn(_stage_pool_worker, 2)
 
 
+def _ws_cycle_worker(rank, world, port, q, cap):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        if cap is not None:
+            os.environ["LFA_WS_CACHE_BYTES"] = str(cap)
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        msg = "ok"
+        held = []
+        for c in range(6):
+            # every cycle: a new endpoint whose workspace grows three times,
+            # then closes — the address pattern of round 4's stale exports
+            ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+            try:
+                ep.set_algo(coll.ALGO_P2P)
+                ep.set_group_chunk(0)
+                for mib in (1, 6, 12):
+                    n = (mib << 20) // 4
+                    x = torch.full((n,), float(rank + 1 + c), device="cuda")
+                    r = torch.empty_like(x)
+                    torch.cuda.synchronize()
+                    ep.wait(ep.allreduce(x, r, n, 8, 2))
+                    want = world * (world + 1) / 2 + world * c
+                    if not bool((r == want).all()):
+                        msg = f"cycle {c}: {mib} MiB allreduce wrong"
+            finally:
+                ep.close()
+            held.append(coll.ws_cached_bytes())
+            dist.barrier()
+        if cap is None:
+            # every size released in cycle 0 is taken back by cycle 1 and
+            # released again: the cache holds the same bytes every cycle
+            if not held[0] or len(set(held)) != 1:
+                msg = f"kept workspace bytes per cycle {held}"
+        elif max(held) > cap:
+            msg = f"kept {max(held)} B over the {cap} B cap"
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [None, 40 << 20], ids=["default", "cap40mib"])
+def test_released_workspaces_are_reused(cap):
+    """Round 4: an exported workspace freed and a new one
+    allocated at its address was refused an export, or exported as the OLD
+    memory, so its owner waited for posts that landed elsewhere.  Released
+    workspaces are now kept and taken back by the next growth of that size;
+    every peer also checks the owner's identity word through its mapping.
+    Four processes, six endpoint cycles, three growths each."""
+    _spawn(_ws_cycle_worker, 4, args=(cap,))
+
+
 def _chunk_error_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
