@@ -1182,6 +1182,80 @@ static void launch_dyn(u32x4 *d, const u32x4 *v, size_t nvec, hipStream_t s) {
                      nvec, ctr);
 }
 
+// Tapered tail: the per-wave stamps put a launch's fixed
+// cost in its drain — the last round of waves, each living ~4.6 us, finishing
+// over ~2.4 us at 32 MiB.  Here the last `tail` vectors go to workgroups
+// whose waves own UT < UH KiB each, dispatched last (the highest block ids),
+// so the waves still running at the end are shorter ones.
+template <int UH, int UT, int SAUX>
+__device__ __forceinline__ void taper_tile(u32x4 *__restrict__ dst,
+                                           const u32x4 *__restrict__ src, size_t nvec,
+                                           size_t base, u32x4 (*lds)[kLdsWaves][UH][64],
+                                           unsigned w, unsigned l) {
+  constexpr int U = UT;
+  if (base + 64 * U <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      u32x4 v = apply_vec<OP_SUM, float>(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == kStoreNt)
+        st<true>(dst + base + u * 64 + l, v);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
+template <int UH, int UT, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_taper(u32x4 *__restrict__ dst,
+                                                               const u32x4 *__restrict__ src,
+                                                               size_t nvec, size_t split,
+                                                               unsigned head_blocks) {
+  __shared__ u32x4 lds[2][kLdsWaves][UH][64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const unsigned b = blockIdx.x;
+  if (b < head_blocks)
+    taper_tile<UH, UH, SAUX>(dst, src, split,
+                             (size_t)b * (kLdsWaves * 64 * UH) + (size_t)w * 64 * UH, lds, w, l);
+  else
+    taper_tile<UH, UT, SAUX>(dst, src, nvec,
+                             split + (size_t)(b - head_blocks) * (kLdsWaves * 64 * UT) +
+                                 (size_t)w * 64 * UT,
+                             lds, w, l);
+}
+
+template <int UH, int UT>
+static void launch_taper(u32x4 *d, const u32x4 *v, size_t nvec, unsigned tail_div,
+                         hipStream_t s) {
+  const size_t hv = (size_t)kLdsWaves * 64 * UH, tv = (size_t)kLdsWaves * 64 * UT;
+  size_t split = nvec - nvec / tail_div;
+  split -= split % hv;
+  const unsigned head = (unsigned)(split / hv);
+  const unsigned tail = (unsigned)((nvec - split + tv - 1) / tv);
+  if (nvec * 16 < kSc1Bytes)
+    hipLaunchKernelGGL((combine_taper<UH, UT, kStoreSc1>), dim3(head + tail),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
+  else
+    hipLaunchKernelGGL((combine_taper<UH, UT, kStoreNt>), dim3(head + tail),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_t nvec,
@@ -1211,6 +1285,13 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 82: lfa::launch_dyn<2, lfa::kStoreSc1, true>(d, v, nvec, s); break;
     case 83: lfa::launch_dyn<4, lfa::kStoreSc1, false>(d, v, nvec, s); break;
     case 84: lfa::launch_dyn<8, lfa::kStoreSc1, true>(d, v, nvec, s); break;
+    // tapered tail: head tiles 4 KiB per wave, the last 1/div of the data in
+    // UT-KiB tiles
+    case 85: lfa::launch_taper<4, 2>(d, v, nvec, 8, s); break;
+    case 86: lfa::launch_taper<4, 2>(d, v, nvec, 4, s); break;
+    case 87: lfa::launch_taper<4, 1>(d, v, nvec, 8, s); break;
+    case 88: lfa::launch_taper<4, 1>(d, v, nvec, 16, s); break;
+    case 89: lfa::launch_taper<4, 2>(d, v, nvec, 16, s); break;
     case 77:
       if (nvec * 16 < lfa::kSc1Bytes)
         hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreSc1, false>), g4,

@@ -23,6 +23,8 @@
 #   host2        2-process host-buffer allreduce, default vs group chunks
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
 #   ipcab        the same with exported workspaces freed (cache 0), then kept
+#   procs        8-process one-shot latency: parent with / without a GPU context,
+#                7 workers + GPU parent, 8 workers at 4 queues
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
 #   solo         launch -> completion word of one small kernel, by part
@@ -80,6 +82,14 @@ for stage in "$@"; do
       # then kept (the default)
       $S ipc_growth_nocache 420 python3 -u tools/probe_ipc_growth.py --cache-bytes 0 && \
       $S ipc_growth_cache 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
+    procs)
+      # one-shot latency at 8 processes: with the parent holding a GPU context
+      # or not (9 or 8 processes on the GPU), 7 workers + a GPU parent, and
+      # 8 workers at 4 hardware queues each
+      $S procs_8 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick && \
+      $S procs_8_parent 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick --parent-gpu && \
+      $S procs_7_parent 150 python3 -u tools/probe_p2p_latency.py --world 7 --reps 100 --quick --parent-gpu && \
+      GPU_MAX_HW_QUEUES=4 $S procs_8_q4 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick || exit 99 ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)

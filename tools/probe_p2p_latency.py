@@ -9,7 +9,10 @@ kernels and its host submit/complete cost.  Beside it, the TREE schedule on
 the same domain, whose transfers go through the owner's (gloo) transport.
 Not xGMI: the peers' workspaces are this GPU's own HBM.
 
-  python tools/probe_p2p_latency.py [--world 2] [--reps 300]
+  python tools/probe_p2p_latency.py [--world 2] [--reps 300] [--quick] [--parent-gpu]
+--quick: the 4 KiB P2P allreduce only.  --parent-gpu: this (parent) process
+holds a GPU context of its own while the workers run, as pytest's process
+does after the in-process GPU tests — one more process on the GPU.
 prints one JSON line (median / p10 / p90 us per allreduce, per size, Python-timed;
 c_loop_mean_us: the same operations submitted and reaped in C).
 """
@@ -33,7 +36,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, reps, q):
+def _worker(rank, world, port, reps, quick, q):
     try:
         import torch
         import torch.distributed as dist
@@ -47,9 +50,12 @@ def _worker(rank, world, port, reps, q):
         ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
         out = {}
         try:
-            for name, algo, sizes, n in (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
-                                         ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
-                                         ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10))):
+            plan = (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                    ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                    ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10)))
+            if quick:
+                plan = (("p2p", coll.ALGO_P2P, (4096,), reps),)
+            for name, algo, sizes, n in plan:
                 ep.set_algo(algo)
                 for nbytes in sizes:
                     if name == "p2p_rs":   # double PROD reduce_scatter (config 5's op)
@@ -102,22 +108,40 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--reps", type=int, default=300)
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--parent-gpu", action="store_true")
     a = ap.parse_args()
     import torch.multiprocessing as mp
+    if a.parent_gpu:
+        import torch
+        torch.cuda.set_device(0)
+        hold = torch.ones(1 << 20, device="cuda")
+        torch.cuda.synchronize()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.reps, q))
+    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.reps, a.quick, q))
              for r in range(a.world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(a.world))
+    res = {}
+    t0 = time.time()
+    try:
+        for _ in range(a.world):
+            r, v = q.get(timeout=120)
+            res[r] = v
+    except Exception:  # noqa: BLE001  (queue.Empty: a rank did not finish)
+        res["timeout"] = f"no result within 120 s; {len(res)} ranks reported"
+    wall = round(time.time() - t0, 1)
     for p in procs:
         p.join(timeout=30)
         if p.is_alive():
             p.kill()
     print(json.dumps({"world": a.world, "device": "one MI355X shared by all ranks",
-                      "rank0": res[0], "rank1": res.get(1)}), flush=True)
+                      "parent_gpu": a.parent_gpu,
+                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "2" if a.world > 4 else "4"),
+                      "wall_s": wall, "timeout": res.get("timeout"),
+                      "rank0": res.get(0), "rank1": res.get(1)}), flush=True)
     if not all(isinstance(v, dict) for v in res.values()):
         sys.exit(1)
 
