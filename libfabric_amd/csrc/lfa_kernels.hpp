@@ -212,6 +212,70 @@ __global__ __launch_bounds__(kLdsWaves * 64) void combine_lds(
   }
 }
 
+// Tapered tail.  Per-wave timestamps (tools/probe_ramp.py)
+// put a launch's fixed cost in its drain: the waves still running at the end
+// each live ~4.6 us, and at 32 MiB per operand the last ones finish over
+// ~2.4 us.  Here workgroups [0, head) take U-KiB tiles (the body above) up to
+// vector `split`, and the rest — dispatched last, the highest block ids —
+// take 1-KiB tiles, so the waves that end the launch are short ones.  Worth
+// it where the launch runs at least two rounds of waves; below that the extra
+// waves cost more than the drain saves (tools/tune_combine.py variants 85-88,
+// profiles/r04_tune_combine_taper*.json: 32 MiB -1.9 %, 48 and 64 MiB -1.3 %,
+// 16 MiB +2.1 %, 256 MiB on the nt path +1 %).
+template <int OP, typename T, int U, int UA, int SAUX>
+__device__ __forceinline__ void lds_tile(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src,
+                                         size_t nvec, size_t base,
+                                         u32x4 (*lds)[kLdsWaves][UA][64], unsigned w,
+                                         unsigned l) {
+  if (base + 64 * U <= nvec) {
+    if constexpr (OP != OP_WRITE) {  // ATOMIC_WRITE never reads dst
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, /*aux: nt*/ 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      u32x4 v;
+      if constexpr (OP == OP_WRITE) v = lds[1][w][u][l];
+      else v = apply_vec<OP, T>(lds[0][w][u][l], lds[1][w][u][l]);
+      if constexpr (SAUX == kStoreNt)
+        st<true>(dst + base + u * 64 + l, v);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec)
+        st<true>(dst + i, apply_vec<OP, T>(ld<true>(dst + i), ld<true>(src + i)));
+    }
+  }
+}
+
+template <int OP, typename T, int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_lds_taper(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec, size_t split,
+    unsigned head) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const unsigned b = blockIdx.x;
+  if (b < head)
+    lds_tile<OP, T, U, U, SAUX>(dst, src, split,
+                                (size_t)b * (kLdsWaves * 64 * U) + (size_t)w * 64 * U, lds, w, l);
+  else
+    lds_tile<OP, T, 1, U, SAUX>(dst, src, nvec,
+                                split + (size_t)(b - head) * (kLdsWaves * 64) + (size_t)w * 64,
+                                lds, w, l);
+}
+
 // Grid-stride variant (for the tuning sweep): a fixed grid of G workgroups
 // walks the buffer; each thread holds U vectors spaced kBlock apart.
 template <int OP, typename T, int U, bool NTL, bool NTS>
@@ -994,6 +1058,10 @@ __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds(F f, size_t nvec) {
 // bench.py --tune; see DESIGN.md "Kernel tuning"): LDS-DMA staging, 4 KiB of
 // each operand per wave, nt loads and stores.
 constexpr int kUnroll = 4;
+// combine_lds_taper from this many bytes per operand (up to kSc1Bytes; the
+// nt-store path above keeps the uniform grid), the last 1/kTaperDiv tapered
+constexpr size_t kTaperBytes = (size_t)32 << 20;
+constexpr size_t kTaperDiv = 8;
 
 static inline unsigned grid_for(size_t work, size_t per_block, unsigned cap) {
   size_t g = (work + per_block - 1) / per_block;
@@ -1026,7 +1094,16 @@ static int launch_write(void *dst, const void *src, size_t cnt,
         u32x4 *d = (u32x4 *)((char *)dst + head * E);
         const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
         const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll, 0x7fffffffu));
-        if (nvec * 16 < kSc1Bytes)
+        if (nvec * 16 >= kTaperBytes && nvec * 16 < kSc1Bytes) {
+          // the last 1/kTaperDiv of the vectors in 1-KiB tiles
+          const size_t hv = (size_t)kLdsWaves * 64 * kUnroll;
+          size_t split = nvec - nvec / kTaperDiv;
+          split -= split % hv;
+          const unsigned head = (unsigned)(split / hv);
+          const unsigned tail = (unsigned)((nvec - split + kLdsWaves * 64 - 1) / (kLdsWaves * 64));
+          hipLaunchKernelGGL((combine_lds_taper<OP, T, kUnroll, kStoreSc1>), dim3(head + tail),
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
+        } else if (nvec * 16 < kSc1Bytes)
           hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreSc1>), grid,
                              dim3(kLdsWaves * 64), 0, s, d, v, nvec);
         else

@@ -1292,6 +1292,14 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 87: lfa::launch_taper<4, 1>(d, v, nvec, 8, s); break;
     case 88: lfa::launch_taper<4, 1>(d, v, nvec, 16, s); break;
     case 89: lfa::launch_taper<4, 2>(d, v, nvec, 16, s); break;
+    case 78:  // the round-3 product: uniform 4-KiB tiles at every size
+      if (nvec * 16 < lfa::kSc1Bytes)
+        hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreSc1>), g4, b4, 0,
+                           s, d, v, nvec);
+      else
+        hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreNt>), g4, b4, 0,
+                           s, d, v, nvec);
+      break;
     case 77:
       if (nvec * 16 < lfa::kSc1Bytes)
         hipLaunchKernelGGL((lfa::combine_lds<lfa::OP_SUM, float, 4, lfa::kStoreSc1, false>), g4,

@@ -256,7 +256,23 @@ def _share_gpu(world):
     slow enough to time tests out.  One process per GPU (the product's
     layout) never meets this."""
     if world > 4:
-        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LFA_TEST_HW_QUEUES", "2")
+        # the test process itself holds queues too (every GPU test before this
+        # one ran in it): 8 workers at 2 queues each beside it crossed the
+        # limit in one round-4 suite run (the 8-process test timed out there
+        # and passed alone), so 6+ workers take 1 queue each — 47 us per
+        # 4 KiB one-shot at 8 processes against 31 us at 2 queues and 10.6 ms
+        # at 3 (tools/gpu.sh procs, profiles/r04_procs_queues.jsonl)
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("LFA_TEST_HW_QUEUES",
+                                                         "1" if world > 5 else "2")
+
+
+def _kfd_queues(pid=None):
+    """Hardware queues the process holds on the GPU (KFD's sysfs view), or
+    None where that is not readable."""
+    try:
+        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{pid or os.getpid()}/queues"))
+    except OSError:
+        return None
 
 def _log_stderr(tag, rank, world):
     """PEER_LOG_DIR set: this rank's stderr (LFA_DEBUG / LFA_TRACE lines) goes
@@ -320,7 +336,8 @@ def test_c_executor_gpu_kernels_across_processes(world):
             if p.is_alive():
                 p.kill()
     bad = {r: results.get(r) for r in range(world) if results.get(r) != "ok"}
-    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
+    assert not bad, (f"test process holds {_kfd_queues()} GPU queues; " +
+                     "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items())))
 
 
 def _growth_worker(rank, world, port, q):

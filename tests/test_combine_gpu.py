@@ -348,6 +348,39 @@ def test_nt_store_path_every_op_family(lfa, op, dt):
         assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
 
 
+@pytest.mark.parametrize("op,dt", [(0, 8), (1, 6), (3, 9), (6, 5), (11, 4), (8, 1), (9, 7)])
+@pytest.mark.parametrize("mib", [32, 100])
+def test_tapered_tail_every_op_family(lfa, op, dt, mib):
+    """From 32 MiB to 192 MiB per operand the combine runs as
+    combine_lds_taper: 4-KiB tiles up to a split, 1-KiB tiles after it
+    (DESIGN.md §4).  One op of every family, ATOMIC_WRITE included, at
+    `mib` MiB + a ragged tail, oracle-checked on windows at both ends, across
+    the split and across the last full tile."""
+    nd = oracle.DT_NP[dt]
+    e = nd.itemsize
+    n = ((mib << 20) + 4 * 999 + e * 5) // e
+    g = torch.Generator(device=DEV).manual_seed(op * 13 + dt + mib)
+    if nd.kind == "f":
+        f = torch.float32 if e == 4 else torch.float64
+        d0 = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
+        sv = (torch.rand(n, device=DEV, generator=g, dtype=f) + 0.5).view(torch.uint8)
+    else:
+        d0 = torch.randint(0, 256, (n * e,), dtype=torch.uint8, device=DEV, generator=g)
+        sv = torch.randint(0, 256, (n * e,), dtype=torch.uint8, device=DEV, generator=g)
+    d = d0.clone()
+    assert lfa.write_ptr(op, dt, d.data_ptr(), sv.data_ptr(), n) == 0
+    torch.cuda.synchronize()
+    nvec = n * e // 16                  # torch buffers are 16-B aligned: no head
+    split = nvec - nvec // 8
+    split -= split % 1024
+    at = split * 16 // e                # first element of the 1-KiB tiles
+    for lo in (0, at - 2500, n // 2, n - 70_000, n - 5000):
+        hi = min(n, lo + 5000)
+        want = d0[lo * e:hi * e].cpu().numpy().view(nd).copy()
+        oracle.write(op, dt, want, sv[lo * e:hi * e].cpu().numpy().view(nd).copy())
+        assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
+
+
 def test_tree_put_errors(lfa):
     import ctypes
     from libfabric_amd import _native

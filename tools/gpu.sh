@@ -86,10 +86,12 @@ for stage in "$@"; do
       # one-shot latency at 8 processes: with the parent holding a GPU context
       # or not (9 or 8 processes on the GPU), 7 workers + a GPU parent, and
       # 8 workers at 4 hardware queues each
-      $S procs_8 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick && \
-      $S procs_8_parent 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick --parent-gpu && \
-      $S procs_7_parent 150 python3 -u tools/probe_p2p_latency.py --world 7 --reps 100 --quick --parent-gpu && \
-      GPU_MAX_HW_QUEUES=4 $S procs_8_q4 150 python3 -u tools/probe_p2p_latency.py --world 8 --reps 100 --quick || exit 99 ;;
+      for cfg in "8 2 -" "8 2 p" "8 1 p" "7 2 p" "8 1 -" "6 2 p" "8 3 -"; do
+        set -- $cfg
+        par=""; [ "$3" = p ] && par="--parent-gpu"
+        $S "procs_w$1_q$2_$3" 150 python3 -u tools/probe_p2p_latency.py --world $1 --reps 100 \
+          --quick --worker-queues $2 $par || exit 99
+      done ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)
@@ -99,7 +101,7 @@ for stage in "$@"; do
     solo)
       $S solo 200 python3 -u tools/probe_solo_latency.py || exit 99 ;;
     tunecomb)
-      $S tune_combine 500 python3 -u tools/tune_combine.py --sizes 32,64,256 \
+      $S tune_combine 500 python3 -u tools/tune_combine.py --sizes "${COMBINE_SIZES:-32,64,256}" \
         --variants "${COMBINE_VARIANTS:-30,80,81,82,83,84}" --rounds "${COMBINE_ROUNDS:-12}" || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;

@@ -36,6 +36,14 @@ def _port():
     return p
 
 
+def _kfd_queues(pid=None):
+    """Hardware queues the process holds (KFD sysfs), None if unreadable."""
+    try:
+        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{pid or os.getpid()}/queues"))
+    except OSError:
+        return None
+
+
 def _worker(rank, world, port, reps, quick, q):
     try:
         import torch
@@ -94,6 +102,7 @@ def _worker(rank, world, port, reps, quick, q):
                     dt_, op_ = (9, 3) if name == "p2p_rs" else (8, 2)
                     out[f"{name}_{nbytes}"]["c_loop_mean_us"] = round(
                         ep.bench_loop(kind, x, r, cnt, dt_, op_, reps=n), 1)
+            out["kfd_queues"] = _kfd_queues()
         finally:
             ep.close()
         dist.barrier()
@@ -110,13 +119,23 @@ def main():
     ap.add_argument("--reps", type=int, default=300)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--parent-gpu", action="store_true")
+    ap.add_argument("--worker-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES of the workers only (0: inherit); "
+                         "the parent keeps the environment's")
     a = ap.parse_args()
     import torch.multiprocessing as mp
+    parent_queues = os.environ.get("GPU_MAX_HW_QUEUES", "default")
     if a.parent_gpu:
         import torch
         torch.cuda.set_device(0)
         hold = torch.ones(1 << 20, device="cuda")
+        # as pytest's process after GPU tests: work on several streams
+        for _ in range(4):
+            with torch.cuda.stream(torch.cuda.Stream()):
+                hold.add_(1)
         torch.cuda.synchronize()
+    if a.worker_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.worker_queues)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -139,7 +158,9 @@ def main():
             p.kill()
     print(json.dumps({"world": a.world, "device": "one MI355X shared by all ranks",
                       "parent_gpu": a.parent_gpu,
-                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "2" if a.world > 4 else "4"),
+                      "parent_hw_queues": parent_queues if a.parent_gpu else None,
+                      "parent_kfd_queues": _kfd_queues(),
+                      "worker_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
                       "wall_s": wall, "timeout": res.get("timeout"),
                       "rank0": res.get(0), "rank1": res.get(1)}), flush=True)
     if not all(isinstance(v, dict) for v in res.values()):
