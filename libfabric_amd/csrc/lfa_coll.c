@@ -1318,7 +1318,7 @@ static void ws_give(char *p)
 	void *base = NULL;
 	size_t bytes = 0;
 	int dev = -1, slot = -1;
-	char *evict[WS_CACHE_SLOTS];
+	char *evict[WS_CACHE_SLOTS + 1];        /* a full cache's LRU + every slot */
 	int ne = 0;
 
 	hipPointerAttribute_t at;
@@ -1590,9 +1590,15 @@ static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, size_t r
 			uint64_t id = 0;
 
 			va_note('I', mc->sym[k], 0);
-			if (lfa_hip_note(why, hipMemcpy(&id, mc->sym[k] + 2 * region + LFA_SIG_ID_OFF,
-							sizeof(id), hipMemcpyDeviceToHost),
-					 "P2P identity read") != hipSuccess) {
+			/* on the endpoint's stream (idle here: the growth synchronised
+			 * it), not the null stream, which would wait for the
+			 * application's own queued work */
+			if (lfa_hip_note(why, hipMemcpyAsync(&id, mc->sym[k] + 2 * region +
+								     LFA_SIG_ID_OFF, sizeof(id),
+							     hipMemcpyDeviceToHost, mc->ep->stream),
+					 "P2P identity read") != hipSuccess ||
+			    lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
+					 "P2P identity read sync") != hipSuccess) {
 				ret = -LFA_EIO;
 			} else if (id != recs[k].id) {
 				lfa_hip_note(why, hipErrorInvalidValue, "P2P workspace identity");
