@@ -248,7 +248,7 @@ def _worker(rank, world, queues, seed, nops, q, dev=False, host_rank=-1, gchunk=
             if world > 4:
                 # past the scheduler's queue slots the GPU time-slices the
                 # processes' queues (tests/test_coll_peer_gpu.py::_share_gpu)
-                os.environ["GPU_MAX_HW_QUEUES"] = "2"
+                os.environ["GPU_MAX_HW_QUEUES"] = "1" if world > 5 else "2"
             torch.cuda.set_device(0)
             # host_rank: that member hands in host buffers on its GPU peer
             # domain (staged), the others device buffers — one schedule

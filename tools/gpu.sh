@@ -23,6 +23,7 @@
 #   host2        2-process host-buffer allreduce, default vs group chunks
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
 #   ipcab        the same with exported workspaces freed (cache 0), then kept
+#   soak         random collective programs over more seeds (stress_soak.py)
 #   procs        8-process one-shot latency: parent with / without a GPU context,
 #                7 workers + GPU parent, 8 workers at 4 queues
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
@@ -92,6 +93,14 @@ for stage in "$@"; do
         $S "procs_w$1_q$2_$3" 150 python3 -u tools/probe_p2p_latency.py --world $1 --reps 100 \
           --quick --worker-queues $2 $par || exit 99
       done ;;
+    soak)
+      # random programs of collectives (tests/test_coll_stress.py) over more
+      # seeds: device members at 2-8 processes, then a host-buffer member
+      # with every 4th post refused
+      $S soak_dev 560 python3 -u tools/stress_soak.py --dev --worlds 2,3,5,8 --seeds 300-309 \
+        --nops 200 && \
+      $S soak_host 400 python3 -u tools/stress_soak.py --dev --worlds 2,3,5 --seeds 400-407 \
+        --nops 160 --host-rank 1 --refuse-every 4 || exit 99 ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)
