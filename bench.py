@@ -692,7 +692,9 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     # one rank's kernel could not wait for the other's)
     import ctypes
     region, flag_off = 1 << 20, 2 << 20
-    ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device=dev) for _ in range(2)]
+    from libfabric_amd.coll import sig_area_bytes
+    ws = [torch.zeros(flag_off + sig_area_bytes(), dtype=torch.uint8, device=dev)
+          for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
     status = torch.full((1,), -1, dtype=torch.int64).pin_memory()   # LFA_SIG_NONE
     # two priorities: HIP keeps a hardware-queue pool per priority, so the

@@ -254,6 +254,15 @@ def group_chunk(setting: int, nranks: int, nbytes: int) -> int:
     return lib().lfa_coll_group_chunk(setting, nranks, nbytes)
 
 
+def sig_area_bytes() -> int:
+    """LFA_SIG_AREA_BYTES: the flag area that ends every P2P workspace (flag
+    rows, LL one-shot words, identity word) — for a workspace built by hand."""
+    from ._native import lib as native
+    f = native("lfa").lfa__sig_area_bytes
+    f.restype = ctypes.c_size_t
+    return f()
+
+
 def ws_cached_bytes() -> int:
     """lfa_coll_ws_cached_bytes: released P2P workspaces kept for reuse."""
     return lib().lfa_coll_ws_cached_bytes()

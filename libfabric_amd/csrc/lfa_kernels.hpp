@@ -362,8 +362,8 @@ __device__ __forceinline__ V apply_any(V d, V s) {
 // Evaluate the tree for one element (or one 16-B vector); load(k) fetches
 // input k.  Leaf order, pairing and merge order are compile-time except the
 // kernel-argument (wave-uniform) pair test.
-template <int OP, typename T, typename V, int NLEAF, typename L>
-__device__ __forceinline__ V tree_eval_with(const TreeArgs &a, L &&load) {
+template <int OP, typename T, typename V, int NLEAF, typename L, typename A = TreeArgs>
+__device__ __forceinline__ V tree_eval_with(const A &a, L &&load) {
   V stack[6];
   int depth = 0;
 #pragma unroll
@@ -820,6 +820,144 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   //    one system-scope release (its waves share a CU and an L2) before it
   //    counts itself; the last workgroup resets the counter for the next
   //    launch on the stream and publishes done_val to the host
+  if (a.done_word) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      if (seen + 1 == gridDim.x) {
+        __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LL one-shot (lfa_signal.h): parts of at most LFA_OS_LL_BYTES.  Lane c owns
+// bytes [16c, 16c + 16) of every part: it pushes its 16 bytes of each peer's
+// part as two 16-byte stores of {data, flag, data, flag} into that peer's LL
+// slot for this rank, then polls its own slots' words until every peer's four
+// flags read 2·epoch + 1 — the 8-byte {data, flag} pairs are written and read
+// whole, so a matching flag carries its data — and reduces the values in
+// prov/coll's association order.  No acknowledgement wait, fence or flag post
+// between push and wait, and the poll is the read.  Same completion word and
+// timeout as oneshot_reduce.
+// ---------------------------------------------------------------------------
+struct LlArgs {
+  const char *send;
+  char *result;
+  char *push[kOsMax];          // peer k's LL slot of this rank, this parity
+  const char *own;             // this rank's LL slots, this parity
+  uint64_t *status;
+  uint64_t ticket, timeout;    // timeout: wall-clock ticks
+  uint32_t *done_ctr;
+  uint64_t *done_word;
+  uint64_t done_val;
+  uint32_t soff[kOsMax], slen[kOsMax];
+  uint32_t flag;
+  int n, rank, vec;            // vec: every part start and result 16-B aligned
+  signed char hi[kOsMax], lo[kOsMax];  // the association tree's leaves
+};
+
+// 16 bytes at base + off, bytes at or past len read as zero (registers only)
+__device__ __forceinline__ u32x4 ll_in(const char *base, uint32_t off, uint32_t len, int vec) {
+  if (vec && off + 16 <= len) return *(const u32x4 *)(base + off);
+  u32x4 v = {0, 0, 0, 0};
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t i = off + 4 * w + b;
+      if (i < len) x |= (uint32_t)(unsigned char)base[i] << (8 * b);
+    }
+    v[w] = x;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void ll_out(char *base, uint32_t off, uint32_t len, int vec, u32x4 v) {
+  if (vec && off + 16 <= len) {
+    *(u32x4 *)(base + off) = v;
+    return;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t i = off + 4 * w + b;
+      if (i < len) base[i] = (char)(v[w] >> (8 * b));
+    }
+}
+
+// vals[k] for a wave-uniform k without indexing registers dynamically
+__device__ __forceinline__ u32x4 ll_pick(const u32x4 (&v)[kOsMax], int k) {
+  u32x4 r = v[0];
+#pragma unroll
+  for (int i = 1; i < kOsMax; i++)
+    if (k == i) r = v[i];
+  return r;
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void oneshot_ll(LlArgs a) {
+  const unsigned t = threadIdx.x;
+  const uint32_t off = ((uint32_t)blockIdx.x * kBlock + t) * 16u;
+  // 1. push this lane's 16 bytes of every peer's part
+#pragma unroll
+  for (int k = 0; k < kOsMax; k++) {
+    if (k >= a.n || k == a.rank || off >= a.slen[k]) continue;
+    const u32x4 v = ll_in(a.send + a.soff[k], off, a.slen[k], a.vec);
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(a.push[k], LFA_SIG_LL_SLOT);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], a.flag, v[1], a.flag}, r, 2 * off, 0,
+                                           kSysAux);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[2], a.flag, v[3], a.flag}, r, 2 * off + 16,
+                                           0, kSysAux);
+  }
+  // 2. this rank's part: poll every peer's words until their flags match
+  const uint32_t own = a.slen[a.rank];
+  if (off < own) {
+    u32x4 vals[kOsMax];
+    uint32_t pending = 0;
+    const u32x4 mine = ll_in(a.send + a.soff[a.rank], off, own, a.vec);
+#pragma unroll
+    for (int k = 0; k < kOsMax; k++) {
+      vals[k] = k == a.rank ? mine : u32x4{0, 0, 0, 0};
+      if (k < a.n && k != a.rank) pending |= 1u << k;
+    }
+    const uint64_t t0 = wall_clock64();
+    while (pending) {
+#pragma unroll
+      for (int k = 0; k < kOsMax; k++) {
+        if (!(pending >> k & 1u)) continue;
+        const __amdgpu_buffer_rsrc_t r =
+            tile_rsrc(a.own + (size_t)k * LFA_SIG_LL_SLOT, LFA_SIG_LL_SLOT);
+        const u32x4 w0 = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 2 * off, 0, kSysLoadAux));
+        const u32x4 w1 = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 2 * off + 16, 0, kSysLoadAux));
+        if (w0[1] == a.flag && w0[3] == a.flag && w1[1] == a.flag && w1[3] == a.flag) {
+          vals[k] = u32x4{w0[0], w0[2], w1[0], w1[2]};
+          pending &= ~(1u << k);
+        }
+      }
+      if (pending) {
+        if (wall_clock64() - t0 > a.timeout) {
+          lfa_sig_note_timeout(a.status, a.ticket);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    ll_out(a.result, off, own, a.vec,
+           tree_eval_with<OP, T, u32x4, NLEAF>(a, [&](int k) { return ll_pick(vals, k); }));
+  }
+  // 3. completion word, as oneshot_reduce's step 5
   if (a.done_word) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1353,6 +1491,17 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
   }
 }
 
+// LFA_OS_LL=0: the flagged one-shot for every size (A/B; the same setting on
+// every member of a group, as both sides of the exchange follow it)
+static inline bool ll_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("LFA_OS_LL");
+    on = !(e && e[0] == '0');
+  }
+  return on;
+}
+
 template <int OP, typename T>
 static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
   if constexpr (!supported<OP, T>()) {
@@ -1397,6 +1546,49 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       }
     }
     const int pof2 = tree_leaves(a.t, srcs, n);
+    if (n > 1 && most <= LFA_OS_LL_BYTES && ll_enabled()) {
+      // LL one-shot: the words live in the flag area (lfa_signal.h)
+      LlArgs l;
+      memset(&l, 0, sizeof(l));
+      const size_t lpar = (size_t)(h.epoch & 1) * LFA_SIG_LL_PARITY;
+      for (int k = 0; k < n; k++) {
+        l.soff[k] = (uint32_t)a.soff[k];
+        l.slen[k] = (uint32_t)a.slen[k];
+        if (k != r)
+          l.push[k] = h.sym[k] + h.flag_off + LFA_SIG_LL_OFF + lpar + (size_t)r * LFA_SIG_LL_SLOT;
+        l.hi[k] = a.t.hi[k];
+        l.lo[k] = a.t.lo[k];
+      }
+      l.own = h.sym[r] + h.flag_off + LFA_SIG_LL_OFF + lpar;
+      l.send = (const char *)h.send;
+      l.result = (char *)h.result;
+      l.status = h.status;
+      l.ticket = h.ticket;
+      l.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
+      l.done_ctr = h.done_ctr;
+      l.done_word = h.done_word;
+      l.done_val = h.done_val;
+      l.flag = h.epoch * 2u + 1u;
+      l.n = n;
+      l.rank = r;
+      l.vec = mis == 0;
+      // the same grid on every member: `most` depends only on count and n
+      const unsigned grid = (unsigned)(((most + 15) / 16 + kBlock - 1) / kBlock);
+      switch (pof2) {
+        case 2:
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, l);
+          break;
+        case 4:
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, l);
+          break;
+        case 8:
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, l);
+          break;
+        default:
+          return -LFA_EINVAL;
+      }
+      return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
+    }
     a.wait = n > 1 ? (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF) : nullptr;
     a.done_ctr = h.done_ctr;
     a.done_word = h.done_word;

@@ -21,7 +21,7 @@ extern "C" {
 #endif
 
 #define LFA_SIG_MAX 32                  /* ranks (= LFA_TREE_MAX) */
-#define LFA_SIG_AREA_BYTES (64u << 10)  /* flag area after the two regions */
+#define LFA_SIG_AREA_BYTES (1u << 20)   /* flag area after the two regions */
 #define LFA_SIG_BAR_OFF 0               /* barrier row: uint32[LFA_SIG_MAX] */
 /* one-shot rows: uint32[LFA_SIG_OS_CHUNKS][LFA_SIG_MAX], word [b][k] written
  * by rank k's workgroup b */
@@ -32,6 +32,24 @@ extern "C" {
  * (lfa_coll.c sym_open) */
 #define LFA_SIG_ID_OFF (LFA_SIG_AREA_BYTES - 64u)
 #define LFA_OS_MAX_RANKS 8              /* one-shot groups: 1..8 members */
+/*
+ * LL one-shot (parts of at most LFA_OS_LL_BYTES): every 4 bytes of a part
+ * travel as one 8-byte word {data, flag} with flag = 2·epoch + 1, written
+ * and read whole, so the data's arrival is its own signal — no separate
+ * flag, no acknowledgement wait before it, no second read.  The words live in
+ * the flag area (zeroed at every workspace growth, never holding raw data):
+ * per parity (epoch & 1) LFA_OS_MAX_RANKS slots of LFA_SIG_LL_SLOT bytes, the
+ * slot of rank k holding what rank k sent.  LFA_OS_LL=0 in the environment
+ * (the same on every member) keeps the flagged kernel for every size.
+ */
+#define LFA_OS_LL_BYTES (16u << 10)
+#define LFA_SIG_LL_SLOT (2u * LFA_OS_LL_BYTES)
+#define LFA_SIG_LL_PARITY (LFA_OS_MAX_RANKS * LFA_SIG_LL_SLOT)
+#define LFA_SIG_LL_OFF (64u << 10)
+#if LFA_SIG_LL_OFF + 2 * LFA_SIG_LL_PARITY > LFA_SIG_ID_OFF || \
+    LFA_SIG_OS_OFF + 4 * LFA_SIG_OS_CHUNKS * LFA_SIG_MAX > LFA_SIG_LL_OFF
+#error "flag area layout"
+#endif
 
 /*
  * Timed-out waits.  *status is one host-mapped word per group holding the
@@ -137,6 +155,8 @@ static __device__ __forceinline__ void lfa_sig_note_timeout(uint64_t *status,
 
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
 uint64_t lfa__wallclock_ticks_per_us(void);
+/* LFA_SIG_AREA_BYTES, for callers that build a workspace by hand (tests). */
+size_t lfa__sig_area_bytes(void);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,8 @@ extern "C" int lfa_solo_copy_async(void *result, const void *send, size_t bytes,
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
 
+extern "C" size_t lfa__sig_area_bytes(void) { return LFA_SIG_AREA_BYTES; }
+
 extern "C" uint64_t lfa__wallclock_ticks_per_us(void) {
   static uint64_t t = 0;
   if (!t) {

@@ -481,7 +481,8 @@ def test_gpu_oneshot_misaligned_buffers(dt, mode, offs):
     sends = [_operand(dt, count, rng, 0.05) for _ in range(2)]
     full = oracle.allreduce(op, dt, [x.view(nd) for x in sends])[0].view(np.uint8)
     region, flag_off = 1 << 20, 2 << 20
-    ws = [torch.zeros(flag_off + (64 << 10), dtype=torch.uint8, device="cuda")
+    from libfabric_amd.coll import sig_area_bytes
+    ws = [torch.zeros(flag_off + sig_area_bytes(), dtype=torch.uint8, device="cuda")
           for _ in range(2)]
     sym = (ctypes.c_void_p * 2)(*[w.data_ptr() for w in ws])
     status = torch.full((1,), -1, dtype=torch.int64).pin_memory()

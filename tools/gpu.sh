@@ -19,6 +19,7 @@
 #   treeput_pmc  counters of the 8->8 tree_put (TREEPUT_PMC_VARIANT)
 #   clat         small-collective latency: world-1 RCCL domain and 2-process
 #                P2P, C-timed loop (liblfa_bench.so) and its breakdown
+#   clatll       2-process P2P latency, flagged one-shot vs LL
 #   sizes        combine kernel durations vs size under --kernel-trace
 #   host2        2-process host-buffer allreduce, default vs group chunks
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
@@ -72,6 +73,10 @@ for stage in "$@"; do
       done ;;
     clat)
       $S clat 300 python3 -u tools/probe_latency.py || exit 99 ;;
+    clatll)
+      # 2-process P2P latency with the flagged one-shot (LFA_OS_LL=0), then LL
+      LFA_OS_LL=0 $S clat_flagged 200 python3 -u tools/probe_latency.py --skip-world1 && \
+      $S clat_ll 200 python3 -u tools/probe_latency.py --skip-world1 || exit 99 ;;
     sizes)
       $S ksizes 300 $P -d gpurun_out/ksizes -o run -- python3 bench.py --only-extra sizes || exit 99 ;;
     host2)

@@ -45,7 +45,8 @@ def main() -> None:
     n, k_iters = 2, 200
     region = 8 << 20
     flag_off = 2 * region
-    ws = [torch.zeros(2 * region + (64 << 10), dtype=torch.uint8, device="cuda")
+    from libfabric_amd.coll import sig_area_bytes
+    ws = [torch.zeros(2 * region + sig_area_bytes(), dtype=torch.uint8, device="cuda")
           for _ in range(n)]
     sym = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws])
     status = ctypes.c_void_p()
