@@ -967,9 +967,10 @@ def test_oneshot_ops_in_flight_mixed(world, seed, nops):
     assert not bad, "\n".join(f"rank {r}: {m}" for r, m in sorted(bad.items()))
 
 
-def _every_entry_worker(rank, world, port, q):
+def _every_entry_worker(rank, world, port, q, ll="1"):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1",
+                          LFA_OS_LL=ll)
         _share_gpu(world)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -1028,19 +1029,21 @@ def _every_entry_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
-def test_oneshot_every_reducing_entry(world):
+@pytest.mark.parametrize("world,ll", [(2, "1"), (3, "1"), (4, "1"), (5, "1"), (8, "1"),
+                                      (2, "0"), (5, "0")])
+def test_oneshot_every_reducing_entry(world, ll):
     """Every (op, datatype) of the write table with a reducing op (MIN..BXOR,
     int8..uint64, float, double, float complex, int128) through LFA_ALGO_P2P's
     one-shot allreduce, reduce_scatter and reduce (roots in turn, non-roots
     passing no result buffer) across processes, on the golden
     fixtures' operands with their edge lanes (±0, ±inf, NaN, extremes):
     equal to prov/coll's recursive-doubling result (the oracle), bit for bit
-    (NaN lanes: NaN on both sides)."""
+    (NaN lanes: NaN on both sides).  ll "1": parts of these sizes take the
+    LL kernel; "0" (LFA_OS_LL=0 on every member) the flagged one."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_every_entry_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_every_entry_worker, args=(r, world, port, q, ll))
              for r in range(world)]
     for p in procs:
         p.start()
