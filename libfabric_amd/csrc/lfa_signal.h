@@ -39,8 +39,12 @@ extern "C" {
  * flag, no acknowledgement wait before it, no second read.  The words live in
  * the flag area (zeroed at every workspace growth, never holding raw data):
  * per parity (epoch & 1) LFA_OS_MAX_RANKS slots of LFA_SIG_LL_SLOT bytes, the
- * slot of rank k holding what rank k sent.  LFA_OS_LL=0 in the environment
- * (the same on every member) keeps the flagged kernel for every size.
+ * slot of rank k holding what rank k sent.  A word left in a slot matches a
+ * later operation's flag only 2^31 one-shots later at the same position (the
+ * parity halves alternate, so consecutive uses differ by 2 epochs).  It relies
+ * on an aligned 8-byte store reaching a peer whole, over xGMI as on one GPU;
+ * LFA_OS_LL=0 in the environment (the same on every member) keeps the flagged
+ * kernel for every size.
  */
 #define LFA_OS_LL_BYTES (16u << 10)
 #define LFA_SIG_LL_SLOT (2u * LFA_OS_LL_BYTES)
