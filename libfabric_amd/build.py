@@ -77,6 +77,32 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     objs.append(o)
     if _newer(o, [sig, os.path.join(CSRC, "lfa_signal.h"), os.path.join(INC, "lfa_fabric.h")]):
         steps.append([HIPCC, *HIP_FLAGS, "-c", sig, "-o", o])
+    # the direct-dispatch code object: a plain gfx950 ELF of lfa_direct_k.hip,
+    # embedded as bytes (lfa_direct.cpp loads it into its own HSA executable)
+    dk = os.path.join(CSRC, "lfa_direct_k.hip")
+    co = os.path.join(BUILD, "lfa_direct.hsaco")
+    co_c = os.path.join(BUILD, "lfa_direct_co.c")
+    co_o = os.path.join(BUILD, "lfa_direct_co.o")
+    objs.append(co_o)
+    if _newer(co_o, [dk]):
+        _run([os.path.join(ROCM, "lib", "llvm", "bin", "clang++"), "-x", "hip",
+              "--offload-device-only", "--offload-arch=" + ARCH, "--no-gpu-bundle-output",
+              "-O3", "-std=c++17", "-o", co, dk])
+        data = open(co, "rb").read()
+        with open(co_c, "w") as f:
+            f.write("#include <stddef.h>\n"
+                    "const unsigned char lfa_direct_co[] __attribute__((aligned(4096))) = {\n")
+            for i in range(0, len(data), 16):
+                f.write(",".join(str(b) for b in data[i:i + 16]) + ",\n")
+            f.write("};\nconst size_t lfa_direct_co_size = sizeof(lfa_direct_co);\n")
+        _run(["gcc", "-O2", "-fPIC", "-c", co_c, "-o", co_o])
+    direct = os.path.join(CSRC, "lfa_direct.cpp")
+    o = os.path.join(BUILD, "lfa_direct.o")
+    objs.append(o)
+    if _newer(o, [direct, os.path.join(CSRC, "lfa_signal.h")]):
+        steps.append(["g++", "-O2", "-fPIC", "-std=c++17", "-Wall",
+                      "-D__HIP_PLATFORM_AMD__", "-I" + INC,
+                      "-I" + os.path.join(ROCM, "include"), "-c", direct, "-o", o])
     capi = os.path.join(CSRC, "lfa_capi.cpp")
     o = os.path.join(BUILD, "lfa_capi.o")
     objs.append(o)
@@ -99,7 +125,8 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
                 f.result()
     if steps or _newer(LIB_LFA, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_LFA,
-              *objs, "-Wl,-soname,liblfa.so"])
+              *objs, "-L" + os.path.join(ROCM, "lib"), "-lhsa-runtime64",
+              "-Wl,-soname,liblfa.so"])
     if _newer(LIB_TUNE, tune_objs + [LIB_LFA]):
         # the tuning forms share the product's launchers, which call into
         # liblfa.so (lfa__wallclock_ticks_per_us)

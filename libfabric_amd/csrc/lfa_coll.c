@@ -159,6 +159,25 @@ static int done_word_init(struct lfa_coll_ep *ep)
 
 static void done_word_free(struct lfa_coll_ep *ep)
 {
+	if (ep->direct) {
+		/* the direct queue's kernels are on no stream: wait (bounded)
+		 * for the last one's word before its counter and word go */
+		struct timespec a, b;
+
+		clock_gettime(CLOCK_MONOTONIC, &a);
+		do {
+			clock_gettime(CLOCK_MONOTONIC, &b);
+		} while (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq &&
+			 b.tv_sec - a.tv_sec < 5);
+		lfa_direct_close(ep->direct);
+		ep->direct = NULL;
+	}
+	if (ep->ddone_ctr)
+		hipFree(ep->ddone_ctr);
+	if (ep->ddone_word)
+		hipHostFree(ep->ddone_word);
+	ep->ddone_ctr = NULL;
+	ep->ddone_word = NULL;
 	if (ep->done_ctr)
 		hipFree(ep->done_ctr);
 	if (ep->done_word)
@@ -573,7 +592,7 @@ static struct pending *queue_slot(struct lfa_coll_ep *ep)
 
 static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 			      void *context, int kind, struct lfa_coll_mc *mc,
-			      uint64_t done_val)
+			      uint64_t done_val, const uint64_t *done_w)
 {
 	struct pending *p = queue_slot(ep);
 
@@ -584,6 +603,7 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 		/* the one-shot kernel stores done_val into the completion word:
 		 * no event to record or query */
 		p->done_val = done_val;
+		p->done_w = done_w;
 		p->context = context;
 		p->kind = kind;
 		p->mc = mc;
@@ -955,7 +975,8 @@ static int pending_state(const struct lfa_coll_ep *ep, const struct pending *p,
 		return p->hop->done ? 0 : 1;
 	}
 	if (p->done_val)
-		return *(volatile uint64_t *)ep->done_word >= p->done_val ? 0 : 1;
+		return *(const volatile uint64_t *)(p->done_w ? p->done_w : ep->done_word) >=
+		       p->done_val ? 0 : 1;
 	hipError_t e = hipEventQuery(p->ev);
 
 	if (e == hipErrorNotReady)
@@ -1921,10 +1942,45 @@ static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
  * completion word, so the operation completes without an event (VERDICT r3
  * #4; the plan would be one COPY item plus an event record and query).
  */
+/* The direct queue for this endpoint's device, opened at first use. */
+static struct lfa_direct *direct_of(struct lfa_coll_ep *ep)
+{
+	const char *e;
+
+	if (ep->direct || ep->direct_tried)
+		return ep->direct;
+	ep->direct_tried = 1;
+	e = getenv("LFA_DIRECT");
+	if (e && e[0] == '0')
+		return NULL;
+	if (hipMalloc((void **)&ep->ddone_ctr, sizeof(uint32_t)) != hipSuccess ||
+	    hipMemset(ep->ddone_ctr, 0, sizeof(uint32_t)) != hipSuccess ||
+	    hipHostMalloc((void **)&ep->ddone_word, sizeof(uint64_t),
+			  hipHostMallocCoherent) != hipSuccess) {
+		(void)hipGetLastError();
+		return NULL;
+	}
+	*(volatile uint64_t *)ep->ddone_word = 0;
+	ep->direct = lfa_direct_open(ep->dom->device);
+	return ep->direct;
+}
+
 static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
 		    enum lfa_datatype dt)
 {
 	int ret;
+
+	ep->op_done_w = NULL;
+	if (ep->allow_direct && direct_of(ep)) {
+		/* no HIP launch: ~3 us less host time */
+		ret = lfa_direct_solo_copy(ep->direct, result, buf, count * lfa_datatype_size(dt),
+					   ep->ddone_ctr, ep->ddone_word, ep->ddone_seq + 1);
+		if (ret)
+			return ret;
+		ep->op_done_val = ++ep->ddone_seq;
+		ep->op_done_w = ep->ddone_word;
+		return 0;
+	}
 
 	/* the one-shot kernel with n = 1 gives the same bytes; this kernel's
 	 * arguments are 48 bytes instead of ~700, about 1 us less from launch
@@ -1952,6 +2008,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	int ret;
 
 	ep->op_done_val = 0;
+	ep->op_done_w = NULL;
 	if (algo == LFA_ALGO_RCCL && mc->size > 1 &&
 	    try_rccl(mc, coll, buf, result, count, root, dt, op, s, &ret))
 		return ret;
@@ -2388,6 +2445,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	struct lfa_coll_mc *mc;
 	size_t esz, chunk;
 	uint64_t t0, done_val = 0;
+	const uint64_t *done_w = NULL;
 	int root = -1, ret, host, chunkable;
 
 	if (!ep)
@@ -2463,9 +2521,13 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	} else if (!host) {
 		/* a small bucket's one-shot kernel ends in the completion word */
 		ep->op_done_val = 0;
+		ep->op_done_w = NULL;
+		ep->allow_direct = 1;
 		ret = run_device(ep, mc, coll, buf, result, count, root, dt, op,
 				 ep->stream, ep->algo);
+		ep->allow_direct = 0;
 		done_val = ep->op_done_val;
+		done_w = ep->op_done_w;
 	} else if (chunkable) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op, chunk);
@@ -2485,7 +2547,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 				     root, dt, op);
 	}
 	if (!ret)
-		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, done_val);
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, done_val, done_w);
 	if (!ret)
 		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
@@ -2610,7 +2672,8 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 				 (uint64_t *)ep->barrier_dev + 1, 1, -1, LFA_UINT64,
 				 LFA_BAND, ep->stream, ep->algo);
 	if (!ret)
-		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, ep->op_done_val);
+		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, ep->op_done_val,
+					 ep->op_done_w);
 	if (!ret)
 		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);
@@ -2849,7 +2912,7 @@ static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 					       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
 		}
 		if (!ret)
-			ret = enqueue_completion(ep, ep->stream, context, 1, mc, 0);
+			ret = enqueue_completion(ep, ep->stream, context, 1, mc, 0, NULL);
 		if (!ret)
 			tag_p2p(ep, over, t0);
 	}

@@ -116,8 +116,10 @@ struct pending {
 	uint64_t ticket;
 	int timed_out;
 	/* device domains: completes when the endpoint's completion word reaches
-	 * done_val (the one-shot kernel wrote it; no event), 0: the event */
+	 * done_val (the one-shot kernel wrote it; no event), 0: the event;
+	 * done_w: that word (NULL: the endpoint's done_word) */
 	uint64_t done_val;
+	const uint64_t *done_w;
 	/* the chunks of one chunked operation (peer_submit_chunked) share a
 	 * nonzero chain id: the operation posts ONE completion — the first
 	 * chunk's error, or the last chunk's success */
@@ -171,6 +173,18 @@ struct lfa_coll_ep {
 	uint64_t *done_word;        /* host-mapped */
 	uint64_t done_seq;
 	uint64_t op_done_val;       /* run_device's last launch's value, or 0 */
+	const uint64_t *op_done_w;  /* ... and its word (NULL: done_word) */
+	/* direct dispatch (lfa_signal.h lfa_direct_*): a one-member group's
+	 * small reducing collective as liblfa's own AQL packet on its own HSA
+	 * queue, with its own counter and word (kernels there are not ordered
+	 * with ep->stream).  Opened at first use; LFA_DIRECT=0 keeps the HIP
+	 * launch.  allow_direct: set by submit around a caller's operation (the
+	 * barrier's own staging copy is stream-ordered, so it never goes direct) */
+	struct lfa_direct *direct;
+	int direct_tried, allow_direct;
+	uint32_t *ddone_ctr;
+	uint64_t *ddone_word;
+	uint64_t ddone_seq;
 	int nev;
 	struct plan_cache {         /* last schedules built, keyed by shape */
 		int valid, coll, algo, rank, n, root;

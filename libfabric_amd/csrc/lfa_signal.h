@@ -157,6 +157,19 @@ static __device__ __forceinline__ void lfa_sig_note_timeout(uint64_t *status,
 }
 #endif
 
+/*
+ * Direct dispatch (lfa_direct.cpp): lfa_solo_copy_async's kernel launched
+ * with this library's own AQL packet on its own HSA queue of `device` instead
+ * of a HIP stream — no ordering with any stream; kernels on the queue run in
+ * order.  open returns NULL where the queue cannot be set up (the caller keeps
+ * the HIP launch).  done_ctr must not be shared with kernels on other queues.
+ */
+struct lfa_direct;
+struct lfa_direct *lfa_direct_open(int device);
+int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send, size_t bytes,
+			 uint32_t *done_ctr, uint64_t *done_word, uint64_t done_val);
+void lfa_direct_close(struct lfa_direct *d);
+
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
 uint64_t lfa__wallclock_ticks_per_us(void);
 /* LFA_SIG_AREA_BYTES, for callers that build a workspace by hand (tests). */

@@ -11,6 +11,7 @@
 //             round trip), then ds_read_b128 -> add -> global store
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <errno.h>
 #include <string.h>
 #include <time.h>
 
@@ -1453,6 +1454,7 @@ extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size
     return -LFA_EIO;
   }
   *(volatile uint64_t *)word = 0;
+  struct lfa_direct *direct = nullptr;
   const unsigned nvec = (unsigned)(bytes / 16);
   struct lfa_oneshot a;
   memset(&a, 0, sizeof(a));
@@ -1489,11 +1491,29 @@ extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size
       case 6:
         rc = lfa_solo_copy_async(dst, src, bytes, ctr, word, val, s);
         break;
+      case 7:  // the same kernel through liblfa's own HSA queue (lfa_direct.cpp)
+        if (!direct) {
+          int dev = 0;
+          hipGetDevice(&dev);
+          direct = lfa_direct_open(dev);
+          if (!direct) {
+            rc = -LFA_ENOSYS;
+            break;
+          }
+        }
+        rc = lfa_direct_solo_copy(direct, dst, src, bytes, ctr, word, val);
+        break;
       default: rc = -LFA_EINVAL;
     }
+    // bounded: a word that never comes is an error, not a hang
+    struct timespec w0, w1;
+    clock_gettime(CLOCK_MONOTONIC, &w0);
     while (!rc && *(volatile uint64_t *)word < val) {
+      clock_gettime(CLOCK_MONOTONIC, &w1);
+      if (w1.tv_sec - w0.tv_sec > 2) rc = -ETIMEDOUT;
     }
   }
+  if (direct) lfa_direct_close(direct);
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   *us = (ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3 - t0) / reps;
