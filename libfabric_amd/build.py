@@ -80,21 +80,27 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     # the direct-dispatch code object: a plain gfx950 ELF of lfa_direct_k.hip,
     # embedded as bytes (lfa_direct.cpp loads it into its own HSA executable)
     dk = os.path.join(CSRC, "lfa_direct_k.hip")
-    co = os.path.join(BUILD, "lfa_direct.hsaco")
     co_c = os.path.join(BUILD, "lfa_direct_co.c")
     co_o = os.path.join(BUILD, "lfa_direct_co.o")
     objs.append(co_o)
     if _newer(co_o, [dk]):
-        _run([os.path.join(ROCM, "lib", "llvm", "bin", "clang++"), "-x", "hip",
-              "--offload-device-only", "--offload-arch=" + ARCH, "--no-gpu-bundle-output",
-              "-O3", "-std=c++17", "-o", co, dk])
-        data = open(co, "rb").read()
+        # two code objects: the kernel as is, and with its arguments preloaded
+        # into SGPRs by the packet processor (lfa_direct_k.hip)
         with open(co_c, "w") as f:
-            f.write("#include <stddef.h>\n"
-                    "const unsigned char lfa_direct_co[] __attribute__((aligned(4096))) = {\n")
-            for i in range(0, len(data), 16):
-                f.write(",".join(str(b) for b in data[i:i + 16]) + ",\n")
-            f.write("};\nconst size_t lfa_direct_co_size = sizeof(lfa_direct_co);\n")
+            f.write("#include <stddef.h>\n")
+            for sym, extra in (("lfa_direct_co", []),
+                               ("lfa_direct_co_pl",
+                                ["-DLFA_DIRECT_NAME=lfa_direct_solo_copy_pl", "-mllvm",
+                                 "-amdgpu-kernarg-preload-count=14"])):
+                co = os.path.join(BUILD, sym + ".hsaco")
+                _run([os.path.join(ROCM, "lib", "llvm", "bin", "clang++"), "-x", "hip",
+                      "--offload-device-only", "--offload-arch=" + ARCH,
+                      "--no-gpu-bundle-output", "-O3", "-std=c++17", *extra, "-o", co, dk])
+                data = open(co, "rb").read()
+                f.write(f"const unsigned char {sym}[] __attribute__((aligned(4096))) = {{\n")
+                for i in range(0, len(data), 16):
+                    f.write(",".join(str(b) for b in data[i:i + 16]) + ",\n")
+                f.write(f"}};\nconst size_t {sym}_size = sizeof({sym});\n")
         _run(["gcc", "-O2", "-fPIC", "-c", co_c, "-o", co_o])
     direct = os.path.join(CSRC, "lfa_direct.cpp")
     o = os.path.join(BUILD, "lfa_direct.o")

@@ -27,8 +27,8 @@
 #include "lfa_fabric.h"
 #include "lfa_signal.h"
 
-extern "C" const unsigned char lfa_direct_co[];
-extern "C" const size_t lfa_direct_co_size;
+extern "C" const unsigned char lfa_direct_co[], lfa_direct_co_pl[];
+extern "C" const size_t lfa_direct_co_size, lfa_direct_co_pl_size;
 
 namespace {
 
@@ -92,13 +92,13 @@ hsa_status_t find_kernarg(hsa_region_t r, void *data) {
 struct lfa_direct {
   hsa_agent_t gpu;
   hsa_queue_t *q;
-  hsa_code_object_reader_t reader;
+  hsa_code_object_reader_t reader, reader_pl;
   hsa_executable_t exe;
   uint64_t solo_kobj;
   uint32_t solo_private, solo_group;
   char *kernarg;                            // kQueueSize slots of 64 B
   pthread_mutex_t lock;
-  int hsa_up, have_reader, have_exe;
+  int hsa_up, have_reader, have_reader_pl, have_exe;
 };
 
 extern "C" void lfa_direct_close(struct lfa_direct *d) {
@@ -107,6 +107,7 @@ extern "C" void lfa_direct_close(struct lfa_direct *d) {
   if (d->kernarg) hsa_memory_free(d->kernarg);
   if (d->have_exe) hsa_executable_destroy(d->exe);
   if (d->have_reader) hsa_code_object_reader_destroy(d->reader);
+  if (d->have_reader_pl) hsa_code_object_reader_destroy(d->reader_pl);
   if (d->hsa_up) hsa_shut_down();
   pthread_mutex_destroy(&d->lock);
   free(d);
@@ -136,17 +137,25 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
   bool ok = f.found;
   d->gpu = f.agent;
   ok = ok && hsa_agent_iterate_regions(d->gpu, find_kernarg, &karg) == HSA_STATUS_INFO_BREAK;
+  // LFA_DIRECT_PRELOAD=1: the build whose arguments the packet processor
+  // preloads into SGPRs (lfa_direct_k.hip)
+  const char *pe = getenv("LFA_DIRECT_PRELOAD");
+  const bool pl = pe && pe[0] == '1';
   ok = ok && hsa_code_object_reader_create_from_memory(lfa_direct_co, lfa_direct_co_size,
                                                        &d->reader) == HSA_STATUS_SUCCESS;
   d->have_reader = ok;
+  ok = ok && hsa_code_object_reader_create_from_memory(lfa_direct_co_pl, lfa_direct_co_pl_size,
+                                                       &d->reader_pl) == HSA_STATUS_SUCCESS;
+  d->have_reader_pl = ok;
   ok = ok && hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT,
                                        nullptr, &d->exe) == HSA_STATUS_SUCCESS;
   d->have_exe = ok;
-  ok = ok && hsa_executable_load_agent_code_object(d->exe, d->gpu, d->reader, nullptr,
-                                                   nullptr) == HSA_STATUS_SUCCESS &&
+  ok = ok && hsa_executable_load_agent_code_object(d->exe, d->gpu, pl ? d->reader_pl : d->reader,
+                                                   nullptr, nullptr) == HSA_STATUS_SUCCESS &&
        hsa_executable_freeze(d->exe, nullptr) == HSA_STATUS_SUCCESS &&
-       hsa_executable_get_symbol_by_name(d->exe, "lfa_direct_solo_copy.kd", &d->gpu, &sym) ==
-           HSA_STATUS_SUCCESS &&
+       hsa_executable_get_symbol_by_name(
+           d->exe, pl ? "lfa_direct_solo_copy_pl.kd" : "lfa_direct_solo_copy.kd", &d->gpu,
+           &sym) == HSA_STATUS_SUCCESS &&
        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT,
                                       &d->solo_kobj) == HSA_STATUS_SUCCESS &&
        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE,

@@ -11,7 +11,14 @@
 // completion word: workgroup b copies bytes [b·4 KiB, (b+1)·4 KiB), 16 B per
 // lane when both pointers are 16-B aligned, byte-wise otherwise and for the
 // tail; the last workgroup to finish publishes `val`.
-extern "C" __global__ __launch_bounds__(256) void lfa_direct_solo_copy(
+// Built twice: as lfa_direct_solo_copy, and as lfa_direct_solo_copy_pl with
+// -mllvm -amdgpu-kernarg-preload-count=14, where the packet processor loads
+// the 56-byte argument block into SGPRs before the wave starts instead of the
+// wave's first scalar loads fetching it from host memory (build.py).
+#ifndef LFA_DIRECT_NAME
+#define LFA_DIRECT_NAME lfa_direct_solo_copy
+#endif
+extern "C" __global__ __launch_bounds__(256) void LFA_DIRECT_NAME(
     char *dst, const char *src, uint64_t bytes, uint32_t nblocks, uint32_t *ctr,
     uint64_t *word, uint64_t val) {
   const unsigned t = __builtin_amdgcn_workitem_id_x();

@@ -114,6 +114,9 @@ for stage in "$@"; do
       $S ramp 300 python3 -u tools/probe_ramp.py || exit 99 ;;
     solo)
       $S solo 200 python3 -u tools/probe_solo_latency.py || exit 99 ;;
+    solopl)
+      # the same with the direct-dispatch kernel's arguments preloaded
+      LFA_DIRECT_PRELOAD=1 $S solo_pl 200 python3 -u tools/probe_solo_latency.py || exit 99 ;;
     tunecomb)
       $S tune_combine 500 python3 -u tools/tune_combine.py --sizes "${COMBINE_SIZES:-32,64,256}" \
         --variants "${COMBINE_VARIANTS:-30,80,81,82,83,84}" --rounds "${COMBINE_ROUNDS:-12}" || exit 99 ;;
