@@ -97,6 +97,7 @@ struct lfa_direct {
   uint64_t solo_kobj;
   uint32_t solo_private, solo_group;
   char *kernarg;                            // kQueueSize slots of 64 B
+  uint16_t header;                          // the dispatch packets' header
   pthread_mutex_t lock;
   int hsa_up, have_reader, have_reader_pl, have_exe;
 };
@@ -175,6 +176,22 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
     lfa_direct_close(d);
     return nullptr;
   }
+  // The packet's acquire / release fence scopes.  The kernel itself releases
+  // its stores at system scope before it publishes the completion word, so
+  // the packet's end-of-kernel release adds nothing the host or a later kernel
+  // needs; at system scope it is a cache writeback that the next packet (the
+  // barrier bit) waits for.  LFA_DIRECT_FENCE: two letters, acquire then
+  // release, s(ystem) / a(gent) / n(one); default "an".
+  const char *fe = getenv("LFA_DIRECT_FENCE");
+  auto scope = [](char c) {
+    return c == 's' ? HSA_FENCE_SCOPE_SYSTEM : c == 'a' ? HSA_FENCE_SCOPE_AGENT
+                                                        : HSA_FENCE_SCOPE_NONE;
+  };
+  const char acq = fe && fe[0] ? fe[0] : 'a', rel = fe && fe[0] && fe[1] ? fe[1] : 'n';
+  d->header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                         (1u << HSA_PACKET_HEADER_BARRIER) |
+                         (scope(acq) << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                         (scope(rel) << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   return d;
 }
 
@@ -220,11 +237,7 @@ extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const vo
   p->kernarg_address = ka;
   p->reserved2 = 0;
   p->completion_signal.handle = 0;
-  const uint16_t header =
-      (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                 (1u << HSA_PACKET_HEADER_BARRIER) |
-                 (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                 (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t header = d->header;
   const uint16_t setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(d->q->doorbell_signal, (hsa_signal_value_t)idx);

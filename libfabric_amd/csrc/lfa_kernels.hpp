@@ -1491,13 +1491,19 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
   }
 }
 
-// LFA_OS_LL=0: the flagged one-shot for every size (A/B; the same setting on
-// every member of a group, as both sides of the exchange follow it)
+// LFA_OS_LL=1: the LL one-shot for small allreduce / reduce_scatter parts
+// (the same setting on every member of a group, as both sides of the
+// exchange follow it).  Off by default: on one MI355X shared by two processes
+// it measured 0.6-1.7 us SLOWER than the flagged kernel (256 lanes polling
+// uncached words against the peer's incoming stores).
+// Not for reduce: its non-root members wait for nothing, so one could run two
+// operations ahead and overwrite the root's words of the same parity before
+// the root read them (the flagged kernel posts and waits on every member).
 static inline bool ll_enabled() {
   static int on = -1;
   if (on < 0) {
     const char *e = getenv("LFA_OS_LL");
-    on = !(e && e[0] == '0');
+    on = e && e[0] == '1';
   }
   return on;
 }
@@ -1546,7 +1552,8 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       }
     }
     const int pof2 = tree_leaves(a.t, srcs, n);
-    if (n > 1 && most <= LFA_OS_LL_BYTES && ll_enabled()) {
+    if (n > 1 && most <= LFA_OS_LL_BYTES &&
+        (h.mode == LFA_ONESHOT_ALL || h.mode == LFA_ONESHOT_SCATTER) && ll_enabled()) {
       // LL one-shot: the words live in the flag area (lfa_signal.h)
       LlArgs l;
       memset(&l, 0, sizeof(l));

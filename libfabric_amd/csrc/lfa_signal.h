@@ -42,9 +42,10 @@ extern "C" {
  * slot of rank k holding what rank k sent.  A word left in a slot matches a
  * later operation's flag only 2^31 one-shots later at the same position (the
  * parity halves alternate, so consecutive uses differ by 2 epochs).  It relies
- * on an aligned 8-byte store reaching a peer whole, over xGMI as on one GPU;
- * LFA_OS_LL=0 in the environment (the same on every member) keeps the flagged
- * kernel for every size.
+ * on an aligned 8-byte store reaching a peer whole, over xGMI as on one GPU.
+ * Allreduce and reduce_scatter only, and only with LFA_OS_LL=1 in the
+ * environment (the same on every member): measured slower than the flagged
+ * kernel on one GPU (lfa_kernels.hpp ll_enabled).
  */
 #define LFA_OS_LL_BYTES (16u << 10)
 #define LFA_SIG_LL_SLOT (2u * LFA_OS_LL_BYTES)

@@ -20,6 +20,7 @@
 #   clat         small-collective latency: world-1 RCCL domain and 2-process
 #                P2P, C-timed loop (liblfa_bench.so) and its breakdown
 #   clatll       2-process P2P latency, flagged one-shot vs LL
+#   solofence    direct-dispatch latency by packet fence scopes and preload
 #   sizes        combine kernel durations vs size under --kernel-trace
 #   host2        2-process host-buffer allreduce, default vs group chunks
 #   ipc          8 processes growing P2P workspaces 4x per cycle (export path)
@@ -74,9 +75,16 @@ for stage in "$@"; do
     clat)
       $S clat 300 python3 -u tools/probe_latency.py || exit 99 ;;
     clatll)
-      # 2-process P2P latency with the flagged one-shot (LFA_OS_LL=0), then LL
+      # 2-process P2P latency with the flagged one-shot (the default), then LL
       LFA_OS_LL=0 $S clat_flagged 200 python3 -u tools/probe_latency.py --skip-world1 && \
-      $S clat_ll 200 python3 -u tools/probe_latency.py --skip-world1 || exit 99 ;;
+      LFA_OS_LL=1 $S clat_ll 200 python3 -u tools/probe_latency.py --skip-world1 || exit 99 ;;
+    solofence)
+      # direct dispatch by packet fence scopes (acquire, release) and preload
+      for f in ss an aa sn; do
+        LFA_DIRECT_FENCE=$f $S "solo_fence_$f" 200 python3 -u tools/probe_solo_latency.py || exit 99
+      done
+      LFA_DIRECT_FENCE=an LFA_DIRECT_PRELOAD=1 $S solo_fence_an_pl 200 \
+        python3 -u tools/probe_solo_latency.py || exit 99 ;;
     sizes)
       $S ksizes 300 $P -d gpurun_out/ksizes -o run -- python3 bench.py --only-extra sizes || exit 99 ;;
     host2)
