@@ -339,9 +339,10 @@ def test_rccl_allreduce_device_and_host(coll, ep):
 
 def test_completion_word_interleaved_with_events(coll, ep):
     """a one-member group runs small reducing collectives as
-    the n = 1 one-shot kernel, which completes through the endpoint's
-    completion word (no event); larger ones, allgather, broadcast and the
-    barrier keep events.  Sixty operations of both kinds in flight at once,
+    a copy kernel dispatched on liblfa's own HSA queue, which completes
+    through that queue's completion word (no event); larger ones, allgather,
+    broadcast and the barrier stay on the endpoint's stream with events.
+    Sixty operations of both kinds in flight at once,
     every op and datatype class, unaligned buffers among them: completions
     in issue order, every result the copy the reference defines."""
     rng = np.random.default_rng(11)
@@ -379,6 +380,31 @@ def test_completion_word_interleaved_with_events(coll, ep):
         got = res[off:off + nb].cpu().numpy().view(oracle.DT_NP[dt])
         assert got.tobytes() == src.tobytes(), (dt, op, count, off, kind)
         assert not res[:off].any() and not res[off + nb:].any(), "wrote outside"
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_small_ops_past_the_direct_queue_ring(coll, direct, monkeypatch):
+    """700 small allreduces in flight at once on a one-member group, more
+    than the direct queue's 256 packets and kernarg slots (lfa_direct.cpp):
+    the submitter waits for the ring, every completion comes back in issue
+    order and every result is its own input.  direct "0" (LFA_DIRECT=0): the
+    same through the HIP launch on the endpoint's stream."""
+    monkeypatch.setenv("LFA_DIRECT", direct)
+    e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    try:
+        n = 700
+        srcs = torch.arange(n * 257, dtype=torch.float32, device=DEV).view(n, 257)
+        outs = torch.zeros_like(srcs)
+        torch.cuda.synchronize()
+        ctxs = [e.allreduce(srcs[i], outs[i], 257, 8, 2) for i in range(n)]
+        done = []
+        while len(done) < n:
+            done += e.cq_read()
+        assert done == ctxs
+        torch.cuda.synchronize()
+        assert torch.equal(srcs, outs)
+    finally:
+        e.close()
 
 
 def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
