@@ -798,7 +798,10 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
             u32x4, __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.t.in[k], (unsigned)own),
                                                          (unsigned)o, 0, kSysLoadAux));
       });
-      *(u32x4 *)(a.result + o) = v;
+      // write-through: the release before the completion word then has no
+      // dirty result lines to write back
+      __builtin_amdgcn_raw_buffer_store_b128(v, tile_rsrc(a.result, (unsigned)own), (unsigned)o,
+                                             0, kSysAux);
     }
     if (a.unal) {
       // the caller's own input and result, byte-wise (local memory); the
@@ -823,7 +826,11 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   if (a.done_word) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && gridDim.x == 1) {
+      // one workgroup: no counter to count in (one device atomic less)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (t == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
                                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -961,7 +968,11 @@ __global__ __launch_bounds__(kBlock) void oneshot_ll(LlArgs a) {
   if (a.done_word) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && gridDim.x == 1) {
+      // one workgroup: no counter to count in (one device atomic less)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (t == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
                                                    __HIP_MEMORY_SCOPE_AGENT);

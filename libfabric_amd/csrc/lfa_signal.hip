@@ -60,14 +60,22 @@ __global__ __launch_bounds__(256) void solo_copy(char *dst, const char *src, siz
   const size_t vhi = vec ? lo + ((hi - lo) & ~(size_t)15) : lo;
   if (lo + (size_t)t * 16 < vhi) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    *(u32x4 *)(dst + lo + (size_t)t * 16) = *(const u32x4 *)(src + lo + (size_t)t * 16);
+    // write-through (sc0 sc1): the release below has no dirty lines to write
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + lo, 0, 4096, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(src + lo + (size_t)t * 16), r,
+                                           t * 16, 0, 17);
   }
   for (size_t o = vhi + t; o < hi; o += 256) dst[o] = src[o];
   // the completion word: this workgroup's stores acknowledged and released
-  // at system scope, then the last workgroup publishes `val` (lfa_signal.h)
+  // at system scope, then the last workgroup publishes `val` (lfa_signal.h);
+  // a single workgroup publishes it without the counter
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && gridDim.x == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else if (t == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     const uint32_t seen =
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
