@@ -718,12 +718,23 @@ constexpr int kOsMax = LFA_OS_MAX_RANKS;
 #define LFA_OS_WAVE_FENCES 0
 #endif
 
+// The one-shot's association tree over at most kOsMax leaves (TreeArgs has
+// room for 32): the kernel's argument block is 376 bytes instead of ~670, one
+// 64-byte line of it read per 64 bytes on every launch — the n = 1 kernel
+// with the larger block took ~1 us longer from launch to completion word
+// than a 48-byte one (profiles/r04_solo_2.json).
+struct OsTree {
+  const void *in[kOsMax];      // own input range (k == rank) or own slot k
+  signed char hi[kOsMax];
+  signed char lo[kOsMax];
+};
+
 struct OsArgs {
-  TreeArgs t;                  // in[k]: own input range (k == rank) or own slot k
+  OsTree t;
   char *push[kOsMax];          // peer k's slot of this rank (k != rank)
   uint32_t *post[kOsMax];      // peer k's one-shot rows, column `rank`
-  size_t soff[kOsMax];         // input range pushed to k (k == rank: reduced)
-  size_t slen[kOsMax];
+  uint32_t soff[kOsMax];       // input range pushed to k (k == rank: reduced)
+  uint32_t slen[kOsMax];
   const uint32_t *wait;        // own one-shot rows
   const char *send;
   char *result;
@@ -739,6 +750,7 @@ struct OsArgs {
   uint64_t *done_word;
   uint64_t done_val;
 };
+static_assert(sizeof(OsArgs) == 376, "the one-shot's argument block (see OsTree)");
 
 template <int OP, typename T, int NLEAF>
 __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
@@ -1532,17 +1544,23 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     if (h.count == 0) return 0;
     OsArgs a;
     memset(&a, 0, sizeof(a));
-    size_t most = 0;
+    size_t most = 0, slen[kOsMax] = {}, soff[kOsMax] = {};
     for (int k = 0; k < n; k++) {
       if (h.mode == LFA_ONESHOT_SCATTER) {  // lfa_coll_block's partition
         const size_t base = h.count / (size_t)n, extra = h.count % (size_t)n;
         const size_t kk = (size_t)k;
-        a.slen[k] = (base + (kk < extra ? 1 : 0)) * E;
-        a.soff[k] = (kk * base + (kk < extra ? kk : extra)) * E;
+        slen[k] = (base + (kk < extra ? 1 : 0)) * E;
+        soff[k] = (kk * base + (kk < extra ? kk : extra)) * E;
       } else {
-        a.slen[k] = h.mode == LFA_ONESHOT_ALL || h.mode == k ? h.count * E : 0;
+        slen[k] = h.mode == LFA_ONESHOT_ALL || h.mode == k ? h.count * E : 0;
       }
-      if (a.slen[k] > most) most = a.slen[k];
+      if (slen[k] > most) most = slen[k];
+    }
+    // 32-bit ranges in the argument block
+    if (h.count > 0xffffffffu / E) return -LFA_EINVAL;
+    for (int k = 0; k < n; k++) {
+      a.slen[k] = (uint32_t)slen[k];
+      a.soff[k] = (uint32_t)soff[k];
     }
     if (!h.send || (!h.result && a.slen[r]) || most > 0xffffffffu ||
         (n > 1 && (h.slot_bytes < most || h.slot_bytes % 256 || h.parity_off % 256 ||
@@ -1562,7 +1580,13 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
         a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
       }
     }
-    const int pof2 = tree_leaves(a.t, srcs, n);
+    TreeArgs tree;
+    const int pof2 = tree_leaves(tree, srcs, n);
+    for (int k = 0; k < kOsMax; k++) {
+      a.t.in[k] = k < n ? tree.in[k] : nullptr;
+      a.t.hi[k] = tree.hi[k];
+      a.t.lo[k] = tree.lo[k];
+    }
     if (n > 1 && most <= LFA_OS_LL_BYTES &&
         (h.mode == LFA_ONESHOT_ALL || h.mode == LFA_ONESHOT_SCATTER) && ll_enabled()) {
       // LL one-shot: the words live in the flag area (lfa_signal.h)
