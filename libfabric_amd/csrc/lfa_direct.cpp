@@ -171,7 +171,8 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
   ok = ok && hsa_memory_allocate(karg, (size_t)kQueueSize * 64, (void **)&d->kernarg) ==
                  HSA_STATUS_SUCCESS;
   ok = ok && hsa_queue_create(d->gpu, kQueueSize, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
-                              UINT32_MAX, UINT32_MAX, &d->q) == HSA_STATUS_SUCCESS;
+                              UINT32_MAX, UINT32_MAX, &d->q) == HSA_STATUS_SUCCESS &&
+       d->q->size >= kQueueSize;    // the ring wait below counts kernarg slots
   if (!ok) {
     lfa_direct_close(d);
     return nullptr;
@@ -211,7 +212,7 @@ extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const vo
   const uint64_t idx = hsa_queue_add_write_index_relaxed(d->q, 1);
   // a full ring: wait until the packet kQueueSize before this one has
   // completed (see above)
-  while (idx - hsa_queue_load_read_index_scacquire(d->q) >= d->q->size - 1) {
+  while (idx - hsa_queue_load_read_index_scacquire(d->q) >= kQueueSize - 1) {
   }
   SoloArgs *ka = (SoloArgs *)(d->kernarg + (idx % kQueueSize) * 64);
   ka->dst = result;
