@@ -1212,7 +1212,9 @@ def extra_collectives(rank, world, stream, emit=None):
                 # of fi_allreduce + fi_cq_read sees, without the Python
                 # wrapper's ~10 us per call
                 barrier(world)
-                c_us = max_over_ranks(ep.bench_loop(3, a, b, 1024, 8, 2, reps=200), world)
+                ep.bench_loop(3, a, b, 1024, 8, 2, reps=200)        # warm-up
+                barrier(world)
+                c_us = max_over_ranks(ep.bench_loop(3, a, b, 1024, 8, 2, reps=2000), world)
                 out[name.replace("_us", "_c_loop_us")] = round(c_us, 1)
                 if algo == coll.ALGO_TREE:
                     ref4k = b.clone()
