@@ -83,20 +83,19 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     co_c = os.path.join(BUILD, "lfa_direct_co.c")
     co_o = os.path.join(BUILD, "lfa_direct_co.o")
     objs.append(co_o)
-    if _newer(co_o, [dk] + hdrs + [os.path.join(CSRC, "lfa_signal.h")]):
+    if _newer(co_o, [dk]):
         # two code objects: the kernel as is, and with its arguments preloaded
         # into SGPRs by the packet processor (lfa_direct_k.hip)
         with open(co_c, "w") as f:
             f.write("#include <stddef.h>\n")
             for sym, extra in (("lfa_direct_co", []),
                                ("lfa_direct_co_pl",
-                                ["-DLFA_DIRECT_NAME=lfa_dk_solo_copy_pl", "-mllvm",
+                                ["-DLFA_DIRECT_NAME=lfa_direct_solo_copy_pl", "-mllvm",
                                  "-amdgpu-kernarg-preload-count=14"])):
                 co = os.path.join(BUILD, sym + ".hsaco")
                 _run([os.path.join(ROCM, "lib", "llvm", "bin", "clang++"), "-x", "hip",
                       "--offload-device-only", "--offload-arch=" + ARCH,
-                      "--no-gpu-bundle-output", "-O3", "-std=c++17", "-ffp-contract=off",
-                      "-I" + INC, *extra, "-o", co, dk])
+                      "--no-gpu-bundle-output", "-O3", "-std=c++17", *extra, "-o", co, dk])
                 data = open(co, "rb").read()
                 f.write(f"const unsigned char {sym}[] __attribute__((aligned(4096))) = {{\n")
                 for i in range(0, len(data), 16):

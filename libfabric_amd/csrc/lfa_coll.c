@@ -648,9 +648,6 @@ struct hop {
 	/* a device hop whose every item is on the stream: a later P2P hop may
 	 * enqueue behind it (stream order) without waiting for it to finish */
 	int issued;
-	/* its one-shot went to the direct queue (direct_oneshot_hop): ordered
-	 * with later direct hops only, so a later stream hop waits for it */
-	int direct;
 	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
 	 * (they share the symmetric workspace), then grow it if needed through
 	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
@@ -886,7 +883,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 				LFA_TRACE("hop cid %#x issued", (unsigned)h->r.cid);
 			}
 			if (h->r.x.done_val) {
-				if (*(volatile uint64_t *)h->r.x.done_word >= h->r.x.done_val) {
+				if (*(volatile uint64_t *)ep->done_word >= h->r.x.done_val) {
 					h->done = 1;
 					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
 				}
@@ -1646,20 +1643,6 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		      const void *buf, void *result, size_t count, int root,
 		      enum lfa_datatype dt, enum lfa_op op, int dev,
 		      enum lfa_coll_algo algo);
-static struct lfa_direct *direct_of(struct lfa_coll_ep *ep);
-
-/* LFA_DIRECT_P2P=0: a P2P group's one-shot keeps the HIP launch */
-static int direct_p2p_enabled(void)
-{
-	static int on = -1;
-
-	if (on < 0) {
-		const char *e = getenv("LFA_DIRECT_P2P");
-
-		on = !(e && e[0] == '0');
-	}
-	return on;
-}
 
 /* A handshake collective of hop `h` on its reserved seq (host buffers). */
 static int sub_start(struct lfa_coll_ep *ep, struct hop *h, enum lfa_collective_op coll,
@@ -1721,9 +1704,7 @@ static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
 			/* a device hop with every item on the stream is far enough:
 			 * this one's items queue behind it (a growth below first
 			 * synchronises the stream) */
-			/* ... and one on the other queue (direct / stream) only
-			 * once it is done: nothing orders the two */
-			if (p && !p->done && (!p->issued || p->direct != h->direct))
+			if (p && !p->done && !p->issued)
 				return 0;
 		}
 		LFA_TRACE("hop cid %#x prologue: prior hops done or issued, need %zu have %zu",
@@ -2330,16 +2311,6 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 		h->r.x.done_ctr = ep->done_ctr;
 		h->r.x.done_word = ep->done_word;
 		h->r.x.done_seq = &ep->done_seq;
-		if (direct_p2p_enabled() && direct_of(ep) &&
-		    lfa_direct_oneshot_ok(ep->direct, (int)op, (int)dt, mc->size)) {
-			/* ... on liblfa's own queue, no HIP launch (DESIGN.md
-			 * §6b); hop_prologue keeps it apart from stream hops */
-			h->direct = 1;
-			h->r.x.direct = ep->direct;
-			h->r.x.done_ctr = ep->ddone_ctr;
-			h->r.x.done_word = ep->ddone_word;
-			h->r.x.done_seq = &ep->ddone_seq;
-		}
 	}
 	if (dev) {
 		hipSetDevice(ep->dom->device);

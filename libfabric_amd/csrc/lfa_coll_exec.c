@@ -229,8 +229,7 @@ LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st)
 		a.done_word = r->x.done_word;
 		a.done_val = *r->x.done_seq + 1;
 	}
-	ret = r->x.direct ? lfa_direct_oneshot(r->x.direct, r->op, r->dt, &a) :
-			    lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
+	ret = lfa_oneshot_reduce_async(r->op, r->dt, &a, r->stream);
 	if (!ret && a.done_word)
 		r->x.done_val = ++*r->x.done_seq;
 	LFA_TRACE("cid %#x one-shot launched (epoch %u, rc %d)", (unsigned)r->cid, a.epoch, ret);

@@ -49,9 +49,6 @@ struct xctx {
 	uint64_t *done_word;
 	uint64_t *done_seq;
 	uint64_t done_val;
-	/* non-NULL: launch that one-shot on this direct queue (lfa_signal.h
-	 * lfa_direct_oneshot) instead of the stream; done_* are the queue's */
-	struct lfa_direct *direct;
 };
 
 /* ====================================================================== */

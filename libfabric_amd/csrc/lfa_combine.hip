@@ -112,21 +112,6 @@ extern "C" int LFA_CAT(lfa__tree_op, LFA_OP)(int dt, void *dst,
   });
 }
 
-#if LFA_OP == 0
-// The flagged one-shot's argument block for the direct-dispatch path
-// (lfa_signal.h): built once, in this translation unit of the twelve.
-extern "C" int lfa__oneshot_fill(const lfa_oneshot *a, size_t esz, void *args, size_t cap,
-                                 int *pof2, unsigned *grid) {
-  if (!a || !args || !pof2 || !grid || cap < sizeof(lfa::OsArgs) || !esz) return -LFA_EINVAL;
-  lfa::OsArgs o;
-  size_t most = 0;
-  uintptr_t mis = 0;
-  const int rc = lfa::os_fill(*a, esz, o, pof2, &most, &mis, grid);
-  if (rc == 0) memcpy(args, &o, sizeof(o));
-  return rc;
-}
-#endif
-
 extern "C" int LFA_CAT(lfa__oneshot_op, LFA_OP)(int dt, const lfa_oneshot *a,
                                                 void *stream) {
   return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {

@@ -33,9 +33,6 @@ extern "C" const size_t lfa_direct_co_size, lfa_direct_co_pl_size;
 namespace {
 
 constexpr uint32_t kQueueSize = 256;        // packets; also the kernarg slots
-constexpr size_t kSlot = 512;               // bytes per kernarg slot
-constexpr size_t kOsArgs = 376;             // lfa::OsArgs (lfa_kernels.hpp)
-constexpr int kOsOps = 10, kOsTypes = 10;   // lfa_op / lfa_datatype values below
 
 struct SoloArgs {                           // lfa_direct_solo_copy's kernarg block
   void *dst;
@@ -47,7 +44,7 @@ struct SoloArgs {                           // lfa_direct_solo_copy's kernarg bl
   uint64_t *word;
   uint64_t val;
 };
-static_assert(sizeof(SoloArgs) == 56, "kernarg layout of lfa_dk_solo_copy");
+static_assert(sizeof(SoloArgs) == 56, "kernarg layout of lfa_direct_solo_copy");
 
 struct FindGpu {
   uint32_t bdf;
@@ -99,11 +96,7 @@ struct lfa_direct {
   hsa_executable_t exe;
   uint64_t solo_kobj;
   uint32_t solo_private, solo_group;
-  char *kernarg;                            // kQueueSize slots of kSlot bytes
-  struct OsKernel {
-    uint64_t kobj;
-    uint32_t private_size, group_size;
-  } os[kOsOps][kOsTypes][3];                // leaves 2, 4, 8
+  char *kernarg;                            // kQueueSize slots of 64 B
   uint16_t header;                          // the dispatch packets' header
   pthread_mutex_t lock;
   int hsa_up, have_reader, have_reader_pl, have_exe;
@@ -162,7 +155,7 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
                                                    nullptr, nullptr) == HSA_STATUS_SUCCESS &&
        hsa_executable_freeze(d->exe, nullptr) == HSA_STATUS_SUCCESS &&
        hsa_executable_get_symbol_by_name(
-           d->exe, pl ? "lfa_dk_solo_copy_pl.kd" : "lfa_dk_solo_copy.kd", &d->gpu,
+           d->exe, pl ? "lfa_direct_solo_copy_pl.kd" : "lfa_direct_solo_copy.kd", &d->gpu,
            &sym) == HSA_STATUS_SUCCESS &&
        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT,
                                       &d->solo_kobj) == HSA_STATUS_SUCCESS &&
@@ -175,31 +168,8 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
                                       &d->solo_group) == HSA_STATUS_SUCCESS;
   // the kernarg block must be exactly the argument struct (no hidden arguments)
   ok = ok && kernarg_size == sizeof(SoloArgs) && d->solo_kobj;
-  ok = ok && hsa_memory_allocate(karg, (size_t)kQueueSize * kSlot, (void **)&d->kernarg) ==
+  ok = ok && hsa_memory_allocate(karg, (size_t)kQueueSize * 64, (void **)&d->kernarg) ==
                  HSA_STATUS_SUCCESS;
-  // the one-shot kernels this code object holds (lfa_direct_k.hip LFA_OS_T)
-  for (int op = 0; ok && op < kOsOps; op++)
-    for (int dt = 0; dt < kOsTypes; dt++)
-      for (int li = 0; li < 3; li++) {
-        char name[48];
-        hsa_executable_symbol_t os;
-        uint32_t ksz = 0;
-        snprintf(name, sizeof(name), "lfa_os_%d_%d_%d.kd", op, dt, 2 << li);
-        auto &k = d->os[op][dt][li];
-        if (hsa_executable_get_symbol_by_name(d->exe, name, &d->gpu, &os) != HSA_STATUS_SUCCESS ||
-            hsa_executable_symbol_get_info(os, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT,
-                                           &k.kobj) != HSA_STATUS_SUCCESS ||
-            hsa_executable_symbol_get_info(
-                os, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &ksz) !=
-                HSA_STATUS_SUCCESS ||
-            hsa_executable_symbol_get_info(
-                os, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.private_size) !=
-                HSA_STATUS_SUCCESS ||
-            hsa_executable_symbol_get_info(os, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE,
-                                           &k.group_size) != HSA_STATUS_SUCCESS ||
-            ksz != kOsArgs + 4)       // OsArgs, then the workgroup count: nothing hidden
-          k.kobj = 0;
-      }
   ok = ok && hsa_queue_create(d->gpu, kQueueSize, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
                               UINT32_MAX, UINT32_MAX, &d->q) == HSA_STATUS_SUCCESS &&
        d->q->size >= kQueueSize;    // the ring wait below counts kernarg slots
@@ -231,16 +201,28 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
 // processor has consumed packet i + 1, whose barrier bit held it until packet
 // i's kernel completed — so the writer waits for that before reusing i's slot
 // (one slot of the ring stays unused).
-static void dispatch(struct lfa_direct *d, uint64_t kobj, uint32_t private_size,
-                     uint32_t group_size, uint32_t nblocks, const void *args, size_t bytes) {
+extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send,
+                                    size_t bytes, uint32_t *done_ctr, uint64_t *done_word,
+                                    uint64_t done_val) {
+  if (!bytes) return 0;
+  if (!d || !result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
+    return -LFA_EINVAL;
+  const uint32_t nblocks = (uint32_t)((bytes + 4095) / 4096);
   pthread_mutex_lock(&d->lock);
   const uint64_t idx = hsa_queue_add_write_index_relaxed(d->q, 1);
   // a full ring: wait until the packet kQueueSize before this one has
   // completed (see above)
   while (idx - hsa_queue_load_read_index_scacquire(d->q) >= kQueueSize - 1) {
   }
-  char *ka = d->kernarg + (idx % kQueueSize) * kSlot;
-  memcpy(ka, args, bytes);
+  SoloArgs *ka = (SoloArgs *)(d->kernarg + (idx % kQueueSize) * 64);
+  ka->dst = result;
+  ka->src = send;
+  ka->bytes = bytes;
+  ka->nblocks = nblocks;
+  ka->pad = 0;
+  ka->ctr = done_ctr;
+  ka->word = done_word;
+  ka->val = done_val;
   hsa_kernel_dispatch_packet_t *p =
       (hsa_kernel_dispatch_packet_t *)d->q->base_address + (idx % d->q->size);
   p->workgroup_size_x = 256;
@@ -250,9 +232,9 @@ static void dispatch(struct lfa_direct *d, uint64_t kobj, uint32_t private_size,
   p->grid_size_x = nblocks * 256u;
   p->grid_size_y = 1;
   p->grid_size_z = 1;
-  p->private_segment_size = private_size;
-  p->group_segment_size = group_size;
-  p->kernel_object = kobj;
+  p->private_segment_size = d->solo_private;
+  p->group_segment_size = d->solo_group;
+  p->kernel_object = d->solo_kobj;
   p->kernarg_address = ka;
   p->reserved2 = 0;
   p->completion_signal.handle = 0;
@@ -261,52 +243,5 @@ static void dispatch(struct lfa_direct *d, uint64_t kobj, uint32_t private_size,
   __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(d->q->doorbell_signal, (hsa_signal_value_t)idx);
   pthread_mutex_unlock(&d->lock);
-}
-
-extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send,
-                                    size_t bytes, uint32_t *done_ctr, uint64_t *done_word,
-                                    uint64_t done_val) {
-  if (!bytes) return 0;
-  if (!d || !result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
-    return -LFA_EINVAL;
-  SoloArgs ka;
-  ka.dst = result;
-  ka.src = send;
-  ka.bytes = bytes;
-  ka.nblocks = (uint32_t)((bytes + 4095) / 4096);
-  ka.pad = 0;
-  ka.ctr = done_ctr;
-  ka.word = done_word;
-  ka.val = done_val;
-  dispatch(d, d->solo_kobj, d->solo_private, d->solo_group, ka.nblocks, &ka, sizeof(ka));
-  return 0;
-}
-
-static int leaf_index(int n) {
-  int pof2 = 1;
-  while (pof2 * 2 <= n) pof2 *= 2;
-  return pof2 == 2 ? 0 : pof2 == 4 ? 1 : pof2 == 8 ? 2 : -1;
-}
-
-extern "C" int lfa_direct_oneshot_ok(struct lfa_direct *d, int op, int dt, int n) {
-  const int li = leaf_index(n);
-  return d && op >= 0 && op < kOsOps && dt >= 0 && dt < kOsTypes && li >= 0 &&
-         n <= LFA_OS_MAX_RANKS && d->os[op][dt][li].kobj != 0;
-}
-
-extern "C" int lfa_direct_oneshot(struct lfa_direct *d, int op, int dt,
-                                  const struct lfa_oneshot *a) {
-  if (!a || !lfa_direct_oneshot_ok(d, op, dt, a->n)) return -LFA_ENOSYS;
-  alignas(8) char args[kOsArgs + 8];
-  int pof2 = 0;
-  unsigned grid = 0;
-  const size_t esz = dt == 4 || dt == 5 || dt == 8 ? 4 : 8;  // the table's datatypes
-  const int rc = lfa__oneshot_fill(a, esz, args, kOsArgs, &pof2, &grid);
-  if (rc) return rc < 0 ? rc : 0;
-  const int li = leaf_index(a->n);
-  if (pof2 != (2 << li)) return -LFA_EINVAL;
-  memcpy(args + kOsArgs, &grid, sizeof(grid));
-  const auto &k = d->os[op][dt][li];
-  dispatch(d, k.kobj, k.private_size, k.group_size, grid, args, kOsArgs + 4);
   return 0;
 }

@@ -12,12 +12,12 @@
 // lane when both pointers are 16-B aligned, byte-wise otherwise and for the
 // tail; the last workgroup to finish publishes `val` (a single workgroup
 // publishes it without the counter).
-// Built twice: as lfa_dk_solo_copy, and as lfa_dk_solo_copy_pl with
+// Built twice: as lfa_direct_solo_copy, and as lfa_direct_solo_copy_pl with
 // -mllvm -amdgpu-kernarg-preload-count=14, where the packet processor loads
 // the 56-byte argument block into SGPRs before the wave starts instead of the
 // wave's first scalar loads fetching it from host memory (build.py).
 #ifndef LFA_DIRECT_NAME
-#define LFA_DIRECT_NAME lfa_dk_solo_copy
+#define LFA_DIRECT_NAME lfa_direct_solo_copy
 #endif
 extern "C" __global__ __launch_bounds__(256) void LFA_DIRECT_NAME(
     char *dst, const char *src, uint64_t bytes, uint32_t nblocks, uint32_t *ctr,
@@ -58,31 +58,3 @@ extern "C" __global__ __launch_bounds__(256) void LFA_DIRECT_NAME(
     }
   }
 }
-
-// The flagged one-shot (lfa_kernels.hpp oneshot_body) for the common
-// (op, datatype) pairs of a P2P group's small buckets, named
-// lfa_os_<op>_<datatype>_<leaves> with the lfa_op / lfa_datatype values.  The
-// argument block is lfa::OsArgs followed by the workgroup count (the body
-// reads no hidden arguments: the count replaces gridDim.x).  Pairs the write
-// table does not define compile to empty kernels the host never picks
-// (lfa_direct_oneshot_ok).
-#include "lfa_kernels.hpp"
-
-#define LFA_OS_K(OPV, OPC, DTV, T, N)                                                     \
-  extern "C" __global__ __launch_bounds__(256) void lfa_os_##OPV##_##DTV##_##N(            \
-      lfa::OsArgs a, uint32_t nblocks) {                                                   \
-    if constexpr (lfa::supported<lfa::OPC, T>()) lfa::oneshot_body<lfa::OPC, T, N>(a, nblocks); \
-  }
-#define LFA_OS_N(OPV, OPC, DTV, T) \
-  LFA_OS_K(OPV, OPC, DTV, T, 2) LFA_OS_K(OPV, OPC, DTV, T, 4) LFA_OS_K(OPV, OPC, DTV, T, 8)
-#define LFA_OS_T(OPV, OPC)                                                            \
-  LFA_OS_N(OPV, OPC, 4, int32_t) LFA_OS_N(OPV, OPC, 5, uint32_t)                       \
-  LFA_OS_N(OPV, OPC, 6, int64_t) LFA_OS_N(OPV, OPC, 7, uint64_t)                       \
-  LFA_OS_N(OPV, OPC, 8, float) LFA_OS_N(OPV, OPC, 9, double)
-LFA_OS_T(0, OP_MIN)
-LFA_OS_T(1, OP_MAX)
-LFA_OS_T(2, OP_SUM)
-LFA_OS_T(3, OP_PROD)
-LFA_OS_T(6, OP_BOR)
-LFA_OS_T(7, OP_BAND)
-LFA_OS_T(9, OP_BXOR)

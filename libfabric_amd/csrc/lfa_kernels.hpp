@@ -752,10 +752,8 @@ struct OsArgs {
 };
 static_assert(sizeof(OsArgs) == 376, "the one-shot's argument block (see OsTree)");
 
-// The kernel's body, also built into the direct-dispatch code object
-// (lfa_direct_k.hip), where the grid size comes as an argument: nblocks.
 template <int OP, typename T, int NLEAF>
-__device__ __forceinline__ void oneshot_body(const OsArgs &a, unsigned nblocks) {
+__global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   constexpr size_t E = sizeof(T);
   const unsigned t = threadIdx.x;
   const size_t b = blockIdx.x;
@@ -840,7 +838,7 @@ __device__ __forceinline__ void oneshot_body(const OsArgs &a, unsigned nblocks) 
   if (a.done_word) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (t == 0 && nblocks == 1) {
+    if (t == 0 && gridDim.x == 1) {
       // one workgroup: no counter to count in (one device atomic less)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -848,7 +846,7 @@ __device__ __forceinline__ void oneshot_body(const OsArgs &a, unsigned nblocks) 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
                                                    __HIP_MEMORY_SCOPE_AGENT);
-      if (seen + 1 == nblocks) {
+      if (seen + 1 == gridDim.x) {
         __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED,
@@ -856,11 +854,6 @@ __device__ __forceinline__ void oneshot_body(const OsArgs &a, unsigned nblocks) 
       }
     }
   }
-}
-
-template <int OP, typename T, int NLEAF>
-__global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
-  oneshot_body<OP, T, NLEAF>(a, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1538,99 +1531,62 @@ static inline bool ll_enabled() {
   return on;
 }
 
-// The flagged one-shot's argument block, shared by launch_oneshot and the
-// direct-dispatch path (lfa__oneshot_fill, lfa_direct.cpp): 0, 1 when there
-// is nothing to do (count 0), or -LFA_EINVAL.  *pof2: the tree's leaf count
-// (the kernel variant); *most: the largest part in bytes; *mis: the low bits
-// of every range start and the result (0: all 16-B aligned); *grid: the
-// workgroups — the same on every member, `most` depends only on count and n.
-static inline int os_fill(const lfa_oneshot &h, size_t E, OsArgs &a, int *pof2, size_t *most_out,
-                          uintptr_t *mis_out, unsigned *grid) {
-  const int n = h.n, r = h.rank;
-  if (n < 1 || n > kOsMax || r < 0 || r >= n || (n > 1 && (!h.sym || !h.status)) ||
-      h.mode < LFA_ONESHOT_SCATTER || h.mode >= n || (h.done_word && !h.done_ctr))
-    return -LFA_EINVAL;
-  if (h.count == 0) return 1;
-  memset(&a, 0, sizeof(a));
-  size_t most = 0, slen[kOsMax] = {}, soff[kOsMax] = {};
-  for (int k = 0; k < n; k++) {
-    if (h.mode == LFA_ONESHOT_SCATTER) {  // lfa_coll_block's partition
-      const size_t base = h.count / (size_t)n, extra = h.count % (size_t)n;
-      const size_t kk = (size_t)k;
-      slen[k] = (base + (kk < extra ? 1 : 0)) * E;
-      soff[k] = (kk * base + (kk < extra ? kk : extra)) * E;
-    } else {
-      slen[k] = h.mode == LFA_ONESHOT_ALL || h.mode == k ? h.count * E : 0;
-    }
-    if (slen[k] > most) most = slen[k];
-  }
-  // 32-bit ranges in the argument block
-  if (h.count > 0xffffffffu / E) return -LFA_EINVAL;
-  for (int k = 0; k < n; k++) {
-    a.slen[k] = (uint32_t)slen[k];
-    a.soff[k] = (uint32_t)soff[k];
-  }
-  if (!h.send || (!h.result && a.slen[r]) || most > 0xffffffffu ||
-      (n > 1 && (h.slot_bytes < most || h.slot_bytes % 256 || h.parity_off % 256 ||
-                 (size_t)n * h.slot_bytes > h.parity_off)))
-    return -LFA_EINVAL;
-  for (int k = 0; k < n && n > 1; k++)
-    if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
-  const void *srcs[kOsMax];
-  const size_t par = (size_t)(h.epoch & 1) * h.parity_off;
-  uintptr_t mis = (uintptr_t)h.result % 16;
-  for (int k = 0; k < n; k++) {
-    mis |= ((uintptr_t)h.send + a.soff[k]) % 16;
-    srcs[k] = k == r ? (const char *)h.send + a.soff[r]
-                     : h.sym[r] + par + (size_t)k * h.slot_bytes;
-    if (k != r) {
-      a.push[k] = h.sym[k] + par + (size_t)r * h.slot_bytes;
-      a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
-    }
-  }
-  TreeArgs tree;
-  *pof2 = tree_leaves(tree, srcs, n);
-  for (int k = 0; k < kOsMax; k++) {
-    a.t.in[k] = k < n ? tree.in[k] : nullptr;
-    a.t.hi[k] = tree.hi[k];
-    a.t.lo[k] = tree.lo[k];
-  }
-  a.wait = n > 1 ? (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF) : nullptr;
-  a.done_ctr = h.done_ctr;
-  a.done_word = h.done_word;
-  a.done_val = h.done_val;
-  a.send = (const char *)h.send;
-  a.result = (char *)h.result;
-  a.status = h.status;
-  a.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
-  size_t chunk = (most + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
-  chunk = (chunk + 15) & ~(size_t)15;
-  a.chunk = chunk < 4096 ? 4096 : chunk;
-  a.epoch = h.epoch;
-  a.ticket = h.ticket;
-  a.n = n;
-  a.rank = r;
-  a.unal = (uintptr_t)h.send % E || (uintptr_t)h.result % E;
-  a.vec = mis == 0 && E <= 16 && !a.unal;
-  *grid = (unsigned)((most + a.chunk - 1) / a.chunk);
-  *most_out = most;
-  *mis_out = mis;
-  return 0;
-}
-
 template <int OP, typename T>
 static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
   if constexpr (!supported<OP, T>()) {
     return -LFA_EOPNOTSUPP;
   } else {
+    constexpr size_t E = sizeof(T);
     const int n = h.n, r = h.rank;
+    if (n < 1 || n > kOsMax || r < 0 || r >= n || (n > 1 && (!h.sym || !h.status)) ||
+        h.mode < LFA_ONESHOT_SCATTER || h.mode >= n || (h.done_word && !h.done_ctr))
+      return -LFA_EINVAL;
+    if (h.count == 0) return 0;
     OsArgs a;
-    int pof2 = 0;
-    size_t most = 0;
-    uintptr_t mis = 0;
-    unsigned grid = 0;
-    const int rc = os_fill(h, sizeof(T), a, &pof2, &most, &mis, &grid);
-    if (rc) return rc < 0 ? rc : 0;
+    memset(&a, 0, sizeof(a));
+    size_t most = 0, slen[kOsMax] = {}, soff[kOsMax] = {};
+    for (int k = 0; k < n; k++) {
+      if (h.mode == LFA_ONESHOT_SCATTER) {  // lfa_coll_block's partition
+        const size_t base = h.count / (size_t)n, extra = h.count % (size_t)n;
+        const size_t kk = (size_t)k;
+        slen[k] = (base + (kk < extra ? 1 : 0)) * E;
+        soff[k] = (kk * base + (kk < extra ? kk : extra)) * E;
+      } else {
+        slen[k] = h.mode == LFA_ONESHOT_ALL || h.mode == k ? h.count * E : 0;
+      }
+      if (slen[k] > most) most = slen[k];
+    }
+    // 32-bit ranges in the argument block
+    if (h.count > 0xffffffffu / E) return -LFA_EINVAL;
+    for (int k = 0; k < n; k++) {
+      a.slen[k] = (uint32_t)slen[k];
+      a.soff[k] = (uint32_t)soff[k];
+    }
+    if (!h.send || (!h.result && a.slen[r]) || most > 0xffffffffu ||
+        (n > 1 && (h.slot_bytes < most || h.slot_bytes % 256 || h.parity_off % 256 ||
+                   (size_t)n * h.slot_bytes > h.parity_off)))
+      return -LFA_EINVAL;
+    for (int k = 0; k < n && n > 1; k++)
+      if (!h.sym[k] || (uintptr_t)h.sym[k] % 256) return -LFA_EINVAL;
+    const void *srcs[kOsMax];
+    const size_t par = (size_t)(h.epoch & 1) * h.parity_off;
+    uintptr_t mis = (uintptr_t)h.result % 16;
+    for (int k = 0; k < n; k++) {
+      mis |= ((uintptr_t)h.send + a.soff[k]) % 16;
+      srcs[k] = k == r ? (const char *)h.send + a.soff[r]
+                       : h.sym[r] + par + (size_t)k * h.slot_bytes;
+      if (k != r) {
+        a.push[k] = h.sym[k] + par + (size_t)r * h.slot_bytes;
+        a.post[k] = (uint32_t *)(h.sym[k] + h.flag_off + LFA_SIG_OS_OFF) + r;
+      }
+    }
+    TreeArgs tree;
+    const int pof2 = tree_leaves(tree, srcs, n);
+    for (int k = 0; k < kOsMax; k++) {
+      a.t.in[k] = k < n ? tree.in[k] : nullptr;
+      a.t.hi[k] = tree.hi[k];
+      a.t.lo[k] = tree.lo[k];
+    }
     if (n > 1 && most <= LFA_OS_LL_BYTES &&
         (h.mode == LFA_ONESHOT_ALL || h.mode == LFA_ONESHOT_SCATTER) && ll_enabled()) {
       // LL one-shot: the words live in the flag area (lfa_signal.h)
@@ -1638,8 +1594,8 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       memset(&l, 0, sizeof(l));
       const size_t lpar = (size_t)(h.epoch & 1) * LFA_SIG_LL_PARITY;
       for (int k = 0; k < n; k++) {
-        l.soff[k] = a.soff[k];
-        l.slen[k] = a.slen[k];
+        l.soff[k] = (uint32_t)a.soff[k];
+        l.slen[k] = (uint32_t)a.slen[k];
         if (k != r)
           l.push[k] = h.sym[k] + h.flag_off + LFA_SIG_LL_OFF + lpar + (size_t)r * LFA_SIG_LL_SLOT;
         l.hi[k] = a.t.hi[k];
@@ -1650,7 +1606,7 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       l.result = (char *)h.result;
       l.status = h.status;
       l.ticket = h.ticket;
-      l.timeout = a.timeout;
+      l.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
       l.done_ctr = h.done_ctr;
       l.done_word = h.done_word;
       l.done_val = h.done_val;
@@ -1658,22 +1614,42 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
       l.n = n;
       l.rank = r;
       l.vec = mis == 0;
-      const unsigned lgrid = (unsigned)(((most + 15) / 16 + kBlock - 1) / kBlock);
+      // the same grid on every member: `most` depends only on count and n
+      const unsigned grid = (unsigned)(((most + 15) / 16 + kBlock - 1) / kBlock);
       switch (pof2) {
         case 2:
-          hipLaunchKernelGGL((oneshot_ll<OP, T, 2>), dim3(lgrid), dim3(kBlock), 0, s, l);
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 2>), dim3(grid), dim3(kBlock), 0, s, l);
           break;
         case 4:
-          hipLaunchKernelGGL((oneshot_ll<OP, T, 4>), dim3(lgrid), dim3(kBlock), 0, s, l);
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 4>), dim3(grid), dim3(kBlock), 0, s, l);
           break;
         case 8:
-          hipLaunchKernelGGL((oneshot_ll<OP, T, 8>), dim3(lgrid), dim3(kBlock), 0, s, l);
+          hipLaunchKernelGGL((oneshot_ll<OP, T, 8>), dim3(grid), dim3(kBlock), 0, s, l);
           break;
         default:
           return -LFA_EINVAL;
       }
       return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
     }
+    a.wait = n > 1 ? (const uint32_t *)(h.sym[r] + h.flag_off + LFA_SIG_OS_OFF) : nullptr;
+    a.done_ctr = h.done_ctr;
+    a.done_word = h.done_word;
+    a.done_val = h.done_val;
+    a.send = (const char *)h.send;
+    a.result = (char *)h.result;
+    a.status = h.status;
+    a.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
+    size_t chunk = (most + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
+    chunk = (chunk + 15) & ~(size_t)15;
+    a.chunk = chunk < 4096 ? 4096 : chunk;
+    a.epoch = h.epoch;
+    a.ticket = h.ticket;
+    a.n = n;
+    a.rank = r;
+    a.unal = (uintptr_t)h.send % E || (uintptr_t)h.result % E;
+    a.vec = mis == 0 && E <= 16 && !a.unal;
+    // the same grid on every member: `most` depends only on count and n
+    const unsigned grid = (unsigned)((most + a.chunk - 1) / a.chunk);
     switch (pof2) {
       case 1:
         hipLaunchKernelGGL((oneshot_reduce<OP, T, 1>), dim3(grid), dim3(kBlock), 0, s, a);

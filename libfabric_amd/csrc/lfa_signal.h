@@ -170,17 +170,6 @@ struct lfa_direct *lfa_direct_open(int device);
 int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send, size_t bytes,
 			 uint32_t *done_ctr, uint64_t *done_word, uint64_t done_val);
 void lfa_direct_close(struct lfa_direct *d);
-/* The flagged one-shot (struct lfa_oneshot, as lfa_oneshot_reduce_async)
- * through the direct queue, for the (op, datatype) pairs and group sizes its
- * code object holds: lfa_direct_oneshot_ok says which.  Nothing orders it
- * with the caller's streams; the group's kernels must not overlap on this
- * member (lfa_coll.c hop_prologue waits for that). */
-int lfa_direct_oneshot_ok(struct lfa_direct *d, int op, int datatype, int n);
-int lfa_direct_oneshot(struct lfa_direct *d, int op, int datatype, const struct lfa_oneshot *a);
-/* launch_oneshot's argument block for `a` (internal): 0, 1 nothing to do,
- * or -LFA_E*; *pof2 the tree's leaves, *grid the workgroups. */
-int lfa__oneshot_fill(const struct lfa_oneshot *a, size_t esz, void *args, size_t cap,
-		      int *pof2, unsigned *grid);
 
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
 uint64_t lfa__wallclock_ticks_per_us(void);

@@ -19,7 +19,6 @@
 #   treeput_pmc  counters of the 8->8 tree_put (TREEPUT_PMC_VARIANT)
 #   clat         small-collective latency: world-1 RCCL domain and 2-process
 #                P2P, C-timed loop (liblfa_bench.so) and its breakdown
-#   clatp2p      2-process P2P latency, one-shot through HIP vs direct dispatch
 #   clatll       2-process P2P latency, flagged one-shot vs LL
 #   solofence    direct-dispatch latency by packet fence scopes and preload
 #   sizes        combine kernel durations vs size under --kernel-trace
@@ -75,10 +74,6 @@ for stage in "$@"; do
       done ;;
     clat)
       $S clat 300 python3 -u tools/probe_latency.py || exit 99 ;;
-    clatp2p)
-      # 2-process P2P latency: the one-shot through the HIP launch, then direct
-      LFA_DIRECT_P2P=0 $S clat_p2p_hip 200 python3 -u tools/probe_latency.py --skip-world1 && \
-      $S clat_p2p_direct 200 python3 -u tools/probe_latency.py --skip-world1 || exit 99 ;;
     clatll)
       # 2-process P2P latency with the flagged one-shot (the default), then LL
       LFA_OS_LL=0 $S clat_flagged 200 python3 -u tools/probe_latency.py --skip-world1 && \
