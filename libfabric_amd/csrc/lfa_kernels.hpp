@@ -431,6 +431,37 @@ __global__ __launch_bounds__(kBlock) void reduce_tree_chunk(TreeArgs a,
   }
 }
 
+// Tapered chunk form (variant 12, the combine's tapered tail applied to the
+// tree): workgroups [0, head) take U = 2 vectors per lane up to vector
+// `split`, the rest — dispatched last — one vector per lane, so the waves that
+// end the launch are shorter.  Write-through stores (the chunk form's sc1).
+template <int OP, typename T, int NLEAF, int U>
+__device__ __forceinline__ void tree_chunk_at(const TreeArgs &a, u32x4 *dst, size_t nvec,
+                                              size_t wg0) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const size_t i = wg0 + (size_t)u * kBlock + threadIdx.x;
+    if (i < nvec) {
+      u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(
+          a, [&](int k) { return ld<true>((const u32x4 *)a.in[k] + i); });
+      const size_t wb = wg0 + (size_t)u * kBlock + (size_t)wave_id() * 64;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          v, __builtin_amdgcn_make_buffer_rsrc(dst + wb, 0, 64 * 16, 0x00020000),
+          (threadIdx.x % 64) * 16, 0, kStoreSc1);
+    }
+  }
+}
+
+template <int OP, typename T, int NLEAF>
+__global__ __launch_bounds__(kBlock) void reduce_tree_taper(TreeArgs a, u32x4 *dst, size_t nvec,
+                                                            size_t split, unsigned head) {
+  const unsigned b = blockIdx.x;
+  if (b < head)
+    tree_chunk_at<OP, T, NLEAF, 2>(a, dst, split, (size_t)b * (kBlock * 2));
+  else
+    tree_chunk_at<OP, T, NLEAF, 1>(a, dst, nvec, split + (size_t)(b - head) * kBlock);
+}
+
 // LDS-DMA form: each wave DMAs U KiB of every input into its own LDS slots
 // (global_load_lds_dwordx4, nt), waits on its vmcnt, then evaluates U trees
 // per lane from LDS and stores nt.  Dynamic LDS: nin · W · U KiB per
@@ -1329,6 +1360,17 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
       hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 1>),
                          dim3(grid_for(nvec, (size_t)kBlock, 0x7fffffffu)),
                          dim3(kBlock), 0, s, b, dst, nvec);
+      return;
+    }
+  } else if (variant == 12) {
+    if constexpr (ALL) {
+      // the last 1/8 of the vectors one per lane (reduce_tree_taper)
+      size_t split = nvec - nvec / 8;
+      split -= split % ((size_t)kBlock * 2);
+      const unsigned head = (unsigned)(split / ((size_t)kBlock * 2));
+      const unsigned tail = (unsigned)((nvec - split + kBlock - 1) / kBlock);
+      hipLaunchKernelGGL((reduce_tree_taper<OP, T, NLEAF>), dim3(head + tail), dim3(kBlock), 0,
+                         s, b, dst, nvec, split, head);
       return;
     }
   }

@@ -16,6 +16,7 @@
 #   pmc          the headline kernel's FETCH_SIZE / WRITE_SIZE in separate passes
 #   treeput      bench.py --tune-treeput A/B (TREEPUT_VARIANTS, default 0), in
 #                separate allocations and in one skewed pool
+#   treetune     bench.py --tune-tree A/B (TREE_VARIANTS, default -1,12)
 #   treeput_pmc  counters of the 8->8 tree_put (TREEPUT_PMC_VARIANT)
 #   clat         small-collective latency: world-1 RCCL domain and 2-process
 #                P2P, C-timed loop (liblfa_bench.so) and its breakdown
@@ -64,6 +65,10 @@ for stage in "$@"; do
         $S "tune_treeput_$lay" 400 python3 -u bench.py --tune-treeput --treeput-layout $lay \
           --variants "${TREEPUT_VARIANTS:-0}" --tune-rounds "${TREEPUT_ROUNDS:-10}" || exit 99
       done ;;
+    treetune)
+      # N -> 1 tree forms over 256 MiB of inputs (TREE_VARIANTS; 12: tapered tail)
+      $S tune_tree 400 python3 -u bench.py --tune-tree --variants "${TREE_VARIANTS:--1,12}" \
+        --tune-rounds "${TREE_ROUNDS:-10}" || exit 99 ;;
     treeput_pmc)
       for c in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES" \
                "TA_BUSY_avr GRBM_GUI_ACTIVE" "WRITE_SIZE" "FETCH_SIZE"; do
