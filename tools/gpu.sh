@@ -67,7 +67,7 @@ for stage in "$@"; do
       done ;;
     treetune)
       # N -> 1 tree forms over 256 MiB of inputs (TREE_VARIANTS; 12: tapered tail)
-      $S tune_tree 400 python3 -u bench.py --tune-tree --variants "${TREE_VARIANTS:--1,12}" \
+      $S tune_tree 400 python3 -u bench.py --tune-tree --variants="${TREE_VARIANTS:--1,12}" \
         --tune-rounds "${TREE_ROUNDS:-10}" || exit 99 ;;
     treeput_pmc)
       for c in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES" \
