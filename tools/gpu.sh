@@ -115,7 +115,8 @@ for stage in "$@"; do
       # random programs of collectives (tests/test_coll_stress.py) over more
       # seeds: device members at 2-8 processes, then a host-buffer member
       # with every 4th post refused
-      $S soak_dev 560 python3 -u tools/stress_soak.py --dev --worlds 2,3,5,8 --seeds 300-309 \
+      $S soak_dev 560 python3 -u tools/stress_soak.py --dev --worlds 2,3,5,8 \
+        --seeds "${SOAK_SEEDS:-300-309}" \
         --nops 200 && \
       $S soak_host 400 python3 -u tools/stress_soak.py --dev --worlds 2,3,5 --seeds 400-407 \
         --nops 160 --host-rank 1 --refuse-every 4 || exit 99 ;;
