@@ -969,8 +969,36 @@ __global__ __launch_bounds__(kBlock) void oneshot_ll(LlArgs a) {
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[2], a.flag, v[3], a.flag}, r, 2 * off + 16,
                                            0, kSysAux);
   }
-  // 2. this rank's part: poll every peer's words until their flags match
+  // 2. this rank's part.  First one lane per wave polls, per peer, the words
+  //    of the wave's last chunk (one 16-B load per peer per round instead of
+  //    the wave's 128), then every lane reads its own words and polls them
+  //    until their flags match — most do on the first read
   const uint32_t own = a.slen[a.rank];
+  const uint32_t lane = t & 63u, wave0 = off - lane * 16u;
+  if (wave0 < own && lane == 0) {
+    const uint32_t last_chunk = (own - 1u) / 16u * 16u;
+    const uint32_t last = wave0 + 63u * 16u < last_chunk ? wave0 + 63u * 16u : last_chunk;
+    uint32_t pending = 0;
+#pragma unroll
+    for (int k = 0; k < kOsMax; k++)
+      if (k < a.n && k != a.rank) pending |= 1u << k;
+    const uint64_t t0 = wall_clock64();
+    while (pending) {
+#pragma unroll
+      for (int k = 0; k < kOsMax; k++) {
+        if (!(pending >> k & 1u)) continue;
+        const u32x4 w1 = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       tile_rsrc(a.own + (size_t)k * LFA_SIG_LL_SLOT, LFA_SIG_LL_SLOT),
+                       2 * last + 16, 0, kSysLoadAux));
+        if (w1[1] == a.flag && w1[3] == a.flag) pending &= ~(1u << k);
+      }
+      if (pending) {
+        if (wall_clock64() - t0 > a.timeout) break;   // the lanes below note it
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
   if (off < own) {
     u32x4 vals[kOsMax];
     uint32_t pending = 0;
