@@ -157,6 +157,47 @@ static int done_word_init(struct lfa_coll_ep *ep)
 	return hipMemset(ep->done_ctr, 0, sizeof(uint32_t)) == hipSuccess ? 0 : -1;
 }
 
+/*
+ * One direct queue per device and process, shared by its endpoints (each
+ * keeps its own counter and completion word): a hardware queue is a scarce
+ * resource — past ~20 on the GPU the scheduler time-slices —
+ * and the queue's packets run in order whichever endpoint wrote them.
+ */
+#define DIRECT_DEVS 64
+static struct {
+	struct lfa_direct *d;
+	int refs, failed;
+} shared_direct[DIRECT_DEVS];
+static pthread_mutex_t direct_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static struct lfa_direct *direct_acquire(int dev)
+{
+	struct lfa_direct *d = NULL;
+
+	if (dev < 0 || dev >= DIRECT_DEVS)
+		return NULL;
+	pthread_mutex_lock(&direct_lock);
+	if (!shared_direct[dev].d && !shared_direct[dev].failed) {
+		shared_direct[dev].d = lfa_direct_open(dev);
+		shared_direct[dev].failed = !shared_direct[dev].d;
+	}
+	d = shared_direct[dev].d;
+	if (d)
+		shared_direct[dev].refs++;
+	pthread_mutex_unlock(&direct_lock);
+	return d;
+}
+
+static void direct_release(int dev)
+{
+	pthread_mutex_lock(&direct_lock);
+	if (shared_direct[dev].d && --shared_direct[dev].refs == 0) {
+		lfa_direct_close(shared_direct[dev].d);
+		shared_direct[dev].d = NULL;
+	}
+	pthread_mutex_unlock(&direct_lock);
+}
+
 static void done_word_free(struct lfa_coll_ep *ep)
 {
 	if (ep->direct) {
@@ -169,7 +210,7 @@ static void done_word_free(struct lfa_coll_ep *ep)
 			clock_gettime(CLOCK_MONOTONIC, &b);
 		} while (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq &&
 			 b.tv_sec - a.tv_sec < 5);
-		lfa_direct_close(ep->direct);
+		direct_release(ep->dom->device);
 		ep->direct = NULL;
 	}
 	if (ep->ddone_ctr)
@@ -1961,7 +2002,7 @@ static struct lfa_direct *direct_of(struct lfa_coll_ep *ep)
 		return NULL;
 	}
 	*(volatile uint64_t *)ep->ddone_word = 0;
-	ep->direct = lfa_direct_open(ep->dom->device);
+	ep->direct = direct_acquire(ep->dom->device);
 	return ep->direct;
 }
 

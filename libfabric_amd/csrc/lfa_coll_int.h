@@ -176,8 +176,9 @@ struct lfa_coll_ep {
 	const uint64_t *op_done_w;  /* ... and its word (NULL: done_word) */
 	/* direct dispatch (lfa_signal.h lfa_direct_*): a one-member group's
 	 * small reducing collective as liblfa's own AQL packet on its own HSA
-	 * queue, with its own counter and word (kernels there are not ordered
-	 * with ep->stream).  Opened at first use; LFA_DIRECT=0 keeps the HIP
+	 * queue (one per device and process, shared by its endpoints), with its
+	 * own counter and word (kernels there are not ordered with ep->stream).
+	 * Taken at first use; LFA_DIRECT=0 keeps the HIP
 	 * launch.  allow_direct: set by submit around a caller's operation (the
 	 * barrier's own staging copy is stream-ordered, so it never goes direct) */
 	struct lfa_direct *direct;

@@ -407,6 +407,47 @@ def test_small_ops_past_the_direct_queue_ring(coll, direct, monkeypatch):
         e.close()
 
 
+def test_two_endpoints_share_the_direct_queue(coll):
+    """Endpoints of one process share one direct queue per device, each with
+    its own counter and completion word: small operations of two one-member
+    endpoints interleaved, 300 in flight on each, every completion back on
+    its own endpoint in issue order and every result its own input; closing
+    one endpoint leaves the other's queue working."""
+    e1 = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    e2 = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    try:
+        n = 300
+        srcs = torch.arange(2 * n * 129, dtype=torch.float32, device=DEV).view(2, n, 129)
+        outs = torch.zeros_like(srcs)
+        torch.cuda.synchronize()
+        c1, c2 = [], []
+        for i in range(n):
+            c1.append(e1.allreduce(srcs[0, i], outs[0, i], 129, 8, 2))
+            c2.append(e2.allreduce(srcs[1, i], outs[1, i], 129, 8, 2))
+        d1, d2 = [], []
+        while len(d1) < n or len(d2) < n:
+            d1 += e1.cq_read()
+            d2 += e2.cq_read()
+        assert d1 == c1 and d2 == c2
+        torch.cuda.synchronize()
+        assert torch.equal(srcs, outs)
+        e1.close()
+        e1 = None
+        outs.zero_()
+        torch.cuda.synchronize()
+        c2 = [e2.allreduce(srcs[1, i], outs[1, i], 129, 8, 2) for i in range(20)]
+        d2 = []
+        while len(d2) < 20:
+            d2 += e2.cq_read()
+        assert d2 == c2
+        torch.cuda.synchronize()
+        assert torch.equal(srcs[1, :20], outs[1, :20])
+    finally:
+        if e1 is not None:
+            e1.close()
+        e2.close()
+
+
 def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
     """reduce and reduce_scatter on host buffers go through the chunked
     H2D / collective / D2H pipeline (reduce_scatter: one 2-D H2D per chunk);
