@@ -381,6 +381,34 @@ def test_tapered_tail_every_op_family(lfa, op, dt, mib):
         assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
 
 
+@pytest.mark.parametrize("off", [4, 8, 12])
+def test_tapered_tail_with_a_head(lfa, off):
+    """dst and src `off` bytes past 16-B alignment: a head of elements goes
+    through the element kernel and the 40 MiB body through the tapered form
+    from the first aligned vector; float SUM, oracle-checked at the head, the
+    split and the tail."""
+    n = ((40 << 20) + 4 * 333) // 4
+    g = torch.Generator(device=DEV).manual_seed(off)
+    base_d = torch.rand(n + 8, device=DEV, generator=g)
+    base_s = torch.rand(n + 8, device=DEV, generator=g)
+    d0 = base_d.clone()
+    d = base_d.view(torch.uint8)[off:off + 4 * n]
+    s_ = base_s.view(torch.uint8)[off:off + 4 * n]
+    assert lfa.write_ptr(2, 8, d.data_ptr(), s_.data_ptr(), n) == 0
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().view(np.float32)
+    want = d0.view(torch.uint8)[off:off + 4 * n].cpu().numpy().view(np.float32).copy()
+    oracle.write(2, 8, want, s_.cpu().numpy().view(np.float32).copy())
+    head = ((16 - off % 16) % 16) // 4
+    nvec = (n - head) * 4 // 16
+    split = nvec - nvec // 8
+    split -= split % 1024
+    at = head + split * 4
+    for lo in (0, at - 3000, n - 3000):
+        assert_parity(8, got[lo:lo + 3000].view(np.uint8), want[lo:lo + 3000].view(np.uint8),
+                      f"[{lo}, {lo + 3000})")
+
+
 def test_tree_put_errors(lfa):
     import ctypes
     from libfabric_amd import _native
