@@ -272,6 +272,23 @@ int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
  * operations across 2^32 without issuing 4 billion of them.  0 or
  * -LFA_EINVAL (unknown group, or operations of the group in flight). */
 int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ticket);
+/* Test entry for the completion-word error path.  Small operations complete
+ * through a host-mapped word instead of an event; one whose word does not
+ * come within the bound (LFA_SIG_TIMEOUT_MS, default 20 s) completes once, in
+ * error, through lfa_cq_readerr (err ETIMEDOUT; EIO when the queue owing it
+ * failed).  drop_next: the next drop_next word operations wait for a value
+ * their word never reaches; timeout_ms > 0: this endpoint's bound;
+ * fail_direct: mark the endpoint's direct queue failed (as a runtime queue
+ * error would).  0 or -LFA_EINVAL. */
+int lfa_coll_ep_test_word(struct lfa_coll_ep *ep, int drop_next, long timeout_ms,
+			  int fail_direct);
+/* 1 when the endpoint's one-member small operations go through the direct
+ * queue, 2 when that queue has failed (they take the HIP launch), 0 when it
+ * was never opened (diagnostics, tests). */
+int lfa_coll_ep_uses_direct(struct lfa_coll_ep *ep);
+/* Operations of the endpoint reaped through a completion word rather than
+ * an event (diagnostics: which completion path small buckets took). */
+uint64_t lfa_coll_ep_word_ops(struct lfa_coll_ep *ep);
 
 /* ---- fi_ops_collective ------------------------------------------------ */
 

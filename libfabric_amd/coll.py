@@ -114,6 +114,12 @@ def lib() -> ctypes.CDLL:
     L.lfa_mc_counters.argtypes = [c_void_p, c_uint64, P(McCounters)]
     L.lfa_mc_seed_ticket.restype = c_int
     L.lfa_mc_seed_ticket.argtypes = [c_void_p, c_uint64, c_uint64]
+    L.lfa_coll_ep_test_word.restype = c_int
+    L.lfa_coll_ep_test_word.argtypes = [c_void_p, c_int, ctypes.c_long, c_int]
+    L.lfa_coll_ep_uses_direct.restype = c_int
+    L.lfa_coll_ep_uses_direct.argtypes = [c_void_p]
+    L.lfa_coll_ep_word_ops.restype = c_uint64
+    L.lfa_coll_ep_word_ops.argtypes = [c_void_p]
     L.lfa_coll_domain_close.restype = c_int
     L.lfa_coll_domain_close.argtypes = [c_void_p]
     L.lfa_coll_ep_open.restype = c_int
@@ -428,6 +434,33 @@ class Endpoint:
         from `ticket`; every member seeds the same value."""
         _chk(lib().lfa_mc_seed_ticket(self.ep, coll_addr or self.world, ticket),
              "lfa_mc_seed_ticket")
+
+    def test_word(self, drop_next: int = 0, timeout_ms: int = 0,
+                  fail_direct: bool = False) -> None:
+        """lfa_coll_ep_test_word (test entry): the next `drop_next` word
+        operations wait for a value their word never reaches; timeout_ms > 0
+        bounds this endpoint's word waits; fail_direct marks its direct queue
+        failed."""
+        _chk(lib().lfa_coll_ep_test_word(self.ep, drop_next, timeout_ms, int(fail_direct)),
+             "lfa_coll_ep_test_word")
+
+    def uses_direct(self) -> int:
+        """lfa_coll_ep_uses_direct: 1 direct queue in use, 2 failed, 0 none."""
+        return _chk(lib().lfa_coll_ep_uses_direct(self.ep), "lfa_coll_ep_uses_direct")
+
+    def word_ops(self) -> int:
+        """lfa_coll_ep_word_ops: operations reaped through a completion word."""
+        return lib().lfa_coll_ep_word_ops(self.ep)
+
+    def cq_readerr(self):
+        """lfa_cq_readerr: (err, prov_errno, op_context) of the pending error
+        entry, or None."""
+        e = CqErrEntry()
+        n = lib().lfa_cq_readerr(self.ep, ctypes.byref(e))
+        if n == -EAGAIN:
+            return None
+        _chk(n, "lfa_cq_readerr")
+        return e.err, e.prov_errno, e.op_context
 
     def close(self) -> None:
         L = lib()

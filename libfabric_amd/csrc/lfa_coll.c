@@ -141,6 +141,65 @@ int lfa_coll_domain_close(struct lfa_coll_domain *d)
 	return 0;
 }
 
+static uint64_t mono_ns(void)
+{
+	struct timespec t;
+
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+/*
+ * Operations completed by a host-mapped word.  The host reads
+ * the word on every poll; a word that never comes — the queue or stream owing
+ * it failed, or its kernel never ran — would otherwise hold every later
+ * completion of the endpoint (they are reaped in issue order).  So at most
+ * every LFA_WORD_CHECK_NS a poll also asks the direct queue whether it has
+ * failed, or the stream whether it reports an error, and past the deadline
+ * (LFA_SIG_TIMEOUT_MS after the submit, the bound of every other GPU wait of
+ * the provider) the operation fails with ETIMEDOUT.  The failing operation
+ * is reaped once, as an error entry; the word's later arrival is harmless,
+ * the words only ever grow.
+ */
+#define LFA_WORD_CHECK_NS 1000000ull
+
+static void word_wait_start(const struct lfa_coll_ep *ep, struct word_wait *ww)
+{
+	ww->checked_ns = mono_ns();
+	ww->deadline_ns = ww->checked_ns + ep->word_timeout_ns;
+}
+
+/* A word not yet at its value: 1 still pending, -1 failed with *perr =
+ * ETIMEDOUT, EIO (the direct queue failed) or the stream's HIP error code. */
+static int word_overdue(const struct lfa_coll_ep *ep, const uint64_t *w, hipStream_t s,
+			struct word_wait *ww, int *perr)
+{
+	const uint64_t now = mono_ns();
+
+	if (now - ww->checked_ns < LFA_WORD_CHECK_NS)
+		return 1;
+	ww->checked_ns = now;
+	if (ep->direct && w == ep->ddone_word) {
+		if (lfa_direct_failed(ep->direct)) {
+			*perr = EIO;
+			return -1;
+		}
+	} else if (s) {
+		hipError_t e = hipStreamQuery(s);
+
+		if (e != hipSuccess && e != hipErrorNotReady) {
+			(void)hipGetLastError();
+			*perr = (int)e;
+			return -1;
+		}
+	}
+	if (now >= ww->deadline_ns) {
+		*perr = ETIMEDOUT;
+		return -1;
+	}
+	return 1;
+}
+
 /* The completion word and its counter (device endpoints), zeroed. */
 static int done_word_init(struct lfa_coll_ep *ep)
 {
@@ -198,20 +257,42 @@ static void direct_release(int dev)
 	pthread_mutex_unlock(&direct_lock);
 }
 
-static void done_word_free(struct lfa_coll_ep *ep)
+/*
+ * `stream_ok`: the endpoint's streams drained (lfa_coll_ep_flush), so no
+ * kernel on them still writes done_ctr / done_word.  The direct queue's
+ * kernels are on no stream: its last word is awaited (bounded).  A counter
+ * or word that a packet still queued may write is never freed:
+ * it is left allocated, with the queue reference that keeps the queue alive,
+ * and the leak is reported on stderr.
+ */
+static void done_word_free(struct lfa_coll_ep *ep, int stream_ok)
 {
 	if (ep->direct) {
-		/* the direct queue's kernels are on no stream: wait (bounded)
-		 * for the last one's word before its counter and word go */
-		struct timespec a, b;
+		const uint64_t t0 = mono_ns();
 
-		clock_gettime(CLOCK_MONOTONIC, &a);
-		do {
-			clock_gettime(CLOCK_MONOTONIC, &b);
-		} while (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq &&
-			 b.tv_sec - a.tv_sec < 5);
-		direct_release(ep->dom->device);
+		/* a failed queue's kernels may still finish (a test marks a
+		 * working queue failed): a short grace, else the full bound */
+		while (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq &&
+		       mono_ns() - t0 < (lfa_direct_failed(ep->direct) ? 100000000ull
+								 : ep->word_timeout_ns))
+			sched_yield();
+		if (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq) {
+			fprintf(stderr, "lfa: endpoint closed with direct-queue word %llu of %llu: "
+				"its counter, word and queue are left allocated\n",
+				(unsigned long long)*(volatile uint64_t *)ep->ddone_word,
+				(unsigned long long)ep->ddone_seq);
+			ep->ddone_ctr = NULL;
+			ep->ddone_word = NULL;
+		} else {
+			direct_release(ep->dom->device);
+		}
 		ep->direct = NULL;
+	}
+	if (!stream_ok && ep->done_word) {
+		fprintf(stderr, "lfa: endpoint closed with its stream not drained: its "
+			"completion counter and word are left allocated\n");
+		ep->done_ctr = NULL;
+		ep->done_word = NULL;
 	}
 	if (ep->ddone_ctr)
 		hipFree(ep->ddone_ctr);
@@ -230,7 +311,7 @@ static void done_word_free(struct lfa_coll_ep *ep)
 /* Frees whatever lfa_coll_ep_open managed to create (open's error path). */
 static void ep_release(struct lfa_coll_ep *ep)
 {
-	done_word_free(ep);
+	done_word_free(ep, 1);
 	if (ep->barrier_dev)
 		hipFree(ep->barrier_dev);
 	if (ep->ctl_dev)
@@ -266,6 +347,12 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	/* device domains choose per bucket; peer domains run the tree */
 	ep->algo = d->host ? LFA_ALGO_TREE : LFA_ALGO_AUTO;
 	ep->chunk = LFA_DEFAULT_CHUNK;
+	{
+		const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+		const long ms = e ? atol(e) : 0;
+
+		ep->word_timeout_ns = (uint64_t)(ms > 0 ? ms : 20000) * 1000000ull;
+	}
 	{
 		const char *e = getenv("LFA_GROUP_CHUNK_BYTES");
 
@@ -379,9 +466,11 @@ static int p2p_timed_out(const struct pending *p)
 
 int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 {
+	int drained;
+
 	if (!ep)
 		return -LFA_EINVAL;
-	lfa_coll_ep_flush(ep);
+	drained = lfa_coll_ep_flush(ep) == 0;
 	if (ep->dom->host) {
 		for (size_t i = 0; i < ep->qlen; i++)
 			hop_free(ep->q[(ep->qhead + i) % ep->qcap].hop);
@@ -398,7 +487,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 				hipFree(ep->stage[i].p);
 		for (int i = 0; i < ep->nev; i++)
 			hipEventDestroy(ep->evpool[i]);
-		done_word_free(ep);
+		done_word_free(ep, drained);
 		free(ep->ctl_host);
 		free(ep->q);
 		pthread_mutex_destroy(&ep->lock);
@@ -414,7 +503,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 			hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
 	for (int i = 0; i < ep->nev; i++)
 		hipEventDestroy(ep->evpool[i]);
-	done_word_free(ep);
+	done_word_free(ep, drained);
 	for (int i = 0; i < 8; i++)
 		if (ep->pc[i].valid)
 			plan_free(&ep->pc[i].pl);
@@ -528,6 +617,40 @@ int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 			 (mc->sig_word && *(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE);
 	pthread_mutex_unlock(&ep->lock);
 	return 0;
+}
+
+int lfa_coll_ep_test_word(struct lfa_coll_ep *ep, int drop_next, long timeout_ms,
+			  int fail_direct)
+{
+	if (!ep || drop_next < 0)
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	ep->drop_words = drop_next;
+	if (timeout_ms > 0)
+		ep->word_timeout_ns = (uint64_t)timeout_ms * 1000000ull;
+	if (fail_direct && ep->direct)
+		lfa__direct_mark_failed(ep->direct);
+	pthread_mutex_unlock(&ep->lock);
+	return 0;
+}
+
+uint64_t lfa_coll_ep_word_ops(struct lfa_coll_ep *ep)
+{
+	uint64_t n;
+
+	if (!ep)
+		return 0;
+	pthread_mutex_lock(&ep->lock);
+	n = ep->word_ops;
+	pthread_mutex_unlock(&ep->lock);
+	return n;
+}
+
+int lfa_coll_ep_uses_direct(struct lfa_coll_ep *ep)
+{
+	if (!ep)
+		return -LFA_EINVAL;
+	return ep->direct ? (lfa_direct_failed(ep->direct) ? 2 : 1) : 0;
 }
 
 int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ticket)
@@ -645,6 +768,12 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 		 * no event to record or query */
 		p->done_val = done_val;
 		p->done_w = done_w;
+		word_wait_start(ep, &p->ww);
+		if (ep->drop_words > 0) {
+			/* test knob: a value the word never reaches */
+			ep->drop_words--;
+			p->done_val |= 1ull << 62;
+		}
 		p->context = context;
 		p->kind = kind;
 		p->mc = mc;
@@ -689,6 +818,7 @@ struct hop {
 	/* a device hop whose every item is on the stream: a later P2P hop may
 	 * enqueue behind it (stream order) without waiting for it to finish */
 	int issued;
+	struct word_wait ww;    /* a hop ending in the completion word */
 	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
 	 * (they share the symmetric workspace), then grow it if needed through
 	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
@@ -896,6 +1026,11 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 
 			if (!h->issued && h->r.x.done_val) {
 				h->issued = 1;
+				word_wait_start(ep, &h->ww);
+				if (ep->drop_words > 0) {
+					ep->drop_words--;
+					h->r.x.done_val |= 1ull << 62;
+				}
 				LFA_TRACE("hop cid %#x issued (completion word %llu)",
 					  (unsigned)h->r.cid, (unsigned long long)h->r.x.done_val);
 			}
@@ -924,9 +1059,20 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 				LFA_TRACE("hop cid %#x issued", (unsigned)h->r.cid);
 			}
 			if (h->r.x.done_val) {
+				int werr = 0;
+
 				if (*(volatile uint64_t *)ep->done_word >= h->r.x.done_val) {
+					ep->word_ops++;
 					h->done = 1;
 					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
+				} else if (word_overdue(ep, ep->done_word, h->r.stream, &h->ww,
+							&werr) < 0) {
+					/* ETIMEDOUT / EIO as the error entry's err;
+					 * a stream's HIP code as its prov_errno */
+					if (werr != ETIMEDOUT && werr != EIO)
+						h->r.hip_err = werr;
+					h->err = werr == ETIMEDOUT ? -ETIMEDOUT : -LFA_EIO;
+					LFA_TRACE("hop cid %#x word overdue (%d)", (unsigned)h->r.cid, werr);
 				}
 				continue;
 			}
@@ -1004,7 +1150,7 @@ static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
 
 /* Completion state of a queued operation: 0 done, 1 pending, <0 / hip error
  * code (>0 in *perr) failed. */
-static int pending_state(const struct lfa_coll_ep *ep, const struct pending *p,
+static int pending_state(const struct lfa_coll_ep *ep, struct pending *p,
 			 int *perr)
 {
 	if (p->hop) {
@@ -1015,9 +1161,13 @@ static int pending_state(const struct lfa_coll_ep *ep, const struct pending *p,
 		}
 		return p->hop->done ? 0 : 1;
 	}
-	if (p->done_val)
-		return *(const volatile uint64_t *)(p->done_w ? p->done_w : ep->done_word) >=
-		       p->done_val ? 0 : 1;
+	if (p->done_val) {
+		const uint64_t *w = p->done_w ? p->done_w : ep->done_word;
+
+		if (*(const volatile uint64_t *)w >= p->done_val)
+			return 0;
+		return word_overdue(ep, w, ep->stream, &p->ww, perr);
+	}
 	hipError_t e = hipEventQuery(p->ev);
 
 	if (e == hipErrorNotReady)
@@ -1070,7 +1220,10 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 		} else if (st < 0) {
 			ep->err.op_context = p->context;
 			ep->err.flags = LFA_COLLECTIVE;
-			ep->err.err = p->hop ? perr : LFA_EIO;
+			/* a word operation's own cause (ETIMEDOUT / EIO), else EIO
+			 * with the HIP code as prov_errno */
+			ep->err.err = p->hop || (p->done_val && (perr == ETIMEDOUT || perr == EIO))
+				      ? perr : LFA_EIO;
 			ep->err.prov_errno = perr;
 			ep->have_err = 1;
 			if (p->chain)
@@ -1089,6 +1242,8 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 			c->op_context = p->context;
 			c->flags = LFA_COLLECTIVE;
 		}
+		if (st == 0 && p->done_val)
+			ep->word_ops++;
 		pending_release(ep, p);
 		ep->qhead = (ep->qhead + 1) % ep->qcap;
 		ep->qlen--;
@@ -2012,15 +2167,19 @@ static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_
 	int ret;
 
 	ep->op_done_w = NULL;
-	if (ep->allow_direct && direct_of(ep)) {
+	if (ep->allow_direct && direct_of(ep) && !lfa_direct_failed(ep->direct)) {
 		/* no HIP launch: ~3 us less host time */
 		ret = lfa_direct_solo_copy(ep->direct, result, buf, count * lfa_datatype_size(dt),
 					   ep->ddone_ctr, ep->ddone_word, ep->ddone_seq + 1);
-		if (ret)
+		if (!ret) {
+			ep->op_done_val = ++ep->ddone_seq;
+			ep->op_done_w = ep->ddone_word;
+			return 0;
+		}
+		if (ret != -LFA_EIO)
 			return ret;
-		ep->op_done_val = ++ep->ddone_seq;
-		ep->op_done_w = ep->ddone_word;
-		return 0;
+		/* the queue failed (nothing was enqueued): the HIP launch below;
+		 * the operations it still owes fail in word_overdue */
 	}
 
 	/* the one-shot kernel with n = 1 gives the same bytes; this kernel's

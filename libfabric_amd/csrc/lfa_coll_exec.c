@@ -559,7 +559,7 @@ static const struct xport xport_rccl = {
 
 /* Enqueue a whole schedule on `s` (one xrun_advance pass runs it all). */
 LFA_INTERNAL int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
-		     const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
+		     struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
 		     hipStream_t s)
 {
 	struct xrun r;
@@ -574,5 +574,8 @@ LFA_INTERNAL int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
 	r.dt = dt;
 	r.stream = s;
 	ret = xrun_advance(&r);
+	/* sig_oneshot reports the word value in the run's copy (the
+	 * caller's stayed 0, so device-domain one-shots completed by event) */
+	x->done_val = r.x.done_val;
 	return ret == 1 ? 0 : ret ? ret : -LFA_EIO;
 }

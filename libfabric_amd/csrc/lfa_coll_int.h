@@ -120,6 +120,12 @@ struct pending {
 	 * done_w: that word (NULL: the endpoint's done_word) */
 	uint64_t done_val;
 	const uint64_t *done_w;
+	/* word operations: when the operation fails if its word has not come,
+	 * and when the queue or stream owing it was last asked for an error
+	 * (lfa_coll.c word_overdue) */
+	struct word_wait {
+		uint64_t deadline_ns, checked_ns;
+	} ww;
 	/* the chunks of one chunked operation (peer_submit_chunked) share a
 	 * nonzero chain id: the operation posts ONE completion — the first
 	 * chunk's error, or the last chunk's success */
@@ -186,6 +192,12 @@ struct lfa_coll_ep {
 	uint32_t *ddone_ctr;
 	uint64_t *ddone_word;
 	uint64_t ddone_seq;
+	/* bound on a word operation's wait (LFA_SIG_TIMEOUT_MS at open, as every
+	 * GPU wait of the provider), and the test knob that makes the next
+	 * drop_words words unreachable (lfa_coll_ep_test_word) */
+	uint64_t word_timeout_ns;
+	int drop_words;
+	uint64_t word_ops;          /* operations reaped through a word */
 	int nev;
 	struct plan_cache {         /* last schedules built, keyed by shape */
 		int valid, coll, algo, rank, n, root;
@@ -293,8 +305,10 @@ LFA_INTERNAL int xrun_advance(struct xrun *r);
 LFA_INTERNAL int sig_barrier(struct xrun *r);
 /* ONESHOT step: the one-kernel small allreduce (lfa_signal.h). */
 LFA_INTERNAL int sig_oneshot(struct xrun *r, const struct lfa_step *st);
+/* x->done_val receives the one-shot launch's completion-word value (0: the
+ * operation completes through an event). */
 LFA_INTERNAL int exec_plan(struct lfa_coll_mc *mc, const struct plan *pl,
-			   const struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
+			   struct xctx *x, enum lfa_op op, enum lfa_datatype dt,
 			   hipStream_t s);
 LFA_INTERNAL extern const struct xport xport_peer, xport_peer_dev;
 

@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "lfa_fabric.h"
 #include "lfa_signal.h"
@@ -100,10 +101,129 @@ struct lfa_direct {
   uint16_t header;                          // the dispatch packets' header
   pthread_mutex_t lock;
   int hsa_up, have_reader, have_reader_pl, have_exe;
+  // 0, or why the queue is no longer used: 1 the runtime reported a queue
+  // error (queue_error), 2 the ring stayed full for ring_timeout_ns (its
+  // kernels do not finish), 3 marked by a test.  Once set, every submit
+  // returns -LFA_EIO and the provider fails the operations whose words the
+  // queue still owed (lfa_coll.c word_state).
+  int failed;
+  uint64_t ring_timeout_ns;
+  // Stub queue (CPU tests, lfa__direct_stub_open): no HSA; the packets go to
+  // a host ring and the read index is the caller's word.
+  int stub;
+  uint64_t stub_write;
+  const volatile uint64_t *stub_read;
+  hsa_kernel_dispatch_packet_t *stub_ring;
 };
+
+namespace {
+
+uint64_t now_ns() {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+// The ring's bound: LFA_SIG_TIMEOUT_MS, the provider's bound on every GPU
+// wait (default 20 s).
+uint64_t ring_timeout_ns() {
+  const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+  const long ms = e ? atol(e) : 0;
+  return (uint64_t)(ms > 0 ? ms : 20000) * 1000000ull;
+}
+
+void mark_failed(struct lfa_direct *d, int why) {
+  int none = 0;
+  if (__atomic_compare_exchange_n(&d->failed, &none, why, false, __ATOMIC_ACQ_REL,
+                                  __ATOMIC_ACQUIRE))
+    fprintf(stderr, "lfa: direct queue %s: its operations fail with EIO, later ones "
+            "take the HIP launch\n",
+            why == 1 ? "error reported by the runtime"
+                     : why == 2 ? "ring full past LFA_SIG_TIMEOUT_MS" : "marked failed");
+}
+
+// hsa_queue_create's error callback: the runtime found the queue broken
+// (an invalid packet, a kernel that faulted on it).
+void queue_error(hsa_status_t status, hsa_queue_t *, void *data) {
+  fprintf(stderr, "lfa: direct queue: hsa_status %#x\n", (unsigned)status);
+  mark_failed((struct lfa_direct *)data, 1);
+}
+
+uint64_t read_index(const struct lfa_direct *d) {
+  return d->stub ? __atomic_load_n(d->stub_read, __ATOMIC_ACQUIRE)
+                 : hsa_queue_load_read_index_scacquire(d->q);
+}
+
+// Room for packet idx: the kernarg slot of packet idx - kQueueSize is free
+// once the read index has passed idx - (kQueueSize - 1) (see
+// lfa_direct_solo_copy).  Bounded: 0, or -LFA_EIO when the queue has failed
+// or the ring has not moved for ring_timeout_ns — the queue is then marked
+// failed, since a ring that does not drain holds kernels that do not finish.
+int ring_wait(struct lfa_direct *d, uint64_t idx) {
+  if (idx - read_index(d) < kQueueSize - 1) return 0;
+  const uint64_t t0 = now_ns();
+  while (idx - read_index(d) >= kQueueSize - 1) {
+    if (__atomic_load_n(&d->failed, __ATOMIC_ACQUIRE)) return -LFA_EIO;
+    if (now_ns() - t0 > d->ring_timeout_ns) {
+      mark_failed(d, 2);
+      return -LFA_EIO;
+    }
+    __builtin_ia32_pause();
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int lfa_direct_failed(const struct lfa_direct *d) {
+  return d ? __atomic_load_n(&d->failed, __ATOMIC_ACQUIRE) : 0;
+}
+
+// Test hook: the queue as if the runtime had reported an error.
+extern "C" void lfa__direct_mark_failed(struct lfa_direct *d) {
+  if (d) mark_failed(d, 3);
+}
+
+// Test hook: a stub queue with no HSA behind it (CPU tests of the bounded
+// ring wait).  Its packets land in a host ring; `read_index` plays the
+// packet processor's read index; the ring bound is timeout_ms.
+extern "C" struct lfa_direct *lfa__direct_stub_open(const volatile uint64_t *read_index,
+                                                    uint64_t timeout_ms) {
+  if (!read_index) return nullptr;
+  struct lfa_direct *d = (struct lfa_direct *)calloc(1, sizeof(*d));
+  if (!d) return nullptr;
+  d->stub_ring =
+      (hsa_kernel_dispatch_packet_t *)calloc(kQueueSize, sizeof(hsa_kernel_dispatch_packet_t));
+  d->kernarg = (char *)calloc(kQueueSize, 64);
+  if (!d->stub_ring || !d->kernarg) {
+    free(d->stub_ring);
+    free(d->kernarg);
+    free(d);
+    return nullptr;
+  }
+  pthread_mutex_init(&d->lock, nullptr);
+  d->stub = 1;
+  d->stub_read = read_index;
+  d->ring_timeout_ns = timeout_ms * 1000000ull;
+  d->header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                         (1u << HSA_PACKET_HEADER_BARRIER));
+  return d;
+}
+
+// Test hook: packets written to the stub queue so far.
+extern "C" uint64_t lfa__direct_stub_written(const struct lfa_direct *d) {
+  return d && d->stub ? d->stub_write : 0;
+}
 
 extern "C" void lfa_direct_close(struct lfa_direct *d) {
   if (!d) return;
+  if (d->stub) {
+    free(d->stub_ring);
+    free(d->kernarg);
+    pthread_mutex_destroy(&d->lock);
+    free(d);
+    return;
+  }
   if (d->q) hsa_queue_destroy(d->q);
   if (d->kernarg) hsa_memory_free(d->kernarg);
   if (d->have_exe) hsa_executable_destroy(d->exe);
@@ -170,7 +290,10 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
   ok = ok && kernarg_size == sizeof(SoloArgs) && d->solo_kobj;
   ok = ok && hsa_memory_allocate(karg, (size_t)kQueueSize * 64, (void **)&d->kernarg) ==
                  HSA_STATUS_SUCCESS;
-  ok = ok && hsa_queue_create(d->gpu, kQueueSize, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr,
+  // single producer (every write under d->lock); the runtime reports a broken
+  // queue to queue_error instead of leaving its words unwritten silently
+  d->ring_timeout_ns = ring_timeout_ns();
+  ok = ok && hsa_queue_create(d->gpu, kQueueSize, HSA_QUEUE_TYPE_SINGLE, queue_error, d,
                               UINT32_MAX, UINT32_MAX, &d->q) == HSA_STATUS_SUCCESS &&
        d->q->size >= kQueueSize;    // the ring wait below counts kernarg slots
   if (!ok) {
@@ -200,20 +323,29 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
 // packet i + kQueueSize.  The read index passes i + 1 only once the packet
 // processor has consumed packet i + 1, whose barrier bit held it until packet
 // i's kernel completed — so the writer waits for that before reusing i's slot
-// (one slot of the ring stays unused).
+// (one slot of the ring stays unused).  The wait is bounded (ring_wait) and
+// happens before the write index moves, so a submit that gives up leaves no
+// hole in the ring: 0, -LFA_EINVAL, or -LFA_EIO (the queue failed; the
+// caller launches through HIP instead).
 extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send,
                                     size_t bytes, uint32_t *done_ctr, uint64_t *done_word,
                                     uint64_t done_val) {
   if (!bytes) return 0;
   if (!d || !result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
     return -LFA_EINVAL;
+  if (__atomic_load_n(&d->failed, __ATOMIC_ACQUIRE)) return -LFA_EIO;
   const uint32_t nblocks = (uint32_t)((bytes + 4095) / 4096);
   pthread_mutex_lock(&d->lock);
-  const uint64_t idx = hsa_queue_add_write_index_relaxed(d->q, 1);
-  // a full ring: wait until the packet kQueueSize before this one has
-  // completed (see above)
-  while (idx - hsa_queue_load_read_index_scacquire(d->q) >= kQueueSize - 1) {
+  const uint64_t idx = d->stub ? d->stub_write : hsa_queue_load_write_index_relaxed(d->q);
+  const int rc = ring_wait(d, idx);
+  if (rc) {
+    pthread_mutex_unlock(&d->lock);
+    return rc;
   }
+  if (d->stub)
+    d->stub_write = idx + 1;
+  else
+    hsa_queue_store_write_index_relaxed(d->q, idx + 1);
   SoloArgs *ka = (SoloArgs *)(d->kernarg + (idx % kQueueSize) * 64);
   ka->dst = result;
   ka->src = send;
@@ -224,7 +356,8 @@ extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const vo
   ka->word = done_word;
   ka->val = done_val;
   hsa_kernel_dispatch_packet_t *p =
-      (hsa_kernel_dispatch_packet_t *)d->q->base_address + (idx % d->q->size);
+      d->stub ? d->stub_ring + (idx % kQueueSize)
+              : (hsa_kernel_dispatch_packet_t *)d->q->base_address + (idx % d->q->size);
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
@@ -241,7 +374,7 @@ extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const vo
   const uint16_t header = d->header;
   const uint16_t setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
-  hsa_signal_store_screlease(d->q->doorbell_signal, (hsa_signal_value_t)idx);
+  if (!d->stub) hsa_signal_store_screlease(d->q->doorbell_signal, (hsa_signal_value_t)idx);
   pthread_mutex_unlock(&d->lock);
   return 0;
 }

@@ -167,9 +167,22 @@ static __device__ __forceinline__ void lfa_sig_note_timeout(uint64_t *status,
  */
 struct lfa_direct;
 struct lfa_direct *lfa_direct_open(int device);
+/* 0, -LFA_EINVAL, or -LFA_EIO: the queue has failed (a runtime queue error,
+ * or a full ring that did not drain within LFA_SIG_TIMEOUT_MS); nothing was
+ * enqueued, and the caller launches through HIP instead. */
 int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const void *send, size_t bytes,
 			 uint32_t *done_ctr, uint64_t *done_word, uint64_t done_val);
+/* Nonzero once the queue has failed: the words its packets owe may never
+ * come (the provider fails those operations with EIO). */
+int lfa_direct_failed(const struct lfa_direct *d);
 void lfa_direct_close(struct lfa_direct *d);
+/* Test hooks: mark a queue failed; a stub queue without HSA whose read index
+ * is *read_index and whose ring bound is timeout_ms (CPU tests), and the
+ * packets written to it. */
+void lfa__direct_mark_failed(struct lfa_direct *d);
+struct lfa_direct *lfa__direct_stub_open(const volatile uint64_t *read_index,
+					 uint64_t timeout_ms);
+uint64_t lfa__direct_stub_written(const struct lfa_direct *d);
 
 /* GPU wall-clock ticks per microsecond (the kernels' timeout unit). */
 uint64_t lfa__wallclock_ticks_per_us(void);
