@@ -368,11 +368,19 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep);
  * after lfa_coll_ep_flush (diagnostics, tests). */
 size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep);
 /* Device bytes of released P2P workspaces this process keeps for reuse
- * (LFA_WS_CACHE_BYTES, default 4 GiB; 0 frees them).  An exported workspace
- * is never handed back to the allocator below that cap: a fresh allocation at
- * a once-exported address may be refused an export, or exported as the
- * earlier memory.  Diagnostics, tests. */
+ * (LFA_WS_CACHE_BYTES, default 4 GiB; 0 frees them).  While a GPU domain is
+ * open, an exported workspace is never handed back to the allocator below
+ * the cache and quarantine caps: a fresh allocation at a once-exported
+ * address may be refused an export, or exported as the earlier memory
+ * (DESIGN.md §12).  0 after the process's last GPU domain closes.
+ * Diagnostics, tests. */
 size_t lfa_coll_ws_cached_bytes(void);
+/* Device bytes of released P2P workspaces held but never reused: those of
+ * groups whose P2P wait timed out (a stalled peer may still post into them),
+ * and those evicted above the cache's cap (LFA_WS_QUARANTINE_BYTES, default
+ * 4 GiB).  Both kinds are freed when the process's last GPU domain closes.
+ * Diagnostics, tests. */
+size_t lfa_coll_ws_quarantined_bytes(void);
 
 /* ---- schedules as data ------------------------------------------------ */
 

@@ -146,6 +146,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_ep_stage_bytes.argtypes = [c_void_p]
     L.lfa_coll_ws_cached_bytes.restype = c_size_t
     L.lfa_coll_ws_cached_bytes.argtypes = []
+    L.lfa_coll_ws_quarantined_bytes.restype = c_size_t
+    L.lfa_coll_ws_quarantined_bytes.argtypes = []
     L.lfa_coll_world_addr.restype = c_uint64
     L.lfa_coll_world_addr.argtypes = [c_void_p]
     L.lfa_join_collective.restype = c_int
@@ -272,6 +274,11 @@ def sig_area_bytes() -> int:
 def ws_cached_bytes() -> int:
     """lfa_coll_ws_cached_bytes: released P2P workspaces kept for reuse."""
     return lib().lfa_coll_ws_cached_bytes()
+
+
+def ws_quarantined_bytes() -> int:
+    """lfa_coll_ws_quarantined_bytes: released P2P workspaces held, never reused."""
+    return lib().lfa_coll_ws_quarantined_bytes()
 
 
 def member_chunk(nranks: int, host: bool, group_chunk: int, local_chunk: int) -> int:

@@ -60,6 +60,7 @@ static int is_device_ptr(const void *p)
 
 
 static void p2p_release(struct lfa_coll_mc *mc);
+static void ws_domain_ref(int delta);
 
 int lfa_coll_get_unique_id(void *id, size_t len)
 {
@@ -96,6 +97,7 @@ int lfa_coll_domain_open(int device, int rank, int nranks, const void *id,
 		free(d);
 		return -LFA_EIO;
 	}
+	ws_domain_ref(1);
 	*domain = d;
 	return 0;
 }
@@ -127,6 +129,8 @@ int lfa_coll_domain_open_peer(int device, int rank, int nranks,
 	d->host = 1;
 	d->xops = *ops;
 	d->xctx = ctx;
+	if (d->device >= 0)
+		ws_domain_ref(1);
 	*domain = d;
 	return 0;
 }
@@ -137,6 +141,8 @@ int lfa_coll_domain_close(struct lfa_coll_domain *d)
 		return -LFA_EINVAL;
 	if (!d->host)
 		ncclCommDestroy(d->comm);
+	if (d->device >= 0)
+		ws_domain_ref(-1);
 	free(d);
 	return 0;
 }
@@ -1483,30 +1489,60 @@ static void va_explain(const char *what, const void *p, size_t bytes)
  * endpoint close goes to this cache; the next workspace of the same size on
  * the same device takes it back and exports it again — the same memory
  * under the same address — so no fresh allocation ever lands on an address
- * that was exported.  Above the cap the least recently used go back to HIP.
+ * that was exported while a domain is open.
+ *
+ * Two kinds of released workspace are never handed out again but held
+ * (quarantine, VERDICT r4 #3 / ADVICE r4):
+ *   - one whose group had a P2P wait time out: a stalled peer may still run
+ *     its old kernel, pushing data and posting its old epoch through its old
+ *     mapping; in a reused workspace those posts would satisfy the new
+ *     group's waits (its epochs restart at 1) with stale data;
+ *   - the least recently used above the cap: returning it to hipFree would
+ *     reopen the address hazard above.
+ * The quarantine is bounded too (LFA_WS_QUARANTINE_BYTES, default 4 GiB):
+ * past it the oldest goes back to hipFree, and a later workspace at that
+ * address is caught by the export fallback and the identity check
+ * (sym_prepare, sym_open: the growth fails on every member with EIO rather
+ * than mapping the wrong memory).  When the last GPU domain of the process
+ * closes, every kept workspace is freed (lfa_coll_ws_cached_bytes() and
+ * lfa_coll_ws_quarantined_bytes() are then 0).
  */
 #define WS_CACHE_SLOTS 64
+#define WS_QUAR_SLOTS 256
 static struct ws_slot {
 	char *p;
 	size_t bytes;
 	int dev;
 	unsigned long long used;
-} ws_cache[WS_CACHE_SLOTS];
-static size_t ws_held;
+} ws_cache[WS_CACHE_SLOTS], ws_quar[WS_QUAR_SLOTS];
+static size_t ws_held, ws_quar_held;
 static unsigned long long ws_clock;
+static int ws_domains;          /* open domains with a GPU (workspace users) */
 static pthread_mutex_t ws_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t env_bytes(const char *name, long long dflt)
+{
+	const char *e = getenv(name);
+	long long v = e ? atoll(e) : dflt;
+
+	return v < 0 ? 0 : (size_t)v;
+}
 
 static size_t ws_cap(void)
 {
 	static long long cap = -1;
 
-	if (cap < 0) {
-		const char *e = getenv("LFA_WS_CACHE_BYTES");
+	if (cap < 0)
+		cap = (long long)env_bytes("LFA_WS_CACHE_BYTES", 4ll << 30);
+	return (size_t)cap;
+}
 
-		cap = e ? atoll(e) : (4ll << 30);
-		if (cap < 0)
-			cap = 0;
-	}
+static size_t ws_quar_cap(void)
+{
+	static long long cap = -1;
+
+	if (cap < 0)
+		cap = (long long)env_bytes("LFA_WS_QUARANTINE_BYTES", 4ll << 30);
 	return (size_t)cap;
 }
 
@@ -1529,19 +1565,52 @@ static char *ws_take(size_t bytes)
 	return p;
 }
 
-/* Keep workspace `p` (its whole allocation) for a later ws_take. */
-static void ws_give(char *p)
+/* Hold `s` in the quarantine (ws_lock held); what leaves it to make room is
+ * added to evict[]. */
+static void ws_quarantine(struct ws_slot s, char **evict, int *ne)
+{
+	int slot = -1;
+
+	for (int i = 0; i < WS_QUAR_SLOTS && slot < 0; i++)
+		if (!ws_quar[i].p)
+			slot = i;
+	if (slot < 0) {         /* every slot held: the oldest goes */
+		slot = 0;
+		for (int i = 1; i < WS_QUAR_SLOTS; i++)
+			if (ws_quar[i].used < ws_quar[slot].used)
+				slot = i;
+		evict[(*ne)++] = ws_quar[slot].p;
+		ws_quar_held -= ws_quar[slot].bytes;
+	}
+	s.used = ++ws_clock;
+	ws_quar[slot] = s;
+	ws_quar_held += s.bytes;
+	while (ws_quar_held > ws_quar_cap()) {
+		int old = -1;
+
+		for (int i = 0; i < WS_QUAR_SLOTS; i++)
+			if (ws_quar[i].p && (old < 0 || ws_quar[i].used < ws_quar[old].used))
+				old = i;
+		evict[(*ne)++] = ws_quar[old].p;
+		ws_quar_held -= ws_quar[old].bytes;
+		ws_quar[old].p = NULL;
+	}
+}
+
+/* Keep workspace `p` (its whole allocation) for a later ws_take, or — when
+ * `tainted` (its group timed out) — in the quarantine, never to be reused. */
+static void ws_give(char *p, int tainted)
 {
 	void *base = NULL;
 	size_t bytes = 0;
 	int dev = -1, slot = -1;
-	char *evict[WS_CACHE_SLOTS + 1];        /* a full cache's LRU + every slot */
+	char *evict[WS_CACHE_SLOTS + WS_QUAR_SLOTS + 2];
 	int ne = 0;
 
 	hipPointerAttribute_t at;
 
 	memset(&at, 0, sizeof(at));
-	if (!ws_cap() || hipMemGetAddressRange(&base, &bytes, p) != hipSuccess ||
+	if ((!ws_cap() && !tainted) || hipMemGetAddressRange(&base, &bytes, p) != hipSuccess ||
 	    base != (void *)p || hipPointerGetAttributes(&at, p) != hipSuccess) {
 		(void)hipGetLastError();
 		hipFree(p);
@@ -1549,6 +1618,10 @@ static void ws_give(char *p)
 	}
 	dev = at.device;
 	pthread_mutex_lock(&ws_lock);
+	if (tainted) {
+		ws_quarantine((struct ws_slot){ p, bytes, dev, 0 }, evict, &ne);
+		goto out;
+	}
 	for (int i = 0; i < WS_CACHE_SLOTS && slot < 0; i++)
 		if (!ws_cache[i].p)
 			slot = i;
@@ -1557,8 +1630,8 @@ static void ws_give(char *p)
 		for (int i = 1; i < WS_CACHE_SLOTS; i++)
 			if (ws_cache[i].used < ws_cache[slot].used)
 				slot = i;
-		evict[ne++] = ws_cache[slot].p;
 		ws_held -= ws_cache[slot].bytes;
+		ws_quarantine(ws_cache[slot], evict, &ne);
 	}
 	ws_cache[slot] = (struct ws_slot){ p, bytes, dev, ++ws_clock };
 	ws_held += bytes;
@@ -1571,11 +1644,39 @@ static void ws_give(char *p)
 				lru = i;
 		if (lru < 0)
 			lru = slot;
-		evict[ne++] = ws_cache[lru].p;
 		ws_held -= ws_cache[lru].bytes;
+		ws_quarantine(ws_cache[lru], evict, &ne);
 		ws_cache[lru].p = NULL;
 		if (lru == slot)
 			break;
+	}
+out:
+	pthread_mutex_unlock(&ws_lock);
+	for (int i = 0; i < ne; i++)
+		hipFree(evict[i]);
+}
+
+/* A GPU domain opened / closed: the last close frees every kept workspace. */
+static void ws_domain_ref(int delta)
+{
+	char *evict[WS_CACHE_SLOTS + WS_QUAR_SLOTS];
+	int ne = 0;
+
+	pthread_mutex_lock(&ws_lock);
+	ws_domains += delta;
+	if (ws_domains == 0) {
+		for (int i = 0; i < WS_CACHE_SLOTS; i++)
+			if (ws_cache[i].p) {
+				evict[ne++] = ws_cache[i].p;
+				ws_cache[i].p = NULL;
+			}
+		for (int i = 0; i < WS_QUAR_SLOTS; i++)
+			if (ws_quar[i].p) {
+				evict[ne++] = ws_quar[i].p;
+				ws_quar[i].p = NULL;
+			}
+		ws_held = 0;
+		ws_quar_held = 0;
 	}
 	pthread_mutex_unlock(&ws_lock);
 	for (int i = 0; i < ne; i++)
@@ -1592,6 +1693,24 @@ size_t lfa_coll_ws_cached_bytes(void)
 	return n;
 }
 
+size_t lfa_coll_ws_quarantined_bytes(void)
+{
+	size_t n;
+
+	pthread_mutex_lock(&ws_lock);
+	n = ws_quar_held;
+	pthread_mutex_unlock(&ws_lock);
+	return n;
+}
+
+/* A P2P wait of the group timed out (reaped, or recorded by a kernel in the
+ * status word): its workspace may still receive a stalled peer's posts. */
+static int mc_tainted(const struct lfa_coll_mc *mc)
+{
+	return mc->sig_failed ||
+	       (mc->sig_word && *(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE);
+}
+
 /* Unmap the peers' workspaces in `sym` and release this rank's `local`. */
 static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 {
@@ -1605,7 +1724,7 @@ static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
 	}
 	if (local) {
 		va_note('F', local, 0);
-		ws_give(local);
+		ws_give(local, mc_tainted(mc));
 	}
 }
 

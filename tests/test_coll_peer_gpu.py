@@ -559,6 +559,9 @@ def _ws_cycle_worker(rank, world, port, q, cap):
         from libfabric_amd import coll
         msg = "ok"
         held = []
+        # a second GPU domain open throughout: the cache lives while any GPU
+        # domain of the process is open and is freed at the last close
+        anchor = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
         for c in range(6):
             # every cycle: a new endpoint whose workspace grows three times,
             # then closes — the address pattern of round 4's stale exports
@@ -586,6 +589,10 @@ def _ws_cycle_worker(rank, world, port, q, cap):
                 msg = f"kept workspace bytes per cycle {held}"
         elif max(held) > cap:
             msg = f"kept {max(held)} B over the {cap} B cap"
+        anchor.close()
+        if msg == "ok" and (coll.ws_cached_bytes() or coll.ws_quarantined_bytes()):
+            msg = (f"after the last domain closed: {coll.ws_cached_bytes()} B cached, "
+                   f"{coll.ws_quarantined_bytes()} B quarantined")
         dist.destroy_process_group()
         q.put((rank, msg))
     except Exception:  # noqa: BLE001
@@ -601,7 +608,9 @@ def test_released_workspaces_are_reused(cap):
     memory, so its owner waited for posts that landed elsewhere.  Released
     workspaces are now kept and taken back by the next growth of that size;
     every peer also checks the owner's identity word through its mapping.
-    Four processes, six endpoint cycles, three growths each."""
+    Four processes, six endpoint cycles, three growths each, beside a
+    second GPU domain that stays open; once that one closes too (the last
+    GPU domain of the process), nothing is kept."""
     _spawn(_ws_cycle_worker, 4, args=(cap,))
 
 
@@ -1137,3 +1146,96 @@ def test_lost_one_shot_word_fails_that_operation_once():
     after the bound; the one queued behind it completes normally on both
     members; every result is exact and the group keeps working."""
     _spawn(_word_drop_worker, 2)
+
+
+def _late_member_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                          LFA_SIG_TIMEOUT_MS="300")
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import time
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        msg = "ok"
+        n = 4096
+        sends = [_inputs(oracle, 8, n, world, 70 + k) for k in range(3)]
+        wants = [oracle.allreduce(2, 8, s)[0] for s in sends]
+        xs = [_dev(s[rank]) for s in sends]
+        anchor = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        ep.set_algo(coll.ALGO_P2P)
+        r = torch.zeros(n, dtype=torch.float32, device="cuda")
+        _ready()
+        ep.wait(ep.allreduce(xs[0], r, n, 8, 2))                  # A, both
+        if r.cpu().numpy().tobytes() != wants[0].tobytes():
+            msg = "A wrong"
+        cached0, quar0 = coll.ws_cached_bytes(), coll.ws_quarantined_bytes()
+        rb = torch.zeros(n, dtype=torch.float32, device="cuda")
+        _ready()
+        if rank == 1:
+            # B: rank 0 is late; this member's one-shot gives up after 300 ms
+            try:
+                ep.wait(ep.allreduce(xs[1], rb, n, 8, 2), timeout_s=30)
+                msg = "B did not time out"
+            except coll.CollError as e:
+                if "prov_errno 110" not in str(e):
+                    msg = f"B: {e}"
+            ep.close()                   # the timed-out group's workspace
+            if msg == "ok" and not (coll.ws_quarantined_bytes() > quar0 and
+                                    coll.ws_cached_bytes() == cached0):
+                msg = (f"after close: cached {cached0} -> {coll.ws_cached_bytes()}, "
+                       f"quarantined {quar0} -> {coll.ws_quarantined_bytes()}")
+            ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+            ep.set_algo(coll.ALGO_P2P)
+            rc = torch.zeros(n, dtype=torch.float32, device="cuda")
+            _ready()
+            ctx_c = ep.allreduce(xs[2], rc, n, 8, 2)   # new group: workspace reset now
+            dist.barrier()                              # 1: rank 0 may run its late B
+            ep.wait(ctx_c)
+        else:
+            dist.barrier()                              # 1
+            # the late member: its B kernel pushes into rank 1's OLD
+            # workspace and posts B's epoch there through its old mapping
+            ep.wait(ep.allreduce(xs[1], rb, n, 8, 2), timeout_s=30)
+            ep.close()
+            ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+            ep.set_algo(coll.ALGO_P2P)
+            rc = torch.zeros(n, dtype=torch.float32, device="cuda")
+            _ready()
+            ep.wait(ep.allreduce(xs[2], rc, n, 8, 2))
+        # C on the re-made group: rank 1's new workspace is not the one the
+        # late kernel wrote into, so C's wait cannot pass on B's stale post
+        if msg == "ok" and rc.cpu().numpy().tobytes() != wants[2].tobytes():
+            msg = "C after the re-join wrong (stale post or slot data)"
+        for _ in range(3):
+            rc.zero_()
+            _ready()
+            ep.wait(ep.allreduce(xs[2], rc, n, 8, 2))
+            if msg == "ok" and rc.cpu().numpy().tobytes() != wants[2].tobytes():
+                msg = "a later C wrong"
+        ep.close()
+        anchor.close()
+        if msg == "ok" and (coll.ws_cached_bytes() or coll.ws_quarantined_bytes()):
+            msg = "workspaces kept after the last GPU domain closed"
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_rejoin_after_timeout_does_not_reuse_the_timed_out_workspace():
+    """after a P2P timeout the fix is to close and re-join
+    the group.  The re-join used to take the SAME workspace back from the
+    cache while the late member's kernel could still push data and post its
+    old epoch through its old mapping — satisfying the new group's first wait
+    with stale slots.  A timed-out group's workspace is now quarantined (held,
+    never reused): the member that timed out keeps it out of the cache, the
+    late member runs its old operation into it, and the re-made group's
+    operations are exact.  Every kept workspace is freed with the last GPU
+    domain."""
+    _spawn(_late_member_worker, 2)

@@ -120,6 +120,14 @@ for stage in "$@"; do
         --nops 200 && \
       $S soak_host 400 python3 -u tools/stress_soak.py --dev --worlds 2,3,5 --seeds 400-407 \
         --nops 160 --host-rank 1 --refuse-every 4 || exit 99 ;;
+    ipcanchor)
+      # the growth probe with a second GPU domain open across the cycles
+      # (the workspace cache lives between them), then without (the cache is
+      # freed at every cycle's last domain close)
+      $S ipc_growth_anchor 420 python3 -u tools/probe_ipc_growth.py --anchor && \
+      $S ipc_growth_noanchor 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
+    env)
+      $S env 30 bash -c 'env | grep -E "^(HSA_|HIP_|GPU_|AMD_|ROC|OMP_NUM)" | sort' || exit 99 ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)

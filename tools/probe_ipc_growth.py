@@ -39,7 +39,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, cycles, logdir, trace, cache, q):
+def _worker(rank, world, port, cycles, logdir, trace, cache, anchor, q):
     try:
         log = open(os.path.join(logdir, f"r{rank}.log"), "w", buffering=1)
         os.dup2(log.fileno(), 2)
@@ -60,6 +60,10 @@ def _worker(rank, world, port, cycles, logdir, trace, cache, q):
         bad = 0
         failed = []
         churn = []
+        # --anchor: a second GPU domain open across the cycles, so released
+        # workspaces stay cached between them (the cache is freed when the
+        # process's last GPU domain closes, i.e. every cycle without it)
+        keep = coll.HostEndpoint(rank, world, GlooXfer(), device=0) if anchor else None
         for c in range(cycles):
             ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
             try:
@@ -92,9 +96,12 @@ def _worker(rank, world, port, cycles, logdir, trace, cache, q):
             finally:
                 ep.close()
             dist.barrier()
+        if keep is not None:
+            keep.close()
         dist.destroy_process_group()
         log.flush()
-        q.put((rank, {"wrong_results": bad, "failed_growths": failed}))
+        q.put((rank, {"wrong_results": bad, "failed_growths": failed,
+                      "ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "unset")}))
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, traceback.format_exc()))
@@ -105,18 +112,23 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--cycles", type=int, default=24)
     ap.add_argument("--trace", action="store_true", help="LFA_TRACE=1 in every rank")
+    ap.add_argument("--anchor", action="store_true",
+                    help="keep a second GPU domain open across the cycles")
     ap.add_argument("--cache-bytes", type=int, default=None,
                     help="LFA_WS_CACHE_BYTES in every rank (0: workspaces freed)")
     a = ap.parse_args()
+    # the IPC mode of every multi-process GPU run (bench.py, tests/conftest.py)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import torch.multiprocessing as mp
     logdir = os.path.join(ROOT, "gpurun_out",
-                          "ipc_growth_logs" + ("" if a.cache_bytes is None else f"_c{a.cache_bytes}"))
+                          "ipc_growth_logs" + ("" if a.cache_bytes is None else f"_c{a.cache_bytes}")
+                          + ("_anchor" if a.anchor else ""))
     os.makedirs(logdir, exist_ok=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.cycles, logdir, a.trace,
-                                                 a.cache_bytes, q))
+                                                 a.cache_bytes, a.anchor, q))
              for r in range(a.world)]
     for p in procs:
         p.start()
@@ -139,6 +151,8 @@ def main():
         ids += sum("mapped onto other memory" in ln for ln in lines)
         notes += [f"r{r}: {ln}" for ln in lines if "overlaps event" not in ln][:40]
     out = {"world": a.world, "cycles": a.cycles, "ws_cache_bytes": a.cache_bytes,
+           "anchor_domain": a.anchor,
+           "hsa_enable_ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"),
            "identity_mismatches_logged": ids,
            "exports": a.world * a.cycles * 4, "export_failures": fails,
            "per_rank": res, "diagnostics": notes[:200]}
