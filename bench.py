@@ -775,31 +775,50 @@ def extra_tree(dev, stream, nsrc=8):
     return out
 
 
-def extra_tree_put(dev, stream, nsrc=8):
+def extra_tree_put(dev, stream, nsrc=8, reps=5, nsets=3, launches=30):
     """The LFA_ALGO_P2P kernel on local HBM: 8 x 32 MiB float blocks -> 1
     and -> 8 outputs, system-scope (sc0 sc1) loads and stores.  Traffic
     (nsrc + ndst)·B per launch.  On the 8-GPU node 7 of the inputs and 7 of
-    the outputs are peers' HBM over xGMI instead."""
+    the outputs are peers' HBM over xGMI instead.
+
+    The 8 -> 8 time depends on where the allocator put the 16 blocks (84-98 us
+    by buffer set on one box), so one set is not a figure
+    that compares across runs: each of `reps` repetitions
+    allocates `nsets` FRESH sets (3 x 16 x 32 MiB = 1.5 GiB at 8 -> 8, past the
+    256 MB Infinity Cache) and times `launches` launches rotating over them
+    with one event pair; the row reports the median over repetitions and the
+    range."""
     from libfabric_amd import atomic
     blk = 32 * 1024 * 1024 // 4
     out = {}
     for ndst in (1, 8):
-        sets = []
-        for k in range(2):
-            srcs = [torch.rand(blk, device=dev) for _ in range(nsrc)]
-            sets.append((srcs, [torch.empty(blk, device=dev) for _ in range(ndst)]))
+        per = []
+        for rep in range(reps):
+            sets = []
+            for k in range(nsets):
+                srcs = [torch.rand(blk, device=dev) for _ in range(nsrc)]
+                sets.append((srcs, [torch.empty(blk, device=dev) for _ in range(ndst)]))
 
-        def fn(i):
-            srcs, dsts = sets[i % 2]
-            atomic.reduce_tree_put(2, 8, dsts, srcs, blk, stream)
-        for i in range(4):
-            fn(i)
-        ms = _kernel_events(fn, 20, stream)
-        gbps = (nsrc + ndst) * blk * 4 / (ms * 1e-3) / 1e9
-        out[f"{nsrc}to{ndst}"] = {"kernel_us": round(ms * 1e3, 2),
-                                  "achieved_gbs": round(gbps, 1),
-                                  "frac": round(gbps / PEAK_GBPS, 4)}
-        del sets
+            def fn(i, sets=sets):
+                srcs, dsts = sets[i % nsets]
+                atomic.reduce_tree_put(2, 8, dsts, srcs, blk, stream)
+            for i in range(2 * nsets):
+                fn(i)
+            per.append(_kernel_events(fn, launches, stream))
+            del sets, fn
+            torch.cuda.empty_cache()
+        ms = statistics.median(per)
+        nb = (nsrc + ndst) * blk * 4
+
+        def frac(t):
+            return round(nb / (t * 1e-3) / 1e9 / PEAK_GBPS, 4)
+        out[f"{nsrc}to{ndst}"] = {
+            "kernel_us": round(ms * 1e3, 2), "achieved_gbs": round(nb / (ms * 1e-3) / 1e9, 1),
+            "frac": frac(ms),
+            "kernel_us_range": [round(min(per) * 1e3, 2), round(max(per) * 1e3, 2)],
+            "frac_range": [frac(max(per)), frac(min(per))],
+            "samples": f"median of {reps} repetitions, each {launches} launches over "
+                       f"{nsets} freshly allocated buffer sets"}
     return out
 
 
@@ -832,6 +851,7 @@ def extra_host_allreduce(ep, world, reps=3, sweep=False):
     """fi_allreduce on HOST buffers (what a libfabric caller hands over):
     the provider streams 32 MiB chunks H2D -> collective -> D2H on three HIP
     streams (both PCIe directions busy at once).  Rate = buffer bytes / wall time, PCIe-inclusive."""
+    from libfabric_amd import coll
     hx = torch.rand(COUNT).pin_memory()
     hy = torch.empty(COUNT).pin_memory()
     ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
@@ -977,18 +997,117 @@ def extra_e2e_staged(reps=3):
             "note": "pinned host dst/src, pipelined H2D / combine / D2H on two streams"}
 
 
+ORACLE_SLICE = 65536                   # elements per checked slice
+
+
+def oracle_ranges(count: int, world: int, kind: str, m: int = ORACLE_SLICE):
+    """Element ranges of a collective's result that the N > 1 leg checks
+    against the oracle, merged and sorted: allreduce — three
+    fixed m-element slices (start, middle, end); reduce_scatter — the first
+    and last m elements of every rank's block, the blocks as the reference
+    semantics define them (oracle.slice_bounds: the first count % N ranks one
+    element more)."""
+    import oracle
+    if kind == "allreduce":
+        m = min(m, count)
+        mid = count // 2 - m // 2
+        cand = [(0, m), (mid, mid + m), (count - m, count)]
+    else:
+        cand = []
+        for lo, hi in oracle.slice_bounds(count, world):
+            k = min(m, hi - lo)
+            cand += [(lo, lo + k), (hi - k, hi)]
+    out = []
+    for a, b in sorted(cand):
+        if a >= b:
+            continue
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
+
+
+def oracle_check(x, y, count: int, rank: int, world: int, dt: int, op: int, kind: str,
+                 m: int = ORACLE_SLICE) -> dict:
+    """The N > 1 leg's parity check.  Every rank's input at
+    oracle_ranges and its output there — the whole range for allreduce, the
+    part inside its own block for reduce_scatter — are gathered to every rank;
+    rank 0 runs the oracle's prov/coll allreduce (recursive doubling,
+    coll_coll.c:409-430's `hi OP lo` order) over the gathered inputs and
+    compares every rank's output with it bit for bit.  The oracle is only the
+    checker, outside any timed region.  Collective over the job (every rank
+    calls it); returns {"oracle_exact", "elements", "mismatches"} on rank 0,
+    {} elsewhere."""
+    import numpy as np
+    import oracle
+    ranges = oracle_ranges(count, world, kind, m)
+    total = sum(b - a for a, b in ranges)
+    if kind == "allreduce":
+        yout = torch.cat([y[a:b] for a, b in ranges])
+        mask = torch.ones(total, dtype=torch.uint8, device=y.device)
+    else:
+        lo, hi = oracle.slice_bounds(count, world)[rank]
+        yout = torch.zeros(total, dtype=y.dtype, device=y.device)
+        mask = torch.zeros(total, dtype=torch.uint8, device=y.device)
+        pos = 0
+        for a, b in ranges:
+            c, d = max(a, lo), min(b, hi)
+            if c < d:
+                yout[pos + c - a:pos + d - a] = y[c - lo:d - lo]
+                mask[pos + c - a:pos + d - a] = 1
+            pos += b - a
+    xin = torch.cat([x[a:b] for a, b in ranges])
+    if world > 1:
+        gloo = dist.get_backend() == "gloo"
+        parts = []
+        for t in (xin, yout, mask):
+            t = t.cpu() if gloo else t.contiguous()
+            lst = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(lst, t)
+            parts.append([u.cpu() for u in lst])
+        xs, ys, ms = parts
+    else:
+        xs, ys, ms = [xin.cpu()], [yout.cpu()], [mask.cpu()]
+    if rank != 0:
+        return {}
+    want = oracle.allreduce(op, dt, [t.numpy() for t in xs])[0]
+    uint = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[want.dtype.itemsize]
+    w = want.view(uint)
+    bad, covered = 0, np.zeros(total, dtype=bool)
+    for yk, mk in zip(ys, ms):
+        sel = mk.numpy().astype(bool)
+        covered |= sel
+        bad += int((yk.numpy().view(uint)[sel] != w[sel]).sum())
+    bad += int((~covered).sum())            # an element no rank holds
+    return {"oracle_exact": bad == 0, "elements": total, "mismatches": bad}
+
+
+def topology() -> dict:
+    """What the N-GPU run saw: devices and the hipDeviceCanAccessPeer matrix
+    (torch.cuda.can_device_access_peer)."""
+    n = torch.cuda.device_count()
+    return {"hip_device_count": n,
+            "peer_access": [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j))
+                             for j in range(n)] for i in range(n)]}
+
+
 def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
-    """double PROD reduce_scatter, 4 KiB .. 256 MiB per rank (configs[4])."""
+    """double PROD reduce_scatter, 4 KiB .. 256 MiB per rank (configs[4]); each
+    size's result checked against the oracle on slices (oracle_check)."""
     from libfabric_amd import coll
     ep.set_algo(algo)
     sweep = {}
-    for nbytes in [4096 * 4 ** k for k in range(9)]:   # 4 KiB .. 256 MiB
+    for k, nbytes in enumerate([4096 * 4 ** k for k in range(9)]):   # 4 KiB .. 256 MiB
         cnt = nbytes // 8
-        a = torch.rand(cnt, device="cuda", dtype=torch.float64) * 0.2 + 0.9
+        g = torch.Generator(device="cuda").manual_seed(5000 + 97 * rank + k)
+        a = torch.rand(cnt, device="cuda", dtype=torch.float64, generator=g) * 0.2 + 0.9
         off, ln = coll.block(cnt, world, rank)
         b = torch.empty(max(ln, 1), device="cuda", dtype=torch.float64)
         torch.cuda.synchronize()
         ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
+        torch.cuda.synchronize()
+        chk = oracle_check(a, b, cnt, rank, world, 9, 3, "reduce_scatter")
         barrier(world)
         reps = 20 if nbytes < (16 << 20) else 5
         t0 = time.perf_counter()
@@ -997,6 +1116,7 @@ def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
         t = max_over_ranks(time.perf_counter() - t0, world) / reps
         sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
+        sweep[str(nbytes)].update(chk)
         if nbytes <= (1 << 20):
             # latency: one operation submitted and reaped at a time, in C
             # (liblfa_bench.so), without the Python wrapper's ~10 us per call
@@ -1098,13 +1218,29 @@ def extra_collectives(rank, world, stream, emit=None):
         except Exception as e:  # noqa: BLE001 — a probe must not hide the rest
             xgmi = {"error": f"{type(e).__name__}: {e}"[:200]}
     out = {"xgmi_peer_copy_256mib": xgmi} if xgmi else {}
+    out["topology"] = topology()
     emit(out)
-    ep = coll.Endpoint.from_torch_dist()
+    if REHEARSE and world > 1:
+        # ranks share a GPU here and RCCL refuses that: the same executor
+        # and kernels through a peer-transfer domain (gloo carries the
+        # transfers) so the rows, and their oracle checks, still run
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from gloo_xfer import GlooXfer
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=torch.cuda.current_device())
+        out["endpoint"] = "peer-transfer domain over gloo (rehearsal)"
+    else:
+        ep = coll.Endpoint.from_torch_dist()
+        try:
+            out["rccl_nranks"] = ep.rccl_nranks()
+        except coll.CollError as e:
+            out["rccl_nranks"] = f"error: {e}"
+    emit(out)
     # TREE unless a row selects another: the P2P forms (and LFA_ALGO_AUTO,
     # the device-domain default, whose small buckets are P2P) run last
     ep.set_algo(coll.ALGO_TREE)
     try:
-        x = torch.rand(COUNT, device="cuda")
+        g = torch.Generator(device="cuda").manual_seed(7000 + rank)
+        x = torch.rand(COUNT, device="cuda", generator=g) * 2 - 1
         y = torch.empty_like(x)
         ref = None
         # P2P (cross-GPU IPC mappings + system-scope kernel) last: the
@@ -1121,7 +1257,16 @@ def extra_collectives(rank, world, stream, emit=None):
                 # its own
                 torch.cuda.synchronize()
                 ep.wait(ep.allreduce(x, y, COUNT, 8, 2))
-                row = {}
+                torch.cuda.synchronize()
+                # every algorithm's bits against the oracle on three slices
+                # (RCCL's ring order is not prov/coll's: informational there)
+                row = oracle_check(x, y, COUNT, rank, world, 8, 2, "allreduce")
+                if algo == coll.ALGO_RCCL and row:
+                    row = {"oracle_bitwise_equal": row["oracle_exact"],
+                           "oracle_elements": row["elements"],
+                           "oracle_mismatches": row["mismatches"],
+                           "oracle_note": "RCCL's ring order is not prov/coll's: "
+                                          "tolerance, not bits (DESIGN §6)"}
                 if algo != coll.ALGO_RCCL:
                     if ref is None:
                         ref = y.clone()
@@ -1161,7 +1306,10 @@ def extra_collectives(rank, world, stream, emit=None):
             emit(out)
         del ref
         ep.set_algo(coll.ALGO_TREE)
-        out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
+        try:
+            out["allreduce_host_buffers_256mib"] = extra_host_allreduce(ep, world)
+        except Exception as e:  # noqa: BLE001
+            out["allreduce_host_buffers_256mib"] = {"error": f"{e}"[:200]}
         try:
             out["reduce_scatter_host_buffers_256mib"] = extra_host_reduce_scatter(
                 ep, rank, world)
@@ -1190,7 +1338,7 @@ def extra_collectives(rank, world, stream, emit=None):
             ep.set_algo(coll.ALGO_TREE)
             emit(out)
         # configs[0] shape on the GPU path: 4 KiB float SUM allreduce latency
-        a = torch.rand(1024, device="cuda")
+        a = torch.rand(1024, device="cuda", generator=g)
         b = torch.empty_like(a)
         torch.cuda.synchronize()
         for name, algo in (("allreduce_4kib_float_sum_us", coll.ALGO_TREE),
@@ -1216,6 +1364,11 @@ def extra_collectives(rank, world, stream, emit=None):
                 barrier(world)
                 c_us = max_over_ranks(ep.bench_loop(3, a, b, 1024, 8, 2, reps=2000), world)
                 out[name.replace("_us", "_c_loop_us")] = round(c_us, 1)
+                torch.cuda.synchronize()
+                if algo != coll.ALGO_RCCL:
+                    c4 = oracle_check(a, b, 1024, rank, world, 8, 2, "allreduce")
+                    if rank == 0:
+                        out[name.replace("_us", "_oracle_exact")] = c4["oracle_exact"]
                 if algo == coll.ALGO_TREE:
                     ref4k = b.clone()
                 elif algo == coll.ALGO_P2P and world > 1:
@@ -1394,9 +1547,10 @@ def tune_treeput(args) -> None:
     # channels at the same offset)
     skew = args.treeput_layout == "skew"
     rows = []
+    nsets = args.tune_sets
     for ndst in (1, 8):
         sets = []
-        for _ in range(2):
+        for _ in range(nsets):
             if skew:
                 pitch = blk * 4 + 6144
                 pool = torch.empty((nsrc + ndst) * pitch, dtype=torch.uint8, device="cuda")
@@ -1426,7 +1580,7 @@ def tune_treeput(args) -> None:
                 evs = [(torch.cuda.Event(enable_timing=True),
                         torch.cuda.Event(enable_timing=True)) for _ in range(10)]
                 for i, (a, b) in enumerate(evs):
-                    srcs, dsts, sa, da, _ = sets[i % 2]
+                    srcs, dsts, sa, da, _ = sets[i % nsets]
                     a.record()
                     L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h)
                     b.record()
@@ -1538,6 +1692,8 @@ def main() -> None:
     ap.add_argument("--tune-bytes", type=int, default=S_BYTES)
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--tune-tree-layout", action="store_true")
+    ap.add_argument("--tune-sets", type=int, default=2,
+                    help="--tune-treeput: buffer sets rotated (each 9 or 16 x 32 MiB)")
     ap.add_argument("--tune-treeput", action="store_true")
     ap.add_argument("--treeput-layout", choices=("sep", "skew"), default="sep",
                     help="--tune-treeput: separate allocations or one skewed pool")

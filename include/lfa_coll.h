@@ -160,6 +160,10 @@ int lfa_coll_domain_open_host(int rank, int nranks,
 int lfa_coll_domain_open_peer(int device, int rank, int nranks,
 			      const struct lfa_peer_xfer_ops *ops, void *ctx,
 			      struct lfa_coll_domain **domain);
+/* Ranks in the RCCL communicator of a device domain (ncclCommCount): what
+ * RCCL itself sees, beside the rank count the caller passed.  0,
+ * -LFA_EINVAL, -LFA_EOPNOTSUPP (peer-transfer domain), -LFA_EIO. */
+int lfa_coll_domain_comm_count(struct lfa_coll_domain *d, int *count);
 int lfa_coll_domain_close(struct lfa_coll_domain *domain);
 
 /* An endpoint owns one HIP stream (its progress context), a work-item

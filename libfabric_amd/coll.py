@@ -122,6 +122,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_ep_word_ops.argtypes = [c_void_p]
     L.lfa_coll_domain_close.restype = c_int
     L.lfa_coll_domain_close.argtypes = [c_void_p]
+    L.lfa_coll_domain_comm_count.restype = c_int
+    L.lfa_coll_domain_comm_count.argtypes = [c_void_p, P(c_int)]
     L.lfa_coll_ep_open.restype = c_int
     L.lfa_coll_ep_open.argtypes = [c_void_p, P(c_void_p)]
     L.lfa_coll_ep_close.restype = c_int
@@ -454,6 +456,14 @@ class Endpoint:
     def uses_direct(self) -> int:
         """lfa_coll_ep_uses_direct: 1 direct queue in use, 2 failed, 0 none."""
         return _chk(lib().lfa_coll_ep_uses_direct(self.ep), "lfa_coll_ep_uses_direct")
+
+    def rccl_nranks(self) -> int:
+        """lfa_coll_domain_comm_count: ranks in the domain's RCCL communicator
+        (ncclCommCount); raises CollError on a peer-transfer domain."""
+        n = c_int(0)
+        _chk(lib().lfa_coll_domain_comm_count(self.dom, ctypes.byref(n)),
+             "lfa_coll_domain_comm_count")
+        return n.value
 
     def word_ops(self) -> int:
         """lfa_coll_ep_word_ops: operations reaped through a completion word."""

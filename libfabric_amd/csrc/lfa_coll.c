@@ -135,6 +135,15 @@ int lfa_coll_domain_open_peer(int device, int rank, int nranks,
 	return 0;
 }
 
+int lfa_coll_domain_comm_count(struct lfa_coll_domain *d, int *count)
+{
+	if (!d || !count)
+		return -LFA_EINVAL;
+	if (d->host)
+		return -LFA_EOPNOTSUPP;
+	return ncclCommCount(d->comm, count) == ncclSuccess ? 0 : -LFA_EIO;
+}
+
 int lfa_coll_domain_close(struct lfa_coll_domain *d)
 {
 	if (!d)

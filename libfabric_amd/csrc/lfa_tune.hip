@@ -730,6 +730,46 @@ __global__ __launch_bounds__(kBlock) void tp_split(PutArgs a, size_t nvec) {
   }
 }
 
+// Round 5 forms of the 8 -> M push, product body and scope
+// bits.  XCD: workgroups are dispatched round-robin over the 8 XCDs, so by
+// default XCD x streams tiles x, x + 8, ...; remapped, XCD x takes one
+// contiguous run of tiles (a bijection for any grid), so each XCD's 16
+// streams move through contiguous DRAM rows.  The occupancy cap (dynamic
+// LDS that the body never touches, set at launch) bounds the workgroups per
+// CU and so the bytes in flight: 136 VGPRs already allow 3 waves per SIMD
+// (12 per CU, ~384 KiB of loads in flight per CU), far past what hides
+// HBM latency, and fewer concurrent streams may keep more DRAM rows open.
+template <int U, int LAUX, int SAUX, bool XCD, int NW = kBlock / 64>
+__global__ __launch_bounds__(NW * 64) void tp_r5(PutArgs a, size_t nvec) {
+  unsigned b = blockIdx.x;
+  if constexpr (XCD) {
+    const unsigned n = gridDim.x, q = n / 8, r = n % 8, x = b % 8;
+    b = x * q + (x < r ? x : r) + b / 8;
+  }
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t wbase = (size_t)b * (NW * 64 * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, LAUX));
+    });
+  }
+  for (int j = 0; j < a.nout; j++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
@@ -796,6 +836,34 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 29: TPG(tp_split, 2); break;
     case 30: TPG(tp_split, 1); break;
 #undef TPG
+#define TP5(U, XCD, LDS)                                                             \
+  hipLaunchKernelGGL((tp_r5<U, 19, 17, XCD>),                                        \
+                     dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)), dim3(kBlock), \
+                     (LDS) << 10, s, a, nvec)
+    case 31: TP5(4, false, 0); break;     // = the product body, this harness
+    case 32: TP5(4, true, 0); break;      // XCD-contiguous tiles
+    case 33: TP5(4, false, 41); break;    // <= 3 workgroups per CU (12 waves)
+    case 34: TP5(4, false, 54); break;    // <= 2 workgroups per CU (8 waves)
+    case 35: TP5(4, false, 81); break;    // 1 workgroup per CU (4 waves)
+    case 36: TP5(4, true, 54); break;
+    case 37: TP5(2, false, 54); break;
+    case 38: TP5(2, true, 0); break;
+    case 39: TP5(2, false, 81); break;    // U = 2, 1 workgroup per CU
+    case 40: TP5(2, false, 41); break;    // U = 2, 3 workgroups per CU
+    case 41: TP5(1, false, 54); break;
+    case 42: TP5(1, false, 81); break;
+#undef TP5
+#define TPW(U, NW, LDS)                                                              \
+  hipLaunchKernelGGL((tp_r5<U, 19, 17, false, NW>),                                  \
+                     dim3(grid_for(nvec, (size_t)64 * NW * U, 0x7fffffffu)),           \
+                     dim3(64 * NW), (LDS) << 10, s, a, nvec)
+    case 43: TPW(2, 2, 41); break;        // 2-wave workgroups, 3 per CU (6 waves)
+    case 44: TPW(2, 2, 54); break;        // 2-wave workgroups, 2 per CU (4 waves)
+    case 45: TPW(2, 8, 81); break;        // 8-wave workgroups, 1 per CU
+    case 46: TPW(4, 8, 81); break;
+    case 47: TPW(2, 1, 27); break;        // 1-wave workgroups, 5 per CU
+    case 48: TPW(2, 1, 20); break;        // 1-wave workgroups, 8 per CU
+#undef TPW
     default: return -LFA_EINVAL;
   }
 #undef TP

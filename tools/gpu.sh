@@ -128,6 +128,19 @@ for stage in "$@"; do
       $S ipc_growth_noanchor 420 python3 -u tools/probe_ipc_growth.py || exit 99 ;;
     env)
       $S env 30 bash -c 'env | grep -E "^(HSA_|HIP_|GPU_|AMD_|ROC|OMP_NUM)" | sort' || exit 99 ;;
+    rehearse2)
+      # the N > 1 flow at 2 ranks sharing this GPU (LFA_BENCH_REHEARSE): the
+      # provider rows through a peer-transfer domain, with their oracle checks
+      LFA_BENCH_REHEARSE=1 $S rehearse2 600 python3 -u bench.py --gpus 2 --steps 5 \
+        --warmup 2 --no-cpu || exit 99 ;;
+    treeputx)
+      # the bench extra (fresh buffer sets rotated, median + range)
+      $S treeput_extra 300 python3 -u bench.py --only-extra tree_put || exit 99 ;;
+    treeput5)
+      # round-5 forms against the product, 3 buffer sets rotated
+      $S tune_treeput5 500 python3 -u bench.py --tune-treeput \
+        --variants "${TREEPUT_VARIANTS:-0,31,32,33,34,36,37,38,35}" \
+        --tune-rounds "${TREEPUT_ROUNDS:-8}" --tune-sets 3 || exit 99 ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)
