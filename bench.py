@@ -682,7 +682,9 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
             if i >= warm:
                 ts.append(time.perf_counter() - t0)
         ok = all(torch.equal(r, want) for r in results)
-        out[name] = round(statistics.median(ts) * 1e6, 1)
+        st = sample_stats([t * 1e6 for t in ts], 1)
+        out[name] = st["median_us"]
+        out[name.replace("_us", "_stats")] = st
         out[name.replace("_us", "_bitwise_ok")] = bool(ok)
     out["note"] = ("2 ranks on one GPU, loopback transport; median of 1000 after 100 "
                    "warm-up; wall time incl. hipStreamSynchronize")
@@ -720,6 +722,8 @@ def extra_config1_loopback(dev, stream, reps=1000, warm=100):
         if i >= warm:
             ts.append(time.perf_counter() - t0)
     out["oneshot_kernel_only_us"] = round(statistics.median(ts) * 1e6, 1) if ts else None
+    if ts:
+        out["oneshot_kernel_only_stats"] = sample_stats([t * 1e6 for t in ts], 1)
     out["oneshot_bitwise_ok"] = bool(all(torch.equal(r, want) for r in results)
                                      and int(status.item()) == -1)
     out["oneshot_note"] = ("KERNEL ONLY: the LFA_ALGO_P2P one-shot kernel launched directly, "
@@ -1092,9 +1096,40 @@ def topology() -> dict:
                              for j in range(n)] for i in range(n)]}
 
 
+def sample_stats(samples_us, world: int) -> dict:
+    """Latency rows as a distribution: the per-sample max
+    over ranks (an operation is done when its last member is), then median,
+    p10 and p90 over the n samples."""
+    t = torch.tensor(samples_us, dtype=torch.float64,
+                     device="cpu" if (REHEARSE or world == 1) else "cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    v = sorted(t.cpu().tolist())
+
+    def q(p):
+        return v[min(len(v) - 1, int(round(p * (len(v) - 1))))]
+    return {"median_us": round(statistics.median(v), 2), "p10_us": round(q(0.1), 2),
+            "p90_us": round(q(0.9), 2), "n": len(v)}
+
+
+def _py_samples(submit_wait, n: int) -> list[float]:
+    """Microseconds of `n` operations one at a time (submit, then wait for
+    that one), timed from Python — for buckets whose time dwarfs the
+    wrapper's ~10 us per call."""
+    out = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        submit_wait()
+        out.append((time.perf_counter() - t0) * 1e6)
+    return out
+
+
 def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
     """double PROD reduce_scatter, 4 KiB .. 256 MiB per rank (configs[4]); each
-    size's result checked against the oracle on slices (oracle_check)."""
+    size's result checked against the oracle on slices (oracle_check).  Per
+    size: "us" is the median latency of n operations one at a time (p10 /
+    p90 beside it, max over ranks per sample); "pipelined_us" the mean per
+    operation with a batch in flight, from which busbw is computed."""
     from libfabric_amd import coll
     ep.set_algo(algo)
     sweep = {}
@@ -1108,21 +1143,30 @@ def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
         ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3))
         torch.cuda.synchronize()
         chk = oracle_check(a, b, cnt, rank, world, 9, 3, "reduce_scatter")
+        # latency, one operation submitted and reaped at a time: n samples,
+        # median with p10 / p90.  Up to 1 MiB timed in C
+        # (liblfa_bench.so), without the Python wrapper's ~10 us per call
+        barrier(world)
+        if nbytes <= (1 << 20):
+            lat = ep.bench_samples(5, a, b, cnt, 9, 3, reps=200)
+            how = "C loop (lfa_bench_samples)"
+        else:
+            n = 20 if REHEARSE and nbytes >= (16 << 20) else 100
+            lat = _py_samples(lambda: ep.wait(ep.reduce_scatter(a, b, cnt, 9, 3)), n)
+            how = "Python submit + wait"
+        st = sample_stats(lat, world)
+        # throughput with operations in flight (the busbw figure)
         barrier(world)
         reps = 20 if nbytes < (16 << 20) else 5
         t0 = time.perf_counter()
         ctxs = [ep.reduce_scatter(a, b, cnt, 9, 3) for _ in range(reps)]
         ep.wait(ctxs[-1])
         t = max_over_ranks(time.perf_counter() - t0, world) / reps
-        sweep[str(nbytes)] = {"us": round(t * 1e6, 1),
+        sweep[str(nbytes)] = {"us": st["median_us"], "p10_us": st["p10_us"],
+                              "p90_us": st["p90_us"], "n": st["n"], "timed": how,
+                              "pipelined_us": round(t * 1e6, 1),
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
         sweep[str(nbytes)].update(chk)
-        if nbytes <= (1 << 20):
-            # latency: one operation submitted and reaped at a time, in C
-            # (liblfa_bench.so), without the Python wrapper's ~10 us per call
-            barrier(world)
-            sweep[str(nbytes)]["latency_c_loop_us"] = round(max_over_ranks(
-                ep.bench_loop(5, a, b, cnt, 9, 3, reps=200), world), 1)
         if algo == coll.ALGO_AUTO:
             # the per-bucket choice (lfa_coll_auto_algo; the same on every rank)
             chosen = coll.auto_algo(5, cnt, world, 8)
@@ -1362,8 +1406,9 @@ def extra_collectives(rank, world, stream, emit=None):
                 barrier(world)
                 ep.bench_loop(3, a, b, 1024, 8, 2, reps=200)        # warm-up
                 barrier(world)
-                c_us = max_over_ranks(ep.bench_loop(3, a, b, 1024, 8, 2, reps=2000), world)
-                out[name.replace("_us", "_c_loop_us")] = round(c_us, 1)
+                st = sample_stats(ep.bench_samples(3, a, b, 1024, 8, 2, reps=2000), world)
+                out[name.replace("_us", "_c_loop_us")] = st["median_us"]
+                out[name.replace("_us", "_c_loop_stats")] = st
                 torch.cuda.synchronize()
                 if algo != coll.ALGO_RCCL:
                     c4 = oracle_check(a, b, 1024, rank, world, 8, 2, "allreduce")
@@ -1548,7 +1593,7 @@ def tune_treeput(args) -> None:
     skew = args.treeput_layout == "skew"
     rows = []
     nsets = args.tune_sets
-    for ndst in (1, 8):
+    for ndst in [int(x) for x in args.tune_ndst.split(",")]:
         sets = []
         for _ in range(nsets):
             if skew:
@@ -1692,6 +1737,8 @@ def main() -> None:
     ap.add_argument("--tune-bytes", type=int, default=S_BYTES)
     ap.add_argument("--tune-tree", action="store_true")
     ap.add_argument("--tune-tree-layout", action="store_true")
+    ap.add_argument("--tune-ndst", default="1,8",
+                    help="--tune-treeput: output counts to time (8 inputs each)")
     ap.add_argument("--tune-sets", type=int, default=2,
                     help="--tune-treeput: buffer sets rotated (each 9 or 16 x 32 MiB)")
     ap.add_argument("--tune-treeput", action="store_true")

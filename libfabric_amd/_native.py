@@ -114,5 +114,7 @@ def lib(name: str = "lfa") -> ctypes.CDLL:
         L.lfa_bench_loop.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_size_t,
                                      c.c_int, c.c_int, c.c_int, c.c_uint64, c.c_int, c.c_int,
                                      c.POINTER(c.c_double)]
+        L.lfa_bench_samples.restype = c.c_int
+        L.lfa_bench_samples.argtypes = L.lfa_bench_loop.argtypes
     _loaded[name] = L
     return L

@@ -605,6 +605,18 @@ class Endpoint:
                                             timeout_ms, ctypes.byref(us)), "lfa_bench_loop")
         return us.value
 
+    def bench_samples(self, coll: int, buf, result, count: int, dt: int, op: int,
+                      root: int = 0, reps: int = 200, coll_addr: int | None = None,
+                      timeout_ms: int = 20000) -> list[float]:
+        """Bench only (liblfa_bench.so lfa_bench_samples): the same loop as
+        bench_loop, returning every operation's microseconds."""
+        from ._native import lib as native
+        out = (ctypes.c_double * reps)()
+        _chk(native("bench").lfa_bench_samples(self.ep, coll, _ptr(buf), _ptr(result), count,
+                                               root, dt, op, coll_addr or self.world, reps,
+                                               timeout_ms, out), "lfa_bench_samples")
+        return list(out)
+
     # completions
     def cq_read(self, max_entries: int = 16) -> list[int]:
         ents = self._ents if max_entries <= 16 else (CqEntry * max_entries)()

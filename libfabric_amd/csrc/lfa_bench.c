@@ -80,6 +80,59 @@ int lfa_bench_loop(struct lfa_coll_ep *ep, int coll, const void *buf, void *resu
 }
 
 /*
+ * The same loop keeping every operation's time (latency rows
+ * as medians with a spread, not one mean): samples[i] = microseconds from
+ * operation i's submit call to its completion read.  0 or as lfa_bench_loop.
+ */
+int lfa_bench_samples(struct lfa_coll_ep *ep, int coll, const void *buf, void *result,
+		      size_t count, int root, int dt, int op, lfa_addr_t coll_addr,
+		      int reps, int timeout_ms, double *samples)
+{
+	struct lfa_cq_entry e;
+	double t0, deadline;
+	ssize_t ret;
+
+	if (!ep || reps <= 0 || !samples)
+		return -LFA_EINVAL;
+	for (int i = 0; i < reps; i++) {
+		void *ctx = (void *)(uintptr_t)(0x6c666300u + (unsigned)i);
+
+		t0 = now_us();
+		switch (coll) {
+		case LFA_ALLREDUCE:
+			ret = lfa_allreduce(ep, buf, count, NULL, result, NULL, coll_addr,
+					    (enum lfa_datatype)dt, (enum lfa_op)op, 0, ctx);
+			break;
+		case LFA_REDUCE_SCATTER:
+			ret = lfa_reduce_scatter(ep, buf, count, NULL, result, NULL, coll_addr,
+						 (enum lfa_datatype)dt, (enum lfa_op)op, 0, ctx);
+			break;
+		case LFA_REDUCE:
+			ret = lfa_reduce(ep, buf, count, NULL, result, NULL, coll_addr,
+					 (lfa_addr_t)root, (enum lfa_datatype)dt,
+					 (enum lfa_op)op, 0, ctx);
+			break;
+		default:
+			return -LFA_EINVAL;
+		}
+		if (ret)
+			return (int)ret;
+		deadline = now_us() + 1e3 * timeout_ms;
+		for (;;) {
+			ret = lfa_cq_read(ep, &e, 1);
+			if (ret == 1 && e.op_context == ctx)
+				break;
+			if (ret < 0 && ret != -LFA_EAGAIN)
+				return (int)ret;
+			if (now_us() > deadline)
+				return -ETIMEDOUT;
+		}
+		samples[i] = now_us() - t0;
+	}
+	return 0;
+}
+
+/*
  * The same loop with its time split: out[0] mean us per
  * operation, out[1] of it inside the submit call, out[2] polling lfa_cq_read
  * until the operation completed, out[3] mean lfa_cq_read calls per operation.

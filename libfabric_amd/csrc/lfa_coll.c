@@ -751,21 +751,34 @@ static hipEvent_t event_get(struct lfa_coll_ep *ep)
 	return hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess ? ev : NULL;
 }
 
-/* A free slot at the tail of the FIFO of in-flight operations. */
-static struct pending *queue_slot(struct lfa_coll_ep *ep)
+/* Room for `n` more operations in the FIFO of in-flight operations (the
+ * ring doubles as needed): 0 or -LFA_ENOMEM. */
+static int queue_reserve(struct lfa_coll_ep *ep, size_t n)
 {
-	if (ep->qlen == ep->qcap) {
-		struct pending *nq = calloc(ep->qcap * 2, sizeof(*nq));
+	size_t cap = ep->qcap;
+
+	while (cap - ep->qlen < n)
+		cap *= 2;
+	if (cap != ep->qcap) {
+		struct pending *nq = calloc(cap, sizeof(*nq));
 
 		if (!nq)
-			return NULL;
+			return -LFA_ENOMEM;
 		for (size_t i = 0; i < ep->qlen; i++)
 			nq[i] = ep->q[(ep->qhead + i) % ep->qcap];
 		free(ep->q);
 		ep->q = nq;
 		ep->qhead = 0;
-		ep->qcap *= 2;
+		ep->qcap = cap;
 	}
+	return 0;
+}
+
+/* A free slot at the tail of the FIFO of in-flight operations. */
+static struct pending *queue_slot(struct lfa_coll_ep *ep)
+{
+	if (queue_reserve(ep, 1))
+		return NULL;
 	return &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
 }
 
@@ -2739,15 +2752,23 @@ static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 	const size_t esz = lfa_datatype_size(dt);
 	const uint64_t chain = ++ep->next_chain;
 	size_t per = chunk / esz;
+	int ret;
 
 	if (!per)
 		per = 1;
+	/* every chunk's queue slot before the first chunk is posted (ADVICE
+	 * r4): a full ring can then not stop the operation partway, which
+	 * would leave the members with different operations on the group */
+	ret = queue_reserve(ep, (count + per - 1) / per);
+	if (ret)
+		return ret;
 	for (size_t off = 0; off < count; off += per) {
 		const size_t n = count - off < per ? count - off : per;
 		const int last = off + n == count;
 		void *r = result ? (char *)result + off * esz : NULL;
-		int ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
-				      dt, op, context, last ? 0 : 3, NULL, dev, ep->algo);
+
+		ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
+				  dt, op, context, last ? 0 : 3, NULL, dev, ep->algo);
 
 		if (ret) {
 			/* the caller is told the operation never started: the

@@ -1504,6 +1504,21 @@ static int launch_tree(void *dst, const void *const *srcs, int nsrc,
   }
 }
 
+// Wide fan-out (LFA_ALGO_P2P's allreduce push: every member's block to all
+// N members) with the occupancy held at ONE workgroup per CU.  The body never
+// touches LDS; the dynamic LDS a launch reserves (over half of the CU's
+// 160 KiB) only keeps a second workgroup off the CU.  At 8 inputs -> 8
+// outputs the 136-VGPR body otherwise runs 12 waves per CU with ~32 KiB of
+// loads and 32 KiB of stores in flight per wave, which over-subscribes HBM
+// with 16 concurrent streams: 4 waves per CU with 2 KiB tiles (64 KiB of
+// loads in flight per CU) ran 8 x 32 MiB -> 8 in 90.0 us against 96.1-97.1
+// (two boxes, 3 fresh buffer sets rotated, bench.py --tune-treeput variants
+// 39 vs 0, profiles/r05_tune_treeput_occupancy_*.json).  At 4 outputs the
+// forms tie (66-68 us), at 1-2 outputs the reads want the full occupancy
+// (49.3 vs 52.7 us at 8 -> 1), so only wide fan-outs take this form.
+constexpr int kPutNarrowOuts = 6;
+constexpr unsigned kPutNarrowLds = 96u << 10;
+
 template <int OP, typename T, int NLEAF, int UF = 0>
 static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head,
                              hipStream_t s) {
@@ -1513,15 +1528,21 @@ static int launch_tree_put_n(const PutArgs &a, size_t cnt, bool vec, size_t head
   // elements.  Wider fan-in or byte/short lanes keep 2 KiB (U = 4 there
   // needs > 256 VGPRs and gave wrong uint8 results at 16 leaves).
   constexpr int U = UF ? UF : (NLEAF <= 8 && E >= 4) ? 4 : 2;
+  constexpr bool kNarrowable = UF == 0 && NLEAF <= 8 && E >= 4;
   size_t nvec = vec ? (cnt - head) * E / 16 : 0;
   if (nvec) {
     PutArgs b = a;
     for (int k = 0; k < kMaxLeaf; k++)
       if (b.t.in[k]) b.t.in[k] = (const char *)b.t.in[k] + head * E;
     for (int j = 0; j < b.nout; j++) b.out[j] = (char *)b.out[j] + head * E;
-    hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, U>),
-                       dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)),
-                       dim3(kBlock), 0, s, b, nvec);
+    if (kNarrowable && b.nout >= kPutNarrowOuts)
+      hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, 2>),
+                         dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                         dim3(kBlock), kPutNarrowLds, s, b, nvec);
+    else
+      hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, U>),
+                         dim3(grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu)),
+                         dim3(kBlock), 0, s, b, nvec);
   }
   size_t body = nvec * 16 / E;
   size_t n0 = vec ? head : cnt;

@@ -256,6 +256,39 @@ def test_tree_put_vs_oracle(lfa, nsrc, ndst, dt):
         assert not o[:esz].any() and not o[(n + 1) * esz:].any(), "wrote outside [0, n)"
 
 
+@pytest.mark.parametrize("nsrc,ndst", [(8, 8), (6, 6), (8, 6), (4, 8), (8, 5)])
+@pytest.mark.parametrize("dt", [8, 9, 5])
+def test_tree_put_wide_fanout_many_tiles(lfa, nsrc, ndst, dt):
+    """Fan-outs of 6 or more outputs run the one-workgroup-per-CU form
+    (lfa_kernels.hpp kPutNarrowOuts); 5 outputs the full-occupancy one.
+    3,000,017 elements (thousands of workgroups, a partial last tile) with a
+    misaligned head, every output bit-exact against the oracle."""
+    op = 3 if dt in (8, 9) else 2
+    nd = oracle.DT_NP[dt]
+    esz = nd.itemsize
+    n = 3_000_017
+    rng = np.random.default_rng(nsrc * 7 + ndst + dt)
+    if dt in (8, 9):
+        sends = [rng.uniform(0.9, 1.1, n + 2).astype(nd) for _ in range(nsrc)]
+    else:
+        info = np.iinfo(nd)
+        sends = [rng.integers(info.min, info.max, n + 2, dtype=nd, endpoint=True)
+                 for _ in range(nsrc)]
+    want = oracle.allreduce(op, dt, [x[1:n + 1].copy() for x in sends])[0]
+    srcs = [torch.from_numpy(x.view(np.uint8).copy()).to(DEV) for x in sends]
+    outs = [torch.zeros((n + 2) * esz, dtype=torch.uint8, device=DEV) for _ in range(ndst)]
+    import ctypes
+    from libfabric_amd import _native
+    sa = (ctypes.c_void_p * nsrc)(*[t.data_ptr() + esz for t in srcs])
+    da = (ctypes.c_void_p * ndst)(*[t.data_ptr() + esz for t in outs])
+    assert _native.lib().lfa_reduce_tree_put_async(op, dt, da, ndst, sa, nsrc, n, None) == 0
+    torch.cuda.synchronize()
+    for j, o in enumerate(outs):
+        o = o.cpu().numpy()
+        assert_parity(dt, o[esz:(n + 1) * esz].view(nd), want, f"out{j}")
+        assert not o[:esz].any() and not o[(n + 1) * esz:].any(), "wrote outside [0, n)"
+
+
 @pytest.mark.parametrize("dt", [0, 1, 2, 3])       # int8, uint8, int16, uint16
 def test_tree_put_narrow_lanes_16_32_leaves(lfa, dt):
     """reduce_tree_put on 1- and 2-byte lanes at 16 and 32

@@ -140,7 +140,8 @@ for stage in "$@"; do
       # round-5 forms against the product, 3 buffer sets rotated
       $S tune_treeput5 500 python3 -u bench.py --tune-treeput \
         --variants "${TREEPUT_VARIANTS:-0,31,32,33,34,36,37,38,35}" \
-        --tune-rounds "${TREEPUT_ROUNDS:-8}" --tune-sets 3 || exit 99 ;;
+        --tune-rounds "${TREEPUT_ROUNDS:-8}" --tune-sets 3 \
+        --tune-ndst "${TREEPUT_NDST:-1,8}" || exit 99 ;;
     ipctrace)
       $S ipc_growth_trace 500 python3 -u tools/probe_ipc_growth.py --trace || exit 99 ;;
     tplayout)
