@@ -1265,9 +1265,18 @@ def extra_collectives(rank, world, stream, emit=None):
     out["topology"] = topology()
     emit(out)
     if REHEARSE and world > 1:
-        # ranks share a GPU here and RCCL refuses that: the same executor
-        # and kernels through a peer-transfer domain (gloo carries the
-        # transfers) so the rows, and their oracle checks, still run
+        # ranks share a GPU here and RCCL refuses that (its refusal is the
+        # rccl_nranks field): the same executor and kernels through a
+        # peer-transfer domain (gloo carries the transfers), so the rows and
+        # their oracle checks still run
+        try:
+            probe = coll.Endpoint.from_torch_dist()
+            try:
+                out["rccl_nranks"] = probe.rccl_nranks()
+            finally:
+                probe.close()
+        except Exception as e:  # noqa: BLE001
+            out["rccl_nranks"] = f"error: {type(e).__name__}: {e}"[:160]
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from gloo_xfer import GlooXfer
         ep = coll.HostEndpoint(rank, world, GlooXfer(), device=torch.cuda.current_device())

@@ -178,11 +178,11 @@ static ssize_t owner_trecvmsg(struct fid_ep *ep, const struct fi_msg_tagged *m,
 		;
 	if ((x = *pp)) {             /* arrived before it was posted */
 		*pp = x->next;
+		own.bytes_recv += x->len;       /* under the lock: deliver() counts too */
 		pthread_mutex_unlock(&own.lock);
 		CHECK(x->len == m->msg_iov[0].iov_len, "length %zu vs %zu", x->len,
 		      m->msg_iov[0].iov_len);
 		memcpy(m->msg_iov[0].iov_base, x->data, x->len);
-		own.bytes_recv += x->len;
 		complete_xfer(m->context, FI_RECV, x->len, x->tag);
 		free(x->data);
 		free(x);

@@ -136,6 +136,10 @@ for stage in "$@"; do
     treeputx)
       # the bench extra (fresh buffer sets rotated, median + range)
       $S treeput_extra 300 python3 -u bench.py --only-extra tree_put || exit 99 ;;
+    treeputprof)
+      # the tree_put extra under rocprofv3 --kernel-trace --stats
+      $S prof_treeput 300 $P -d gpurun_out/prof_treeput -o run -- python3 bench.py \
+        --only-extra tree_put || exit 99 ;;
     treeput5)
       # round-5 forms against the product, 3 buffer sets rotated
       $S tune_treeput5 500 python3 -u bench.py --tune-treeput \
