@@ -1555,6 +1555,8 @@ def tune_tree(args) -> None:
         ref = None
         for v in variants:  # correctness: every form equals the product's bits
             srcs, out, arr = sets[0]
+            out.fill_(float("nan"))           # a form that wrote nothing fails
+            torch.cuda.synchronize()
             assert L.lfa__tune_tree_f32(v, out.data_ptr(), arr, nsrc, blk, h) == 0
             torch.cuda.synchronize()
             if ref is None:
@@ -1622,6 +1624,9 @@ def tune_treeput(args) -> None:
         ref = None
         for v in variants:
             srcs, dsts, sa, da, _ = sets[0]
+            for d in dsts:
+                d.fill_(float("nan"))         # a form that wrote nothing fails
+            torch.cuda.synchronize()
             assert L.lfa__tune_treeput_f32(v, da, ndst, sa, nsrc, blk, h) == 0
             torch.cuda.synchronize()
             if ref is None:

@@ -1390,6 +1390,22 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                          dim3(kBlock), 0, s, b, dst, nvec);
       return;
     }
+  } else if (variant >= 20 && variant <= 24) {
+    if constexpr (ALL) {
+      // round 5: the write-through chunk form at capped occupancy (dynamic
+      // LDS the body never touches) and at 4 vectors per lane
+      constexpr unsigned kCap[5] = {41u << 10, 54u << 10, 81u << 10, 0u, 54u << 10};
+      const unsigned lds = kCap[variant - 20];
+      if (variant < 23)
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
+                           dim3(kBlock), lds, s, b, dst, nvec);
+      else
+        hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 4, kStoreSc1>),
+                           dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)),
+                           dim3(kBlock), lds, s, b, dst, nvec);
+      return;
+    }
   } else if (variant == 12) {
     if constexpr (ALL) {
       // the last 1/8 of the vectors one per lane (reduce_tree_taper)

@@ -136,6 +136,10 @@ for stage in "$@"; do
     treeputx)
       # the bench extra (fresh buffer sets rotated, median + range)
       $S treeput_extra 300 python3 -u bench.py --only-extra tree_put || exit 99 ;;
+    tree5)
+      # round-5 occupancy-capped forms of the N -> 1 tree against the product
+      $S tune_tree5 400 python3 -u bench.py --tune-tree --variants="${TREE_VARIANTS:--1,20,21,22,23,24}" \
+        --tune-rounds "${TREE_ROUNDS:-8}" || exit 99 ;;
     treeputprof)
       # the tree_put extra under rocprofv3 --kernel-trace --stats
       $S prof_treeput 300 $P -d gpurun_out/prof_treeput -o run -- python3 bench.py \
