@@ -9,17 +9,20 @@ step   : one pass of the hot path — ofi_atomic_write_handler(FI_SUM, FI_FLOAT,
 value  : whole-job traffic rate, 3·S bytes per step (read dst, read src,
          write dst) × steps ÷ the max-over-ranks wall time, in GiB/s.
          The buffer rate S/t is reported beside it.
-N > 1  : one process per GPU.  The headline is STRONG-scaled (SURVEY §8(e),
-         BASELINE configs[3]): the one 256 MiB buffer pair is partitioned into
-         N contiguous 4 KiB-aligned shards and GPU g combines shard g with no
-         exchange, so a step is still one 256 MiB combine, done by N GPUs.  The
-         weak-scaled figure (every rank its own 256 MiB pair) sits beside it in
-         extras.  `python bench.py --gpus N` without RANK in the environment
-         starts the N rank processes itself (before any GPU call); under
-         torch.distributed.run it is one of them.  A world size that differs
-         from --gpus is an error (exit 2).  The N > 1 provider extras
-         (allreduce / reduce_scatter over RCCL, xGMI P2P) run as a child job
-         of the ranks (run_isolated), so a fault there cannot lose the line.
+N > 1  : one process per GPU.  The headline is WEAK-scaled (the tier's rule
+         for a path that partitions: independent objects sharded across ranks
+         with no data-path collective): every rank combines its own 256 MiB
+         pair per step, so a step is N independent 256 MiB combines and value =
+         3·S·N·steps ÷ the max-over-ranks wall time.  The strong-scaled figure
+         (one 256 MiB pair split into N contiguous 4 KiB-aligned shards, GPU g
+         combining shard g — SURVEY §8(e), BASELINE configs[3]'s "8 GPUs each
+         combine S/8") sits beside it in extras.  `python bench.py --gpus N`
+         without RANK in the environment starts the N rank processes itself
+         (before any GPU call); under torch.distributed.run it is one of them.
+         A world size that differs from --gpus is an error (exit 2).  The N > 1
+         provider extras (allreduce / reduce_scatter over RCCL, xGMI P2P) run as
+         a child job of the ranks (run_isolated), so a fault there cannot lose
+         the line.
 
 Extra objects on the JSON line:
   roofline      dominant kernel (combine_lds<SUM,float>): algorithmic bytes per
@@ -636,7 +639,7 @@ def extra_fetch_tables(dev, stream):
 
 def extra_sizes(dev, stream, reps: int = 100, prewarm_s: float = 0.1):
     """The product float SUM combine vs size per operand (the shard sizes of
-    the strong-scaled headline: 256 MiB / N): average launch duration from an
+    the strong-scaled extra: 256 MiB / N): average launch duration from an
     event pair around 100 back-to-back launches over >= 1 GiB of rotated
     operands, after a clock prewarm."""
     from libfabric_amd import atomic
@@ -1840,14 +1843,15 @@ def main() -> None:
                 dist.destroy_process_group()
         return
 
-    # Headline: ONE 256 MiB buffer pair, sharded over the N GPUs (strong).
-    off, cnt = shard_of(COUNT, world, rank)
+    # Headline: every rank its own 256 MiB buffer pair per step (weak: the
+    # combine partitions with no exchange, so N GPUs do N independent units).
+    cnt = COUNT
     r = timed_combine(dev, stream, cnt, 1000 + rank, args, world)
     elapsed, kern_ms, kern_med = r["elapsed"], r["kern_ms"], r["kern_med"]
     shard_bytes = cnt * 4
-    value = 3 * S_BYTES * args.steps / elapsed / 2**30
+    value = 3 * S_BYTES * world * args.steps / elapsed / 2**30
     achieved = 3 * shard_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = read_traffic() if world == 1 else read_traffic_shard(shard_bytes)
+    traffic, traffic_src = read_traffic()
 
     line = {
         "metric": "device-resident GiB/s, float32 FI_SUM reduce, 256 MiB buffers",
@@ -1858,22 +1862,22 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (uniform[-1,1) float32, torch.Generator seeds 1000+rank)",
         "config": {
             "workload": "float32 FI_SUM local combine of one 256 MiB device-resident "
                         "buffer pair per step (BASELINE.json configs[1]), dst += src "
-                        "through lfa_atomic_write_async; at N>1 split into N contiguous "
-                        "4 KiB-aligned shards, GPU g combines shard g (SURVEY §8(e))",
+                        "through lfa_atomic_write_async; at N>1 every GPU combines its "
+                        "own pair per step, no exchange (weak; SURVEY §8(e))",
             "count": COUNT, "buffer_bytes": S_BYTES,
-            "shard_bytes_per_gpu": shard_bytes,
+            "bytes_per_gpu_per_step": 3 * shard_bytes,
             "buffer_sets": r["nsets"],
-            "bytes_per_step": 3 * S_BYTES,
-            "buffer_rate_gib_s": round(S_BYTES * args.steps / elapsed / 2**30, 2),
+            "bytes_per_step": 3 * S_BYTES * world,
+            "buffer_rate_gib_s": round(S_BYTES * world * args.steps / elapsed / 2**30, 2),
             "prewarm_launches": r["prewarm"],
-            "parallelism": f"shard{world} (contiguous shards of one buffer, no exchange)",
+            "parallelism": f"dp{world} (one independent 256 MiB pair per GPU, no exchange)",
         },
         "roofline": {
             "bound": "hbm",
@@ -1932,14 +1936,17 @@ def main() -> None:
         ex = line.setdefault("extras", {})
         try:
             if world > 1:
-                # weak scaling beside the strong headline: every rank its own
-                # full 256 MiB pair per step
-                w = timed_combine(dev, stream, COUNT, 2000 + rank, args, world)
-                ex["weak_scaling_256mib_per_gpu"] = {
-                    "value": round(3 * S_BYTES * args.steps * world / w["elapsed"] / 2**30, 2),
+                # strong scaling beside the weak headline: ONE 256 MiB pair
+                # split into N contiguous 4 KiB-aligned shards
+                off, scnt = shard_of(COUNT, world, rank)
+                w = timed_combine(dev, stream, scnt, 2000 + rank, args, world)
+                ex["strong_scaling_one_256mib_pair_sharded"] = {
+                    "value": round(3 * S_BYTES * args.steps / w["elapsed"] / 2**30, 2),
                     "unit": "GiB/s", "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
+                    "shard_bytes_per_gpu": scnt * 4,
                     "kernel_us": round(w["kern_ms"] * 1e3, 2),
-                    "frac": round(3 * S_BYTES / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4)}
+                    "frac": round(3 * scnt * 4 / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4),
+                    "traffic": read_traffic_shard(scnt * 4)[0]}
                 torch.cuda.empty_cache()
             # independent buckets two streams at a time, at this rank's
             # shard (and at N = 1 at the N = 8 shard, 32 MiB) — only below
@@ -1947,7 +1954,7 @@ def main() -> None:
             # (tools/probe_streams.py), and the headline kernel's rocprofv3
             # statistics stay those of the one-stream headline
             ex["buckets_two_streams"] = extra_two_streams(
-                dev, [c for c in [cnt] + ([COUNT // 8] if world == 1 else [])
+                dev, [c for c in [shard_of(COUNT, world, rank)[1]] + ([COUNT // 8] if world == 1 else [])
                       if c * 4 < (192 << 20)])
             torch.cuda.empty_cache()
             if world == 1:
