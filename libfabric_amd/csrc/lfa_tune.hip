@@ -770,6 +770,42 @@ __global__ __launch_bounds__(NW * 64) void tp_r5(PutArgs a, size_t nvec) {
   }
 }
 
+// Round 5: the outputs split over G workgroups per tile, the G placed on ONE
+// XCD back to back.  Workgroups are dispatched round-robin over the 8 XCDs
+// (XCD = blockIdx mod 8), so XCD x's k-th workgroup is blockIdx x + 8k; it
+// takes tile (k / G)·8 + x and outputs g, g + G, ... (g = k mod G).  Each
+// tile's inputs are fetched from HBM by its first workgroup and from that
+// XCD's L2 by the other G - 1; every workgroup drives nout / G output
+// streams instead of nout.  HBM bytes stay 8 reads + nout writes.
+template <int U, int LAUX, int SAUX, int G>
+__global__ __launch_bounds__(kBlock) void tp_xsplit(PutArgs a, size_t nvec, unsigned ntile) {
+  const unsigned b = blockIdx.x, x = b % 8, k = b / 8, g = k % G;
+  const unsigned tile = (k / G) * 8 + x;
+  if (tile >= ntile) return;
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t wbase = (size_t)tile * (kBlock * U) + (size_t)w * 64 * U;
+  if (wbase >= nvec) return;
+  const size_t left = nvec - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int q) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[q] + wbase, bytes), off, 0, LAUX));
+    });
+  }
+  for (int j = (int)g; j < a.nout; j += G) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
@@ -864,6 +900,23 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 47: TPW(2, 1, 27); break;        // 1-wave workgroups, 5 per CU
     case 48: TPW(2, 1, 20); break;        // 1-wave workgroups, 8 per CU
 #undef TPW
+#define TPX(U, L, G)                                                                 \
+  do {                                                                               \
+    const unsigned nt = grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu);             \
+    hipLaunchKernelGGL((tp_xsplit<U, L, 17, G>), dim3((nt + 7) / 8 * 8 * G), dim3(kBlock), \
+                       0, s, a, nvec, nt);                                           \
+  } while (0)
+    case 49: TPX(4, 19, 2); break;        // outputs over 2 co-located workgroups
+    case 50: TPX(4, 19, 4); break;
+    case 51: TPX(2, 19, 2); break;
+    case 52: TPX(4, 17, 2); break;        // loads without the nt hint (L2 reuse)
+    case 53: TPX(4, 17, 4); break;
+    case 54: TPX(4, 0, 2); break;         // default-policy loads
+    case 55: TPX(4, 0, 4); break;
+    case 56: TPX(2, 17, 4); break;
+    case 57: TPX(4, 17, 8); break;
+    case 58: TPX(4, 19, 1); break;        // G = 1: the remap alone
+#undef TPX
     default: return -LFA_EINVAL;
   }
 #undef TP
