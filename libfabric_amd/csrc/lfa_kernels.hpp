@@ -1356,6 +1356,8 @@ static void launch_tree_lds(const TreeArgs &b, int nsrc, u32x4 *dst,
                      b, nsrc, dst, nvec);
 }
 
+constexpr unsigned kTreeCapLds = 41u << 10;
+
 template <int OP, typename T, int NLEAF, bool ALL = false>
 static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                              size_t nvec, hipStream_t s, int variant = -1) {
@@ -1363,6 +1365,16 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
   // below kSc1Bytes of output the U=2 chunk form with write-through stores
   // wins at every fan-in (2..16 inputs: 58.9/53.4/52.1/51.7 us against
   // 63.2/58.2/53.9/51.7 for the nt-store forms, 256 MiB of inputs).
+  //
+  // Round 5: at 3..8 inputs that form runs with 41 KiB of dynamic LDS the body
+  // never touches, so at most 3 workgroups (12 waves) share a CU: fewer input
+  // streams in flight per CU.  Interleaved A/B on two boxes, 256 MiB of inputs
+  // (bench.py --tune-tree variants -1 / 20, profiles/r05_tune_tree_occupancy_*.json):
+  // 4 inputs 55.44 -> 53.10 and 55.00 -> 53.52 us, 8 inputs 53.98 -> 52.84 and
+  // 53.84 -> 52.92 us; 2 inputs lose (58.8 -> 61.8) and 16 tie, so they keep
+  // the full occupancy.
+  const unsigned cap_lds =
+      (variant < 0 && nvec * 16 < kSc1Bytes && nsrc >= 3 && nsrc <= 8) ? kTreeCapLds : 0u;
   if (variant < 0 && nvec * 16 < kSc1Bytes) variant = 11;
   if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
   // nsrc lies in [NLEAF, 2·NLEAF): only these forms are reachable from the
@@ -1422,7 +1434,7 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
   // chunk form, correct at every size
   hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 2, kStoreSc1>),
                      dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)),
-                     dim3(kBlock), 0, s, b, dst, nvec);
+                     dim3(kBlock), cap_lds, s, b, dst, nvec);
 }
 
 // Leaf pairing of prov/coll's tree for nsrc ranks (see TreeArgs); returns
