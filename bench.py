@@ -1455,11 +1455,18 @@ def extra_collectives(rank, world, stream, emit=None):
                 ep.set_algo(coll.ALGO_AUTO)
                 ep.wait(ep.allreduce(a, b, 1024, 8, 2))
                 barrier(world)
+                words0 = ep.word_ops()
                 t0 = time.perf_counter()
                 for _ in range(200):
                     ep.wait(ep.allreduce(a, b, 1024, 8, 2))
                 t = max_over_ranks(time.perf_counter() - t0, world) / 200
                 out["allreduce_4kib_float_sum_auto_us"] = round(t * 1e6, 1)
+                # AUTO's small bucket is the P2P one-shot: on a device domain
+                # it must complete through the completion word, not an event
+                # (exec_plan used to drop the word's value)
+                missed = 200 - (ep.word_ops() - words0)
+                out["allreduce_4kib_auto_reaped_by_word"] = \
+                    max_over_ranks(float(missed), world) == 0.0
                 out["allreduce_4kib_auto_bitwise_equal_tree"] = \
                     max_over_ranks(0.0 if torch.equal(b, ref4k) else 1.0, world) == 0.0
                 out["auto_counters"] = ep.counters()

@@ -159,3 +159,4 @@ def test_direct_queue_reopens_after_failed_one_is_released(coll, monkeypatch):
         assert e.uses_direct() == 1
     finally:
         e.close()
+
