@@ -147,8 +147,15 @@ def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float) -> dict
     status = "ok"
     with tempfile.TemporaryFile("w+") as out:
         p = _CHILD = subprocess.Popen(cmd, env=env, stdout=out)
-        deadline = time.time() + budget_s
+        t_start = time.time()
+        deadline = t_start + budget_s
+        beat = t_start
         while True:
+            if rank == 0 and time.time() - beat > 20.0:
+                # a heartbeat on stderr: a runner that takes a silent job for
+                # a hung one sees the extras are still going
+                beat = time.time()
+                log(f"bench.py: provider extras running, {beat - t_start:.0f} s")
             rc = p.poll()
             if rc is not None:
                 if rc != 0:
@@ -1838,6 +1845,7 @@ def main() -> None:
         def show(o):
             if rank == 0:
                 print(json.dumps(o), flush=True)
+                log(f"bench.py: provider extras rows so far: {len(o)}")
         try:
             extra_collectives(rank, world, stream, show)
         except Exception as e:  # noqa: BLE001

@@ -30,6 +30,7 @@
 #   procs        8-process one-shot latency: parent with / without a GPU context,
 #                7 workers + GPU parent, 8 workers at 4 queues
 #   tplayout     8->8 tree_put per buffer set and per pool pitch
+#   rehearse2/4  the N > 1 bench flow at 2 / 4 ranks sharing the GPU
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
 #   solo         launch -> completion word of one small kernel, by part
 #   tunecomb     back-to-back combine forms at 32/64/256 MiB (COMBINE_VARIANTS)
@@ -133,6 +134,10 @@ for stage in "$@"; do
       # provider rows through a peer-transfer domain, with their oracle checks
       LFA_BENCH_REHEARSE=1 $S rehearse2 600 python3 -u bench.py --gpus 2 --steps 5 \
         --warmup 2 --no-cpu || exit 99 ;;
+    rehearse4)
+      # the same at 4 ranks sharing this GPU (one-shots and trees at n = 4)
+      LFA_BENCH_REHEARSE=1 $S rehearse4 900 python3 -u bench.py --gpus 4 --steps 5 \
+        --warmup 2 --no-cpu --extras-timeout 800 || exit 99 ;;
     treeputx)
       # the bench extra (fresh buffer sets rotated, median + range)
       $S treeput_extra 300 python3 -u bench.py --only-extra tree_put || exit 99 ;;
