@@ -1178,8 +1178,9 @@ def _rs_sweep(ep, rank, world, algo, egress_gbs=None):
                               "busbw_gbs": round((world - 1) / world * nbytes / t / 1e9, 2)}
         sweep[str(nbytes)].update(chk)
         if algo == coll.ALGO_AUTO:
-            # the per-bucket choice (lfa_coll_auto_algo; the same on every rank)
-            chosen = coll.auto_algo(5, cnt, world, 8)
+            # the per-bucket choice (lfa_coll_auto_algo; the same on every
+            # rank) — device domains only: a peer domain runs AUTO as TREE
+            chosen = coll.ALGO_TREE if REHEARSE else coll.auto_algo(5, cnt, world, 8)
             sweep[str(nbytes)]["algo"] = {coll.ALGO_P2P: "p2p_oneshot",
                                           coll.ALGO_TREE: "tree"}.get(chosen, str(chosen))
         if egress_gbs and world > 1:
@@ -1471,9 +1472,15 @@ def extra_collectives(rank, world, stream, emit=None):
                 # AUTO's small bucket is the P2P one-shot: on a device domain
                 # it must complete through the completion word, not an event
                 # (exec_plan used to drop the word's value)
-                missed = 200 - (ep.word_ops() - words0)
-                out["allreduce_4kib_auto_reaped_by_word"] = \
-                    max_over_ranks(float(missed), world) == 0.0
+                words = float(ep.word_ops() - words0)
+                lo, hi = -max_over_ranks(-words, world), max_over_ranks(words, world)
+                if REHEARSE:
+                    # a peer-transfer domain runs AUTO as TREE (lfa_coll.c
+                    # host_start): no one-shot, so no word to count
+                    out["allreduce_4kib_auto_reaped_by_word"] = "n/a (peer domain: AUTO runs TREE)"
+                else:
+                    out["allreduce_4kib_auto_reaped_by_word"] = lo == hi == 200.0
+                out["allreduce_4kib_auto_word_ops_min_max"] = [int(lo), int(hi)]
                 out["allreduce_4kib_auto_bitwise_equal_tree"] = \
                     max_over_ranks(0.0 if torch.equal(b, ref4k) else 1.0, world) == 0.0
                 out["auto_counters"] = ep.counters()
