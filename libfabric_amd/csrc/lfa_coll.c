@@ -2308,7 +2308,8 @@ static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_
 	int ret;
 
 	ep->op_done_w = NULL;
-	if (ep->allow_direct && direct_of(ep) && !lfa_direct_failed(ep->direct)) {
+	if (ep->allow_direct && count * lfa_datatype_size(dt) <= LFA_DIRECT_SOLO_BYTES &&
+	    direct_of(ep) && !lfa_direct_failed(ep->direct)) {
 		/* no HIP launch: ~3 us less host time */
 		ret = lfa_direct_solo_copy(ep->direct, result, buf, count * lfa_datatype_size(dt),
 					   ep->ddone_ctr, ep->ddone_word, ep->ddone_seq + 1);

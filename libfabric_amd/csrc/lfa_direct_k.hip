@@ -48,10 +48,13 @@ extern "C" __global__ __launch_bounds__(256) void LFA_DIRECT_NAME(
     return;
   }
   if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // lfa_signal.hip solo_copy's ordering: a workgroup whose stores were all
+    // write-through adds with no fence; byte-wise stores are released first
+    if (vhi != hi) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     const uint32_t seen =
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (seen + 1 == nblocks) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1644,3 +1644,130 @@ extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size
   hipStreamDestroy(s);
   return rc;
 }
+
+// ---------------------------------------------------------------------------
+// Round 5: the world-1 solo copy above one workgroup (4 KiB .. 1 MiB), launch
+// -> completion word, by how each workgroup orders its stores before the
+// counter.  The product (lfa_signal.hip solo_copy) gives every workgroup a
+// system-scope release (an L2 write-back) and an agent-scope acq_rel counter
+// add (another write-back and an invalidate), so 64 workgroups at 256 KiB
+// queue 64 of each in the XCDs' L2s.
+//   mode 0  lfa_solo_copy_async (the product, HIP launch)
+//   mode 1  lfa_direct_solo_copy (the product, liblfa's HSA queue)
+//   mode 2  solo_multi<0>: this file's copy of the product body (HIP launch)
+//   mode 3  solo_multi<1>: a workgroup whose stores were all write-through
+//           (sc0 sc1, acknowledged by its s_waitcnt) adds to the counter
+//           relaxed with no fence; the last one acquires, releases at system
+//           scope and stores the word (byte-wise tails keep the release)
+//   mode 4  solo_multi<2>: as 3, the last one without the acquire
+// ---------------------------------------------------------------------------
+namespace lfa {
+
+template <int MODE>
+__global__ __launch_bounds__(256) void solo_multi(char *dst, const char *src, size_t bytes,
+                                                  uint32_t *ctr, uint64_t *word, uint64_t val) {
+  const unsigned t = threadIdx.x;
+  const size_t lo = (size_t)blockIdx.x * 4096;
+  const size_t hi = lo + 4096 < bytes ? lo + 4096 : bytes;
+  const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const size_t vhi = vec ? lo + ((hi - lo) & ~(size_t)15) : lo;
+  if (lo + (size_t)t * 16 < vhi) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + lo, 0, 4096, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(src + lo + (size_t)t * 16), r,
+                                           t * 16, 0, kSysAux);
+  }
+  for (size_t o = vhi + t; o < hi; o += 256) dst[o] = src[o];
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t != 0) return;
+  if (gridDim.x == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  uint32_t seen;
+  if constexpr (MODE == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    seen = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (vhi != hi) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // plain-store tail
+    seen = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (seen + 1 == gridDim.x) {
+    if constexpr (MODE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace lfa
+
+extern "C" int lfa__tune_solo_multi(int mode, void *dst, const void *src, size_t bytes,
+                                    int reps, double *us) {
+  using namespace lfa;
+  hipStream_t s;
+  uint32_t *ctr = nullptr;
+  uint64_t *word = nullptr;
+  if (!bytes || bytes > ((size_t)1 << 20) || reps <= 0 || !us || mode < 0 || mode > 4)
+    return -LFA_EINVAL;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -LFA_EIO;
+  if (hipMalloc((void **)&ctr, 4) != hipSuccess ||
+      hipHostMalloc((void **)&word, 8, hipHostMallocCoherent) != hipSuccess ||
+      hipMemset(ctr, 0, 4) != hipSuccess) {
+    hipStreamDestroy(s);
+    return -LFA_EIO;
+  }
+  *(volatile uint64_t *)word = 0;
+  struct lfa_direct *direct = nullptr;
+  if (mode == 1) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    direct = lfa_direct_open(dev);
+    if (!direct) {
+      hipFree(ctr);
+      hipHostFree(word);
+      hipStreamDestroy(s);
+      return -LFA_ENOSYS;
+    }
+  }
+  const unsigned grid = (unsigned)((bytes + 4095) / 4096);
+  int rc = 0;
+  double t0 = 0;
+  for (int i = -50; i < reps && !rc; i++) {
+    if (i == 0) {
+      struct timespec ts;
+      clock_gettime(CLOCK_MONOTONIC, &ts);
+      t0 = ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+    }
+    const uint64_t val = (uint64_t)(i + 51);
+    switch (mode) {
+      case 0: rc = lfa_solo_copy_async(dst, src, bytes, ctr, word, val, s); break;
+      case 1: rc = lfa_direct_solo_copy(direct, dst, src, bytes, ctr, word, val); break;
+#define SM(M)                                                                          \
+  hipLaunchKernelGGL((solo_multi<M>), dim3(grid), dim3(256), 0, s, (char *)dst,         \
+                     (const char *)src, bytes, ctr, word, val);                          \
+  rc = hipGetLastError() == hipSuccess ? 0 : -LFA_EIO
+      case 2: SM(0); break;
+      case 3: SM(1); break;
+      case 4: SM(2); break;
+#undef SM
+    }
+    struct timespec w0, w1;
+    clock_gettime(CLOCK_MONOTONIC, &w0);
+    while (!rc && *(volatile uint64_t *)word < val) {
+      clock_gettime(CLOCK_MONOTONIC, &w1);
+      if (w1.tv_sec - w0.tv_sec > 2) rc = -ETIMEDOUT;
+    }
+  }
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  *us = (ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3 - t0) / reps;
+  hipStreamSynchronize(s);
+  if (direct) lfa_direct_close(direct);
+  hipFree(ctr);
+  hipHostFree(word);
+  hipStreamDestroy(s);
+  return rc;
+}
