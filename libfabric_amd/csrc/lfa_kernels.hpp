@@ -832,9 +832,11 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
   // 4. reduce chunk b of this rank's own range over every rank's input, rank
   //    order (system-scope loads: the slots were written by peers over xGMI)
   const size_t own = a.slen[a.rank];
+  bool plain = false;  // this workgroup wrote result bytes with plain stores
   if (lo < own) {
     const size_t hi = lo + a.chunk < own ? lo + a.chunk : own;
     const size_t vhi = a.vec ? hi & ~(size_t)15 : lo;
+    plain = a.unal || vhi < hi;
     for (size_t o = lo + (size_t)t * 16; o < vhi; o += (size_t)kBlock * 16) {
       u32x4 v = tree_eval_with<OP, T, u32x4, NLEAF>(a.t, [&](int k) {
         return __builtin_bit_cast(
@@ -862,10 +864,15 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
       }
     }
   }
-  // 5. completion word: this workgroup's result stores acknowledged, then
-  //    one system-scope release (its waves share a CU and an L2) before it
+  // 5. completion word: this workgroup's result stores acknowledged, then it
   //    counts itself; the last workgroup resets the counter for the next
-  //    launch on the stream and publishes done_val to the host
+  //    launch on the stream and publishes done_val to the host.  Write-
+  //    through stores are in memory once acknowledged, so a workgroup that
+  //    made only those adds relaxed with no release of its own (an L2
+  //    write-back saved per workgroup, as in lfa_signal.hip solo_copy); one
+  //    with plain (byte-wise or tail) stores releases them first at system
+  //    scope (its waves share a CU and an L2).  The last one acquires the
+  //    others' adds, then releases before the word.
   if (a.done_word) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -874,10 +881,11 @@ __global__ __launch_bounds__(kBlock) void oneshot_reduce(OsArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL,
+      if (plain) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      const uint32_t seen = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       if (seen + 1 == gridDim.x) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __hip_atomic_store(a.done_word, a.done_val, __ATOMIC_RELAXED,

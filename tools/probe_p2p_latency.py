@@ -44,7 +44,7 @@ def _kfd_queues(pid=None):
         return None
 
 
-def _worker(rank, world, port, reps, quick, q):
+def _worker(rank, world, port, reps, quick, q, only=None):
     try:
         import torch
         import torch.distributed as dist
@@ -63,6 +63,11 @@ def _worker(rank, world, port, reps, quick, q):
                     ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10)))
             if quick:
                 plan = (("p2p", coll.ALGO_P2P, (4096,), reps),)
+            if only:
+                # --only name:size[,size...]
+                name, sizes = only.split(":")
+                plan = tuple((nm, al, tuple(int(x) for x in sizes.split(",")), reps)
+                             for nm, al, _s, _n in plan if nm == name)
             for name, algo, sizes, n in plan:
                 ep.set_algo(algo)
                 for nbytes in sizes:
@@ -119,6 +124,7 @@ def main():
     ap.add_argument("--reps", type=int, default=300)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--parent-gpu", action="store_true")
+    ap.add_argument("--only", default="", help="one row kind and its sizes, e.g. p2p:1048576")
     ap.add_argument("--worker-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES of the workers only (0: inherit); "
                          "the parent keeps the environment's")
@@ -139,7 +145,8 @@ def main():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.reps, a.quick, q))
+    procs = [ctx.Process(target=_worker, args=(r, a.world, port, a.reps, a.quick, q,
+                                                    a.only or None))
              for r in range(a.world)]
     for p in procs:
         p.start()
