@@ -75,7 +75,8 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     sig = os.path.join(CSRC, "lfa_signal.hip")
     o = os.path.join(BUILD, "lfa_signal.o")
     objs.append(o)
-    if _newer(o, [sig, os.path.join(CSRC, "lfa_signal.h"), os.path.join(INC, "lfa_fabric.h")]):
+    if _newer(o, [sig, os.path.join(CSRC, "lfa_signal.h"), os.path.join(CSRC, "lfa_solo_body.hpp"),
+                  os.path.join(INC, "lfa_fabric.h")]):
         steps.append([HIPCC, *HIP_FLAGS, "-c", sig, "-o", o])
     # the direct-dispatch code object: a plain gfx950 ELF of lfa_direct_k.hip,
     # embedded as bytes (lfa_direct.cpp loads it into its own HSA executable)
@@ -83,7 +84,7 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     co_c = os.path.join(BUILD, "lfa_direct_co.c")
     co_o = os.path.join(BUILD, "lfa_direct_co.o")
     objs.append(co_o)
-    if _newer(co_o, [dk]):
+    if _newer(co_o, [dk, os.path.join(CSRC, "lfa_solo_body.hpp")]):
         # two code objects: the kernel as is, and with its arguments preloaded
         # into SGPRs by the packet processor (lfa_direct_k.hip)
         with open(co_c, "w") as f:

@@ -15,14 +15,15 @@
 #define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
 /* a one-member group's reducing collective of at most this many bytes runs
  * as one copy kernel ending in the completion word (run_solo): 1 MiB in
- * 10.4 us from launch to the word against 12.1 us for the TREE plan's copy
+ * 8.4 us from launch to the word against 12.1 us for the TREE plan's copy
  * and event (round 5, tools/probe_solo_multi.py) */
 #define LFA_ONESHOT_SOLO_BYTES (1u << 20)
-/* ... and through liblfa's own HSA queue up to this many (4 workgroups):
- * its kernel arguments sit in host memory and every workgroup fetches them
- * over PCIe, so past a few workgroups the HIP launch (device-memory
- * arguments) wins — 256 KiB 14.6 vs 9.6 us, 1 MiB 34.1 vs 13.7 us */
-#define LFA_DIRECT_SOLO_BYTES (16u << 10)
+/* ... and through liblfa's own HSA queue up to this many (4 workgroups of
+ * 16 KiB): its kernel arguments sit in host memory and every workgroup
+ * fetches them over PCIe, so past a few workgroups the HIP launch
+ * (device-memory arguments) wins — 64 KiB 6.4 vs 7.6 us, 256 KiB 8.8 vs
+ * 8.3 us, 1 MiB 15.4 vs 8.4 us (round 5, tools/probe_solo_multi.py) */
+#define LFA_DIRECT_SOLO_BYTES (64u << 10)
 #define LFA_OS_RS_BYTES (1u << 20)      /* P2P reduce_scatter: one-shot */
 
 /* A heap-allocated plan. */

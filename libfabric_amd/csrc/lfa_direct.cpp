@@ -334,7 +334,7 @@ extern "C" int lfa_direct_solo_copy(struct lfa_direct *d, void *result, const vo
   if (!d || !result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
     return -LFA_EINVAL;
   if (__atomic_load_n(&d->failed, __ATOMIC_ACQUIRE)) return -LFA_EIO;
-  const uint32_t nblocks = (uint32_t)((bytes + 4095) / 4096);
+  const uint32_t nblocks = lfa_solo_blocks(result, send, bytes);
   pthread_mutex_lock(&d->lock);
   const uint64_t idx = d->stub ? d->stub_write : hsa_queue_load_write_index_relaxed(d->q);
   const int rc = ring_wait(d, idx);

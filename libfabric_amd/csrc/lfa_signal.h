@@ -145,6 +145,15 @@ int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 int lfa_solo_copy_async(void *result, const void *send, size_t bytes, uint32_t *done_ctr,
 			uint64_t *done_word, uint64_t done_val, void *stream);
 
+/* The solo copy's workgroup count (lfa_solo_body.hpp): 16 KiB per workgroup
+ * when both pointers are 16-B aligned, 4 KiB otherwise. */
+static inline uint32_t lfa_solo_blocks(const void *result, const void *send, size_t bytes)
+{
+	const size_t tile = (((uintptr_t)result | (uintptr_t)send) & 15) ? 4096 : 16384;
+
+	return (uint32_t)((bytes + tile - 1) / tile);
+}
+
 #ifdef __HIPCC__
 /* A wait of operation `ticket` gave up: lower the group's status word to it
  * (plain system-scope load and store: the group's kernels are stream-ordered,

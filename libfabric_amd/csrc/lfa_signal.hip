@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include "lfa_solo_body.hpp"
 #include "lfa_signal.h"
 #include "../../include/lfa_fabric.h"
 
@@ -47,52 +48,12 @@ __global__ __launch_bounds__(64) void flag_barrier(BarArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
-// One-member copy ending in the completion word (lfa_solo_copy_async).
-// Workgroup b copies bytes [b·4 KiB, (b+1)·4 KiB): 16 B per lane when both
-// pointers are 16-B aligned, byte-wise otherwise and for the tail.
+// One-member copy ending in the completion word (lfa_solo_copy_async):
+// lfa_solo_body.hpp, shared with the direct-dispatch kernel.
 __global__ __launch_bounds__(256) void solo_copy(char *dst, const char *src, size_t bytes,
-                                                 uint32_t *ctr, uint64_t *word,
-                                                 uint64_t val) {
-  const unsigned t = threadIdx.x;
-  const size_t lo = (size_t)blockIdx.x * 4096;
-  const size_t hi = lo + 4096 < bytes ? lo + 4096 : bytes;
-  const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
-  const size_t vhi = vec ? lo + ((hi - lo) & ~(size_t)15) : lo;
-  if (lo + (size_t)t * 16 < vhi) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    // write-through (sc0 sc1): the release below has no dirty lines to write
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(dst + lo, 0, 4096, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4 *)(src + lo + (size_t)t * 16), r,
-                                           t * 16, 0, 17);
-  }
-  for (size_t o = vhi + t; o < hi; o += 256) dst[o] = src[o];
-  // the completion word: this workgroup's stores acknowledged, then the
-  // last workgroup publishes `val` (lfa_signal.h); a single workgroup
-  // publishes it without the counter.  Write-through stores are in memory
-  // once acknowledged (the s_waitcnt), so such a workgroup adds to the
-  // counter with no fence of its own; one with byte-wise (plain) stores
-  // releases them at system scope first.  The last one acquires the others'
-  // adds and releases before the word.  A release per workgroup (an L2
-  // write-back each, and one more in an acq_rel add) cost 3.3 us at 1 MiB
-  // (256 workgroups: 13.7 -> 10.4 us launch to word, round 5,
-  // tools/probe_solo_multi.py).
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (t == 0 && gridDim.x == 1) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else if (t == 0) {
-    if (vhi != hi) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    const uint32_t seen =
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (seen + 1 == gridDim.x) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+                                                 uint32_t nblocks, uint32_t *ctr,
+                                                 uint64_t *word, uint64_t val) {
+  lfa_solo_body(dst, src, bytes, nblocks, ctr, word, val);
 }
 
 }  // namespace
@@ -103,9 +64,9 @@ extern "C" int lfa_solo_copy_async(void *result, const void *send, size_t bytes,
   if (!bytes) return 0;
   if (!result || !send || !done_ctr || !done_word || bytes > ((size_t)1 << 30))
     return -LFA_EINVAL;
-  const unsigned grid = (unsigned)((bytes + 4095) / 4096);
+  const unsigned grid = lfa_solo_blocks(result, send, bytes);
   hipLaunchKernelGGL(solo_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)result,
-                     (const char *)send, bytes, done_ctr, done_word, done_val);
+                     (const char *)send, bytes, grid, done_ctr, done_word, done_val);
   return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
 }
 

@@ -1660,6 +1660,8 @@ extern "C" int lfa__tune_solo_latency(int mode, void *dst, const void *src, size
 //           relaxed with no fence; the last one acquires, releases at system
 //           scope and stores the word (byte-wise tails keep the release)
 //   mode 4  solo_multi<2>: as 3, the last one without the acquire
+//   mode 5..7  solo_tile<2 / 4 / 8>: 8 / 16 / 32 KiB per workgroup, mode 3's
+//           counter (16-B aligned operands only)
 // ---------------------------------------------------------------------------
 namespace lfa {
 
@@ -1702,6 +1704,47 @@ __global__ __launch_bounds__(256) void solo_multi(char *dst, const char *src, si
   }
 }
 
+// Larger workgroup tiles: K·4 KiB per workgroup, every load of the tile
+// issued before its stores (K 16-B loads in flight per lane), then mode 3's
+// counter.  Fewer workgroups, fewer counter adds, one deeper round trip.
+template <int K>
+__global__ __launch_bounds__(256) void solo_tile(char *dst, const char *src, size_t bytes,
+                                                 uint32_t *ctr, uint64_t *word, uint64_t val) {
+  const unsigned t = threadIdx.x;
+  const size_t lo = (size_t)blockIdx.x * (4096 * K);
+  const size_t hi = lo + 4096 * K < bytes ? lo + 4096 * K : bytes;
+  const size_t vhi = lo + ((hi - lo) & ~(size_t)15);   // both pointers 16-B aligned here
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char *>(src) + lo, 0, (int)(vhi - lo), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc(dst + lo, 0, (int)(vhi - lo), 0x00020000);
+  u32x4 v[K];
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, (unsigned)(k * 4096 + t * 16), 0, 0));
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, (unsigned)(k * 4096 + t * 16), 0, kSysAux);
+  for (size_t o = vhi + t; o < hi; o += 256) dst[o] = src[o];
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t != 0) return;
+  if (gridDim.x == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  if (vhi != hi) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  const uint32_t seen = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (seen + 1 == gridDim.x) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune_solo_multi(int mode, void *dst, const void *src, size_t bytes,
@@ -1710,8 +1753,9 @@ extern "C" int lfa__tune_solo_multi(int mode, void *dst, const void *src, size_t
   hipStream_t s;
   uint32_t *ctr = nullptr;
   uint64_t *word = nullptr;
-  if (!bytes || bytes > ((size_t)1 << 20) || reps <= 0 || !us || mode < 0 || mode > 4)
+  if (!bytes || bytes > ((size_t)1 << 20) || reps <= 0 || !us || mode < 0 || mode > 7)
     return -LFA_EINVAL;
+  if (mode >= 5 && (((uintptr_t)dst | (uintptr_t)src) & 15)) return -LFA_EINVAL;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -LFA_EIO;
   if (hipMalloc((void **)&ctr, 4) != hipSuccess ||
       hipHostMalloc((void **)&word, 8, hipHostMallocCoherent) != hipSuccess ||
@@ -1753,6 +1797,14 @@ extern "C" int lfa__tune_solo_multi(int mode, void *dst, const void *src, size_t
       case 3: SM(1); break;
       case 4: SM(2); break;
 #undef SM
+#define ST(K)                                                                          \
+  hipLaunchKernelGGL((solo_tile<K>), dim3((unsigned)((bytes + 4096 * K - 1) / (4096 * K))), \
+                     dim3(256), 0, s, (char *)dst, (const char *)src, bytes, ctr, word, val); \
+  rc = hipGetLastError() == hipSuccess ? 0 : -LFA_EIO
+      case 5: ST(2); break;
+      case 6: ST(4); break;
+      case 7: ST(8); break;
+#undef ST
     }
     struct timespec w0, w1;
     clock_gettime(CLOCK_MONOTONIC, &w0);

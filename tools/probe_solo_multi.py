@@ -23,7 +23,8 @@ def main() -> None:
     L.lfa__tune_solo_multi.restype = ctypes.c_int
     torch.cuda.set_device(0)
     names = {0: "product_hip", 1: "product_direct", 2: "replica_hip",
-             3: "relaxed_counter_acquire_last", 4: "relaxed_counter"}
+             3: "relaxed_counter_acquire_last", 4: "relaxed_counter",
+             5: "tile_8k", 6: "tile_16k", 7: "tile_32k"}
     out = {}
     for nbytes in (4096, 16384, 65536, 262144, 1 << 20):
         src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
