@@ -1658,6 +1658,19 @@ static inline bool ll_enabled() {
   return on;
 }
 
+// The one-shot's smallest per-workgroup chunk (bytes, a multiple of 16):
+// LFA_OS_MIN_CHUNK, the same on every member of a group (the grid and the
+// flag columns follow it); 4096 by default.  A tuning knob.
+static inline size_t os_min_chunk() {
+  static long c = -1;
+  if (c < 0) {
+    const char *e = getenv("LFA_OS_MIN_CHUNK");
+    const long v = e ? atol(e) : 0;
+    c = v >= 16 && v <= (1l << 20) ? (v + 15) & ~15l : 4096;
+  }
+  return (size_t)c;
+}
+
 template <int OP, typename T>
 static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
   if constexpr (!supported<OP, T>()) {
@@ -1768,7 +1781,7 @@ static int launch_oneshot(const lfa_oneshot &h, hipStream_t s) {
     a.timeout = h.timeout_us * lfa__wallclock_ticks_per_us();
     size_t chunk = (most + LFA_SIG_OS_CHUNKS - 1) / LFA_SIG_OS_CHUNKS;
     chunk = (chunk + 15) & ~(size_t)15;
-    a.chunk = chunk < 4096 ? 4096 : chunk;
+    a.chunk = chunk < os_min_chunk() ? os_min_chunk() : chunk;
     a.epoch = h.epoch;
     a.ticket = h.ticket;
     a.n = n;
