@@ -2190,7 +2190,7 @@ int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
 	case LFA_ALLREDUCE:
 	case LFA_REDUCE:
 		/* the planner's one-shot rule (plan_p2p): one kernel */
-		return bytes * (size_t)nranks <= LFA_SMALL_AG_BYTES ? LFA_ALGO_P2P :
+		return bytes * (size_t)nranks <= lfa_os_ag_bytes() ? LFA_ALGO_P2P :
 								     LFA_ALGO_TREE;
 	case LFA_REDUCE_SCATTER:
 		return bytes <= LFA_OS_RS_BYTES ? LFA_ALGO_P2P : LFA_ALGO_TREE;

@@ -497,6 +497,19 @@ static void p2p_unstage_output(struct planner *p, int r, size_t count, size_t es
 	p_copy(p, ref(LFA_BUF_RESULT, 0), sref(LFA_BUF_SYM_OUT, r, 0), count * esz);
 }
 
+size_t lfa_os_ag_bytes(void)
+{
+	static long long v = -1;
+
+	if (v < 0) {
+		const char *e = getenv("LFA_OS_AG_BYTES");
+		const long long x = e ? atoll(e) : 0;
+
+		v = x > 0 && x <= (1ll << 30) ? x : (long long)LFA_OS_AG_BYTES_DEFAULT;
+	}
+	return (size_t)v;
+}
+
 static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 		    int n, int root, size_t count, size_t esz)
 {
@@ -506,7 +519,7 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 	lfa_coll_block(count, n, r, &moff, &mlen);
 	switch (coll) {
 	case LFA_ALLREDUCE:
-		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES && n <= LFA_OS_MAX_RANKS) {
+		if (bytes * (size_t)n <= lfa_os_ag_bytes() && n <= LFA_OS_MAX_RANKS) {
 			/* one kernel: push into the peers' slots, flags, tree */
 			p_oneshot(p, LFA_ONESHOT_ALL, n, count);
 			return 0;
@@ -541,7 +554,7 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 		p_barrier(p);
 		return 0;
 	case LFA_REDUCE:
-		if (bytes * (size_t)n <= LFA_SMALL_AG_BYTES && n <= LFA_OS_MAX_RANKS) {
+		if (bytes * (size_t)n <= lfa_os_ag_bytes() && n <= LFA_OS_MAX_RANKS) {
 			p_oneshot(p, root, n, count);
 			return 0;
 		}

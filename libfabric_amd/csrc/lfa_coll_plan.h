@@ -25,6 +25,16 @@
  * 8.3 us, 1 MiB 15.4 vs 8.4 us (round 5, tools/probe_solo_multi.py) */
 #define LFA_DIRECT_SOLO_BYTES (64u << 10)
 #define LFA_OS_RS_BYTES (1u << 20)      /* P2P reduce_scatter: one-shot */
+/* P2P allreduce / reduce: one kernel (the one-shot) while count·esz·n is at
+ * most this — LFA_OS_AG_BYTES_DEFAULT unless LFA_OS_AG_BYTES (the same on
+ * every member) says otherwise.  The one-shot pushes the whole input to every
+ * peer, so each xGMI link carries count·esz (the staged schedule: a quarter
+ * of that, in five kernels); at 2 MiB over all members a link carries at
+ * most 1 MiB at 2 members and 256 KiB at 8.  On one MI355X shared by 2 / 4
+ * processes the one-shot took 16.9 / 29.3 us at 1 MiB per member against
+ * 30.4 / 35.2 us staged (round 5); 256 KiB before round 5. */
+#define LFA_OS_AG_BYTES_DEFAULT (2u << 20)
+LFA_INTERNAL size_t lfa_os_ag_bytes(void);
 
 /* A heap-allocated plan. */
 struct plan {

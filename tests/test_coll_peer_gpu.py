@@ -630,11 +630,13 @@ def _chunk_error_worker(rank, world, port, q):
         try:
             ep.set_algo(coll.ALGO_P2P)
             # members disagree on the group chunk (a caller error): rank 0
-            # splits 4 MiB into 4 chunks, rank 1 into 2, so rank 0's third
+            # splits 8 MiB into 4 chunks, rank 1 into 2, so rank 0's third
             # chunk waits for a peer that never arrives and fails — a middle
-            # chunk — and its fourth fails behind it
-            ep.set_group_chunk((1 << 20) * (rank + 1))
-            n = 1 << 20
+            # chunk — and its fourth fails behind it.  Chunks of 2 and 4 MiB
+            # both take the staged P2P schedule (above the one-shot's 2 MiB
+            # over the members), whose barriers pair whatever the sizes
+            ep.set_group_chunk((2 << 20) * (rank + 1))
+            n = 2 << 20
             xs = torch.ones(n, dtype=torch.float32, device="cuda")
             rs = torch.zeros(n, dtype=torch.float32, device="cuda")
             _ready()
@@ -909,7 +911,7 @@ def _oneshot_stream_worker(rank, world, port, q, seed=77, nops=48):
                 # the planner's one-shot rule (lfa_coll_plan.c plan_p2p)
                 nb = count * oracle.datatype_size(dt)
                 is_os = (nb <= (1 << 20) if kind == "reduce_scatter"
-                         else nb * world <= (256 << 10))
+                         else nb * world <= (2 << 20))     # LFA_OS_AG_BYTES_DEFAULT
                 meta.append((dt, op, count, n_os if is_os else None))
                 n_os += is_os
             done = []

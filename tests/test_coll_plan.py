@@ -12,6 +12,10 @@ import oracle
 from libfabric_amd import coll
 from tests import _plansim
 
+# P2P allreduce / reduce one-shot bound over all members (lfa_coll_plan.h
+# LFA_OS_AG_BYTES_DEFAULT; 256 KiB before round 5)
+OS_AG_BYTES = 2 << 20
+
 ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BROADCAST, SCATTER = 3, 5, 6, 4, 1, 7
 F32, I64, U8, F64 = 8, 6, 1, 9
 SUM, MIN, BOR, BAND, PROD = 2, 0, 6, 7, 3
@@ -164,10 +168,10 @@ def test_p2p_small_allreduce_is_one_phase():
     s = p.steps[0]
     assert s["count"] == count and s["nsrc"] == n
     assert s["src"] == (coll.BUF_SEND, 0) and s["dst"] == (coll.BUF_RESULT, 0)
-    # the largest bucket that still fits 256 KiB over all members
-    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, (256 << 10) // 32, 4)
+    # the largest bucket that still fits OS_AG_BYTES (2 MiB) over all members
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, OS_AG_BYTES // 32, 4)
     assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT]
-    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, (256 << 10) // 32 + 1, 4)
+    p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, OS_AG_BYTES // 32 + 1, 4)
     assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
     # reduce_scatter up to 1 MiB, reduce up to 256 KiB over all members:
     # one step too, `peer` naming what this rank keeps
@@ -499,11 +503,11 @@ def test_auto_algo_same_choice_on_every_member(n):
     every member's P2P schedule is ONE one-shot step.  Above the thresholds,
     outside 2..8 members, or once the P2P agreement failed: the tree."""
     for kind, esz in ((ALLREDUCE, 4), (REDUCE, 8), (REDUCE_SCATTER, 8), (ALLGATHER, 4)):
-        for count in (1, 1000, (256 << 10) // (4 * max(n, 1)), (256 << 10) // (4 * max(n, 1)) + 1,
+        for count in (1, 1000, OS_AG_BYTES // (4 * max(n, 1)), OS_AG_BYTES // (4 * max(n, 1)) + 1,
                       (1 << 20) // 8, (1 << 20) // 8 + 1, 1 << 24):
             a = coll.auto_algo(kind, count, n, esz)
             nb = count * esz
-            small = (nb * n <= 256 << 10 if kind in (ALLREDUCE, REDUCE) else
+            small = (nb * n <= OS_AG_BYTES if kind in (ALLREDUCE, REDUCE) else
                      nb <= 1 << 20 if kind == REDUCE_SCATTER else False)
             want = coll.ALGO_P2P if (2 <= n <= 8 and small) else coll.ALGO_TREE
             assert a == want, (kind, count, n, esz)
