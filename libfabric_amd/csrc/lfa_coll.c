@@ -2193,7 +2193,7 @@ int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
 		return bytes * (size_t)nranks <= lfa_os_ag_bytes() ? LFA_ALGO_P2P :
 								     LFA_ALGO_TREE;
 	case LFA_REDUCE_SCATTER:
-		return bytes <= LFA_OS_RS_BYTES ? LFA_ALGO_P2P : LFA_ALGO_TREE;
+		return bytes <= lfa_os_rs_bytes() ? LFA_ALGO_P2P : LFA_ALGO_TREE;
 	default:
 		return LFA_ALGO_TREE;
 	}

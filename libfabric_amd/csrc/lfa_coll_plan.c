@@ -510,6 +510,19 @@ size_t lfa_os_ag_bytes(void)
 	return (size_t)v;
 }
 
+size_t lfa_os_rs_bytes(void)
+{
+	static long long v = -1;
+
+	if (v < 0) {
+		const char *e = getenv("LFA_OS_RS_BYTES");
+		const long long x = e ? atoll(e) : 0;
+
+		v = x > 0 && x <= (1ll << 30) ? x : (long long)LFA_OS_RS_BYTES;
+	}
+	return (size_t)v;
+}
+
 static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 		    int n, int root, size_t count, size_t esz)
 {
@@ -545,7 +558,7 @@ static int plan_p2p(struct planner *p, enum lfa_collective_op coll, int r,
 		p2p_unstage_output(p, r, count, esz);
 		return 0;
 	case LFA_REDUCE_SCATTER:
-		if (bytes <= LFA_OS_RS_BYTES && n <= LFA_OS_MAX_RANKS) {
+		if (bytes <= lfa_os_rs_bytes() && n <= LFA_OS_MAX_RANKS) {
 			p_oneshot(p, LFA_ONESHOT_SCATTER, n, count);
 			return 0;
 		}

@@ -24,7 +24,16 @@
  * (device-memory arguments) wins — 64 KiB 6.4 vs 7.6 us, 256 KiB 8.8 vs
  * 8.3 us, 1 MiB 15.4 vs 8.4 us (round 5, tools/probe_solo_multi.py) */
 #define LFA_DIRECT_SOLO_BYTES (64u << 10)
-#define LFA_OS_RS_BYTES (1u << 20)      /* P2P reduce_scatter: one-shot */
+/* P2P reduce_scatter: one-shot up to this many input bytes per member (each
+ * member pushes block k to member k: the staged schedule's bytes per link,
+ * in one kernel instead of four), unless LFA_OS_RS_BYTES in the environment
+ * (the same on every member) says otherwise.  Double PROD across 2 / 4
+ * processes on one MI355X: 2 MiB 26.9 -> 16.6 / 30.8 -> 24.3 us, 4 MiB
+ * 28.2 -> 18.4 / 34.8 -> 28.6 us; from 8 MiB the staged schedule's
+ * full-GPU kernels come within 1-3 us (round 5).  1 MiB before
+ * round 5. */
+#define LFA_OS_RS_BYTES (4u << 20)
+LFA_INTERNAL size_t lfa_os_rs_bytes(void);
 /* P2P allreduce / reduce: one kernel (the one-shot) while count·esz·n is at
  * most this — LFA_OS_AG_BYTES_DEFAULT unless LFA_OS_AG_BYTES (the same on
  * every member) says otherwise.  The one-shot pushes the whole input to every

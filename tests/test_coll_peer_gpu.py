@@ -910,7 +910,7 @@ def _oneshot_stream_worker(rank, world, port, q, seed=77, nops=48):
                 ops.append((kind, r, exp, xs))
                 # the planner's one-shot rule (lfa_coll_plan.c plan_p2p)
                 nb = count * oracle.datatype_size(dt)
-                is_os = (nb <= (1 << 20) if kind == "reduce_scatter"
+                is_os = (nb <= (4 << 20) if kind == "reduce_scatter"   # LFA_OS_RS_BYTES
                          else nb * world <= (2 << 20))     # LFA_OS_AG_BYTES_DEFAULT
                 meta.append((dt, op, count, n_os if is_os else None))
                 n_os += is_os

@@ -12,9 +12,11 @@ import oracle
 from libfabric_amd import coll
 from tests import _plansim
 
-# P2P allreduce / reduce one-shot bound over all members (lfa_coll_plan.h
-# LFA_OS_AG_BYTES_DEFAULT; 256 KiB before round 5)
+# P2P one-shot bounds (lfa_coll_plan.h): allreduce / reduce over all members
+# (LFA_OS_AG_BYTES_DEFAULT; 256 KiB before round 5), reduce_scatter input per
+# member (LFA_OS_RS_BYTES; 1 MiB before round 5)
 OS_AG_BYTES = 2 << 20
+OS_RS_BYTES = 4 << 20
 
 ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BROADCAST, SCATTER = 3, 5, 6, 4, 1, 7
 F32, I64, U8, F64 = 8, 6, 1, 9
@@ -173,11 +175,11 @@ def test_p2p_small_allreduce_is_one_phase():
     assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT]
     p = coll.plan(ALLREDUCE, coll.ALGO_P2P, 0, 8, -1, OS_AG_BYTES // 32 + 1, 4)
     assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
-    # reduce_scatter up to 1 MiB, reduce up to 256 KiB over all members:
+    # reduce_scatter up to OS_RS_BYTES, reduce up to OS_AG_BYTES over all members:
     # one step too, `peer` naming what this rank keeps
-    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, (1 << 20) // 8, 8)
+    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, OS_RS_BYTES // 8, 8)
     assert [(s["type"], s["peer"]) for s in p.steps] == [(coll.STEP_ONESHOT, -2)]
-    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, (1 << 20) // 8 + 1, 8)
+    p = coll.plan(REDUCE_SCATTER, coll.ALGO_P2P, 2, 8, -1, OS_RS_BYTES // 8 + 1, 8)
     assert coll.STEP_ONESHOT not in [s["type"] for s in p.steps]
     p = coll.plan(REDUCE, coll.ALGO_P2P, 2, 4, 3, 1000, 8)       # root 3
     assert [(s["type"], s["peer"]) for s in p.steps] == [(coll.STEP_ONESHOT, 3)]
@@ -504,11 +506,11 @@ def test_auto_algo_same_choice_on_every_member(n):
     outside 2..8 members, or once the P2P agreement failed: the tree."""
     for kind, esz in ((ALLREDUCE, 4), (REDUCE, 8), (REDUCE_SCATTER, 8), (ALLGATHER, 4)):
         for count in (1, 1000, OS_AG_BYTES // (4 * max(n, 1)), OS_AG_BYTES // (4 * max(n, 1)) + 1,
-                      (1 << 20) // 8, (1 << 20) // 8 + 1, 1 << 24):
+                      OS_RS_BYTES // 8, OS_RS_BYTES // 8 + 1, 1 << 24):
             a = coll.auto_algo(kind, count, n, esz)
             nb = count * esz
             small = (nb * n <= OS_AG_BYTES if kind in (ALLREDUCE, REDUCE) else
-                     nb <= 1 << 20 if kind == REDUCE_SCATTER else False)
+                     nb <= OS_RS_BYTES if kind == REDUCE_SCATTER else False)
             want = coll.ALGO_P2P if (2 <= n <= 8 and small) else coll.ALGO_TREE
             assert a == want, (kind, count, n, esz)
             assert coll.auto_algo(kind, count, n, esz, p2p_ok=False) == coll.ALGO_TREE
