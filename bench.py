@@ -669,6 +669,35 @@ def extra_sizes(dev, stream, reps: int = 100, prewarm_s: float = 0.1):
     return out
 
 
+def extra_config1_two_process(timeout_s: float = 120.0) -> dict:
+    """BASELINE configs[0]'s shape on the GPU path between PROCESSES: a 2-rank
+    float FI_SUM allreduce of 4 KiB, two worker processes sharing this GPU
+    through GPU peer domains, LFA_ALGO_P2P's one-shot kernel ending in the
+    completion word (tools/probe_p2p_latency.py --quick, its own processes;
+    this one only waits).  Median / p10 / p90 over Python-timed operations,
+    the mean of a C loop (lfa_bench_loop), and the result checked on both
+    ranks against x1 + x0 (prov/coll's two-rank tree, coll_coll.c:409-430)."""
+    import subprocess
+    try:
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "probe_p2p_latency.py"),
+                            "--quick", "--reps", "1000"], capture_output=True, text=True,
+                           timeout=timeout_s)
+        lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        if p.returncode or not lines:
+            return {"error": f"probe exited {p.returncode}: {p.stderr[-200:]}"}
+        d = json.loads(lines[-1])
+        r = (d.get("rank0") or {}).get("p2p_4096", {})
+        return {"us_median": r.get("median_us"), "us_p10": r.get("p10_us"),
+                "us_p90": r.get("p90_us"), "n": r.get("reps"),
+                "c_loop_mean_us": r.get("c_loop_mean_us"),
+                "exact": bool(r.get("exact")) and bool(
+                    (d.get("rank1") or {}).get("p2p_4096", {}).get("exact")),
+                "what": "2 processes on this GPU, GPU peer domains, LFA_ALGO_P2P one-shot + "
+                        "completion word; Python-timed submit + wait per operation"}
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+
+
 def extra_config1_loopback(dev, stream, reps=1000, warm=100):
     """BASELINE configs[0] at its stated shape on ONE GPU: a 2-rank float
     FI_SUM allreduce of 4 KiB per rank, both ranks' schedules executed by the
@@ -1982,6 +2011,7 @@ def main() -> None:
             if world == 1:
                 ex["config3_int64_64mib"] = extra_config3(dev, stream)
                 ex["config1_2rank_4kib_loopback"] = extra_config1_loopback(dev, stream)
+                ex["config1_2rank_4kib_two_processes"] = extra_config1_two_process()
                 ex["tree8_fused_combine"] = extra_tree(dev, stream)
                 ex["tree8_put_p2p_kernel_local"] = extra_tree_put(dev, stream)
                 ex["fetch_compare_tables_256mib"] = extra_fetch_tables(dev, stream)

@@ -107,6 +107,13 @@ def _worker(rank, world, port, reps, quick, q, only=None):
                     dt_, op_ = (9, 3) if name == "p2p_rs" else (8, 2)
                     out[f"{name}_{nbytes}"]["c_loop_mean_us"] = round(
                         ep.bench_loop(kind, x, r, cnt, dt_, op_, reps=n), 1)
+                    if name == "p2p" and world == 2:
+                        # the result bit for bit: prov/coll's two-rank tree
+                        # is x1 + x0 (coll_coll.c:409-430), one fp32 add
+                        torch.cuda.synchronize()
+                        xs = [torch.empty(cnt) for _ in range(world)]
+                        dist.all_gather(xs, x.cpu())
+                        out[f"{name}_{nbytes}"]["exact"] = bool(torch.equal(r.cpu(), xs[1] + xs[0]))
             out["kfd_queues"] = _kfd_queues()
         finally:
             ep.close()
