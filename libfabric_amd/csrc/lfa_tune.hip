@@ -770,6 +770,72 @@ __global__ __launch_bounds__(NW * 64) void tp_r5(PutArgs a, size_t nvec) {
   }
 }
 
+// Round 5: a resident grid whose waves walk tiles strided by the number of
+// waves and keep the NEXT tile's loads in flight while they reduce and
+// store the current one (two register buffers, ping-pong), so a wave's store
+// phase no longer leaves HBM without reads; 8 inputs, the fixed
+// ((7+6)+(5+4))+((3+2)+(1+0)) tree of a power-of-two member count.
+template <int U>
+__device__ __forceinline__ void tpp_load(u32x4 (&x)[8][U], const PutArgs &a, size_t tile,
+                                         size_t nvec) {
+  const size_t base = tile * (64 * U);
+  const size_t left = nvec - base;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  const unsigned l = threadIdx.x % 64;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc((const u32x4 *)a.t.in[k] + base, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x[k][u] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(u * 64 + l) * 16, 0,
+                                                       kSysLoadAux));
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void tpp_store(const u32x4 (&x)[8][U], const PutArgs &a,
+                                          size_t tile, size_t nvec) {
+  const size_t base = tile * (64 * U);
+  const size_t left = nvec - base;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  const unsigned l = threadIdx.x % 64;
+  auto f = [](u32x4 hi, u32x4 lo) { return apply_vec<OP_SUM, float>(hi, lo); };
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    v[u] = f(f(f(x[7][u], x[6][u]), f(x[5][u], x[4][u])),
+             f(f(x[3][u], x[2][u]), f(x[1][u], x[0][u])));
+  for (int j = 0; j < a.nout; j++) {
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + base, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(v[u], r, (unsigned)(u * 64 + l) * 16, 0, kSysAux);
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void tp_pipe(PutArgs a, size_t nvec) {
+  const size_t nt = (nvec + 64 * U - 1) / (64 * U);
+  const size_t step = (size_t)gridDim.x * (kBlock / 64);
+  size_t t = (size_t)blockIdx.x * (kBlock / 64) + wave_id<true>();
+  if (t >= nt) return;
+  u32x4 A[8][U], B[8][U];
+  tpp_load<U>(A, a, t, nvec);
+  for (;;) {
+    size_t t2 = t + step;
+    if (t2 < nt) tpp_load<U>(B, a, t2, nvec);
+    tpp_store<U>(A, a, t, nvec);
+    if (t2 >= nt) break;
+    t = t2;
+    t2 = t + step;
+    if (t2 < nt) tpp_load<U>(A, a, t2, nvec);
+    tpp_store<U>(B, a, t, nvec);
+    if (t2 >= nt) break;
+    t = t2;
+  }
+}
+
 // Round 5: the outputs split over G workgroups per tile, the G placed on ONE
 // XCD back to back.  Workgroups are dispatched round-robin over the 8 XCDs
 // (XCD = blockIdx mod 8), so XCD x's k-th workgroup is blockIdx x + 8k; it
@@ -900,6 +966,19 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 47: TPW(2, 1, 27); break;        // 1-wave workgroups, 5 per CU
     case 48: TPW(2, 1, 20); break;        // 1-wave workgroups, 8 per CU
 #undef TPW
+#define TPQ(U, WGS, LDS)                                                              \
+  do {                                                                               \
+    int ncu = 256;                                                                   \
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);           \
+    hipLaunchKernelGGL((tp_pipe<U>), dim3((unsigned)(ncu * (WGS))), dim3(kBlock),     \
+                       (LDS) << 10, s, a, nvec);                                      \
+  } while (0)
+    case 59: TPQ(1, 1, 81); break;        // pipelined, 1 KiB tiles, 1 workgroup per CU
+    case 60: TPQ(2, 1, 81); break;        // 2 KiB tiles
+    case 61: TPQ(1, 2, 54); break;        // 2 workgroups per CU
+    case 62: TPQ(2, 2, 54); break;
+    case 63: TPQ(1, 3, 41); break;
+#undef TPQ
 #define TPX(U, L, G)                                                                 \
   do {                                                                               \
     const unsigned nt = grid_for(nvec, (size_t)kBlock * U, 0x7fffffffu);             \
