@@ -2302,6 +2302,21 @@ static struct lfa_direct *direct_of(struct lfa_coll_ep *ep)
 	return ep->direct;
 }
 
+/* The largest world-1 reducing collective run_solo takes: LFA_ONESHOT_SOLO_BYTES
+ * unless LFA_SOLO_BYTES says otherwise (a tuning knob). */
+static size_t solo_bytes(void)
+{
+	static long long v = -1;
+
+	if (v < 0) {
+		const char *e = getenv("LFA_SOLO_BYTES");
+		const long long x = e ? atoll(e) : -1;
+
+		v = x >= 0 && x <= (1ll << 30) ? x : (long long)LFA_ONESHOT_SOLO_BYTES;
+	}
+	return (size_t)v;
+}
+
 static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
 		    enum lfa_datatype dt)
 {
@@ -2356,7 +2371,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		return ret;
 	if (mc->size == 1 && s == ep->stream && ep->done_word &&
 	    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE || coll == LFA_REDUCE_SCATTER) &&
-	    count * esz <= LFA_ONESHOT_SOLO_BYTES)
+	    count * esz <= solo_bytes())
 		return run_solo(ep, buf, result, count, dt);
 	if (algo == LFA_ALGO_AUTO)
 		algo = (enum lfa_coll_algo)lfa_coll_auto_algo(coll, count, mc->size, esz,

@@ -14,10 +14,12 @@
 #define LFA_INTERNAL __attribute__((visibility("hidden")))
 #define LFA_SMALL_AG_BYTES (256u << 10) /* allgather-then-tree below this */
 /* a one-member group's reducing collective of at most this many bytes runs
- * as one copy kernel ending in the completion word (run_solo): 1 MiB in
- * 8.4 us from launch to the word against 12.1 us for the TREE plan's copy
- * and event (round 5, tools/probe_solo_multi.py) */
-#define LFA_ONESHOT_SOLO_BYTES (1u << 20)
+ * as one copy kernel ending in the completion word (run_solo; LFA_SOLO_BYTES
+ * overrides it).  Timed in C through the provider (round 5,
+ * tools/probe_world1_sizes.py): 1 MiB 8.3-8.4 us, 4 MiB 10.4-10.7 us against
+ * 12.7 us for the TREE plan's copy and event; at 16 MiB the copy's
+ * write-through stores lose (19.8 vs 14.5 us), so the TREE plan takes over */
+#define LFA_ONESHOT_SOLO_BYTES (4u << 20)
 /* ... and through liblfa's own HSA queue up to this many (4 workgroups of
  * 16 KiB): its kernel arguments sit in host memory and every workgroup
  * fetches them over PCIe, so past a few workgroups the HIP launch
