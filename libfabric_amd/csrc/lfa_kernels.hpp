@@ -1383,6 +1383,14 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
   // the full occupancy.
   const unsigned cap_lds =
       (variant < 0 && nvec * 16 < kSc1Bytes && nsrc >= 3 && nsrc <= 8) ? kTreeCapLds : 0u;
+  // Round 5: at 8-15 inputs of >= 4-byte lanes the P2P push kernel's body
+  // with one output (4 KiB per wave per input through tile-sized buffer
+  // descriptors, nt loads, write-through stores) beat that form: 8 inputs
+  // 52.28 -> 50.56 us, 16 (as U = 4 float) 52.26 -> 50.68 us; at 4 inputs it
+  // lost (52.74 -> 53.22), at 2 tied (bench.py --tune-tree variants -1 / 25,
+  // profiles/r05_tune_tree_putbody.json)
+  constexpr bool kPutBody = NLEAF == 8 && sizeof(T) >= 4;
+  if (variant < 0 && nvec * 16 < kSc1Bytes && kPutBody) variant = 25;
   if (variant < 0 && nvec * 16 < kSc1Bytes) variant = 11;
   if (variant < 0) variant = nsrc <= 2 ? 3 : nsrc > 8 ? 2 : 1;
   // nsrc lies in [NLEAF, 2·NLEAF): only these forms are reachable from the
@@ -1424,6 +1432,21 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
         hipLaunchKernelGGL((reduce_tree_chunk<OP, T, NLEAF, 4, kStoreSc1>),
                            dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)),
                            dim3(kBlock), lds, s, b, dst, nvec);
+      return;
+    }
+  } else if (variant == 25 || variant == 26) {
+    if constexpr (ALL || kPutBody) {
+      // round 5: the P2P push kernel's body with one output (4 KiB per wave
+      // per input through tile-sized buffer descriptors, system-scope nt
+      // loads, write-through stores); 26 at <= 3 workgroups per CU
+      PutArgs pa;
+      pa.t = b;
+      memset(pa.out, 0, sizeof(pa.out));
+      pa.out[0] = dst;
+      pa.nout = 1;
+      hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, 4>),
+                         dim3(grid_for(nvec, (size_t)kBlock * 4, 0x7fffffffu)), dim3(kBlock),
+                         variant == 26 ? (41u << 10) : 0u, s, pa, nvec);
       return;
     }
   } else if (variant == 12) {
