@@ -518,3 +518,40 @@ def test_auto_algo_same_choice_on_every_member(n):
                 for r in range(n):
                     p = coll.plan(kind, a, r, n, n - 1 if kind == REDUCE else -1, count, esz)
                     assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT], (kind, n, r)
+
+
+def test_one_shot_bounds_follow_their_knobs():
+    """LFA_OS_AG_BYTES / LFA_OS_RS_BYTES (lfa_coll_plan.h) move the P2P
+    one-shot bounds, the same for the planner and LFA_ALGO_AUTO; read once per
+    process, so each setting runs in its own interpreter."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import json\n"
+        "from libfabric_amd import coll\n"
+        "ar = [coll.auto_algo(3, c, 4, 4) for c in (16384, 16385, 131072, 131073)]\n"
+        "rs = [coll.auto_algo(5, c, 4, 8) for c in (65536, 65537, 524288, 524289)]\n"
+        "p = coll.plan(3, coll.ALGO_P2P, 0, 4, -1, 131072, 4)\n"
+        "print(json.dumps([ar, rs, [s['type'] for s in p.steps]]))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(env):
+        e = {k: v for k, v in os.environ.items()
+             if k not in ("LFA_OS_AG_BYTES", "LFA_OS_RS_BYTES")}
+        e.update(env)
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, env=e, check=True,
+                             capture_output=True, text=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+
+    P2P, TREE = coll.ALGO_P2P, coll.ALGO_TREE
+    # defaults: allreduce 2 MiB over 4 members = 131072 floats each;
+    # reduce_scatter 4 MiB per member = 524288 doubles
+    ar, rs, steps = run({})
+    assert ar == [P2P, P2P, P2P, TREE] and rs == [P2P, P2P, P2P, TREE]
+    assert steps == [coll.STEP_ONESHOT]
+    # the pre-round-5 bounds: 256 KiB over the members, 512 KiB per member
+    ar, rs, steps = run({"LFA_OS_AG_BYTES": str(256 << 10), "LFA_OS_RS_BYTES": str(512 << 10)})
+    assert ar == [P2P, TREE, TREE, TREE] and rs == [P2P, TREE, TREE, TREE]
+    assert coll.STEP_ONESHOT not in steps
