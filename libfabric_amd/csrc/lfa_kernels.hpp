@@ -1434,6 +1434,20 @@ static void launch_tree_body(const TreeArgs &b, int nsrc, u32x4 *dst,
                            dim3(kBlock), lds, s, b, dst, nvec);
       return;
     }
+  } else if (variant == 27 || variant == 28) {
+    if constexpr (ALL) {
+      // round 5: the push kernel's body with one output at 2 KiB per wave per
+      // input; 28 at <= 3 workgroups per CU
+      PutArgs pa;
+      pa.t = b;
+      memset(pa.out, 0, sizeof(pa.out));
+      pa.out[0] = dst;
+      pa.nout = 1;
+      hipLaunchKernelGGL((reduce_tree_put<OP, T, NLEAF, 2>),
+                         dim3(grid_for(nvec, (size_t)kBlock * 2, 0x7fffffffu)), dim3(kBlock),
+                         variant == 28 ? (41u << 10) : 0u, s, pa, nvec);
+      return;
+    }
   } else if (variant == 25 || variant == 26) {
     if constexpr (ALL || kPutBody) {
       // round 5: the P2P push kernel's body with one output (4 KiB per wave
