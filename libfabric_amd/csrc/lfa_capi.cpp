@@ -126,8 +126,8 @@ constexpr bool in_swap_table(int op, int dt) {
 // Where an operand lives: the synchronous tables take what their caller has
 // — prov/coll's REDUCE items hand over host memory (coll_coll.c:364, :1058),
 // a GPU-resident caller device memory.  Pinned and registered host memory
-// counts as host: the GPU could read it over PCIe, but the host loop or the
-// staged path is faster for it.
+// counts as host: a small bucket runs the host loop; above it
+// lfa_atomic_write_staged combines it in place over PCIe (zero-copy).
 enum { kDev = 1, kHost = 2 };
 
 int ptr_kind(const void *p) {
@@ -419,6 +419,24 @@ int staging_acquire(StagingCtx &c, size_t bytes) {
   }
   return 0;
 }
+
+// The address a kernel on device `devno` uses for operand p, or null when
+// the operand must be staged: device memory of this device as it is, pinned
+// or registered host memory through its device mapping (zero-copy: the
+// combine reads and writes it over PCIe).  Pageable memory, other devices'
+// memory and LFA_HOST_ZERO_COPY=0 (read per call) stage.
+void *zero_copy_addr(const void *p, int devno) {
+  const char *e = getenv("LFA_HOST_ZERO_COPY");
+  if (e && !strtol(e, nullptr, 0)) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type == hipMemoryTypeHost) return a.devicePointer;
+  if (a.type == hipMemoryTypeDevice && a.device == devno) return const_cast<void *>(p);
+  return nullptr;
+}
 }  // namespace
 
 extern "C" {
@@ -441,7 +459,19 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   if (hipGetDevice(&devno) != hipSuccess || devno < 0 || devno >= kMaxDevices)
     return -LFA_EINVAL;
   StagingCtx &c = g_staging[devno];
+  void *zd = zero_copy_addr(dst, devno);
+  void *zs = zd ? zero_copy_addr(src, devno) : nullptr;
   pthread_mutex_lock(&c.lock);
+  if (zd && zs) {
+    // every operand reachable from the device: one combine over the mapped
+    // buffers, no HBM round trip (256 MiB float SUM, both pinned: 9.96 ms
+    // against 11.22 ms staged, profiles/r05_zero_copy.log)
+    int ret = staging_acquire(c, 0);
+    if (!ret) ret = kWrite[op](dt, zd, zs, cnt, c.s_out);
+    if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
+    pthread_mutex_unlock(&c.lock);
+    return ret;
+  }
   int ret = staging_acquire(c, 4 * slot);
   if (!ret) {
     for (int i = 0; i < 2; i++) hipEventRecord(c.out_done[i], c.s_out);

@@ -630,12 +630,51 @@ def test_staged_host_buffers(lfa):
         d = a.copy()
         assert L.lfa_atomic_write_staged(op, dt, d.ctypes.data, b.ctypes.data, n, 1 << 20) == 0
         assert d.tobytes() == want.tobytes()
-        # pinned buffers, default chunk
-        dp = torch.from_numpy(a.copy()).pin_memory()
-        bp = torch.from_numpy(b.copy()).pin_memory()
-        assert L.lfa_atomic_write_staged(op, dt, dp.data_ptr(), bp.data_ptr(), n, 0) == 0
-        assert dp.numpy().tobytes() == want.tobytes()
+        # pinned buffers, default chunk: zero-copy, then the staged pipeline
+        for zero_copy in ("1", "0"):
+            os.environ["LFA_HOST_ZERO_COPY"] = zero_copy
+            try:
+                dp = torch.from_numpy(a.copy()).pin_memory()
+                bp = torch.from_numpy(b.copy()).pin_memory()
+                assert L.lfa_atomic_write_staged(op, dt, dp.data_ptr(), bp.data_ptr(), n, 0) == 0
+            finally:
+                del os.environ["LFA_HOST_ZERO_COPY"]
+            assert dp.numpy().tobytes() == want.tobytes(), f"zero-copy={zero_copy}"
     assert L.lfa_atomic_write_staged(6, 8, None, None, 4, 0) == -95
+
+
+def test_zero_copy_operand_mixes(lfa):
+    """The zero-copy form of lfa_atomic_write_staged on every operand mix it
+    accepts — pinned/pinned, device dst with pinned src, pinned dst with device
+    src — and on pinned buffers that are not co-aligned mod 16 (src one float
+    off: the element body over PCIe), with a pageable src falling back to
+    staging; bit-exact with the oracle (float SUM, int64 PROD)."""
+    from libfabric_amd import _native
+    L = _native.lib()
+    rng = np.random.default_rng(23)
+    n = 1_000_003
+    for dt, op, nd in ((8, 2, np.float32), (6, 3, np.int64)):
+        a = (rng.uniform(-1, 1, n + 1) if nd is np.float32
+             else rng.integers(-2**62, 2**62, n + 1)).astype(nd)
+        b = (rng.uniform(-1, 1, n + 1) if nd is np.float32
+             else rng.integers(-2**62, 2**62, n + 1)).astype(nd)
+        for mix in ("pinned", "dev_dst", "dev_src", "unaligned", "pageable_src"):
+            src = b[1:] if mix == "unaligned" else b[:n]
+            want = a[:n].copy()
+            oracle.write(op, dt, want, src.copy())
+            td = torch.from_numpy(a[:n].copy())
+            td = td.to(DEV) if mix == "dev_dst" else td.pin_memory()
+            if mix == "pageable_src":
+                ts, sp = None, src.ctypes.data
+            else:
+                full = torch.from_numpy(b.copy())
+                full = full.to(DEV) if mix == "dev_src" else full.pin_memory()
+                ts = full[1:] if mix == "unaligned" else full[:n]
+                sp = ts.data_ptr()
+            torch.cuda.synchronize()
+            assert L.lfa_atomic_write_staged(op, dt, td.data_ptr(), sp, n, 0) == 0
+            got = td.cpu().numpy()
+            assert got.tobytes() == want.tobytes(), mix
 
 
 def _window_check(dt, got_dev, d0_dev, s_dev, op, lo, hi):
