@@ -3,7 +3,14 @@
 src), zero-copy — one combine on the mapped buffers, reading and writing host
 memory over PCIe — against the staged pipeline (LFA_HOST_ZERO_COPY=0: H2D /
 combine / D2H chunked through HBM on two streams), float SUM at 1 MiB ..
-256 MiB, median of 5, every result checked.  One JSON line per size."""
+256 MiB, median of 5, every result checked.  One JSON line per size.
+--small: pinned buffers of 4 KiB .. 2 MiB, the host loop (lfa_host_write,
+what the synchronous table runs up to LFA_HOST_SMALL_BYTES) against the
+zero-copy combine, median of 50.
+--cross: 1 MiB .. 64 MiB, the same two with the caches hot (one buffer pair,
+repeated) and cold (a rotating pool of pairs, 512 MiB per operand, so every
+call touches memory the last calls did not), median of 9 — where the host
+loop stops winning (the synchronous table's LFA_HOST_SMALL_BYTES)."""
 from __future__ import annotations
 
 import ctypes
@@ -18,11 +25,71 @@ sys.path.insert(0, ROOT)
 FI_SUM, FI_FLOAT = 2, 8
 
 
+def small(L, torch) -> None:
+    out = {}
+    for kib in (4, 16, 64, 256, 512, 1024, 2048):
+        n = (kib << 10) // 4
+        hd = torch.rand(n).pin_memory()
+        hs = torch.rand(n).pin_memory()
+        row = {}
+        for name, fn in (("host_loop", lambda: L.lfa_host_write(FI_SUM, FI_FLOAT, hd.data_ptr(),
+                                                                 hs.data_ptr(), n)),
+                         ("zero_copy", lambda: L.lfa_atomic_write_staged(
+                             FI_SUM, FI_FLOAT, hd.data_ptr(), hs.data_ptr(), n, 0))):
+            base = hd.clone()
+            assert fn() == 0
+            ok = bool(torch.equal(hd, base + hs))
+            ts = []
+            for _ in range(50):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            row[name] = {"us": round(statistics.median(ts) * 1e6, 1), "exact": ok}
+        out[f"{kib}kib"] = row
+        print(json.dumps({f"{kib}kib": row}), flush=True)
+    print(json.dumps({"host_loop_vs_zero_copy_pinned": out}), flush=True)
+
+
+def cross(L, torch) -> None:
+    out = {}
+    for mib in (1, 2, 4, 8, 16, 32, 64):
+        n = (mib << 20) // 4
+        k = max(2, 512 // mib)
+        ds = [torch.rand(n).pin_memory() for _ in range(k)]
+        ss = [torch.rand(n).pin_memory() for _ in range(k)]
+        row = {}
+        for name in ("host_loop", "zero_copy"):
+            for temp in ("hot", "cold"):
+                def fn(i):
+                    d, s = (ds[0], ss[0]) if temp == "hot" else (ds[i % k], ss[i % k])
+                    if name == "host_loop":
+                        return L.lfa_host_write(FI_SUM, FI_FLOAT, d.data_ptr(), s.data_ptr(), n)
+                    return L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, d.data_ptr(),
+                                                     s.data_ptr(), n, 0)
+                base = ds[0].clone()
+                assert fn(0) == 0
+                ok = bool(torch.equal(ds[0], base + ss[0]))
+                ts = []
+                for i in range(1, 10):
+                    t0 = time.perf_counter()
+                    fn(i)
+                    ts.append(time.perf_counter() - t0)
+                row[f"{name}_{temp}"] = {"us": round(statistics.median(ts) * 1e6, 1), "exact": ok}
+        del ds, ss
+        out[f"{mib}mib"] = row
+        print(json.dumps({f"{mib}mib": row}), flush=True)
+    print(json.dumps({"host_loop_vs_zero_copy_cross": out}), flush=True)
+
+
 def main() -> None:
     import torch
     from libfabric_amd import _native
     L = _native.lib()
     torch.cuda.set_device(0)
+    if "--small" in sys.argv:
+        return small(L, torch)
+    if "--cross" in sys.argv:
+        return cross(L, torch)
     out = {}
     for mib in (1, 4, 16, 64, 256):
         n = (mib << 20) // 4
