@@ -58,6 +58,25 @@ static int is_device_ptr(const void *p)
 	return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+/* The address device `dev`'s kernels use for p without staging: pinned or
+ * registered host memory through its device mapping (zero-copy over PCIe),
+ * `dev`'s own memory as it is; NULL for pageable memory, another device's,
+ * or when LFA_HOST_ZERO_COPY=0 (the same knob as lfa_atomic_write_staged). */
+static void *zero_copy_of(const void *p, int dev)
+{
+	hipPointerAttribute_t a;
+	const char *e = getenv("LFA_HOST_ZERO_COPY");
+
+	if (!p || (e && !strtol(e, NULL, 0)))
+		return NULL;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return NULL;
+	}
+	if (a.type == hipMemoryTypeHost)
+		return a.devicePointer;
+	return a.type == hipMemoryTypeDevice && a.device == dev ? (void *)p : NULL;
+}
 
 static void p2p_release(struct lfa_coll_mc *mc);
 static void ws_domain_ref(int delta);
@@ -2812,6 +2831,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	uint64_t t0, done_val = 0;
 	const uint64_t *done_w = NULL;
 	int root = -1, ret, host, chunkable;
+	void *zb = NULL, *zr = NULL;
 
 	if (!ep)
 		return -LFA_EINVAL;
@@ -2893,6 +2913,24 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		ep->allow_direct = 0;
 		done_val = ep->op_done_val;
 		done_w = ep->op_done_w;
+	} else if (mc->size == 1 &&
+		   (coll == LFA_ALLREDUCE || coll == LFA_REDUCE ||
+		    coll == LFA_REDUCE_SCATTER) &&
+		   (zb = zero_copy_of(buf, ep->dom->device)) &&
+		   (zr = zero_copy_of(result, ep->dom->device))) {
+		/* a one-member group's reducing collective is a copy; with
+		 * pinned host buffers it runs on their mappings over PCIe, no
+		 * staging (32 MiB 1.35 -> 0.93 ms) */
+		if (count * esz <= solo_bytes()) {
+			ep->op_done_val = 0;
+			ep->op_done_w = NULL;
+			ret = run_solo(ep, zb, zr, count, dt);
+			done_val = ep->op_done_val;
+			done_w = ep->op_done_w;
+		} else {
+			ret = lfa_atomic_write_async(LFA_ATOMIC_WRITE, LFA_UINT8, zr, zb,
+						     count * esz, ep->stream);
+		}
 	} else if (chunkable) {
 		ret = run_host_chunked(ep, mc, coll, buf, result, count, root, dt,
 				       op, chunk);

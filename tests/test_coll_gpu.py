@@ -448,6 +448,50 @@ def test_two_endpoints_share_the_direct_queue(coll):
         e2.close()
 
 
+@pytest.mark.parametrize("zero_copy", ["1", "0"])
+def test_one_member_pinned_host_buffers(coll, ep, zero_copy, monkeypatch):
+    """A one-member group's reducing collectives on PINNED host buffers run
+    zero-copy: the copy kernel reads and writes their device mappings over
+    PCIe — the solo copy ending in the completion word up to 4 MiB, the
+    ATOMIC_WRITE body above — and LFA_HOST_ZERO_COPY=0 restores the staged
+    pipeline.  Sizes on both sides of the bound, an odd byte count at an
+    odd offset (the byte-wise bodies), a device buf with a pinned result
+    and the reverse; several in flight before one wait; every result the
+    copy the reference defines."""
+    monkeypatch.setenv("LFA_HOST_ZERO_COPY", zero_copy)
+    rng = np.random.default_rng(31)
+    cases = []
+    for nbytes, off, dt, nd in ((4096, 0, 8, np.float32), ((1 << 20) + 3, 1, 0, np.int8),
+                                (6 << 20, 0, 9, np.float64), (40 << 10, 8, 6, np.int64)):
+        count = nbytes // nd().itemsize
+        raw = torch.from_numpy(rng.integers(0, 256, nbytes + 64, dtype=np.uint8)).pin_memory()
+        src = raw[off:off + count * nd().itemsize].view(
+            {np.float32: torch.float32, np.int8: torch.int8, np.float64: torch.float64,
+             np.int64: torch.int64}[nd])
+        for coll_name in ("allreduce", "reduce", "reduce_scatter"):
+            dst = torch.zeros(count * nd().itemsize + off, dtype=torch.uint8).pin_memory()
+            out = dst[off:].view(src.dtype)
+            op = 6 if nd in (np.int8, np.int64) else 2     # BOR / SUM
+            if coll_name == "allreduce":
+                ctx = ep.allreduce(src, out, count, dt, op)
+            elif coll_name == "reduce":
+                ctx = ep.reduce(src, out, count, 0, dt, op)
+            else:
+                ctx = ep.reduce_scatter(src, out, count, dt, op)
+            cases.append((ctx, src, out, f"{coll_name} {nbytes} B +{off}"))
+    ep.wait(cases[-1][0], timeout_s=20)   # completions come in issue order
+    for ctx, src, out, what in cases:
+        assert torch.equal(src.view(torch.uint8), out.view(torch.uint8)), what
+    # mixed: device buf with a pinned result, pinned buf with a device result
+    x = torch.rand(3 << 20, device=DEV)
+    hy = torch.zeros(3 << 20).pin_memory()
+    ep.wait(ep.allreduce(x, hy, x.numel(), 8, 2))
+    assert torch.equal(x.cpu(), hy)
+    y = torch.zeros_like(x)
+    ep.wait(ep.allreduce(hy, y, x.numel(), 8, 2))
+    assert torch.equal(y, x)
+
+
 def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
     """reduce and reduce_scatter on host buffers go through the chunked
     H2D / collective / D2H pipeline (reduce_scatter: one 2-D H2D per chunk);

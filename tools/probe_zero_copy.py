@@ -81,6 +81,65 @@ def cross(L, torch) -> None:
     print(json.dumps({"host_loop_vs_zero_copy_cross": out}), flush=True)
 
 
+def copy(L, torch) -> None:
+    """--copy: a world-1 allreduce of pinned host buffers is a copy.  The
+    provider (zero-copy on the mappings: the solo copy up to 4 MiB, the
+    ATOMIC_WRITE body above), the provider with LFA_HOST_ZERO_COPY=0 (H2D /
+    device copy / D2H on three streams), the ATOMIC_WRITE body called
+    directly, and a hipMemcpyAsync between the two pinned buffers."""
+    from libfabric_amd import coll
+    hip = ctypes.CDLL("libamdhip64.so")
+    ep = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    s = torch.cuda.current_stream()
+    out = {}
+    for kib in (4, 256, 4096, 32768, 262144):
+        n = (kib << 10) // 4
+        hx = torch.rand(n).pin_memory()
+        hy = torch.empty(n).pin_memory()
+        row = {}
+
+        def provider():
+            ep.wait(ep.allreduce(hx, hy, n, 8, 2))
+
+        def provider_staged():
+            os.environ["LFA_HOST_ZERO_COPY"] = "0"
+            try:
+                ep.wait(ep.allreduce(hx, hy, n, 8, 2))
+            finally:
+                del os.environ["LFA_HOST_ZERO_COPY"]
+
+        def zero_copy():
+            assert L.lfa_atomic_write_async(11, 1, ctypes.c_void_p(hy.data_ptr()),
+                                            ctypes.c_void_p(hx.data_ptr()),
+                                            ctypes.c_size_t(n * 4),
+                                            ctypes.c_void_p(s.cuda_stream)) == 0
+            torch.cuda.synchronize()
+
+        def memcpy_async():
+            assert hip.hipMemcpyAsync(ctypes.c_void_p(hy.data_ptr()),
+                                      ctypes.c_void_p(hx.data_ptr()),
+                                      ctypes.c_size_t(n * 4), 4,
+                                      ctypes.c_void_p(s.cuda_stream)) == 0
+            torch.cuda.synchronize()
+
+        for name, fn in (("provider", provider), ("provider_staged", provider_staged),
+                         ("zero_copy", zero_copy),
+                         ("hip_memcpy", memcpy_async)):
+            hy.zero_()
+            fn()
+            ok = bool(torch.equal(hy, hx))
+            ts = []
+            for _ in range(7):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            row[name] = {"ms": round(statistics.median(ts) * 1e3, 3), "exact": ok}
+        out[f"{kib}kib"] = row
+        print(json.dumps({f"{kib}kib": row}), flush=True)
+    ep.close()
+    print(json.dumps({"world1_host_allreduce_copy": out}), flush=True)
+
+
 def main() -> None:
     import torch
     from libfabric_amd import _native
@@ -88,6 +147,8 @@ def main() -> None:
     torch.cuda.set_device(0)
     if "--small" in sys.argv:
         return small(L, torch)
+    if "--copy" in sys.argv:
+        return copy(L, torch)
     if "--cross" in sys.argv:
         return cross(L, torch)
     out = {}
