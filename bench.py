@@ -921,6 +921,22 @@ def extra_host_allreduce(ep, world, reps=3, sweep=False):
     row = {"ms": round(t * 1e3, 2), "buffer_gib_s": round(S_BYTES / t / 2**30, 2),
            "note": "pinned host in/out, default chunks; H2D, collective and D2H on "
                    "three streams"}
+    if world == 1:
+        # a one-member group's allreduce is a copy, run on the pinned buffers'
+        # mappings; the staged pipeline it replaces beside it
+        os.environ["LFA_HOST_ZERO_COPY"] = "0"
+        try:
+            ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                ep.wait(ep.allreduce(hx, hy, COUNT, 8, 2))
+                ts.append(time.perf_counter() - t0)
+        finally:
+            del os.environ["LFA_HOST_ZERO_COPY"]
+        row["staged_ms"] = round(statistics.median(ts) * 1e3, 2)
+        row["note"] = ("pinned host in/out; one member: the copy on the buffers' mappings "
+                       "over PCIe (zero-copy); staged_ms = H2D / copy / D2H on three streams")
     if by_chunk:
         row["ms_by_chunk_mib"] = by_chunk
     if world > 1:
@@ -977,18 +993,29 @@ def extra_host_reduce_scatter(ep, rank, world, reps=3):
     ep.wait(ep.reduce_scatter(dx, dy, cnt, 9, 3))
     ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
     row = {"bitwise_equal_device": bool(torch.equal(hy, dy.cpu()))}
-    for name, chunk in (("ms", 0), ("one_chunk_ms", 1 << 40)):
+    # a one-member group copies pinned buffers on their mappings (zero-copy);
+    # its staged forms are timed with LFA_HOST_ZERO_COPY=0
+    forms = [("ms", 0, "1"), ("one_chunk_ms", 1 << 40, "0" if world == 1 else "1")]
+    if world == 1:
+        forms.insert(1, ("staged_ms", 0, "0"))
+    for name, chunk, zc in forms:
         ep.set_chunk(chunk)
-        ts = []
-        for _ in range(reps):
-            barrier(world)
-            t0 = time.perf_counter()
-            ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
-            ts.append(max_over_ranks(time.perf_counter() - t0, world))
+        os.environ["LFA_HOST_ZERO_COPY"] = zc
+        try:
+            ts = []
+            for _ in range(reps):
+                barrier(world)
+                t0 = time.perf_counter()
+                ep.wait(ep.reduce_scatter(hx, hy, cnt, 9, 3))
+                ts.append(max_over_ranks(time.perf_counter() - t0, world))
+        finally:
+            del os.environ["LFA_HOST_ZERO_COPY"]
         row[name] = round(statistics.median(ts) * 1e3, 2)
     ep.set_chunk(0)
     row["buffer_gib_s"] = round(S_BYTES / (row["ms"] * 1e-3) / 2**30, 2)
-    row["note"] = "pinned host in/out; default 32 MiB chunks vs one chunk (serial staging)"
+    row["note"] = ("pinned host in/out; one member: zero-copy on the mappings, staged "
+                   "(32 MiB chunks) and one-chunk staging beside it" if world == 1 else
+                   "pinned host in/out; default 32 MiB chunks vs one chunk (serial staging)")
     return row
 
 
