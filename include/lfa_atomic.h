@@ -144,12 +144,14 @@ int lfa_atomic_swap_async(enum lfa_op op, enum lfa_datatype datatype,
  * Host-resident buffers (what prov/coll's REDUCE items see, coll_coll.c:763):
  * dst/src are streamed through HBM in `chunk_bytes` pieces (0 = 32 MiB) on
  * two HIP streams — chunk c+1's H2D overlaps chunk c's combine and D2H — and
- * the call returns when dst is updated.  Pageable buffers are staged by the
- * HIP runtime.  When every operand is reachable from the device — pinned
- * (hipHostMalloc / hipHostRegister) host memory or this device's memory —
- * there is no staging: one combine runs on the mapped buffers and reads /
- * writes host memory over PCIe (zero-copy; LFA_HOST_ZERO_COPY=0 forces the
- * staged pipeline).  Returns 0 or a negative LFA_E* code.
+ * the call returns when dst is updated.  When every operand is reachable
+ * from the device — pinned (hipHostMalloc / hipHostRegister) host memory or
+ * this device's memory — there is no staging: one combine runs on the mapped
+ * buffers and reads / writes host memory over PCIe (zero-copy).  Pageable
+ * operands are registered for the duration of the call and combined the same
+ * way; if the runtime refuses the registration (e.g. dst and src share
+ * pages) they are staged.  LFA_HOST_ZERO_COPY=0 forces the staged pipeline.
+ * Returns 0 or a negative LFA_E* code.
  */
 int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype datatype,
 			    void *dst, const void *src, size_t cnt,

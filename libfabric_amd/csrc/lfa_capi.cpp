@@ -420,22 +420,45 @@ int staging_acquire(StagingCtx &c, size_t bytes) {
   return 0;
 }
 
+bool zero_copy_on() {
+  const char *e = getenv("LFA_HOST_ZERO_COPY");
+  return !e || strtol(e, nullptr, 0);
+}
+
 // The address a kernel on device `devno` uses for operand p, or null when
 // the operand must be staged: device memory of this device as it is, pinned
 // or registered host memory through its device mapping (zero-copy: the
-// combine reads and writes it over PCIe).  Pageable memory, other devices'
-// memory and LFA_HOST_ZERO_COPY=0 (read per call) stage.
-void *zero_copy_addr(const void *p, int devno) {
-  const char *e = getenv("LFA_HOST_ZERO_COPY");
-  if (e && !strtol(e, nullptr, 0)) return nullptr;
+// combine reads and writes it over PCIe).  *pageable: p is host memory HIP
+// does not know, which the caller may register for the call.
+void *zero_copy_addr(const void *p, int devno, bool *pageable) {
   hipPointerAttribute_t a;
+  *pageable = false;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
+    *pageable = true;
     return nullptr;
   }
+  if (a.type == hipMemoryTypeUnregistered) *pageable = true;
   if (a.type == hipMemoryTypeHost) return a.devicePointer;
   if (a.type == hipMemoryTypeDevice && a.device == devno) return const_cast<void *>(p);
   return nullptr;
+}
+
+// Pin pageable operand p (bytes long) for one call; its device address, or
+// null if the runtime refuses (overlapping registrations, read-only pages):
+// the caller then stages.
+void *register_for_call(const void *p, size_t bytes) {
+  void *d = nullptr;
+  if (hipHostRegister(const_cast<void *>(p), bytes, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    hipHostUnregister(const_cast<void *>(p));
+    return nullptr;
+  }
+  return d;
 }
 }  // namespace
 
@@ -459,8 +482,22 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   if (hipGetDevice(&devno) != hipSuccess || devno < 0 || devno >= kMaxDevices)
     return -LFA_EINVAL;
   StagingCtx &c = g_staging[devno];
-  void *zd = zero_copy_addr(dst, devno);
-  void *zs = zd ? zero_copy_addr(src, devno) : nullptr;
+  bool pd = false, ps = false;
+  const bool zc = zero_copy_on();
+  void *zd = zc ? zero_copy_addr(dst, devno, &pd) : nullptr;
+  void *zs = zc ? zero_copy_addr(src, devno, &ps) : nullptr;
+  const void *reg[2] = {};
+  if ((zd || pd) && (zs || ps) && (pd || ps)) {
+    // pageable operands are pinned for the call: registration + the
+    // zero-copy combine beats the runtime's staging of pageable memory
+    // (4 MiB 0.29 vs 0.46 ms, 256 MiB 12.5 vs 15.6 ms,
+    // profiles/r05_zero_copy_pageable.log)
+    const size_t bytes = cnt * esz;
+    if (pd && (zd = register_for_call(dst, bytes))) reg[0] = dst;
+    if (ps && src == dst) zs = zd;
+    else if (ps && (zs = register_for_call(src, bytes))) reg[1] = src;
+    if (!zd || !zs) zd = zs = nullptr;   // stage instead
+  }
   pthread_mutex_lock(&c.lock);
   if (zd && zs) {
     // every operand reachable from the device: one combine over the mapped
@@ -470,8 +507,12 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     if (!ret) ret = kWrite[op](dt, zd, zs, cnt, c.s_out);
     if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
     pthread_mutex_unlock(&c.lock);
+    for (const void *p : reg)
+      if (p) hipHostUnregister(const_cast<void *>(p));
     return ret;
   }
+  for (const void *p : reg)
+    if (p) hipHostUnregister(const_cast<void *>(p));
   int ret = staging_acquire(c, 4 * slot);
   if (!ret) {
     for (int i = 0; i < 2; i++) hipEventRecord(c.out_done[i], c.s_out);

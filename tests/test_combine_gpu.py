@@ -626,10 +626,17 @@ def test_staged_host_buffers(lfa):
              rng.integers(-2**62, 2**62, n)).astype(nd)
         want = a.copy()
         oracle.write(op, dt, want, b)
-        # pageable numpy buffers, 1 MiB chunks (many pipeline steps)
-        d = a.copy()
-        assert L.lfa_atomic_write_staged(op, dt, d.ctypes.data, b.ctypes.data, n, 1 << 20) == 0
-        assert d.tobytes() == want.tobytes()
+        # pageable numpy buffers: registered for the call (zero-copy), then
+        # the staged pipeline in 1 MiB chunks (many pipeline steps)
+        for zero_copy in ("1", "0"):
+            os.environ["LFA_HOST_ZERO_COPY"] = zero_copy
+            try:
+                d = a.copy()
+                assert L.lfa_atomic_write_staged(op, dt, d.ctypes.data, b.ctypes.data, n,
+                                                 1 << 20) == 0
+            finally:
+                del os.environ["LFA_HOST_ZERO_COPY"]
+            assert d.tobytes() == want.tobytes(), f"pageable zero-copy={zero_copy}"
         # pinned buffers, default chunk: zero-copy, then the staged pipeline
         for zero_copy in ("1", "0"):
             os.environ["LFA_HOST_ZERO_COPY"] = zero_copy
@@ -641,6 +648,29 @@ def test_staged_host_buffers(lfa):
                 del os.environ["LFA_HOST_ZERO_COPY"]
             assert dp.numpy().tobytes() == want.tobytes(), f"zero-copy={zero_copy}"
     assert L.lfa_atomic_write_staged(6, 8, None, None, 4, 0) == -95
+
+
+def test_pageable_operands_sharing_pages(lfa):
+    """Pageable dst and src in ONE allocation (dst's last page is src's
+    first): the second registration is refused, so the call stages; and the
+    in-place form (src == dst, registered once).  Bit-exact, and the pages are
+    left unregistered (a second call registers them again)."""
+    from libfabric_amd import _native
+    L = _native.lib()
+    rng = np.random.default_rng(29)
+    n = 700_001
+    buf = rng.integers(-2**62, 2**62, 2 * n + 1).astype(np.int64)
+    for _ in range(2):
+        d, s = buf[:n], buf[n + 1:]
+        want = d.copy()
+        oracle.write(9, 6, want, s.copy())          # BXOR int64
+        assert L.lfa_atomic_write_staged(9, 6, d.ctypes.data, s.ctypes.data, n, 0) == 0
+        assert d.tobytes() == want.tobytes()
+    x = rng.uniform(-1, 1, n).astype(np.float64)
+    want = x.copy()
+    oracle.write(2, 9, want, x.copy())              # SUM double, in place
+    assert L.lfa_atomic_write_staged(2, 9, x.ctypes.data, x.ctypes.data, n, 0) == 0
+    assert x.tobytes() == want.tobytes()
 
 
 def test_zero_copy_operand_mixes(lfa):

@@ -140,6 +140,65 @@ def copy(L, torch) -> None:
     print(json.dumps({"world1_host_allreduce_copy": out}), flush=True)
 
 
+def pageable(L, torch) -> None:
+    """--pageable: PAGEABLE (numpy) dst / src, float SUM at 4 .. 256 MiB: the
+    staged pipeline (the runtime stages pageable memory itself), the host
+    loop, hipHostRegister of both buffers + the zero-copy combine +
+    hipHostUnregister from Python, and the entry point's default (which does
+    that registration itself), each timed whole, median of 5, results
+    checked."""
+    import numpy as np
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = {}
+    for mib in (4, 32, 256):
+        n = (mib << 20) // 4
+        rng = np.random.default_rng(mib)
+        d0 = rng.random(n, dtype=np.float32)
+        sv = rng.random(n, dtype=np.float32)
+        want = d0 + sv
+        row = {}
+
+        def staged(d):
+            os.environ["LFA_HOST_ZERO_COPY"] = "0"
+            try:
+                assert L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, d.ctypes.data, sv.ctypes.data,
+                                                 n, 0) == 0
+            finally:
+                del os.environ["LFA_HOST_ZERO_COPY"]
+
+        def host_loop(d):
+            assert L.lfa_host_write(FI_SUM, FI_FLOAT, d.ctypes.data, sv.ctypes.data, n) == 0
+
+        def register(d):
+            for a in (d, sv):
+                assert hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data),
+                                           ctypes.c_size_t(a.nbytes), 0) == 0
+            try:
+                assert L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, d.ctypes.data, sv.ctypes.data,
+                                                 n, 0) == 0
+            finally:
+                for a in (d, sv):
+                    hip.hipHostUnregister(ctypes.c_void_p(a.ctypes.data))
+
+        def default(d):
+            assert L.lfa_atomic_write_staged(FI_SUM, FI_FLOAT, d.ctypes.data, sv.ctypes.data,
+                                             n, 0) == 0
+
+        for name, fn in (("staged", staged), ("host_loop", host_loop),
+                         ("register_zero_copy", register), ("default", default)):
+            ts, ok = [], True
+            for _ in range(5):
+                d = d0.copy()
+                t0 = time.perf_counter()
+                fn(d)
+                ts.append(time.perf_counter() - t0)
+                ok = ok and d.tobytes() == want.tobytes()
+            row[name] = {"ms": round(statistics.median(ts) * 1e3, 3), "exact": ok}
+        out[f"{mib}mib"] = row
+        print(json.dumps({f"{mib}mib": row}), flush=True)
+    print(json.dumps({"pageable_host_combine": out}), flush=True)
+
+
 def main() -> None:
     import torch
     from libfabric_amd import _native
@@ -147,6 +206,8 @@ def main() -> None:
     torch.cuda.set_device(0)
     if "--small" in sys.argv:
         return small(L, torch)
+    if "--pageable" in sys.argv:
+        return pageable(L, torch)
     if "--copy" in sys.argv:
         return copy(L, torch)
     if "--cross" in sys.argv:
