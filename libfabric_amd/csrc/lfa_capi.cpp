@@ -444,6 +444,13 @@ void *zero_copy_addr(const void *p, int devno, bool *pageable) {
   return nullptr;
 }
 
+// Temporary registrations (pageable operands pinned for one call) exist
+// only while g_reg_lock is held, and every zero-copy classification takes
+// it (here and lfa_zero_copy_addr, the provider's): so no caller takes a
+// temporary registration for pinned memory and keeps using its mapping
+// after the call that made it has unregistered it.
+pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+
 // Pin pageable operand p (bytes long) for one call; its device address, or
 // null if the runtime refuses (overlapping registrations, read-only pages):
 // the caller then stages.
@@ -482,21 +489,35 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   if (hipGetDevice(&devno) != hipSuccess || devno < 0 || devno >= kMaxDevices)
     return -LFA_EINVAL;
   StagingCtx &c = g_staging[devno];
-  bool pd = false, ps = false;
-  const bool zc = zero_copy_on();
-  void *zd = zc ? zero_copy_addr(dst, devno, &pd) : nullptr;
-  void *zs = zc ? zero_copy_addr(src, devno, &ps) : nullptr;
+  bool pd = false, ps = false, held = false;
+  void *zd = nullptr, *zs = nullptr;
   const void *reg[2] = {};
-  if ((zd || pd) && (zs || ps) && (pd || ps)) {
-    // pageable operands are pinned for the call: registration + the
-    // zero-copy combine beats the runtime's staging of pageable memory
-    // (4 MiB 0.29 vs 0.46 ms, 256 MiB 12.5 vs 15.6 ms,
-    // profiles/r05_zero_copy_pageable.log)
-    const size_t bytes = cnt * esz;
-    if (pd && (zd = register_for_call(dst, bytes))) reg[0] = dst;
-    if (ps && src == dst) zs = zd;
-    else if (ps && (zs = register_for_call(src, bytes))) reg[1] = src;
-    if (!zd || !zs) zd = zs = nullptr;   // stage instead
+  if (zero_copy_on()) {
+    pthread_mutex_lock(&g_reg_lock);
+    held = true;
+    zd = zero_copy_addr(dst, devno, &pd);
+    zs = zero_copy_addr(src, devno, &ps);
+    if ((zd || pd) && (zs || ps) && (pd || ps)) {
+      // pageable operands are pinned for the call: registration + the
+      // zero-copy combine beats the runtime's staging of pageable memory
+      // (4 MiB 0.419 -> 0.256 ms, 256 MiB 15.4 -> 11.5 ms,
+      // profiles/r05_zero_copy_pageable.log)
+      const size_t bytes = cnt * esz;
+      if (pd && (zd = register_for_call(dst, bytes))) reg[0] = dst;
+      if (ps && src == dst) zs = zd;
+      else if (ps && (zs = register_for_call(src, bytes))) reg[1] = src;
+    }
+    if (!zd || !zs) {
+      // stage instead
+      zd = zs = nullptr;
+      for (const void *&p : reg)
+        if (p) hipHostUnregister(const_cast<void *>(p)), p = nullptr;
+    }
+    if (!reg[0] && !reg[1]) {
+      // no temporary registration: nothing to hold the lock for
+      pthread_mutex_unlock(&g_reg_lock);
+      held = false;
+    }
   }
   pthread_mutex_lock(&c.lock);
   if (zd && zs) {
@@ -509,10 +530,9 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     pthread_mutex_unlock(&c.lock);
     for (const void *p : reg)
       if (p) hipHostUnregister(const_cast<void *>(p));
+    if (held) pthread_mutex_unlock(&g_reg_lock);
     return ret;
   }
-  for (const void *p : reg)
-    if (p) hipHostUnregister(const_cast<void *>(p));
   int ret = staging_acquire(c, 4 * slot);
   if (!ret) {
     for (int i = 0; i < 2; i++) hipEventRecord(c.out_done[i], c.s_out);
@@ -535,6 +555,15 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   }
   pthread_mutex_unlock(&c.lock);
   return ret;
+}
+
+void *lfa_zero_copy_addr(const void *p, int device) {
+  if (!p || !zero_copy_on()) return nullptr;
+  bool pageable;
+  pthread_mutex_lock(&g_reg_lock);
+  void *r = zero_copy_addr(p, device, &pageable);
+  pthread_mutex_unlock(&g_reg_lock);
+  return r;
 }
 
 size_t lfa_host_small_bytes(void) {

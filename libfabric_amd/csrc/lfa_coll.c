@@ -58,24 +58,12 @@ static int is_device_ptr(const void *p)
 	return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
-/* The address device `dev`'s kernels use for p without staging: pinned or
- * registered host memory through its device mapping (zero-copy over PCIe),
- * `dev`'s own memory as it is; NULL for pageable memory, another device's,
- * or when LFA_HOST_ZERO_COPY=0 (the same knob as lfa_atomic_write_staged). */
+/* Zero-copy operand address (lfa_zero_copy_addr, liblfa: pinned or
+ * registered host memory through its mapping, `dev`'s memory as it is), or
+ * NULL: stage. */
 static void *zero_copy_of(const void *p, int dev)
 {
-	hipPointerAttribute_t a;
-	const char *e = getenv("LFA_HOST_ZERO_COPY");
-
-	if (!p || (e && !strtol(e, NULL, 0)))
-		return NULL;
-	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-		(void)hipGetLastError();
-		return NULL;
-	}
-	if (a.type == hipMemoryTypeHost)
-		return a.devicePointer;
-	return a.type == hipMemoryTypeDevice && a.device == dev ? (void *)p : NULL;
+	return lfa_zero_copy_addr(p, dev);
 }
 
 static void p2p_release(struct lfa_coll_mc *mc);

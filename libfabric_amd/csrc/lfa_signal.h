@@ -133,6 +133,13 @@ struct lfa_oneshot {
 int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
 				void *stream);
 
+/* The address device `device`'s kernels use for p without staging (liblfa,
+ * lfa_capi.cpp): pinned or registered host memory through its device mapping,
+ * that device's own memory as it is; NULL for pageable memory, another
+ * device's, or LFA_HOST_ZERO_COPY=0.  Never a registration lfa_atomic_write_staged
+ * made for one call of its own. */
+void *lfa_zero_copy_addr(const void *p, int device);
+
 /*
  * A one-member group's small reducing collective (allreduce, reduce and
  * reduce_scatter of one rank are each a copy of the input): `bytes` from

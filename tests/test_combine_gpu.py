@@ -673,6 +673,40 @@ def test_pageable_operands_sharing_pages(lfa):
     assert x.tobytes() == want.tobytes()
 
 
+def test_pageable_registration_concurrent_callers(lfa):
+    """Four threads combine into their own pageable dst from ONE shared
+    pageable src, 12 calls each (ctypes drops the GIL, so the calls
+    overlap): a thread must never run on another call's temporary
+    registration of src after that call unregistered it — every result
+    bit-exact."""
+    import threading
+    from libfabric_amd import _native
+    L = _native.lib()
+    rng = np.random.default_rng(37)
+    n = (3 << 20) + 5
+    src = rng.uniform(-1, 1, n).astype(np.float32)
+    errors = []
+
+    def worker(k):
+        d0 = np.random.default_rng(k).uniform(-1, 1, n).astype(np.float32)
+        want = d0.copy()
+        oracle.write(2, 8, want, src.copy())
+        for i in range(12):
+            d = d0.copy()
+            rc = L.lfa_atomic_write_staged(2, 8, d.ctypes.data, src.ctypes.data, n, 0)
+            if rc != 0 or d.tobytes() != want.tobytes():
+                errors.append((k, i, rc))
+                return
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
+
+
 def test_zero_copy_operand_mixes(lfa):
     """The zero-copy form of lfa_atomic_write_staged on every operand mix it
     accepts — pinned/pinned, device dst with pinned src, pinned dst with device
