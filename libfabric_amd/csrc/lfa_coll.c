@@ -2634,6 +2634,20 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 	int ret, sym;
 
 	h->ep = ep;
+	if (dev == 2) {
+		/* host buffers the GPU reaches (pinned, registered): the device
+		 * schedule runs on their mappings — this member's kernels alone
+		 * touch its buf and result (peers only see the symmetric
+		 * workspaces), so nothing is staged */
+		void *zb = buf ? zero_copy_of(buf, ep->dom->device) : NULL;
+		void *zr = result ? zero_copy_of(result, ep->dom->device) : NULL;
+
+		if ((!buf || zb) && (!result || zr)) {
+			buf = zb;
+			result = zr;
+			dev = 1;
+		}
+	}
 	/* P2P keeps its schedule on device buffers (the peers' symmetric
 	 * workspaces are IPC-mapped device memory; its barriers become zero-byte
 	 * messages); host buffers and RCCL run as TREE */

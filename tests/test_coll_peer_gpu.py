@@ -614,6 +614,79 @@ def test_released_workspaces_are_reused(cap):
     _spawn(_ws_cycle_worker, 4, args=(cap,))
 
 
+def _pinned_member_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        msg = "ok"
+        tdt = {8: torch.float32, 9: torch.float64}
+
+        def buf(a, off=0):
+            # rank 0: pinned host; rank 1: device; rank 2: pinned host at an
+            # offset that is not 16-B aligned (the byte-wise bodies)
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if rank == 1:
+                return t.to("cuda")
+            raw = torch.zeros(t.numel() * t.element_size() + 64, dtype=torch.uint8).pin_memory()
+            o = 8 if rank == 2 else 0
+            v = raw[o:o + t.numel() * t.element_size()].view(t.dtype)
+            v.copy_(t)
+            return v
+
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            ep.set_group_chunk(0)
+            for k, nbytes in enumerate((4096, 1 << 20, (3 << 20) + 8)):
+                n = nbytes // 4
+                sends = _inputs(oracle, 8, n, world, 1200 + k)
+                want = oracle.allreduce(2, 8, sends)[0]
+                x, r = buf(sends[rank]), buf(np.zeros(n, np.float32))
+                _ready()
+                ep.wait(ep.allreduce(x, r, n, 8, 2))
+                if r.cpu().numpy().tobytes() != want.tobytes():
+                    msg = f"allreduce {nbytes} B wrong"
+                # double PROD reduce_scatter, ragged blocks
+                m = nbytes // 8 + 1
+                sd = _inputs(oracle, 9, m, world, 1300 + k)
+                wantd = oracle.allreduce(3, 9, sd)[0]
+                off, ln = coll.block(m, world, rank)
+                xd, rd = buf(sd[rank]), buf(np.zeros(max(ln, 1), np.float64))
+                _ready()
+                ep.wait(ep.reduce_scatter(xd, rd, m, 9, 3))
+                if rd.cpu().numpy()[:ln].tobytes() != wantd[off:off + ln].tobytes():
+                    msg = f"reduce_scatter {nbytes} B wrong"
+                for root in (0, 1):
+                    rr = buf(np.zeros(n, np.float32))
+                    _ready()
+                    ep.wait(ep.reduce(x, rr, n, root, 8, 2))
+                    if rank == root and rr.cpu().numpy().tobytes() != want.tobytes():
+                        msg = f"reduce {nbytes} B to {root} wrong"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_p2p_pinned_host_members():
+    """LFA_ALGO_P2P with PINNED host members (ranks 0 and 2; rank 2's
+    buffers 8 bytes off 16-B alignment) and a device member (rank 1): the
+    host members run the device schedule on their buffers' mappings with
+    nothing staged — the one-shot (4 KiB) and the staged-workspace schedule
+    (1 MiB, 3 MiB + 8 B) — allreduce, ragged double PROD reduce_scatter and
+    reduce to a host and a device root, bit-exact with the oracle."""
+    _spawn(_pinned_member_worker, 3)
+
+
 def _chunk_error_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),

@@ -59,6 +59,7 @@ def _worker(rank, world, port, reps, quick, q, only=None):
         out = {}
         try:
             plan = (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                    ("p2p_host", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10)))
             if quick:
@@ -79,6 +80,13 @@ def _worker(rank, world, port, reps, quick, q, only=None):
 
                         def op():
                             return ep.reduce_scatter(x, r, cnt, 9, 3)
+                    elif name == "p2p_host":   # pinned HOST buffers
+                        cnt = nbytes // 4
+                        x = torch.rand(cnt).pin_memory()
+                        r = torch.empty_like(x).pin_memory()
+
+                        def op():
+                            return ep.allreduce(x, r, cnt, 8, 2)
                     else:
                         cnt = nbytes // 4
                         x = torch.rand(cnt, device="cuda")
@@ -107,7 +115,7 @@ def _worker(rank, world, port, reps, quick, q, only=None):
                     dt_, op_ = (9, 3) if name == "p2p_rs" else (8, 2)
                     out[f"{name}_{nbytes}"]["c_loop_mean_us"] = round(
                         ep.bench_loop(kind, x, r, cnt, dt_, op_, reps=n), 1)
-                    if name == "p2p" and world == 2:
+                    if name in ("p2p", "p2p_host") and world == 2:
                         # the result bit for bit: prov/coll's two-rank tree
                         # is x1 + x0 (coll_coll.c:409-430), one fp32 add
                         torch.cuda.synchronize()
