@@ -687,13 +687,20 @@ def extra_config1_two_process(timeout_s: float = 120.0) -> dict:
             return {"error": f"probe exited {p.returncode}: {p.stderr[-200:]}"}
         d = json.loads(lines[-1])
         r = (d.get("rank0") or {}).get("p2p_4096", {})
+        h = (d.get("rank0") or {}).get("p2p_host_4096", {})
         return {"us_median": r.get("median_us"), "us_p10": r.get("p10_us"),
                 "us_p90": r.get("p90_us"), "n": r.get("reps"),
                 "c_loop_mean_us": r.get("c_loop_mean_us"),
                 "exact": bool(r.get("exact")) and bool(
                     (d.get("rank1") or {}).get("p2p_4096", {}).get("exact")),
+                "pinned_host_buffers": {
+                    "us_median": h.get("median_us"), "us_p10": h.get("p10_us"),
+                    "us_p90": h.get("p90_us"), "c_loop_mean_us": h.get("c_loop_mean_us"),
+                    "exact": bool(h.get("exact")) and bool(
+                        (d.get("rank1") or {}).get("p2p_host_4096", {}).get("exact"))},
                 "what": "2 processes on this GPU, GPU peer domains, LFA_ALGO_P2P one-shot + "
-                        "completion word; Python-timed submit + wait per operation"}
+                        "completion word; Python-timed submit + wait per operation; device "
+                        "buffers, and pinned host buffers (the one-shot on their mappings)"}
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"[:200]}
 

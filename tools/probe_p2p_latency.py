@@ -63,7 +63,8 @@ def _worker(rank, world, port, reps, quick, q, only=None):
                     ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10)))
             if quick:
-                plan = (("p2p", coll.ALGO_P2P, (4096,), reps),)
+                plan = (("p2p", coll.ALGO_P2P, (4096,), reps),
+                        ("p2p_host", coll.ALGO_P2P, (4096,), reps))
             if only:
                 # --only name:size[,size...]
                 name, sizes = only.split(":")
