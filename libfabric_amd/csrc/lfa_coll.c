@@ -507,6 +507,9 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		for (int i = 0; i < LFA_STAGE_POOL; i++)
 			if (ep->stage[i].p)
 				hipFree(ep->stage[i].p);
+		for (int i = 0; i < LFA_BOUNCE_POOL; i++)
+			if (ep->bounce[i].p)
+				hipHostFree(ep->bounce[i].p);
 		for (int i = 0; i < ep->nev; i++)
 			hipEventDestroy(ep->evpool[i]);
 		done_word_free(ep, drained);
@@ -850,6 +853,11 @@ struct hop {
 	size_t out_bytes;
 	hipEvent_t in_ev, out_ev;
 	int in_waited;
+	/* pageable host buffers of a small operation: a pinned bounce block
+	 * (ep->bounce) holds the input and the result; the result is copied to
+	 * bounce_user on the CPU when the hop completes (bounce_finish) */
+	void *bounce, *bounce_out, *bounce_user;
+	size_t bounce_bytes;
 	/* a device hop whose every item is on the stream: a later P2P hop may
 	 * enqueue behind it (stream order) without waiting for it to finish */
 	int issued;
@@ -984,6 +992,43 @@ size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep)
 	return n;
 }
 
+/* A free pinned bounce block (2 x LFA_BOUNCE_BYTES), or NULL when all are
+ * busy or none can be allocated (ep->lock held). */
+static void *bounce_get(struct lfa_coll_ep *ep)
+{
+	for (int i = 0; i < LFA_BOUNCE_POOL; i++) {
+		struct bounce_buf *b = &ep->bounce[i];
+
+		if (b->busy)
+			continue;
+		if (!b->p && hipHostMalloc(&b->p, 2 * (size_t)LFA_BOUNCE_BYTES, 0) != hipSuccess) {
+			(void)hipGetLastError();
+			b->p = NULL;
+			return NULL;
+		}
+		b->busy = 1;
+		return b->p;
+	}
+	return NULL;
+}
+
+static void bounce_put(struct lfa_coll_ep *ep, void *p)
+{
+	for (int i = 0; p && i < LFA_BOUNCE_POOL; i++)
+		if (ep->bounce[i].p == p)
+			ep->bounce[i].busy = 0;
+}
+
+/* A completed hop's result to the caller's pageable buffer (the kernels
+ * wrote it to the bounce block's mapping; the completion word or event
+ * that ended the hop made it visible to the host). */
+static void bounce_finish(struct hop *h)
+{
+	if (h->bounce_bytes)
+		memcpy(h->bounce_user, h->bounce_out, h->bounce_bytes);
+	h->bounce_bytes = 0;
+}
+
 static void hop_free(struct hop *h)
 {
 	if (!h)
@@ -1014,6 +1059,9 @@ static void hop_free(struct hop *h)
 	} else {
 		free(h->tmp);
 	}
+	/* after the stream sync above when the hop had not finished (a hop
+	 * that failed before it became a device hop never launched) */
+	bounce_put(h->ep, h->bounce);
 	free(h->r.reqs);
 	free(h);
 }
@@ -1098,6 +1146,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 
 				if (*(volatile uint64_t *)ep->done_word >= h->r.x.done_val) {
 					ep->word_ops++;
+					bounce_finish(h);
 					h->done = 1;
 					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
 				} else if (word_overdue(ep, ep->done_word, h->r.stream, &h->ww,
@@ -1114,6 +1163,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 			last = h->out_ev ? h->out_ev : h->fin;
 			e = hipEventQuery(last);
 			if (e == hipSuccess) {
+				bounce_finish(h);
 				h->done = 1;
 				LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
 			} else if (e != hipErrorNotReady &&
@@ -2646,6 +2696,32 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 			buf = zb;
 			result = zr;
 			dev = 1;
+		} else if (count * esz <= LFA_BOUNCE_BYTES && (h->bounce = bounce_get(ep))) {
+			/* pageable buffers of a small operation: the input copied
+			 * into a pinned bounce block on the CPU, the schedule run on
+			 * the block's mapping, the result copied back when the hop
+			 * completes — no H2D / D2H copies and their events (2
+			 * processes, 4 KiB: DESIGN.md §7 round 5) */
+			char *bin = h->bounce, *bout = bin + LFA_BOUNCE_BYTES;
+			size_t moff, mlen;
+
+			lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
+			h->bounce_out = bout;
+			h->bounce_user = result;
+			h->bounce_bytes = !result ? 0 : coll == LFA_REDUCE_SCATTER ? mlen * esz :
+					  count * esz;
+			zb = zero_copy_of(bin, ep->dom->device);
+			zr = zero_copy_of(bout, ep->dom->device);
+			if (!zb || !zr) {
+				bounce_put(ep, h->bounce);
+				h->bounce = NULL;
+				h->bounce_bytes = 0;
+			} else {
+				memcpy(bin, buf, count * esz);
+				buf = zb;
+				result = result ? zr : NULL;
+				dev = 1;
+			}
 		}
 	}
 	/* P2P keeps its schedule on device buffers (the peers' symmetric

@@ -27,6 +27,9 @@
 /* Bytes of one P2P handle-exchange record (struct sym_rec, lfa_coll.c). */
 #define LFA_SYM_REC_BYTES 80
 #define LFA_STAGE_POOL 128              /* peer-domain staging buffers kept */
+#define LFA_BOUNCE_POOL 8               /* pinned host bounce blocks kept */
+#define LFA_BOUNCE_BYTES (1u << 20)     /* per operand: the largest operation of a
+					 * pageable host member copied through one */
 #define LFA_EXPORT_TRIES 4              /* workspace allocations per growth
 					 * whose IPC export may be refused */
 /* idle staging bytes the pool keeps by default (the endpoint's
@@ -161,6 +164,14 @@ struct lfa_coll_ep {
 		uint64_t used;      /* stage_clock at the last stage_get */
 	} stage[LFA_STAGE_POOL];
 	uint64_t stage_clock;
+	/* peer domains: pinned host blocks (input half, output half) that a
+	 * pageable host member's small P2P operation is copied through on the
+	 * CPU, so its kernels run on the block's mapping instead of staging the
+	 * buffers through HBM; allocated on first use, freed at close */
+	struct bounce_buf {
+		void *p;
+		int busy;
+	} bounce[LFA_BOUNCE_POOL];
 	size_t stage_cap;           /* idle staging bytes kept */
 	int stage_trim_due;         /* idle bytes passed the cap: trim when the
 				     * queue has drained */

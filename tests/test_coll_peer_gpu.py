@@ -687,6 +687,76 @@ def test_p2p_pinned_host_members():
     _spawn(_pinned_member_worker, 3)
 
 
+def _bounce_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        msg = "ok"
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            ep.set_group_chunk(0)
+            # 20 operations in flight: more than the 8 bounce blocks, so the
+            # later ones stage; sizes on both sides of LFA_BOUNCE_BYTES
+            ops = []
+            for k in range(20):
+                nbytes = (4096, 65536 + 4, 1 << 20, (1 << 20) + 8)[k % 4]
+                kind = ("allreduce", "reduce_scatter", "reduce")[k % 3]
+                n = nbytes // 8
+                sends = _inputs(oracle, 9, n, world, 1500 + k)
+                want = oracle.allreduce(3, 9, sends)[0]
+                # rank 0 pageable numpy, rank 1 device
+                x = sends[rank].copy() if rank == 0 else _dev(sends[rank])
+                if kind == "reduce_scatter":
+                    off, ln = coll.block(n, world, rank)
+                    want = want[off:off + ln]
+                    cnt_out = max(ln, 1)
+                else:
+                    cnt_out = n
+                r = (np.zeros(cnt_out, np.float64) if rank == 0
+                     else torch.zeros(cnt_out * 8, dtype=torch.uint8, device="cuda"))
+                _ready()
+                if kind == "allreduce":
+                    ctx = ep.allreduce(x, r, n, 9, 3)
+                elif kind == "reduce_scatter":
+                    ctx = ep.reduce_scatter(x, r, n, 9, 3)
+                else:
+                    ctx = ep.reduce(x, r, n, k % 2, 9, 3)
+                check = kind != "reduce" or rank == k % 2
+                ops.append((ctx, r, want if check else None, f"{kind} {nbytes} B #{k}"))
+            ep.wait(ops[-1][0], timeout_s=60)
+            for ctx, r, want, what in ops:
+                if want is None:
+                    continue
+                got = r if rank == 0 else r.cpu().numpy().view(np.float64)
+                if got[:want.size].tobytes() != want.tobytes():
+                    msg = f"{what} wrong"
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_p2p_pageable_member_bounce_blocks():
+    """A PAGEABLE host member (numpy) under LFA_ALGO_P2P: operations of at
+    most LFA_BOUNCE_BYTES go through a pinned bounce block (input copied in
+    on the CPU at submit, the schedule on the block's mapping, the result
+    copied out at completion); 20 in flight, more than the pool's 8 blocks,
+    so later ones and the larger ones stage through HBM as before.
+    allreduce, ragged reduce_scatter, reduce to either root, double PROD,
+    bit-exact with the oracle."""
+    _spawn(_bounce_worker, 2)
+
+
 def _chunk_error_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),

@@ -60,6 +60,7 @@ def _worker(rank, world, port, reps, quick, q, only=None):
         try:
             plan = (("p2p", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("p2p_host", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
+                    ("p2p_pageable", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("p2p_rs", coll.ALGO_P2P, (4096, 65536, 1 << 20), reps),
                     ("tree", coll.ALGO_TREE, (4096,), max(reps // 10, 10)))
             if quick:
@@ -81,6 +82,13 @@ def _worker(rank, world, port, reps, quick, q, only=None):
 
                         def op():
                             return ep.reduce_scatter(x, r, cnt, 9, 3)
+                    elif name == "p2p_pageable":   # pageable HOST buffers (malloc)
+                        cnt = nbytes // 4
+                        x = torch.rand(cnt)
+                        r = torch.empty_like(x)
+
+                        def op():
+                            return ep.allreduce(x, r, cnt, 8, 2)
                     elif name == "p2p_host":   # pinned HOST buffers
                         cnt = nbytes // 4
                         x = torch.rand(cnt).pin_memory()
@@ -116,7 +124,7 @@ def _worker(rank, world, port, reps, quick, q, only=None):
                     dt_, op_ = (9, 3) if name == "p2p_rs" else (8, 2)
                     out[f"{name}_{nbytes}"]["c_loop_mean_us"] = round(
                         ep.bench_loop(kind, x, r, cnt, dt_, op_, reps=n), 1)
-                    if name in ("p2p", "p2p_host") and world == 2:
+                    if name in ("p2p", "p2p_host", "p2p_pageable") and world == 2:
                         # the result bit for bit: prov/coll's two-rank tree
                         # is x1 + x0 (coll_coll.c:409-430), one fp32 add
                         torch.cuda.synchronize()
