@@ -67,6 +67,8 @@ static void *zero_copy_of(const void *p, int dev)
 }
 
 static void p2p_release(struct lfa_coll_mc *mc);
+static void bounce_put(struct lfa_coll_ep *ep, void *p);
+static void bounce_free_all(struct lfa_coll_ep *ep, int drained);
 static void ws_domain_ref(int delta);
 
 int lfa_coll_get_unique_id(void *id, size_t len)
@@ -507,9 +509,7 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 		for (int i = 0; i < LFA_STAGE_POOL; i++)
 			if (ep->stage[i].p)
 				hipFree(ep->stage[i].p);
-		for (int i = 0; i < LFA_BOUNCE_POOL; i++)
-			if (ep->bounce[i].p)
-				hipHostFree(ep->bounce[i].p);
+		bounce_free_all(ep, drained);
 		for (int i = 0; i < ep->nev; i++)
 			hipEventDestroy(ep->evpool[i]);
 		done_word_free(ep, drained);
@@ -526,6 +526,9 @@ int lfa_coll_ep_close(struct lfa_coll_ep *ep)
 	for (size_t i = 0; i < ep->qlen; i++)
 		if (ep->q[(ep->qhead + i) % ep->qcap].ev)
 			hipEventDestroy(ep->q[(ep->qhead + i) % ep->qcap].ev);
+	for (size_t i = 0; i < ep->qlen; i++)
+		bounce_put(ep, ep->q[(ep->qhead + i) % ep->qcap].bounce);
+	bounce_free_all(ep, drained);
 	for (int i = 0; i < ep->nev; i++)
 		hipEventDestroy(ep->evpool[i]);
 	done_word_free(ep, drained);
@@ -1019,6 +1022,17 @@ static void bounce_put(struct lfa_coll_ep *ep, void *p)
 			ep->bounce[i].busy = 0;
 }
 
+/* Endpoint close: the pinned bounce blocks back to the runtime, or, when
+ * the endpoint did not drain (a kernel may still write one), kept. */
+static void bounce_free_all(struct lfa_coll_ep *ep, int drained)
+{
+	for (int i = 0; i < LFA_BOUNCE_POOL; i++) {
+		if (ep->bounce[i].p && drained)
+			hipHostFree(ep->bounce[i].p);
+		ep->bounce[i].p = NULL;
+	}
+}
+
 /* A completed hop's result to the caller's pageable buffer (the kernels
  * wrote it to the bounce block's mapping; the completion word or event
  * that ended the hop made it visible to the host). */
@@ -1270,8 +1284,10 @@ static void pending_release(struct lfa_coll_ep *ep, struct pending *p)
 		hop_free(p->hop);
 	else if (p->ev)
 		release_event(ep, p->ev);
+	bounce_put(ep, p->bounce);
 	p->hop = NULL;
 	p->ev = NULL;
+	p->bounce = NULL;
 }
 
 /* Reap completed operations in issue order. */
@@ -1296,6 +1312,11 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 				p->pmc->sig_failed = 1;
 			st = -1;
 			perr = ETIMEDOUT;
+		}
+		if (st == 0 && p->bounce_bytes) {
+			/* a bounced operation's result to the caller's buffer */
+			memcpy(p->bounce_user, p->bounce_out, p->bounce_bytes);
+			p->bounce_bytes = 0;
 		}
 		if (p->chain && p->chain == ep->failed_chain) {
 			/* a chunk of an operation whose error was already
@@ -2908,8 +2929,8 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	size_t esz, chunk;
 	uint64_t t0, done_val = 0;
 	const uint64_t *done_w = NULL;
-	int root = -1, ret, host, chunkable;
-	void *zb = NULL, *zr = NULL;
+	int root = -1, ret, host, chunkable, zc1 = 0;
+	void *zb = NULL, *zr = NULL, *bnc = NULL;
 
 	if (!ep)
 		return -LFA_EINVAL;
@@ -2975,6 +2996,25 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 				      lfa_coll_group_chunk(ep->group_chunk, mc->size,
 							   count * esz),
 				      ep->chunk);
+	if (count && host && mc->size == 1 &&
+	    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE || coll == LFA_REDUCE_SCATTER)) {
+		zb = zero_copy_of(buf, ep->dom->device);
+		zr = zero_copy_of(result, ep->dom->device);
+		if (zb && zr) {
+			zc1 = 1;
+		} else if (count * esz <= LFA_BOUNCE_BYTES && buf && result && !is_device_ptr(buf) &&
+			   !is_device_ptr(result) && (bnc = bounce_get(ep))) {
+			zb = zero_copy_of(bnc, ep->dom->device);
+			zr = zero_copy_of((char *)bnc + LFA_BOUNCE_BYTES, ep->dom->device);
+			if (zb && zr) {
+				memcpy(bnc, buf, count * esz);
+				zc1 = 2;
+			} else {
+				bounce_put(ep, bnc);
+				bnc = NULL;
+			}
+		}
+	}
 	if (!count) {
 		ret = 0;
 	} else if (!host && chunk && chunkable &&
@@ -2991,14 +3031,12 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		ep->allow_direct = 0;
 		done_val = ep->op_done_val;
 		done_w = ep->op_done_w;
-	} else if (mc->size == 1 &&
-		   (coll == LFA_ALLREDUCE || coll == LFA_REDUCE ||
-		    coll == LFA_REDUCE_SCATTER) &&
-		   (zb = zero_copy_of(buf, ep->dom->device)) &&
-		   (zr = zero_copy_of(result, ep->dom->device))) {
+	} else if (zc1) {
 		/* a one-member group's reducing collective is a copy; with
 		 * pinned host buffers it runs on their mappings over PCIe, no
-		 * staging (32 MiB 1.35 -> 0.93 ms) */
+		 * staging (32 MiB 1.35 -> 0.93 ms);
+		 * pageable ones of at most LFA_BOUNCE_BYTES through a pinned
+		 * bounce block (copied in here, out when reaped) */
 		if (count * esz <= solo_bytes()) {
 			ep->op_done_val = 0;
 			ep->op_done_w = NULL;
@@ -3029,6 +3067,18 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 	}
 	if (!ret)
 		ret = enqueue_completion(ep, ep->stream, context, 0, NULL, done_val, done_w);
+	if (!ret && bnc) {
+		struct pending *p = &ep->q[(ep->qhead + ep->qlen - 1) % ep->qcap];
+
+		p->bounce = bnc;
+		p->bounce_out = (char *)bnc + LFA_BOUNCE_BYTES;
+		p->bounce_user = result;
+		p->bounce_bytes = count * esz;   /* one member: its block is everything */
+	} else if (bnc) {
+		/* the copy may be on the stream: wait before reusing the block */
+		hipStreamSynchronize(ep->stream);
+		bounce_put(ep, bnc);
+	}
 	if (!ret)
 		tag_p2p(ep, mc, t0);
 	pthread_mutex_unlock(&ep->lock);

@@ -129,6 +129,11 @@ struct pending {
 	struct word_wait {
 		uint64_t deadline_ns, checked_ns;
 	} ww;
+	/* device domains: a one-member group's operation on pageable host
+	 * buffers run through a pinned bounce block (ep->bounce); its result is
+	 * copied to bounce_user when the operation is reaped */
+	void *bounce, *bounce_out, *bounce_user;
+	size_t bounce_bytes;
 	/* the chunks of one chunked operation (peer_submit_chunked) share a
 	 * nonzero chain id: the operation posts ONE completion — the first
 	 * chunk's error, or the last chunk's success */

@@ -492,6 +492,38 @@ def test_one_member_pinned_host_buffers(coll, ep, zero_copy, monkeypatch):
     assert torch.equal(y, x)
 
 
+def test_one_member_pageable_bounce_blocks(coll, ep):
+    """A one-member group's reducing collectives on PAGEABLE (numpy) buffers
+    of at most LFA_BOUNCE_BYTES go through a pinned bounce block: input
+    copied in at submit, the solo copy on the block's mapping, the result
+    copied out when reaped.  20 in flight (more than the 8 blocks: the rest
+    stage), odd sizes at odd offsets, sizes past the bound, a device buf
+    with a pageable result (staged); every result the copy."""
+    rng = np.random.default_rng(41)
+    cases = []
+    for k in range(20):
+        nbytes = (4096, 65536 + 3, 1 << 20, (1 << 20) + 5)[k % 4]
+        raw = rng.integers(0, 256, nbytes + 8, dtype=np.uint8)
+        src = raw[k % 3:k % 3 + nbytes]
+        out = np.zeros(nbytes + 8, np.uint8)
+        dst = out[(k + 1) % 5:(k + 1) % 5 + nbytes]
+        name = ("allreduce", "reduce", "reduce_scatter")[k % 3]
+        if name == "allreduce":
+            ctx = ep.allreduce(src, dst, nbytes, 0, 6)      # int8 BOR
+        elif name == "reduce":
+            ctx = ep.reduce(src, dst, nbytes, 0, 0, 6)
+        else:
+            ctx = ep.reduce_scatter(src, dst, nbytes, 0, 6)
+        cases.append((src, dst, f"{name} {nbytes} B #{k}"))
+    ep.wait(ctx, timeout_s=30)
+    for src, dst, what in cases:
+        assert np.array_equal(src, dst), what
+    x = torch.randint(0, 256, (4096,), dtype=torch.uint8, device=DEV)
+    hy = np.zeros(4096, np.uint8)
+    ep.wait(ep.allreduce(x, hy, 4096, 0, 6), timeout_s=30)
+    assert np.array_equal(x.cpu().numpy(), hy)
+
+
 def test_rccl_host_reduce_and_reduce_scatter_chunked(coll, ep):
     """reduce and reduce_scatter on host buffers go through the chunked
     H2D / collective / D2H pipeline (reduce_scatter: one 2-D H2D per chunk);

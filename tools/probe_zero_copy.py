@@ -87,6 +87,7 @@ def copy(L, torch) -> None:
     ATOMIC_WRITE body above), the provider with LFA_HOST_ZERO_COPY=0 (H2D /
     device copy / D2H on three streams), the ATOMIC_WRITE body called
     directly, and a hipMemcpyAsync between the two pinned buffers."""
+    import numpy as np
     from libfabric_amd import coll
     hip = ctypes.CDLL("libamdhip64.so")
     ep = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
@@ -108,6 +109,19 @@ def copy(L, torch) -> None:
             finally:
                 del os.environ["LFA_HOST_ZERO_COPY"]
 
+        px = hx.numpy().copy()          # pageable twins
+        py = np.zeros_like(px)
+
+        def provider_pageable():
+            ep.wait(ep.allreduce(px, py, n, 8, 2))
+
+        def provider_pageable_staged():
+            os.environ["LFA_HOST_ZERO_COPY"] = "0"
+            try:
+                ep.wait(ep.allreduce(px, py, n, 8, 2))
+            finally:
+                del os.environ["LFA_HOST_ZERO_COPY"]
+
         def zero_copy():
             assert L.lfa_atomic_write_async(11, 1, ctypes.c_void_p(hy.data_ptr()),
                                             ctypes.c_void_p(hx.data_ptr()),
@@ -123,11 +137,15 @@ def copy(L, torch) -> None:
             torch.cuda.synchronize()
 
         for name, fn in (("provider", provider), ("provider_staged", provider_staged),
+                         ("provider_pageable", provider_pageable),
+                         ("provider_pageable_staged", provider_pageable_staged),
                          ("zero_copy", zero_copy),
                          ("hip_memcpy", memcpy_async)):
             hy.zero_()
+            py[:] = 0
             fn()
-            ok = bool(torch.equal(hy, hx))
+            ok = bool(torch.equal(hy, hx)) if "pageable" not in name else \
+                bool(np.array_equal(py, px))
             ts = []
             for _ in range(7):
                 t0 = time.perf_counter()
