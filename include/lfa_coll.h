@@ -286,6 +286,13 @@ int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ti
  * error would).  0 or -LFA_EINVAL. */
 int lfa_coll_ep_test_word(struct lfa_coll_ep *ep, int drop_next, long timeout_ms,
 			  int fail_direct);
+/* Test entry: a one-member group's reducing collectives of at most
+ * max_bytes run as the solo copy (default LFA_SOLO_BYTES, 4 MiB); 0 sends
+ * them through the schedule of the endpoint's algorithm instead — under
+ * LFA_ALGO_P2P the one-shot kernel at n = 1 and its completion word, the
+ * device-domain one-shot path that otherwise needs two GPUs.  0 or
+ * -LFA_EINVAL. */
+int lfa_coll_ep_test_solo(struct lfa_coll_ep *ep, size_t max_bytes);
 /* 1 when the endpoint's one-member small operations go through the direct
  * queue, 2 when that queue has failed (they take the HIP launch), 0 when it
  * was never opened (diagnostics, tests). */
@@ -385,6 +392,24 @@ size_t lfa_coll_ws_cached_bytes(void);
  * 4 GiB).  Both kinds are freed when the process's last GPU domain closes.
  * Diagnostics, tests. */
 size_t lfa_coll_ws_quarantined_bytes(void);
+/* The allocation flags P2P workspaces are made with (LFA_WS_MEM, read once
+ * per process): hipDeviceMallocUncached (3, the default),
+ * hipDeviceMallocFinegrained (1) or hipDeviceMallocDefault (0, coarse).
+ * Every byte of a workspace is written by peers over xGMI while its owner's
+ * kernels run. */
+int lfa_coll_ws_mem(void);
+/* A group's P2P workspaces as this member maps them (diagnostics, tests):
+ * the kind they were allocated with, the region size (0: none yet), and
+ * hipPointerGetAttributes' allocationFlags of each member's workspace as
+ * mapped here (its own allocation at this rank, the IPC mappings of the
+ * others).  0 or -LFA_E*. */
+struct lfa_ws_info {
+	int mem;
+	int mapped;                     /* workspaces mapped here, own included */
+	size_t region;
+	unsigned alloc_flags[32];       /* [group rank] */
+};
+int lfa_mc_ws_info(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, struct lfa_ws_info *out);
 
 /* ---- schedules as data ------------------------------------------------ */
 

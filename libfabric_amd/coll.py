@@ -114,6 +114,12 @@ def lib() -> ctypes.CDLL:
     L.lfa_mc_counters.argtypes = [c_void_p, c_uint64, P(McCounters)]
     L.lfa_mc_seed_ticket.restype = c_int
     L.lfa_mc_seed_ticket.argtypes = [c_void_p, c_uint64, c_uint64]
+    L.lfa_mc_ws_info.restype = c_int
+    L.lfa_mc_ws_info.argtypes = [c_void_p, c_uint64, P(WsInfo)]
+    L.lfa_coll_ep_test_solo.restype = c_int
+    L.lfa_coll_ep_test_solo.argtypes = [c_void_p, c_size_t]
+    L.lfa_coll_ws_mem.restype = c_int
+    L.lfa_coll_ws_mem.argtypes = []
     L.lfa_coll_ep_test_word.restype = c_int
     L.lfa_coll_ep_test_word.argtypes = [c_void_p, c_int, ctypes.c_long, c_int]
     L.lfa_coll_ep_uses_direct.restype = c_int
@@ -346,6 +352,20 @@ class McCounters(ctypes.Structure):
                 ("flag_barriers", ctypes.c_uint64), ("timed_out", ctypes.c_int)]
 
 
+class WsInfo(ctypes.Structure):
+    """struct lfa_ws_info (include/lfa_coll.h)."""
+    _fields_ = [("mem", ctypes.c_int), ("mapped", ctypes.c_int),
+                ("region", ctypes.c_size_t), ("alloc_flags", ctypes.c_uint * 32)]
+
+
+WS_MEM = {0: "coarse", 1: "fine", 3: "uncached"}   # hipDeviceMalloc* flags
+
+
+def ws_mem() -> str:
+    """lfa_coll_ws_mem: the kind P2P workspaces are allocated as (LFA_WS_MEM)."""
+    return WS_MEM.get(lib().lfa_coll_ws_mem(), "other")
+
+
 class OneShot(ctypes.Structure):
     """struct lfa_oneshot (libfabric_amd/csrc/lfa_signal.h): one rank's
     one-shot reduction over the members' symmetric workspaces."""
@@ -437,6 +457,19 @@ class Endpoint:
     def stage_bytes(self) -> int:
         """lfa_coll_ep_stage_bytes: device bytes in the staging pool."""
         return lib().lfa_coll_ep_stage_bytes(self.ep)
+
+    def ws_info(self, coll_addr: int | None = None) -> dict:
+        """lfa_mc_ws_info: the group's P2P workspaces as mapped here."""
+        w = WsInfo()
+        _chk(lib().lfa_mc_ws_info(self.ep, coll_addr or self.world, ctypes.byref(w)),
+             "lfa_mc_ws_info")
+        return {"mem": WS_MEM.get(w.mem, "other"), "mapped": w.mapped, "region": w.region,
+                "alloc_flags": list(w.alloc_flags[:max(w.mapped, 0)])}
+
+    def test_solo(self, max_bytes: int) -> None:
+        """lfa_coll_ep_test_solo (test entry): one-member reducing collectives
+        above max_bytes leave the solo copy for the algorithm's schedule."""
+        _chk(lib().lfa_coll_ep_test_solo(self.ep, max_bytes), "lfa_coll_ep_test_solo")
 
     def seed_ticket(self, ticket: int, coll_addr: int | None = None) -> None:
         """lfa_mc_seed_ticket (test entry): the group's P2P tickets continue

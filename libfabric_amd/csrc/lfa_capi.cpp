@@ -386,10 +386,13 @@ int lfa_oneshot_reduce_async(int op, int dt, const struct lfa_oneshot *a,
 }  // extern "C"
 
 namespace {
-// Per-device staging context for lfa_atomic_write_staged: two streams, the
-// slot events and an HBM staging buffer that only grows.  Created on first
-// use and kept for the life of the process (a hipMalloc + hipFree per call
-// costs milliseconds and serialises the device).
+// Staging contexts for lfa_atomic_write_staged: two streams, the slot events
+// and an HBM staging buffer that only grows.  kStageSlots per device, each
+// with its own lock, so concurrent host-buffer callers on one device run at
+// once instead of queueing behind one caller's PCIe transfer;
+// a caller takes a free slot, and waits on one only when all are busy.
+// Created on first use and kept for the life of the process (a hipMalloc +
+// hipFree per call costs milliseconds and serialises the device).
 struct StagingCtx {
   pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
   hipStream_t s_in = nullptr, s_out = nullptr;
@@ -398,7 +401,19 @@ struct StagingCtx {
   size_t cap = 0;
 };
 constexpr int kMaxDevices = 64;
-StagingCtx g_staging[kMaxDevices];
+constexpr int kStageSlots = 4;
+StagingCtx g_staging[kMaxDevices][kStageSlots];
+unsigned g_stage_next[kMaxDevices];
+
+// A staging slot of device `devno`, locked; staging_release unlocks it.
+StagingCtx &staging_lock(int devno) {
+  for (StagingCtx &c : g_staging[devno])
+    if (!pthread_mutex_trylock(&c.lock)) return c;
+  StagingCtx &c = g_staging[devno][__atomic_fetch_add(&g_stage_next[devno], 1u,
+                                                      __ATOMIC_RELAXED) % kStageSlots];
+  pthread_mutex_lock(&c.lock);
+  return c;
+}
 
 int staging_acquire(StagingCtx &c, size_t bytes) {
   if (!c.s_in) {
@@ -425,14 +440,50 @@ bool zero_copy_on() {
   return !e || strtol(e, nullptr, 0);
 }
 
+// Temporary registrations: pageable operands lfa_atomic_write_staged pins
+// for one call (hipHostRegister), refcounted by exact (address, length) so
+// callers combining the same buffer share one.  A registration's page range
+// is in this table from before hipHostRegister until after hipHostUnregister
+// (states PENDING -> READY -> DYING), and every classification checks the
+// table first: a page range in it is never handed out as a zero-copy address
+// (the call that made it may unregister it at any moment), and an operand
+// overlapping another call's registration is staged.  g_reg_lock covers the
+// table and the classifications — never a registration, a kernel or a
+// stream synchronisation (holding it across the
+// combine stalled every endpoint's submit for the whole PCIe transfer).
+enum { kRegFree = 0, kRegPending, kRegReady, kRegDying };
+struct TempReg {
+  int state;
+  uintptr_t lo, hi;  // the page range
+  const void *p;
+  size_t bytes;
+  void *d;           // its device address once READY
+  int refs;
+};
+constexpr int kTempRegs = 64;
+TempReg g_temp[kTempRegs];
+pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+constexpr uintptr_t kPage = 4096;
+
+// The entry overlapping the pages of [p, p + bytes), or -1 (g_reg_lock held).
+int temp_find(const void *p, size_t bytes) {
+  const uintptr_t lo = (uintptr_t)p & ~(kPage - 1);
+  const uintptr_t hi = ((uintptr_t)p + (bytes ? bytes : 1) + kPage - 1) & ~(kPage - 1);
+  for (int i = 0; i < kTempRegs; i++)
+    if (g_temp[i].state != kRegFree && g_temp[i].lo < hi && lo < g_temp[i].hi) return i;
+  return -1;
+}
+
 // The address a kernel on device `devno` uses for operand p, or null when
 // the operand must be staged: device memory of this device as it is, pinned
 // or registered host memory through its device mapping (zero-copy: the
-// combine reads and writes it over PCIe).  *pageable: p is host memory HIP
-// does not know, which the caller may register for the call.
-void *zero_copy_addr(const void *p, int devno, bool *pageable) {
+// combine reads and writes it over PCIe) — never a temporary registration.
+// *pageable: p is host memory HIP does not know, which the caller may
+// register for the call.  g_reg_lock held.
+void *zero_copy_addr(const void *p, size_t bytes, int devno, bool *pageable) {
   hipPointerAttribute_t a;
   *pageable = false;
+  if (temp_find(p, bytes) >= 0) return nullptr;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
     *pageable = true;
@@ -443,13 +494,6 @@ void *zero_copy_addr(const void *p, int devno, bool *pageable) {
   if (a.type == hipMemoryTypeDevice && a.device == devno) return const_cast<void *>(p);
   return nullptr;
 }
-
-// Temporary registrations (pageable operands pinned for one call) exist
-// only while g_reg_lock is held, and every zero-copy classification takes
-// it (here and lfa_zero_copy_addr, the provider's): so no caller takes a
-// temporary registration for pinned memory and keeps using its mapping
-// after the call that made it has unregistered it.
-pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
 
 // Pin pageable operand p (bytes long) for one call; its device address, or
 // null if the runtime refuses (overlapping registrations, read-only pages):
@@ -466,6 +510,61 @@ void *register_for_call(const void *p, size_t bytes) {
     return nullptr;
   }
   return d;
+}
+
+// A temporary registration of exactly [p, p + bytes) for this call: a READY
+// one shared (refs + 1), else a new one; its index and device address, or -1
+// (the pages overlap another call's registration, the table is full, or the
+// runtime refused): the caller stages.
+int temp_take(const void *p, size_t bytes, void **d) {
+  pthread_mutex_lock(&g_reg_lock);
+  int i = temp_find(p, bytes);
+  if (i >= 0) {
+    TempReg &t = g_temp[i];
+    const bool share = t.state == kRegReady && t.p == p && t.bytes == bytes;
+    if (share) {
+      t.refs++;
+      *d = t.d;
+    }
+    pthread_mutex_unlock(&g_reg_lock);
+    return share ? i : -1;
+  }
+  for (i = 0; i < kTempRegs && g_temp[i].state != kRegFree; i++) {
+  }
+  if (i == kTempRegs) {
+    pthread_mutex_unlock(&g_reg_lock);
+    return -1;
+  }
+  g_temp[i] = TempReg{kRegPending, (uintptr_t)p & ~(kPage - 1),
+                      ((uintptr_t)p + bytes + kPage - 1) & ~(kPage - 1), p, bytes, nullptr, 1};
+  pthread_mutex_unlock(&g_reg_lock);
+  void *dp = register_for_call(p, bytes);  // outside the lock: milliseconds
+  pthread_mutex_lock(&g_reg_lock);
+  if (dp) {
+    g_temp[i].state = kRegReady;
+    g_temp[i].d = dp;
+  } else {
+    g_temp[i].state = kRegFree;
+  }
+  pthread_mutex_unlock(&g_reg_lock);
+  *d = dp;
+  return dp ? i : -1;
+}
+
+// This call is done with registration i: the last user unregisters it (the
+// pages stay in the table as DYING until hipHostUnregister has returned).
+void temp_drop(int i) {
+  if (i < 0) return;
+  pthread_mutex_lock(&g_reg_lock);
+  const bool last = --g_temp[i].refs == 0;
+  if (last) g_temp[i].state = kRegDying;
+  const void *p = g_temp[i].p;
+  pthread_mutex_unlock(&g_reg_lock);
+  if (!last) return;
+  hipHostUnregister(const_cast<void *>(p));
+  pthread_mutex_lock(&g_reg_lock);
+  g_temp[i].state = kRegFree;
+  pthread_mutex_unlock(&g_reg_lock);
 }
 }  // namespace
 
@@ -488,38 +587,31 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
   int devno = 0;
   if (hipGetDevice(&devno) != hipSuccess || devno < 0 || devno >= kMaxDevices)
     return -LFA_EINVAL;
-  StagingCtx &c = g_staging[devno];
-  bool pd = false, ps = false, held = false;
+  const size_t bytes = cnt * esz;
+  bool pd = false, ps = false;
   void *zd = nullptr, *zs = nullptr;
-  const void *reg[2] = {};
+  int reg[2] = {-1, -1};
   if (zero_copy_on()) {
     pthread_mutex_lock(&g_reg_lock);
-    held = true;
-    zd = zero_copy_addr(dst, devno, &pd);
-    zs = zero_copy_addr(src, devno, &ps);
+    zd = zero_copy_addr(dst, bytes, devno, &pd);
+    zs = zero_copy_addr(src, bytes, devno, &ps);
+    pthread_mutex_unlock(&g_reg_lock);
     if ((zd || pd) && (zs || ps) && (pd || ps)) {
       // pageable operands are pinned for the call: registration + the
       // zero-copy combine beats the runtime's staging of pageable memory
       // (4 MiB 0.419 -> 0.256 ms, 256 MiB 15.4 -> 11.5 ms,
       // profiles/r05_zero_copy_pageable.log)
-      const size_t bytes = cnt * esz;
-      if (pd && (zd = register_for_call(dst, bytes))) reg[0] = dst;
+      if (pd) reg[0] = temp_take(dst, bytes, &zd);
       if (ps && src == dst) zs = zd;
-      else if (ps && (zs = register_for_call(src, bytes))) reg[1] = src;
+      else if (ps) reg[1] = temp_take(src, bytes, &zs);
     }
     if (!zd || !zs) {
       // stage instead
       zd = zs = nullptr;
-      for (const void *&p : reg)
-        if (p) hipHostUnregister(const_cast<void *>(p)), p = nullptr;
-    }
-    if (!reg[0] && !reg[1]) {
-      // no temporary registration: nothing to hold the lock for
-      pthread_mutex_unlock(&g_reg_lock);
-      held = false;
+      for (int &i : reg) temp_drop(i), i = -1;
     }
   }
-  pthread_mutex_lock(&c.lock);
+  StagingCtx &c = staging_lock(devno);
   if (zd && zs) {
     // every operand reachable from the device: one combine over the mapped
     // buffers, no HBM round trip (256 MiB float SUM, both pinned: 9.96 ms
@@ -528,9 +620,7 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     if (!ret) ret = kWrite[op](dt, zd, zs, cnt, c.s_out);
     if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
     pthread_mutex_unlock(&c.lock);
-    for (const void *p : reg)
-      if (p) hipHostUnregister(const_cast<void *>(p));
-    if (held) pthread_mutex_unlock(&g_reg_lock);
+    for (int i : reg) temp_drop(i);
     return ret;
   }
   int ret = staging_acquire(c, 4 * slot);
@@ -561,9 +651,17 @@ void *lfa_zero_copy_addr(const void *p, int device) {
   if (!p || !zero_copy_on()) return nullptr;
   bool pageable;
   pthread_mutex_lock(&g_reg_lock);
-  void *r = zero_copy_addr(p, device, &pageable);
+  void *r = zero_copy_addr(p, 1, device, &pageable);
   pthread_mutex_unlock(&g_reg_lock);
   return r;
+}
+
+int lfa__temp_registrations(void) {
+  int n = 0;
+  pthread_mutex_lock(&g_reg_lock);
+  for (const TempReg &t : g_temp) n += t.state != kRegFree;
+  pthread_mutex_unlock(&g_reg_lock);
+  return n;
 }
 
 size_t lfa_host_small_bytes(void) {

@@ -70,6 +70,7 @@ static void p2p_release(struct lfa_coll_mc *mc);
 static void bounce_put(struct lfa_coll_ep *ep, void *p);
 static void bounce_free_all(struct lfa_coll_ep *ep, int drained);
 static void ws_domain_ref(int delta);
+static size_t solo_bytes(void);
 
 int lfa_coll_get_unique_id(void *id, size_t len)
 {
@@ -191,6 +192,7 @@ static void word_wait_start(const struct lfa_coll_ep *ep, struct word_wait *ww)
 {
 	ww->checked_ns = mono_ns();
 	ww->deadline_ns = ww->checked_ns + ep->word_timeout_ns;
+	ww->armed = 1;
 }
 
 /* A word not yet at its value: 1 still pending, -1 failed with *perr =
@@ -198,8 +200,15 @@ static void word_wait_start(const struct lfa_coll_ep *ep, struct word_wait *ww)
 static int word_overdue(const struct lfa_coll_ep *ep, const uint64_t *w, hipStream_t s,
 			struct word_wait *ww, int *perr)
 {
-	const uint64_t now = mono_ns();
+	uint64_t now;
 
+	if (!ww->armed) {
+		/* first poll at the head of the queue: nothing ahead of this
+		 * operation is still owed, its own bound starts now */
+		word_wait_start(ep, ww);
+		return 1;
+	}
+	now = mono_ns();
 	if (now - ww->checked_ns < LFA_WORD_CHECK_NS)
 		return 1;
 	ww->checked_ns = now;
@@ -371,6 +380,7 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	/* device domains choose per bucket; peer domains run the tree */
 	ep->algo = d->host ? LFA_ALGO_TREE : LFA_ALGO_AUTO;
 	ep->chunk = LFA_DEFAULT_CHUNK;
+	ep->solo_max = solo_bytes();
 	{
 		const char *e = getenv("LFA_SIG_TIMEOUT_MS");
 		const long ms = e ? atol(e) : 0;
@@ -674,6 +684,16 @@ uint64_t lfa_coll_ep_word_ops(struct lfa_coll_ep *ep)
 	return n;
 }
 
+int lfa_coll_ep_test_solo(struct lfa_coll_ep *ep, size_t max_bytes)
+{
+	if (!ep || max_bytes > ((size_t)1 << 30))
+		return -LFA_EINVAL;
+	pthread_mutex_lock(&ep->lock);
+	ep->solo_max = max_bytes;
+	pthread_mutex_unlock(&ep->lock);
+	return 0;
+}
+
 int lfa_coll_ep_uses_direct(struct lfa_coll_ep *ep)
 {
 	if (!ep)
@@ -697,6 +717,36 @@ int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ti
 	else
 		mc->p2p_ticket = ticket;
 	pthread_mutex_unlock(&ep->lock);
+	return ret;
+}
+
+int lfa_mc_ws_info(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, struct lfa_ws_info *out)
+{
+	struct lfa_coll_mc *mc;
+	int ret = 0;
+
+	if (!ep || !out)
+		return -LFA_EINVAL;
+	mc = mc_of(ep, coll_addr);
+	memset(out, 0, sizeof(*out));
+	out->mem = lfa_coll_ws_mem();
+	pthread_mutex_lock(&ep->comm_lock);
+	out->region = mc->sym_region;
+	for (int k = 0; mc->sym && k < mc->size && k < LFA_SIG_MAX && !ret; k++) {
+		hipPointerAttribute_t at;
+
+		memset(&at, 0, sizeof(at));
+		if (!mc->sym[k])
+			continue;
+		if (hipPointerGetAttributes(&at, mc->sym[k]) != hipSuccess) {
+			(void)hipGetLastError();
+			ret = -LFA_EIO;
+			break;
+		}
+		out->alloc_flags[k] = at.allocationFlags;
+		out->mapped++;
+	}
+	pthread_mutex_unlock(&ep->comm_lock);
 	return ret;
 }
 
@@ -809,7 +859,7 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 		 * no event to record or query */
 		p->done_val = done_val;
 		p->done_w = done_w;
-		word_wait_start(ep, &p->ww);
+		/* p->ww stays unarmed: its bound starts at the head of the queue */
 		if (ep->drop_words > 0) {
 			/* test knob: a value the word never reaches */
 			ep->drop_words--;
@@ -1123,7 +1173,7 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 
 			if (!h->issued && h->r.x.done_val) {
 				h->issued = 1;
-				word_wait_start(ep, &h->ww);
+				h->ww.armed = 0;    /* armed at the head of the queue */
 				if (ep->drop_words > 0) {
 					ep->drop_words--;
 					h->r.x.done_val |= 1ull << 62;
@@ -1163,7 +1213,8 @@ static void host_progress_all(struct lfa_coll_ep *ep)
 					bounce_finish(h);
 					h->done = 1;
 					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
-				} else if (word_overdue(ep, ep->done_word, h->r.stream, &h->ww,
+				} else if (i == 0 &&    /* only the head's bound runs */
+					   word_overdue(ep, ep->done_word, h->r.stream, &h->ww,
 							&werr) < 0) {
 					/* ETIMEDOUT / EIO as the error entry's err;
 					 * a stream's HIP code as its prov_errno */
@@ -1839,8 +1890,44 @@ static uint64_t ws_identity(void)
 	       (uint64_t)ts.tv_nsec ^ ((uint64_t)ts.tv_sec << 30) ^ 1;
 }
 
+/*
+ * The memory a P2P workspace is allocated from (LFA_WS_MEM, read once per
+ * process; every member of a group must use the same kind).  Peers write
+ * every byte a member reads from its own workspace — the posted epochs, the
+ * one-shot slots, the pushed blocks — over xGMI while the member's kernels
+ * run, so the workspace is allocated UNCACHED by default
+ * (hipExtMallocWithFlags(hipDeviceMallocUncached), MTYPE UC in the GPU page
+ * tables of the owner AND of every peer that maps it): no L2 of any GPU ever
+ * holds a line of it, so a post or a push is visible to the owner's next
+ * load whatever cache state the owner's earlier accesses left.  HIP's
+ * default device memory is coarse-grained: its coherence is only guaranteed
+ * at kernel boundaries and synchronisation points, which is exactly what a
+ * flag polled inside a running kernel does not have.
+ *   uncached (default)  hipDeviceMallocUncached
+ *   fine                hipDeviceMallocFinegrained
+ *   coarse              hipMalloc's memory (rounds 1-5; A/B only)
+ */
+int lfa_coll_ws_mem(void)
+{
+	static int f = -1;
+
+	if (f < 0) {
+		const char *e = getenv("LFA_WS_MEM");
+
+		f = !e || !*e || !strcmp(e, "uncached") ? hipDeviceMallocUncached :
+		    !strcmp(e, "fine") ? hipDeviceMallocFinegrained :
+		    !strcmp(e, "coarse") ? hipDeviceMallocDefault : hipDeviceMallocUncached;
+	}
+	return f;
+}
+
+static hipError_t ws_malloc(char **p, size_t bytes)
+{
+	return hipExtMallocWithFlags((void **)p, bytes, (unsigned)lfa_coll_ws_mem());
+}
+
 /* A workspace of 2·region + the flag area: a kept one of that size, else a
- * new allocation (hipMalloc's result). */
+ * new allocation of LFA_WS_MEM's kind. */
 static hipError_t ws_alloc(char **p, size_t region)
 {
 	const size_t bytes = 2 * region + LFA_SIG_AREA_BYTES;
@@ -1848,7 +1935,7 @@ static hipError_t ws_alloc(char **p, size_t region)
 	*p = ws_take(bytes);
 	if (*p)
 		return hipSuccess;
-	return hipMalloc((void **)p, bytes);
+	return ws_malloc(p, bytes);
 }
 
 /* The flag area zeroed (epoch 0) and the identity word written, before any
@@ -1911,7 +1998,7 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
 	ok = ok && mc->sym;
 	ok = ok && lfa_hip_note(why, ws_alloc(&mc->sym_local, region),
-				"P2P workspace hipMalloc") == hipSuccess;
+				"P2P workspace allocation") == hipSuccess;
 	if (!ok)
 		mc->sym_local = NULL;
 	mine->id = ws_identity();
@@ -1957,9 +2044,9 @@ static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
 		while (!ok && mc->sym_local && nref < LFA_EXPORT_TRIES) {
 			refused[nref++] = mc->sym_local;
 			mc->sym_local = NULL;
-			ok = lfa_hip_note(why, hipMalloc((void **)&mc->sym_local,
+			ok = lfa_hip_note(why, ws_malloc(&mc->sym_local,
 							 2 * region + LFA_SIG_AREA_BYTES),
-					  "P2P workspace hipMalloc (replacement)") == hipSuccess;
+					  "P2P workspace allocation (replacement)") == hipSuccess;
 			if (!ok) {
 				mc->sym_local = NULL;
 				break;
@@ -2449,7 +2536,7 @@ static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		return ret;
 	if (mc->size == 1 && s == ep->stream && ep->done_word &&
 	    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE || coll == LFA_REDUCE_SCATTER) &&
-	    count * esz <= solo_bytes())
+	    count * esz <= ep->solo_max)
 		return run_solo(ep, buf, result, count, dt);
 	if (algo == LFA_ALGO_AUTO)
 		algo = (enum lfa_coll_algo)lfa_coll_auto_algo(coll, count, mc->size, esz,
@@ -2727,6 +2814,13 @@ static int host_start(struct lfa_coll_ep *ep, struct hop *h,
 			size_t moff, mlen;
 
 			lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
+			/* a non-root member of a reduce has no result: the kernels never
+			 * write the block's output half, so nothing is copied back
+			 * (the half still held an earlier operation's bytes,
+			 * and an in-place caller's input was overwritten with them) —
+			 * the staged path's out_bytes rule below */
+			if (coll == LFA_REDUCE && mc->rank != root)
+				result = NULL;
 			h->bounce_out = bout;
 			h->bounce_user = result;
 			h->bounce_bytes = !result ? 0 : coll == LFA_REDUCE_SCATTER ? mlen * esz :
@@ -3037,7 +3131,7 @@ static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
 		 * staging (32 MiB 1.35 -> 0.93 ms);
 		 * pageable ones of at most LFA_BOUNCE_BYTES through a pinned
 		 * bounce block (copied in here, out when reaped) */
-		if (count * esz <= solo_bytes()) {
+		if (count * esz <= ep->solo_max) {
 			ep->op_done_val = 0;
 			ep->op_done_w = NULL;
 			ret = run_solo(ep, zb, zr, count, dt);

@@ -125,9 +125,12 @@ struct pending {
 	const uint64_t *done_w;
 	/* word operations: when the operation fails if its word has not come,
 	 * and when the queue or stream owing it was last asked for an error
-	 * (lfa_coll.c word_overdue) */
+	 * (lfa_coll.c word_overdue); armed: the bound runs from the first poll
+	 * that finds the operation at the head of the queue, so an operation
+	 * queued behind a long one is not charged for its wait */
 	struct word_wait {
 		uint64_t deadline_ns, checked_ns;
+		int armed;
 	} ww;
 	/* device domains: a one-member group's operation on pageable host
 	 * buffers run through a pinned bounce block (ep->bounce); its result is
@@ -213,6 +216,9 @@ struct lfa_coll_ep {
 	 * drop_words words unreachable (lfa_coll_ep_test_word) */
 	uint64_t word_timeout_ns;
 	int drop_words;
+	/* a one-member group's reducing collectives of at most this many bytes
+	 * run as the solo copy (LFA_SOLO_BYTES at open; lfa_coll_ep_test_solo) */
+	size_t solo_max;
 	uint64_t word_ops;          /* operations reaped through a word */
 	int nev;
 	struct plan_cache {         /* last schedules built, keyed by shape */

@@ -614,6 +614,73 @@ def test_released_workspaces_are_reused(cap):
     _spawn(_ws_cycle_worker, 4, args=(cap,))
 
 
+def _ws_mem_worker(rank, world, port, q, kind):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        if kind is not None:
+            os.environ["LFA_WS_MEM"] = kind
+        _share_gpu(world)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        want_kind = kind or "uncached"
+        assert coll.ws_mem() == want_kind, (coll.ws_mem(), want_kind)
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            ep.set_group_chunk(0)
+            # one-shot (flags + slots), then the two-barrier form (staging
+            # copy, flag barriers, system-scope tree_put over the peers'
+            # workspaces, unstage) and a growth, then one-shots again on the
+            # grown workspace: every word a peer writes lives in the kind
+            for k, (dt, op, n) in enumerate(((8, 2, 1024), (9, 3, 5000), (8, 2, 3 << 20),
+                                             (6, 6, 700_001), (8, 2, 4097), (1, 7, 33))):
+                sends = _inputs(oracle, dt, n, world, 31 + k)
+                want = oracle.allreduce(op, dt, sends)[0]
+                xs = _dev(sends[rank])
+                r = torch.zeros_like(xs)
+                _ready()
+                ep.wait(ep.allreduce(xs, r, n, dt, op))
+                assert r.cpu().numpy().tobytes() == want.tobytes(), f"allreduce {k}"
+                off, ln = coll.block(n, world, rank)
+                rs = torch.zeros(max(ln, 1), dtype=xs.dtype, device="cuda")
+                _ready()
+                ep.wait(ep.reduce_scatter(xs, rs, n, dt, op))
+                assert rs[:ln].cpu().numpy().tobytes() == want[off:off + ln].tobytes(), \
+                    f"reduce_scatter {k}"
+            c = ep.counters()
+            assert c["oneshot"] >= 6 and c["flag_barriers"] >= 4, c
+            info = ep.ws_info()
+            assert info["mem"] == want_kind and info["mapped"] == world, info
+            assert info["region"] >= (3 << 20) * 4, info
+            assert not ep.transport_errors, ep.transport_errors
+        finally:
+            ep.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,kind", [(2, None), (3, None), (8, None), (2, "fine"),
+                                        (2, "coarse")],
+                         ids=["2-uncached-default", "3-uncached-default", "8-uncached-default",
+                              "2-fine", "2-coarse"])
+def test_p2p_workspace_memory_kind(world, kind):
+    """peers post epochs, push one-shot slots and write
+    blocks into a member's workspace while its kernels run, so on the 8-GPU
+    node those writes cross xGMI into the owner's HBM.  The workspace is
+    allocated uncached by default (hipDeviceMallocUncached: no GPU's L2 holds
+    its lines), exported and mapped over IPC like before; the one-shot and
+    two-barrier P2P paths and a growth run on it bit-exact, and every member
+    maps every peer's workspace.  fine / coarse (LFA_WS_MEM) are the A/B."""
+    _spawn(_ws_mem_worker, world, args=(kind,))
+
+
 def _pinned_member_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
@@ -718,7 +785,9 @@ def _bounce_worker(rank, world, port, q):
                     cnt_out = max(ln, 1)
                 else:
                     cnt_out = n
-                r = (np.zeros(cnt_out, np.float64) if rank == 0
+                # a non-root's result is never written — rank 0's
+                # holds a sentinel that must survive
+                r = (np.full(cnt_out, -12345.5, np.float64) if rank == 0
                      else torch.zeros(cnt_out * 8, dtype=torch.uint8, device="cuda"))
                 _ready()
                 if kind == "allreduce":
@@ -728,7 +797,17 @@ def _bounce_worker(rank, world, port, q):
                 else:
                     ctx = ep.reduce(x, r, n, k % 2, 9, 3)
                 check = kind != "reduce" or rank == k % 2
+                if not check and rank == 0:
+                    want = np.full(cnt_out, -12345.5, np.float64)
+                    check = True
                 ops.append((ctx, r, want if check else None, f"{kind} {nbytes} B #{k}"))
+            # a non-root in-place reduce (buf == result) keeps its input
+            n = 4096 // 8
+            sends = _inputs(oracle, 9, n, world, 1777)
+            x = sends[rank].copy() if rank == 0 else _dev(sends[rank])
+            _ready()
+            ops.append((ep.reduce(x, x, n, 1, 9, 3), x,
+                        sends[0] if rank == 0 else None, "in-place non-root reduce"))
             ep.wait(ops[-1][0], timeout_s=60)
             for ctx, r, want, what in ops:
                 if want is None:

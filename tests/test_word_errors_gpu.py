@@ -160,3 +160,88 @@ def test_direct_queue_reopens_after_failed_one_is_released(coll, monkeypatch):
     finally:
         e.close()
 
+
+
+def test_device_domain_one_shot_reaps_through_the_word(coll):
+    """exec_plan hands the one-shot launch's word
+    value back to the submit, so a device domain's one-shot operations
+    complete through the completion word, not an event.  The one-shot plan
+    needs a group of 2..8 on device domains, i.e. two GPUs; lfa_coll_ep_test_solo
+    sends a one-member group's small reducing collectives through the
+    schedule of the endpoint's algorithm instead of the solo copy, so under
+    LFA_ALGO_P2P they run the n = 1 one-shot kernel through the same
+    run_device / exec_plan path.  Each of allreduce, reduce and reduce_scatter
+    must be reaped through the word (lfa_coll_ep_word_ops), counted as a
+    one-shot (lfa_mc_counters) and give its input back; a dropped word then
+    fails that one operation once, with ETIMEDOUT."""
+    e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    try:
+        e.test_solo(0)
+        e.set_algo(coll.ALGO_P2P)
+        src = torch.arange(3 * 1024, dtype=torch.float32, device=DEV).view(3, 1024) - 7.5
+        out = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        w0, c0 = e.word_ops(), e.counters()
+        e.wait(e.allreduce(src[0], out[0], 1024, FLOAT, SUM))
+        e.wait(e.reduce(src[1], out[1], 1024, 0, FLOAT, SUM))
+        e.wait(e.reduce_scatter(src[2], out[2], 1024, FLOAT, SUM))
+        torch.cuda.synchronize()
+        assert torch.equal(out, src)
+        c1 = e.counters()
+        assert c1["oneshot"] - c0["oneshot"] == 3, (c0, c1)
+        assert e.word_ops() - w0 == 3, (w0, e.word_ops())
+        # the word's error path on this form: one dropped word, one entry
+        out.zero_()
+        torch.cuda.synchronize()
+        e.test_word(drop_next=1, timeout_ms=300)
+        k0 = e.allreduce(src[0], out[0], 1024, FLOAT, SUM)
+        k1 = e.allreduce(src[1], out[1], 1024, FLOAT, SUM)
+        ok, errs = _drain(e, 1)
+        assert ok == [k1]
+        assert [(x[0], x[2]) for x in errs] == [(errno.ETIMEDOUT, k0)]
+        assert e.cq_readerr() is None
+        torch.cuda.synchronize()
+        assert torch.equal(out[:2], src[:2])
+    finally:
+        e.close()
+
+
+def test_word_bound_starts_at_the_head_of_the_queue(coll, monkeypatch):
+    """a word operation's bound runs from when it reaches the head
+    of the endpoint's in-order queue, not from its submit.  The endpoint's
+    stream is held ~1 s by a spin kernel, a large allreduce (event-completed)
+    is queued on it, then a small one completed by the word with a 300 ms
+    bound.  The small one's kernel runs ~1 s after its submit, so a bound
+    counted from the submit failed it with ETIMEDOUT; from the head it
+    completes normally."""
+    monkeypatch.setenv("LFA_DIRECT", "0")
+    e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    try:
+        big = torch.rand(8 << 20 >> 2, device=DEV)
+        big_out = torch.zeros_like(big)
+        x = torch.rand(1024, device=DEV)
+        y = torch.zeros_like(x)
+        torch.cuda.synchronize()
+        e.wait(e.allreduce(x, y, 1024, FLOAT, SUM))     # warm: solo path, word
+        # calibrate the spin kernel's cycles per second
+        t0 = time.monotonic()
+        torch.cuda._sleep(50_000_000)
+        torch.cuda.synchronize()
+        per_s = 50_000_000 / max(time.monotonic() - t0, 1e-4)
+        e.test_word(timeout_ms=300)
+        s = torch.cuda.ExternalStream(e.stream_handle(), device=torch.device(DEV))
+        w0 = e.word_ops()
+        t0 = time.monotonic()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(int(per_s * 1.0))
+        k0 = e.allreduce(big, big_out, big.numel(), FLOAT, SUM)
+        k1 = e.allreduce(x, y, 1024, FLOAT, SUM)
+        ok, errs = _drain(e, 2, timeout_s=20.0)
+        took = time.monotonic() - t0
+        assert errs == [] and ok == [k0, k1], (ok, errs)
+        assert took > 0.6, took     # the stream was held: the bound was tested
+        assert e.word_ops() - w0 == 1
+        torch.cuda.synchronize()
+        assert torch.equal(big_out, big) and torch.equal(y, x)
+    finally:
+        e.close()

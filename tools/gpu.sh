@@ -169,6 +169,13 @@ for stage in "$@"; do
     tunecomb)
       $S tune_combine 500 python3 -u tools/tune_combine.py --sizes "${COMBINE_SIZES:-32,64,256}" \
         --variants "${COMBINE_VARIANTS:-30,80,81,82,83,84}" --rounds "${COMBINE_ROUNDS:-12}" || exit 99 ;;
+    wsmem)
+      # P2P workspace memory kinds (LFA_WS_MEM): 2-process P2P allreduce
+      # latency (one-shot sizes) and bulk (two-barrier) per kind
+      for kind in ${WSMEM_KINDS:-uncached coarse fine}; do
+        LFA_WS_MEM=$kind $S "wsmem_$kind" 300 python3 -u tools/probe_p2p_latency.py --world 2 \
+          --reps "${WSMEM_REPS:-300}" --only "p2p:${WSMEM_SIZES:-4096,65536,1048576,16777216,67108864}" || exit 99
+      done ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac

@@ -132,6 +132,8 @@ def _worker(rank, world, port, reps, quick, q, only=None):
                         dist.all_gather(xs, x.cpu())
                         out[f"{name}_{nbytes}"]["exact"] = bool(torch.equal(r.cpu(), xs[1] + xs[0]))
             out["kfd_queues"] = _kfd_queues()
+            out["ws_mem"] = coll.ws_mem()
+            out["ws_info"] = ep.ws_info()
         finally:
             ep.close()
         dist.barrier()
