@@ -149,9 +149,12 @@ def build_coll(verbose: bool = False) -> str | None:
     src = os.path.join(CSRC, "lfa_coll.c")
     if not os.path.exists(src):
         return None
-    # API + groups, executor + transports, planner, single-GPU loopback
+    # API + endpoints, completion words, P2P workspaces, host buffers, group
+    # join, executor + transports, planner, single-GPU loopback
     srcs = [src] + [os.path.join(CSRC, f) for f in
-                    ("lfa_coll_exec.c", "lfa_coll_plan.c", "lfa_coll_loopback.c")]
+                    ("lfa_coll_word.c", "lfa_coll_ws.c", "lfa_coll_host.c",
+                     "lfa_coll_group.c", "lfa_coll_exec.c", "lfa_coll_plan.c",
+                     "lfa_coll_loopback.c")]
     hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "lfa_atomic.h"),
             os.path.join(INC, "lfa_fabric.h"), os.path.join(CSRC, "lfa_coll_plan.h"),
             os.path.join(CSRC, "lfa_coll_int.h"), os.path.join(CSRC, "lfa_signal.h"), LIB_LFA]

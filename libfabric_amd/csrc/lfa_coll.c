@@ -41,36 +41,6 @@
 
 #include "lfa_coll_int.h"
 
-/* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
- * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
-#define LFA_DEFAULT_CHUNK (32u << 20)
-
-static int is_device_ptr(const void *p)
-{
-	hipPointerAttribute_t a;
-
-	if (!p)
-		return 0;
-	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-		(void)hipGetLastError();
-		return 0;
-	}
-	return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
-}
-
-/* Zero-copy operand address (lfa_zero_copy_addr, liblfa: pinned or
- * registered host memory through its mapping, `dev`'s memory as it is), or
- * NULL: stage. */
-static void *zero_copy_of(const void *p, int dev)
-{
-	return lfa_zero_copy_addr(p, dev);
-}
-
-static void p2p_release(struct lfa_coll_mc *mc);
-static void bounce_put(struct lfa_coll_ep *ep, void *p);
-static void bounce_free_all(struct lfa_coll_ep *ep, int drained);
-static void ws_domain_ref(int delta);
-static size_t solo_bytes(void);
 
 int lfa_coll_get_unique_id(void *id, size_t len)
 {
@@ -164,181 +134,6 @@ int lfa_coll_domain_close(struct lfa_coll_domain *d)
 		ws_domain_ref(-1);
 	free(d);
 	return 0;
-}
-
-static uint64_t mono_ns(void)
-{
-	struct timespec t;
-
-	clock_gettime(CLOCK_MONOTONIC, &t);
-	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
-}
-
-/*
- * Operations completed by a host-mapped word.  The host reads
- * the word on every poll; a word that never comes — the queue or stream owing
- * it failed, or its kernel never ran — would otherwise hold every later
- * completion of the endpoint (they are reaped in issue order).  So at most
- * every LFA_WORD_CHECK_NS a poll also asks the direct queue whether it has
- * failed, or the stream whether it reports an error, and past the deadline
- * (LFA_SIG_TIMEOUT_MS after the submit, the bound of every other GPU wait of
- * the provider) the operation fails with ETIMEDOUT.  The failing operation
- * is reaped once, as an error entry; the word's later arrival is harmless,
- * the words only ever grow.
- */
-#define LFA_WORD_CHECK_NS 1000000ull
-
-static void word_wait_start(const struct lfa_coll_ep *ep, struct word_wait *ww)
-{
-	ww->checked_ns = mono_ns();
-	ww->deadline_ns = ww->checked_ns + ep->word_timeout_ns;
-	ww->armed = 1;
-}
-
-/* A word not yet at its value: 1 still pending, -1 failed with *perr =
- * ETIMEDOUT, EIO (the direct queue failed) or the stream's HIP error code. */
-static int word_overdue(const struct lfa_coll_ep *ep, const uint64_t *w, hipStream_t s,
-			struct word_wait *ww, int *perr)
-{
-	uint64_t now;
-
-	if (!ww->armed) {
-		/* first poll at the head of the queue: nothing ahead of this
-		 * operation is still owed, its own bound starts now */
-		word_wait_start(ep, ww);
-		return 1;
-	}
-	now = mono_ns();
-	if (now - ww->checked_ns < LFA_WORD_CHECK_NS)
-		return 1;
-	ww->checked_ns = now;
-	if (ep->direct && w == ep->ddone_word) {
-		if (lfa_direct_failed(ep->direct)) {
-			*perr = EIO;
-			return -1;
-		}
-	} else if (s) {
-		hipError_t e = hipStreamQuery(s);
-
-		if (e != hipSuccess && e != hipErrorNotReady) {
-			(void)hipGetLastError();
-			*perr = (int)e;
-			return -1;
-		}
-	}
-	if (now >= ww->deadline_ns) {
-		*perr = ETIMEDOUT;
-		return -1;
-	}
-	return 1;
-}
-
-/* The completion word and its counter (device endpoints), zeroed. */
-static int done_word_init(struct lfa_coll_ep *ep)
-{
-	if (hipMalloc((void **)&ep->done_ctr, sizeof(uint32_t)) != hipSuccess) {
-		ep->done_ctr = NULL;
-		return -1;
-	}
-	if (hipHostMalloc((void **)&ep->done_word, sizeof(uint64_t),
-			  hipHostMallocCoherent) != hipSuccess) {
-		ep->done_word = NULL;
-		return -1;
-	}
-	*(volatile uint64_t *)ep->done_word = 0;
-	return hipMemset(ep->done_ctr, 0, sizeof(uint32_t)) == hipSuccess ? 0 : -1;
-}
-
-/*
- * One direct queue per device and process, shared by its endpoints (each
- * keeps its own counter and completion word): a hardware queue is a scarce
- * resource — past ~20 on the GPU the scheduler time-slices —
- * and the queue's packets run in order whichever endpoint wrote them.
- */
-#define DIRECT_DEVS 64
-static struct {
-	struct lfa_direct *d;
-	int refs, failed;
-} shared_direct[DIRECT_DEVS];
-static pthread_mutex_t direct_lock = PTHREAD_MUTEX_INITIALIZER;
-
-static struct lfa_direct *direct_acquire(int dev)
-{
-	struct lfa_direct *d = NULL;
-
-	if (dev < 0 || dev >= DIRECT_DEVS)
-		return NULL;
-	pthread_mutex_lock(&direct_lock);
-	if (!shared_direct[dev].d && !shared_direct[dev].failed) {
-		shared_direct[dev].d = lfa_direct_open(dev);
-		shared_direct[dev].failed = !shared_direct[dev].d;
-	}
-	d = shared_direct[dev].d;
-	if (d)
-		shared_direct[dev].refs++;
-	pthread_mutex_unlock(&direct_lock);
-	return d;
-}
-
-static void direct_release(int dev)
-{
-	pthread_mutex_lock(&direct_lock);
-	if (shared_direct[dev].d && --shared_direct[dev].refs == 0) {
-		lfa_direct_close(shared_direct[dev].d);
-		shared_direct[dev].d = NULL;
-	}
-	pthread_mutex_unlock(&direct_lock);
-}
-
-/*
- * `stream_ok`: the endpoint's streams drained (lfa_coll_ep_flush), so no
- * kernel on them still writes done_ctr / done_word.  The direct queue's
- * kernels are on no stream: its last word is awaited (bounded).  A counter
- * or word that a packet still queued may write is never freed:
- * it is left allocated, with the queue reference that keeps the queue alive,
- * and the leak is reported on stderr.
- */
-static void done_word_free(struct lfa_coll_ep *ep, int stream_ok)
-{
-	if (ep->direct) {
-		const uint64_t t0 = mono_ns();
-
-		/* a failed queue's kernels may still finish (a test marks a
-		 * working queue failed): a short grace, else the full bound */
-		while (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq &&
-		       mono_ns() - t0 < (lfa_direct_failed(ep->direct) ? 100000000ull
-								 : ep->word_timeout_ns))
-			sched_yield();
-		if (*(volatile uint64_t *)ep->ddone_word < ep->ddone_seq) {
-			fprintf(stderr, "lfa: endpoint closed with direct-queue word %llu of %llu: "
-				"its counter, word and queue are left allocated\n",
-				(unsigned long long)*(volatile uint64_t *)ep->ddone_word,
-				(unsigned long long)ep->ddone_seq);
-			ep->ddone_ctr = NULL;
-			ep->ddone_word = NULL;
-		} else {
-			direct_release(ep->dom->device);
-		}
-		ep->direct = NULL;
-	}
-	if (!stream_ok && ep->done_word) {
-		fprintf(stderr, "lfa: endpoint closed with its stream not drained: its "
-			"completion counter and word are left allocated\n");
-		ep->done_ctr = NULL;
-		ep->done_word = NULL;
-	}
-	if (ep->ddone_ctr)
-		hipFree(ep->ddone_ctr);
-	if (ep->ddone_word)
-		hipHostFree(ep->ddone_word);
-	ep->ddone_ctr = NULL;
-	ep->ddone_word = NULL;
-	if (ep->done_ctr)
-		hipFree(ep->done_ctr);
-	if (ep->done_word)
-		hipHostFree(ep->done_word);
-	ep->done_ctr = NULL;
-	ep->done_word = NULL;
 }
 
 /* Frees whatever lfa_coll_ep_open managed to create (open's error path). */
@@ -439,63 +234,6 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	}
 	*out = ep;
 	return 0;
-}
-
-static void hop_free(struct hop *h);
-
-static void sig_word_free(struct lfa_coll_mc *mc)
-{
-	if (mc->sig_word)
-		hipHostFree(mc->sig_word);
-	mc->sig_word = NULL;
-}
-
-/*
- * Before a P2P operation of `mc`: its timed-out-wait word exists (allocated
- * at the group's first P2P operation: host-mapped, LFA_SIG_NONE) and no wait
- * of the group has timed out — after one the members' flag epochs disagree
- * and a barrier could pass on stale posts, so the group refuses P2P
- * operations (close and re-join it); other groups are unaffected.
- */
-static int sig_ready(struct lfa_coll_mc *mc)
-{
-	if (mc->sig_failed)
-		return -LFA_EIO;
-	if (!mc->sig_word) {
-		hipSetDevice(mc->ep->dom->device);
-		if (hipHostMalloc((void **)&mc->sig_word, sizeof(uint64_t),
-				  hipHostMallocCoherent) != hipSuccess) {
-			mc->sig_word = NULL;
-			return -LFA_ENOMEM;
-		}
-		*(volatile uint64_t *)mc->sig_word = LFA_SIG_NONE;
-	}
-	if (*(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE)
-		return -LFA_EIO;
-	return 0;
-}
-
-/* The operation just queued ran P2P kernels on `mc` if its ticket moved. */
-static void tag_p2p(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc, uint64_t t0)
-{
-	struct pending *p;
-
-	if (!ep->qlen || mc->p2p_ticket == t0)
-		return;
-	p = &ep->q[(ep->qhead + ep->qlen - 1) % ep->qcap];
-	p->pmc = mc;
-	p->ticket = mc->p2p_ticket;
-}
-
-/* Did a P2P wait of this operation, or of an earlier one of its group, time
- * out?  (The group's kernels run in order; the word holds the lowest failing
- * ticket.) */
-static int p2p_timed_out(const struct pending *p)
-{
-	if (p->timed_out)
-		return 1;
-	return p->pmc && p->ticket && p->pmc->sig_word &&
-	       *(volatile uint64_t *)p->pmc->sig_word <= p->ticket;
 }
 
 int lfa_coll_ep_close(struct lfa_coll_ep *ep)
@@ -630,7 +368,7 @@ int lfa_mc_group_id(struct lfa_coll_mc *mc)
 	return mc->group_id < LFA_MAX_GROUP_ID ? (int)mc->group_id : -LFA_EAGAIN;
 }
 
-static struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a)
+LFA_INTERNAL struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a)
 {
 	if (a == LFA_ADDR_NOTAVAIL || a == 0)
 		return &ep->world;
@@ -657,99 +395,6 @@ int lfa_mc_counters(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
 	return 0;
 }
 
-int lfa_coll_ep_test_word(struct lfa_coll_ep *ep, int drop_next, long timeout_ms,
-			  int fail_direct)
-{
-	if (!ep || drop_next < 0)
-		return -LFA_EINVAL;
-	pthread_mutex_lock(&ep->lock);
-	ep->drop_words = drop_next;
-	if (timeout_ms > 0)
-		ep->word_timeout_ns = (uint64_t)timeout_ms * 1000000ull;
-	if (fail_direct && ep->direct)
-		lfa__direct_mark_failed(ep->direct);
-	pthread_mutex_unlock(&ep->lock);
-	return 0;
-}
-
-uint64_t lfa_coll_ep_word_ops(struct lfa_coll_ep *ep)
-{
-	uint64_t n;
-
-	if (!ep)
-		return 0;
-	pthread_mutex_lock(&ep->lock);
-	n = ep->word_ops;
-	pthread_mutex_unlock(&ep->lock);
-	return n;
-}
-
-int lfa_coll_ep_test_solo(struct lfa_coll_ep *ep, size_t max_bytes)
-{
-	if (!ep || max_bytes > ((size_t)1 << 30))
-		return -LFA_EINVAL;
-	pthread_mutex_lock(&ep->lock);
-	ep->solo_max = max_bytes;
-	pthread_mutex_unlock(&ep->lock);
-	return 0;
-}
-
-int lfa_coll_ep_uses_direct(struct lfa_coll_ep *ep)
-{
-	if (!ep)
-		return -LFA_EINVAL;
-	return ep->direct ? (lfa_direct_failed(ep->direct) ? 2 : 1) : 0;
-}
-
-int lfa_mc_seed_ticket(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, uint64_t ticket)
-{
-	struct lfa_coll_mc *mc;
-	int ret = 0;
-
-	if (!ep)
-		return -LFA_EINVAL;
-	mc = mc_of(ep, coll_addr);
-	if (!mc)
-		return -LFA_EINVAL;
-	pthread_mutex_lock(&ep->lock);
-	if (ep->qlen)
-		ret = -LFA_EINVAL;
-	else
-		mc->p2p_ticket = ticket;
-	pthread_mutex_unlock(&ep->lock);
-	return ret;
-}
-
-int lfa_mc_ws_info(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, struct lfa_ws_info *out)
-{
-	struct lfa_coll_mc *mc;
-	int ret = 0;
-
-	if (!ep || !out)
-		return -LFA_EINVAL;
-	mc = mc_of(ep, coll_addr);
-	memset(out, 0, sizeof(*out));
-	out->mem = lfa_coll_ws_mem();
-	pthread_mutex_lock(&ep->comm_lock);
-	out->region = mc->sym_region;
-	for (int k = 0; mc->sym && k < mc->size && k < LFA_SIG_MAX && !ret; k++) {
-		hipPointerAttribute_t at;
-
-		memset(&at, 0, sizeof(at));
-		if (!mc->sym[k])
-			continue;
-		if (hipPointerGetAttributes(&at, mc->sym[k]) != hipSuccess) {
-			(void)hipGetLastError();
-			ret = -LFA_EIO;
-			break;
-		}
-		out->alloc_flags[k] = at.allocationFlags;
-		out->mapped++;
-	}
-	pthread_mutex_unlock(&ep->comm_lock);
-	return ret;
-}
-
 /* Grow-only device buffer, stream-ordered so in-flight users stay valid. */
 static int grow(void **buf, size_t *size, size_t need, hipStream_t s)
 {
@@ -767,35 +412,11 @@ static int grow(void **buf, size_t *size, size_t need, hipStream_t s)
 	return 0;
 }
 
-/* Both host-staging slots, always the same size. */
-static int grow_staging(struct lfa_coll_ep *ep, size_t need)
-{
-	void *nb[2];
-
-	if (need <= ep->hs_size)
-		return 0;
-	need = (need + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-	for (int i = 0; i < 2; i++) {
-		if (hipMallocAsync(&nb[i], need, ep->stream) != hipSuccess) {
-			if (i)
-				hipFreeAsync(nb[0], ep->stream);
-			return -LFA_ENOMEM;
-		}
-	}
-	for (int i = 0; i < 2; i++) {
-		if (ep->hs[i])
-			hipFreeAsync(ep->hs[i], ep->stream);
-		ep->hs[i] = nb[i];
-	}
-	ep->hs_size = need;
-	return 0;
-}
-
 /* ---------------------------------------------------------------------- */
 /* completion queue                                                        */
 /* ---------------------------------------------------------------------- */
 
-static void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
+LFA_INTERNAL void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
 {
 	if (ep->nev < (int)(sizeof(ep->evpool) / sizeof(ep->evpool[0])))
 		ep->evpool[ep->nev++] = ev;
@@ -805,7 +426,7 @@ static void release_event(struct lfa_coll_ep *ep, hipEvent_t ev)
 
 /* A completion event from the endpoint's pool (ep->lock held): creating
  * one costs a runtime call per operation otherwise.  NULL on failure. */
-static hipEvent_t event_get(struct lfa_coll_ep *ep)
+LFA_INTERNAL hipEvent_t event_get(struct lfa_coll_ep *ep)
 {
 	hipEvent_t ev;
 
@@ -816,7 +437,7 @@ static hipEvent_t event_get(struct lfa_coll_ep *ep)
 
 /* Room for `n` more operations in the FIFO of in-flight operations (the
  * ring doubles as needed): 0 or -LFA_ENOMEM. */
-static int queue_reserve(struct lfa_coll_ep *ep, size_t n)
+LFA_INTERNAL int queue_reserve(struct lfa_coll_ep *ep, size_t n)
 {
 	size_t cap = ep->qcap;
 
@@ -838,14 +459,14 @@ static int queue_reserve(struct lfa_coll_ep *ep, size_t n)
 }
 
 /* A free slot at the tail of the FIFO of in-flight operations. */
-static struct pending *queue_slot(struct lfa_coll_ep *ep)
+LFA_INTERNAL struct pending *queue_slot(struct lfa_coll_ep *ep)
 {
 	if (queue_reserve(ep, 1))
 		return NULL;
 	return &ep->q[(ep->qhead + ep->qlen) % ep->qcap];
 }
 
-static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
+LFA_INTERNAL int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 			      void *context, int kind, struct lfa_coll_mc *mc,
 			      uint64_t done_val, const uint64_t *done_w)
 {
@@ -884,418 +505,6 @@ static int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
 	p->mc = mc;
 	ep->qlen++;
 	return 0;
-}
-
-
-/*
- * One collective on a host domain: prov/coll's util_coll_operation and its
- * work queue (ofi_coll.h:146-163) — the schedule, its own TMP, and the run.
- */
-struct hop {
-	struct xrun r;
-	struct plan pl;
-	void *tmp;              /* host, or device memory for a device hop */
-	int done, err;
-	int dev;                /* device buffers (xport_peer_dev) */
-	hipEvent_t fin;         /* device hop: the stream reached the end */
-	/* host buffers run as a device hop (LFA_ALGO_P2P on a GPU peer domain:
-	 * every member must follow the one schedule): staged copies, H2D on the
-	 * endpoint's copy stream (in_ev: the run's first item waits for it), D2H
-	 * on its d2h stream after the run (out_ev ends the hop) */
-	void *st_in, *st_out, *user_out;
-	size_t out_bytes;
-	hipEvent_t in_ev, out_ev;
-	int in_waited;
-	/* pageable host buffers of a small operation: a pinned bounce block
-	 * (ep->bounce) holds the input and the result; the result is copied to
-	 * bounce_user on the CPU when the hop completes (bounce_finish) */
-	void *bounce, *bounce_out, *bounce_user;
-	size_t bounce_bytes;
-	/* a device hop whose every item is on the stream: a later P2P hop may
-	 * enqueue behind it (stream order) without waiting for it to finish */
-	int issued;
-	struct word_wait ww;    /* a hop ending in the completion word */
-	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
-	 * (they share the symmetric workspace), then grow it if needed through
-	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
-	int phase;
-	size_t sym_need, sym_size;
-	struct hop *sub;
-	uint16_t sub_seq;
-	int32_t agree_in, agree_out;
-	unsigned char mine[LFA_SYM_REC_BYTES];
-	uint64_t scratch[2];    /* barrier word and its result */
-	struct lfa_coll_ep *ep;
-};
-
-/* A device buffer of at least `bytes` from the endpoint's staging pool (the
- * smallest free one that fits and is at most twice the size, else a free
- * slot (re)allocated to `bytes`), or a plain hipMalloc when every slot is
- * busy; NULL on failure.  ep->lock held.  stage_put returns it.  (Without
- * the factor-2 bound, 32 MiB chunks took the idle 64 MiB buffers of an
- * earlier size first and allocated the rest, so every operation passed the
- * cap and the trim churned: 13.1 -> 19.3 ms for 32 MiB chunks after 64.) */
-static void *stage_get(struct lfa_coll_ep *ep, size_t bytes)
-{
-	struct stage_buf *fit = NULL, *spare = NULL;
-	void *p;
-
-	if (!bytes)
-		bytes = 1;
-	for (int i = 0; i < LFA_STAGE_POOL; i++) {
-		struct stage_buf *b = &ep->stage[i];
-
-		if (b->busy)
-			continue;
-		if (b->p && b->bytes >= bytes && b->bytes / 2 <= bytes &&
-		    (!fit || b->bytes < fit->bytes))
-			fit = b;
-		else if (!spare || (spare->p && !b->p))
-			spare = b;      /* prefer an empty slot */
-	}
-	if (fit) {
-		fit->busy = 1;
-		fit->used = ++ep->stage_clock;
-		return fit->p;
-	}
-	if (spare) {
-		if (spare->p)
-			hipFree(spare->p);
-		spare->p = NULL;
-		spare->bytes = 0;
-		if (hipMalloc(&spare->p, bytes) != hipSuccess) {
-			spare->p = NULL;
-			return NULL;
-		}
-		spare->bytes = bytes;
-		spare->busy = 1;
-		spare->used = ++ep->stage_clock;
-		return spare->p;
-	}
-	return hipMalloc(&p, bytes) == hipSuccess ? p : NULL;
-}
-
-/* Idle bytes in the staging pool (ep->lock held). */
-static size_t stage_idle(const struct lfa_coll_ep *ep)
-{
-	size_t idle = 0;
-
-	for (int i = 0; i < LFA_STAGE_POOL; i++)
-		if (ep->stage[i].p && !ep->stage[i].busy)
-			idle += ep->stage[i].bytes;
-	return idle;
-}
-
-/* Free idle staging buffers, least recently used first, until at most `keep`
- * idle bytes remain (ep->lock held).  hipFree waits for the device, so this
- * runs only where nothing of the endpoint is in flight.  (Largest-first
- * evicted the buffers the current operation size had just allocated, so a
- * size sweep reallocated on every operation: 256 MiB whole 20.3 -> 28.9 ms.) */
-static void stage_trim(struct lfa_coll_ep *ep, size_t keep)
-{
-	while (stage_idle(ep) > keep) {
-		struct stage_buf *old = NULL;
-
-		for (int i = 0; i < LFA_STAGE_POOL; i++) {
-			struct stage_buf *b = &ep->stage[i];
-
-			if (b->p && !b->busy && (!old || b->used < old->used))
-				old = b;
-		}
-		if (!old)
-			break;
-		hipFree(old->p);
-		old->p = NULL;
-		old->bytes = 0;
-	}
-}
-
-/* Back to the pool.  When the pool's idle bytes pass the cap
- * (LFA_STAGE_POOL_BYTES; ADVICE r3: a sweep of sizes or many chunks in
- * flight otherwise pinned the sum of every buffer until close) the excess
- * is freed once the endpoint's queue has drained (progress), not here: a
- * hipFree in the middle of a pipelined operation would stall it (a first
- * form freed here and doubled a 2-process 256 MiB host allreduce in 16 MiB
- * chunks, 13.1 -> 25.7 ms). */
-static void stage_put(struct lfa_coll_ep *ep, void *p)
-{
-	if (!p)
-		return;
-	for (int i = 0; i < LFA_STAGE_POOL; i++)
-		if (ep->stage[i].p == p) {
-			ep->stage[i].busy = 0;
-			if (stage_idle(ep) > ep->stage_cap)
-				ep->stage_trim_due = 1;
-			return;
-		}
-	hipFree(p);
-}
-
-size_t lfa_coll_ep_stage_bytes(struct lfa_coll_ep *ep)
-{
-	size_t n = 0;
-
-	if (!ep)
-		return 0;
-	pthread_mutex_lock(&ep->lock);
-	for (int i = 0; i < LFA_STAGE_POOL; i++)
-		if (ep->stage[i].p)
-			n += ep->stage[i].bytes;
-	pthread_mutex_unlock(&ep->lock);
-	return n;
-}
-
-/* A free pinned bounce block (2 x LFA_BOUNCE_BYTES), or NULL when all are
- * busy or none can be allocated (ep->lock held). */
-static void *bounce_get(struct lfa_coll_ep *ep)
-{
-	for (int i = 0; i < LFA_BOUNCE_POOL; i++) {
-		struct bounce_buf *b = &ep->bounce[i];
-
-		if (b->busy)
-			continue;
-		if (!b->p && hipHostMalloc(&b->p, 2 * (size_t)LFA_BOUNCE_BYTES, 0) != hipSuccess) {
-			(void)hipGetLastError();
-			b->p = NULL;
-			return NULL;
-		}
-		b->busy = 1;
-		return b->p;
-	}
-	return NULL;
-}
-
-static void bounce_put(struct lfa_coll_ep *ep, void *p)
-{
-	for (int i = 0; p && i < LFA_BOUNCE_POOL; i++)
-		if (ep->bounce[i].p == p)
-			ep->bounce[i].busy = 0;
-}
-
-/* Endpoint close: the pinned bounce blocks back to the runtime, or, when
- * the endpoint did not drain (a kernel may still write one), kept. */
-static void bounce_free_all(struct lfa_coll_ep *ep, int drained)
-{
-	for (int i = 0; i < LFA_BOUNCE_POOL; i++) {
-		if (ep->bounce[i].p && drained)
-			hipHostFree(ep->bounce[i].p);
-		ep->bounce[i].p = NULL;
-	}
-}
-
-/* A completed hop's result to the caller's pageable buffer (the kernels
- * wrote it to the bounce block's mapping; the completion word or event
- * that ended the hop made it visible to the host). */
-static void bounce_finish(struct hop *h)
-{
-	if (h->bounce_bytes)
-		memcpy(h->bounce_user, h->bounce_out, h->bounce_bytes);
-	h->bounce_bytes = 0;
-}
-
-static void hop_free(struct hop *h)
-{
-	if (!h)
-		return;
-	hop_free(h->sub);
-	plan_free(&h->pl);
-	if (h->dev) {
-		/* a failed run may have left items on the stream that use tmp, and
-		 * staging copies in flight on the copy streams; a finished one
-		 * has passed its events already */
-		if (!h->done)
-			hipStreamSynchronize(h->r.stream);
-		if (h->in_ev) {
-			if (!h->done)
-				hipEventSynchronize(h->in_ev);
-			release_event(h->ep, h->in_ev);
-		}
-		if (h->out_ev) {
-			if (!h->done)
-				hipEventSynchronize(h->out_ev);
-			release_event(h->ep, h->out_ev);
-		}
-		stage_put(h->ep, h->tmp);
-		stage_put(h->ep, h->st_in);
-		stage_put(h->ep, h->st_out);
-		if (h->fin)
-			release_event(h->ep, h->fin);
-	} else {
-		free(h->tmp);
-	}
-	/* after the stream sync above when the hop had not finished (a hop
-	 * that failed before it became a device hop never launched) */
-	bounce_put(h->ep, h->bounce);
-	free(h->r.reqs);
-	free(h);
-}
-
-enum { HOP_RUN, HOP_WAIT_PRIOR, HOP_SYM_GATHER, HOP_SYM_AGREE };
-static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx);
-
-/* Advance every in-flight host operation (ep->lock held). */
-static void host_progress_all(struct lfa_coll_ep *ep)
-{
-	/* device hops issue HIP calls from whichever thread progresses (e.g.
-	 * off_lfa's progress thread): make the domain's GPU current there */
-	if (ep->dom->device >= 0 && ep->qlen)
-		hipSetDevice(ep->dom->device);
-	for (size_t i = 0; i < ep->qlen; i++) {
-		struct hop *h = ep->q[(ep->qhead + i) % ep->qcap].hop;
-		int ret;
-
-		if (!h || h->done || h->err)
-			continue;
-		if (h->phase != HOP_RUN) {
-			ret = hop_prologue(ep, h, i);
-			if (ret < 0)
-				h->err = ret;
-			if (h->phase != HOP_RUN || h->err)
-				continue;
-		}
-		if (h->in_ev && !h->in_waited) {
-			/* the staged input's H2D (copy stream) before the first item */
-			if (lfa_hip_note(&h->r.hip_err, hipStreamWaitEvent(h->r.stream, h->in_ev, 0),
-					 "staged input wait") != hipSuccess) {
-				h->err = -LFA_EIO;
-				continue;
-			}
-			h->in_waited = 1;
-		}
-		ret = h->issued ? 1 : xrun_advance(&h->r);
-		if (ret < 0) {
-			h->err = ret;
-		} else if (ret && h->dev) {
-			/* done once the stream has run the last local items (and, for
-			 * staged host buffers, the D2H behind them) */
-			hipEvent_t last;
-			hipError_t e;
-
-			if (!h->issued && h->r.x.done_val) {
-				h->issued = 1;
-				h->ww.armed = 0;    /* armed at the head of the queue */
-				if (ep->drop_words > 0) {
-					ep->drop_words--;
-					h->r.x.done_val |= 1ull << 62;
-				}
-				LFA_TRACE("hop cid %#x issued (completion word %llu)",
-					  (unsigned)h->r.cid, (unsigned long long)h->r.x.done_val);
-			}
-			if (!h->issued) {
-				if (!(h->fin = event_get(ep)) ||
-				    lfa_hip_note(&h->r.hip_err, hipEventRecord(h->fin, h->r.stream),
-						 "completion event record") != hipSuccess) {
-					h->err = -LFA_EIO;
-					continue;
-				}
-				if (h->out_bytes &&
-				    (!(h->out_ev = event_get(ep)) ||
-				     lfa_hip_note(&h->r.hip_err,
-						  hipStreamWaitEvent(ep->d2h_stream, h->fin, 0),
-						  "staged result wait") != hipSuccess ||
-				     lfa_hip_note(&h->r.hip_err,
-						  hipMemcpyAsync(h->user_out, h->st_out, h->out_bytes,
-								 hipMemcpyDeviceToHost, ep->d2h_stream),
-						  "staged result D2H") != hipSuccess ||
-				     lfa_hip_note(&h->r.hip_err, hipEventRecord(h->out_ev, ep->d2h_stream),
-						  "staged result event record") != hipSuccess)) {
-					h->err = -LFA_EIO;
-					continue;
-				}
-				h->issued = 1;
-				LFA_TRACE("hop cid %#x issued", (unsigned)h->r.cid);
-			}
-			if (h->r.x.done_val) {
-				int werr = 0;
-
-				if (*(volatile uint64_t *)ep->done_word >= h->r.x.done_val) {
-					ep->word_ops++;
-					bounce_finish(h);
-					h->done = 1;
-					LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
-				} else if (i == 0 &&    /* only the head's bound runs */
-					   word_overdue(ep, ep->done_word, h->r.stream, &h->ww,
-							&werr) < 0) {
-					/* ETIMEDOUT / EIO as the error entry's err;
-					 * a stream's HIP code as its prov_errno */
-					if (werr != ETIMEDOUT && werr != EIO)
-						h->r.hip_err = werr;
-					h->err = werr == ETIMEDOUT ? -ETIMEDOUT : -LFA_EIO;
-					LFA_TRACE("hop cid %#x word overdue (%d)", (unsigned)h->r.cid, werr);
-				}
-				continue;
-			}
-			last = h->out_ev ? h->out_ev : h->fin;
-			e = hipEventQuery(last);
-			if (e == hipSuccess) {
-				bounce_finish(h);
-				h->done = 1;
-				LFA_TRACE("hop cid %#x done", (unsigned)h->r.cid);
-			} else if (e != hipErrorNotReady &&
-				 lfa_hip_note(&h->r.hip_err, e, "completion event query"))
-				h->err = -LFA_EIO;
-		} else if (ret) {
-			h->done = 1;
-		}
-	}
-}
-
-static int enqueue_host(struct lfa_coll_ep *ep, struct hop *h, void *context,
-			int kind, struct lfa_coll_mc *mc)
-{
-	struct pending *p = queue_slot(ep);
-
-	if (!p)
-		return -LFA_ENOMEM;
-	memset(p, 0, sizeof(*p));
-	p->hop = h;
-	p->context = context;
-	p->kind = kind;
-	p->mc = mc;
-	ep->qlen++;
-	/* kick: run up to the first transfer now (coll_progress_work) */
-	host_progress_all(ep);
-	return 0;
-}
-
-static void free_mask(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
-{
-	if (!mc->mask_host)
-		return;
-	if (ep->dom->host)
-		free(mc->mask_host);
-	else
-		hipHostFree(mc->mask_host);
-	mc->mask_host = NULL;
-}
-
-static void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc)
-{
-	/* coll_join_comp (coll_coll.c:690-720): group id = lowest set bit of the
-	 * BAND of every member's free-id mask; mark it used locally. */
-	int gid = -1;
-
-	for (int b = 0; b < LFA_MAX_GROUP_ID; b++) {
-		if (mc->mask_host[b / 8] & (1u << (b % 8))) {
-			gid = b;
-			break;
-		}
-	}
-	if (gid >= 0) {
-		mc->group_id = (uint16_t)gid;
-		ep->cid_mask[gid / 8] &= (uint8_t)~(1u << (gid % 8));
-	}
-	mc->seq = 0;
-	free_mask(ep, mc);
-	if (ep->eqn < 64) {
-		size_t i = (ep->eqh + ep->eqn) % 64;
-
-		ep->eq[i].event = LFA_JOIN_COMPLETE;
-		ep->eq[i].entry.fid = mc;
-		ep->eq[i].entry.context = mc->join_context;
-		ep->eq[i].entry.data = 0;
-		ep->eqn++;
-	}
 }
 
 /* Completion state of a queued operation: 0 done, 1 pending, <0 / hip error
@@ -1520,804 +729,6 @@ int lfa_coll_ep_flush(struct lfa_coll_ep *ep)
 	       hipStreamSynchronize(ep->d2h_stream) == hipSuccess ? 0 : -LFA_EIO;
 }
 
-
-/*
- * The P2P symmetric workspace of `mc`, grown to `region` bytes per region.
- * Collective: every member calls it at the same operation (the need depends
- * only on the operation's shape).  The old workspace is released only after
- * this rank's earlier operations have completed — each of which ends with a
- * barrier, so no peer still touches it — and the members learn each other's
- * new handle through one RCCL allgather of {ok, handle} records: a member
- * that failed to allocate makes them all fail together instead of leaving
- * the others waiting in a later barrier.
- */
-struct sym_rec {
-	int32_t ok;
-	int32_t pad;
-	hipIpcMemHandle_t h;
-	uint64_t id;            /* the workspace's identity word (LFA_SIG_ID_OFF) */
-};
-
-/* Open file descriptors of this process (LFA_DEBUG diagnostics: every
- * exported or imported IPC workspace holds a dma-buf descriptor). */
-static int open_fds(void)
-{
-	DIR *d = opendir("/proc/self/fd");
-	int n = 0;
-
-	if (!d)
-		return -1;
-	while (readdir(d))
-		n++;
-	closedir(d);
-	return n - 3;   /* ".", ".." and the directory's own descriptor */
-}
-
-/*
- * LFA_DEBUG: a history of the P2P workspaces' virtual address ranges in this
- * process — 'A'llocated and 'F'reed local workspaces, 'I'mported and 'C'losed
- * peer mappings — so a failed export can be matched against the ranges the
- * same addresses held before (the hipIpcGetMemHandle
- * "invalid argument" seen at a workspace growth).
- */
-#define VA_HIST 256
-static struct va_ev {
-	char kind;
-	const void *p;
-	size_t bytes;
-	unsigned long long seq;
-} va_hist[VA_HIST];
-static unsigned long long va_n;
-static pthread_mutex_t va_lock = PTHREAD_MUTEX_INITIALIZER;
-
-static int va_debug(void)
-{
-	static int on = -1;
-
-	if (on < 0)
-		on = getenv("LFA_DEBUG") != NULL;
-	return on;
-}
-
-static void va_note(char kind, const void *p, size_t bytes)
-{
-	if (!va_debug() || !p)
-		return;
-	if (!bytes) {
-		void *base = NULL;
-		size_t sz = 0;
-
-		if (hipMemGetAddressRange(&base, &sz, (void *)p) == hipSuccess)
-			bytes = sz;
-		else
-			(void)hipGetLastError();
-	}
-	pthread_mutex_lock(&va_lock);
-	va_hist[va_n % VA_HIST] = (struct va_ev){ kind, p, bytes, va_n };
-	va_n++;
-	pthread_mutex_unlock(&va_lock);
-}
-
-/* Everything the history knows about [p, p + bytes), and what HIP says of p. */
-static void va_explain(const char *what, const void *p, size_t bytes)
-{
-	hipPointerAttribute_t at;
-	void *base = NULL;
-	size_t sz = 0;
-	hipError_t e1, e2;
-
-	if (!va_debug())
-		return;
-	memset(&at, 0, sizeof(at));
-	e1 = hipPointerGetAttributes(&at, p);
-	e2 = hipMemGetAddressRange(&base, &sz, (void *)p);
-	(void)hipGetLastError();
-	fprintf(stderr, "lfa: %s: %p + %zu B; attributes rc %d type %d device %d "
-		"devptr %p hostptr %p; range rc %d base %p size %zu; %d fds open\n",
-		what, p, bytes, (int)e1, (int)at.type, at.device, at.devicePointer,
-		at.hostPointer, (int)e2, base, sz, open_fds());
-	pthread_mutex_lock(&va_lock);
-	for (unsigned long long i = va_n > VA_HIST ? va_n - VA_HIST : 0; i < va_n; i++) {
-		const struct va_ev *v = &va_hist[i % VA_HIST];
-		const char *a = v->p, *b = p;
-
-		if (a < b + bytes && b < a + v->bytes)
-			fprintf(stderr, "lfa:   overlaps event #%llu %c %p + %zu B%s\n", v->seq,
-				v->kind, v->p, v->bytes, v->p == p ? " (same base)" : "");
-	}
-	fprintf(stderr, "lfa:   (%llu workspace events so far)\n", va_n);
-	pthread_mutex_unlock(&va_lock);
-}
-
-/*
- * Exported workspaces are kept, not freed (LFA_WS_CACHE_BYTES, default
- * 4 GiB per process; 0 frees them as before).  The runtime remembers an
- * exported address after hipFree: a later allocation at that address — the
- * allocator hands freed ranges straight back — is refused an export
- * (hsa_status 4096), or exported with a handle its peers map onto other
- * memory, so the owner waits for posts that land elsewhere (round 4, DESIGN.md
- * §12: tools/probe_ipc_growth.py).  A workspace released by a growth or an
- * endpoint close goes to this cache; the next workspace of the same size on
- * the same device takes it back and exports it again — the same memory
- * under the same address — so no fresh allocation ever lands on an address
- * that was exported while a domain is open.
- *
- * Two kinds of released workspace are never handed out again but held
- * (quarantine, VERDICT r4 #3 / ADVICE r4):
- *   - one whose group had a P2P wait time out: a stalled peer may still run
- *     its old kernel, pushing data and posting its old epoch through its old
- *     mapping; in a reused workspace those posts would satisfy the new
- *     group's waits (its epochs restart at 1) with stale data;
- *   - the least recently used above the cap: returning it to hipFree would
- *     reopen the address hazard above.
- * The quarantine is bounded too (LFA_WS_QUARANTINE_BYTES, default 4 GiB):
- * past it the oldest goes back to hipFree, and a later workspace at that
- * address is caught by the export fallback and the identity check
- * (sym_prepare, sym_open: the growth fails on every member with EIO rather
- * than mapping the wrong memory).  When the last GPU domain of the process
- * closes, every kept workspace is freed (lfa_coll_ws_cached_bytes() and
- * lfa_coll_ws_quarantined_bytes() are then 0).
- */
-#define WS_CACHE_SLOTS 64
-#define WS_QUAR_SLOTS 256
-static struct ws_slot {
-	char *p;
-	size_t bytes;
-	int dev;
-	unsigned long long used;
-} ws_cache[WS_CACHE_SLOTS], ws_quar[WS_QUAR_SLOTS];
-static size_t ws_held, ws_quar_held;
-static unsigned long long ws_clock;
-static int ws_domains;          /* open domains with a GPU (workspace users) */
-static pthread_mutex_t ws_lock = PTHREAD_MUTEX_INITIALIZER;
-
-static size_t env_bytes(const char *name, long long dflt)
-{
-	const char *e = getenv(name);
-	long long v = e ? atoll(e) : dflt;
-
-	return v < 0 ? 0 : (size_t)v;
-}
-
-static size_t ws_cap(void)
-{
-	static long long cap = -1;
-
-	if (cap < 0)
-		cap = (long long)env_bytes("LFA_WS_CACHE_BYTES", 4ll << 30);
-	return (size_t)cap;
-}
-
-static size_t ws_quar_cap(void)
-{
-	static long long cap = -1;
-
-	if (cap < 0)
-		cap = (long long)env_bytes("LFA_WS_QUARANTINE_BYTES", 4ll << 30);
-	return (size_t)cap;
-}
-
-/* A kept workspace of exactly `bytes` on the current device, or NULL. */
-static char *ws_take(size_t bytes)
-{
-	int dev = -1;
-	char *p = NULL;
-
-	if (hipGetDevice(&dev) != hipSuccess)
-		return NULL;
-	pthread_mutex_lock(&ws_lock);
-	for (int i = 0; i < WS_CACHE_SLOTS && !p; i++)
-		if (ws_cache[i].p && ws_cache[i].bytes == bytes && ws_cache[i].dev == dev) {
-			p = ws_cache[i].p;
-			ws_cache[i].p = NULL;
-			ws_held -= bytes;
-		}
-	pthread_mutex_unlock(&ws_lock);
-	return p;
-}
-
-/* Hold `s` in the quarantine (ws_lock held); what leaves it to make room is
- * added to evict[]. */
-static void ws_quarantine(struct ws_slot s, char **evict, int *ne)
-{
-	int slot = -1;
-
-	for (int i = 0; i < WS_QUAR_SLOTS && slot < 0; i++)
-		if (!ws_quar[i].p)
-			slot = i;
-	if (slot < 0) {         /* every slot held: the oldest goes */
-		slot = 0;
-		for (int i = 1; i < WS_QUAR_SLOTS; i++)
-			if (ws_quar[i].used < ws_quar[slot].used)
-				slot = i;
-		evict[(*ne)++] = ws_quar[slot].p;
-		ws_quar_held -= ws_quar[slot].bytes;
-	}
-	s.used = ++ws_clock;
-	ws_quar[slot] = s;
-	ws_quar_held += s.bytes;
-	while (ws_quar_held > ws_quar_cap()) {
-		int old = -1;
-
-		for (int i = 0; i < WS_QUAR_SLOTS; i++)
-			if (ws_quar[i].p && (old < 0 || ws_quar[i].used < ws_quar[old].used))
-				old = i;
-		evict[(*ne)++] = ws_quar[old].p;
-		ws_quar_held -= ws_quar[old].bytes;
-		ws_quar[old].p = NULL;
-	}
-}
-
-/* Keep workspace `p` (its whole allocation) for a later ws_take, or — when
- * `tainted` (its group timed out) — in the quarantine, never to be reused. */
-static void ws_give(char *p, int tainted)
-{
-	void *base = NULL;
-	size_t bytes = 0;
-	int dev = -1, slot = -1;
-	char *evict[WS_CACHE_SLOTS + WS_QUAR_SLOTS + 2];
-	int ne = 0;
-
-	hipPointerAttribute_t at;
-
-	memset(&at, 0, sizeof(at));
-	if ((!ws_cap() && !tainted) || hipMemGetAddressRange(&base, &bytes, p) != hipSuccess ||
-	    base != (void *)p || hipPointerGetAttributes(&at, p) != hipSuccess) {
-		(void)hipGetLastError();
-		hipFree(p);
-		return;
-	}
-	dev = at.device;
-	pthread_mutex_lock(&ws_lock);
-	if (tainted) {
-		ws_quarantine((struct ws_slot){ p, bytes, dev, 0 }, evict, &ne);
-		goto out;
-	}
-	for (int i = 0; i < WS_CACHE_SLOTS && slot < 0; i++)
-		if (!ws_cache[i].p)
-			slot = i;
-	if (slot < 0) {         /* every slot held: the least recently used goes */
-		slot = 0;
-		for (int i = 1; i < WS_CACHE_SLOTS; i++)
-			if (ws_cache[i].used < ws_cache[slot].used)
-				slot = i;
-		ws_held -= ws_cache[slot].bytes;
-		ws_quarantine(ws_cache[slot], evict, &ne);
-	}
-	ws_cache[slot] = (struct ws_slot){ p, bytes, dev, ++ws_clock };
-	ws_held += bytes;
-	while (ws_held > ws_cap()) {
-		int lru = -1;
-
-		for (int i = 0; i < WS_CACHE_SLOTS; i++)
-			if (ws_cache[i].p && i != slot &&
-			    (lru < 0 || ws_cache[i].used < ws_cache[lru].used))
-				lru = i;
-		if (lru < 0)
-			lru = slot;
-		ws_held -= ws_cache[lru].bytes;
-		ws_quarantine(ws_cache[lru], evict, &ne);
-		ws_cache[lru].p = NULL;
-		if (lru == slot)
-			break;
-	}
-out:
-	pthread_mutex_unlock(&ws_lock);
-	for (int i = 0; i < ne; i++)
-		hipFree(evict[i]);
-}
-
-/* A GPU domain opened / closed: the last close frees every kept workspace. */
-static void ws_domain_ref(int delta)
-{
-	char *evict[WS_CACHE_SLOTS + WS_QUAR_SLOTS];
-	int ne = 0;
-
-	pthread_mutex_lock(&ws_lock);
-	ws_domains += delta;
-	if (ws_domains == 0) {
-		for (int i = 0; i < WS_CACHE_SLOTS; i++)
-			if (ws_cache[i].p) {
-				evict[ne++] = ws_cache[i].p;
-				ws_cache[i].p = NULL;
-			}
-		for (int i = 0; i < WS_QUAR_SLOTS; i++)
-			if (ws_quar[i].p) {
-				evict[ne++] = ws_quar[i].p;
-				ws_quar[i].p = NULL;
-			}
-		ws_held = 0;
-		ws_quar_held = 0;
-	}
-	pthread_mutex_unlock(&ws_lock);
-	for (int i = 0; i < ne; i++)
-		hipFree(evict[i]);
-}
-
-size_t lfa_coll_ws_cached_bytes(void)
-{
-	size_t n;
-
-	pthread_mutex_lock(&ws_lock);
-	n = ws_held;
-	pthread_mutex_unlock(&ws_lock);
-	return n;
-}
-
-size_t lfa_coll_ws_quarantined_bytes(void)
-{
-	size_t n;
-
-	pthread_mutex_lock(&ws_lock);
-	n = ws_quar_held;
-	pthread_mutex_unlock(&ws_lock);
-	return n;
-}
-
-/* A P2P wait of the group timed out (reaped, or recorded by a kernel in the
- * status word): its workspace may still receive a stalled peer's posts. */
-static int mc_tainted(const struct lfa_coll_mc *mc)
-{
-	return mc->sig_failed ||
-	       (mc->sig_word && *(volatile uint64_t *)mc->sig_word != LFA_SIG_NONE);
-}
-
-/* Unmap the peers' workspaces in `sym` and release this rank's `local`. */
-static void sym_free(const struct lfa_coll_mc *mc, char **sym, char *local)
-{
-	if (sym) {
-		for (int k = 0; k < mc->size; k++)
-			if (k != mc->rank && sym[k]) {
-				va_note('C', sym[k], 0);
-				hipIpcCloseMemHandle(sym[k]);
-			}
-		free(sym);
-	}
-	if (local) {
-		va_note('F', local, 0);
-		ws_give(local, mc_tainted(mc));
-	}
-}
-
-/* A new identity word: this process, a count, the clock. */
-static uint64_t ws_identity(void)
-{
-	static uint64_t n;
-	struct timespec ts;
-
-	clock_gettime(CLOCK_MONOTONIC, &ts);
-	return ((uint64_t)getpid() << 40) ^ ((uint64_t)__atomic_add_fetch(&n, 1, __ATOMIC_RELAXED) << 24) ^
-	       (uint64_t)ts.tv_nsec ^ ((uint64_t)ts.tv_sec << 30) ^ 1;
-}
-
-/*
- * The memory a P2P workspace is allocated from (LFA_WS_MEM, read once per
- * process; every member of a group must use the same kind).  Peers write
- * every byte a member reads from its own workspace — the posted epochs, the
- * one-shot slots, the pushed blocks — over xGMI while the member's kernels
- * run, so the workspace is allocated UNCACHED by default
- * (hipExtMallocWithFlags(hipDeviceMallocUncached), MTYPE UC in the GPU page
- * tables of the owner AND of every peer that maps it): no L2 of any GPU ever
- * holds a line of it, so a post or a push is visible to the owner's next
- * load whatever cache state the owner's earlier accesses left.  HIP's
- * default device memory is coarse-grained: its coherence is only guaranteed
- * at kernel boundaries and synchronisation points, which is exactly what a
- * flag polled inside a running kernel does not have.
- *   uncached (default)  hipDeviceMallocUncached
- *   fine                hipDeviceMallocFinegrained
- *   coarse              hipMalloc's memory (rounds 1-5; A/B only)
- */
-int lfa_coll_ws_mem(void)
-{
-	static int f = -1;
-
-	if (f < 0) {
-		const char *e = getenv("LFA_WS_MEM");
-
-		f = !e || !*e || !strcmp(e, "uncached") ? hipDeviceMallocUncached :
-		    !strcmp(e, "fine") ? hipDeviceMallocFinegrained :
-		    !strcmp(e, "coarse") ? hipDeviceMallocDefault : hipDeviceMallocUncached;
-	}
-	return f;
-}
-
-static hipError_t ws_malloc(char **p, size_t bytes)
-{
-	return hipExtMallocWithFlags((void **)p, bytes, (unsigned)lfa_coll_ws_mem());
-}
-
-/* A workspace of 2·region + the flag area: a kept one of that size, else a
- * new allocation of LFA_WS_MEM's kind. */
-static hipError_t ws_alloc(char **p, size_t region)
-{
-	const size_t bytes = 2 * region + LFA_SIG_AREA_BYTES;
-
-	*p = ws_take(bytes);
-	if (*p)
-		return hipSuccess;
-	return ws_malloc(p, bytes);
-}
-
-/* The flag area zeroed (epoch 0) and the identity word written, before any
- * peer can learn the handle and post into it (the agreement follows). */
-static int ws_reset(struct lfa_coll_mc *mc, char *local, size_t region, uint64_t id,
-		    int *why)
-{
-	char *area = local + 2 * region;
-
-	return lfa_hip_note(why, hipMemsetAsync(area, 0, LFA_SIG_AREA_BYTES, mc->ep->stream),
-			    "P2P flag area memset") == hipSuccess &&
-	       lfa_hip_note(why, hipMemcpyAsync(area + LFA_SIG_ID_OFF, &id, sizeof(id),
-						hipMemcpyHostToDevice, mc->ep->stream),
-			    "P2P identity word") == hipSuccess &&
-	       lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
-			    "P2P flag area sync") == hipSuccess;
-}
-
-static void p2p_release(struct lfa_coll_mc *mc)
-{
-	sym_free(mc, mc->sym, mc->sym_local);
-	mc->sym = NULL;
-	mc->sym_local = NULL;
-	mc->sym_region = 0;
-}
-
-_Static_assert(sizeof(struct sym_rec) <= LFA_SYM_REC_BYTES, "sym_rec");
-
-/* The workspace size p2p_ensure grows to for a need of `region` bytes. */
-static size_t sym_grow(const struct lfa_coll_mc *mc, size_t region)
-{
-	if (region < 2 * mc->sym_region)
-		region = 2 * mc->sym_region;
-	if (region < (8u << 20))
-		region = 8u << 20;
-	return (region + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-}
-
-/*
- * p2p_ensure in three local parts around two agreements.  A local failure
- * (no memory for the new workspace or its peer table, no IPC handle) is not
- * returned before the agreements: this rank still takes part with ok = 0, so
- * every member fails together instead of leaving its peers waiting (ADVICE
- * r1).  `ok` comes in false when the old workspace could not be quiesced.
- */
-static void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
-			struct sym_rec *mine, int *why)
-{
-	int n = mc->size;
-	char **old_sym = mc->sym, *old_local = mc->sym_local;
-
-	/* the new workspace is allocated and exported while the old one is
-	 * still held, so its IPC handle can never repeat the old one's (an
-	 * exporter resource freed and reused at once); the old mappings and
-	 * memory go right after */
-	mc->sym = NULL;
-	mc->sym_local = NULL;
-	mc->sym_region = 0;
-	memset(mine, 0, sizeof(*mine));
-	mc->sym = calloc((size_t)n, sizeof(*mc->sym));
-	ok = ok && mc->sym;
-	ok = ok && lfa_hip_note(why, ws_alloc(&mc->sym_local, region),
-				"P2P workspace allocation") == hipSuccess;
-	if (!ok)
-		mc->sym_local = NULL;
-	mine->id = ws_identity();
-	ok = ok && ws_reset(mc, mc->sym_local, region, mine->id, why);
-	/* every member grows at the same operation: the epochs restart with the
-	 * zeroed flags, so a count past 2^31 never meets a zero word that reads
-	 * as "ahead"  */
-	mc->bar_epoch = 0;
-	mc->os_epoch = 0;
-	if (ok)
-		va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
-	if (ok && n > 1 && hipIpcGetMemHandle(&mine->h, mc->sym_local) != hipSuccess) {
-		/*
-		 * The runtime refuses to export some fresh allocations: ROCr's IPC
-		 * create returns HSA_STATUS_ERROR (AMD_LOG_LEVEL=1: "Failed to
-		 * create memory for IPC, failed with hsa_status: 4096"), which
-		 * hipIpcGetMemHandle reports as "invalid argument".  Round 4 pinned
-		 * it down (tools/probe_ipc_growth.py): 2 to 8 of
-		 * 384 to 768 exports; the allocation is ordinary (device memory,
-		 * its own base and size), the SAME allocation fails on every retry,
-		 * and a replacement allocated after freeing it lands at the same
-		 * address and can fail again — the failure follows the address,
-		 * which earlier workspaces of this process held and exported.  So
-		 * the replacement is allocated while the refused allocation is
-		 * still held, which gives it another address, and the refused ones
-		 * are freed afterwards; after LFA_EXPORT_TRIES the growth fails on
-		 * every member (the agreement below).  With the workspace cache
-		 * (ws_give) no fresh allocation lands on a once-exported address,
-		 * and this path is the fallback for LFA_WS_CACHE_BYTES=0 and for
-		 * workspaces evicted above the cap.
-		 */
-		hipError_t e = hipGetLastError();
-		char *refused[LFA_EXPORT_TRIES];
-		int nref = 0;
-
-		if (va_debug()) {
-			fprintf(stderr, "lfa: P2P workspace export failed (%s)\n",
-				hipGetErrorString(e));
-			va_explain("failed export", mc->sym_local,
-				   2 * region + LFA_SIG_AREA_BYTES);
-		}
-		ok = 0;
-		while (!ok && mc->sym_local && nref < LFA_EXPORT_TRIES) {
-			refused[nref++] = mc->sym_local;
-			mc->sym_local = NULL;
-			ok = lfa_hip_note(why, ws_malloc(&mc->sym_local,
-							 2 * region + LFA_SIG_AREA_BYTES),
-					  "P2P workspace allocation (replacement)") == hipSuccess;
-			if (!ok) {
-				mc->sym_local = NULL;
-				break;
-			}
-			va_note('A', mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
-			ok = ws_reset(mc, mc->sym_local, region, mine->id, why) &&
-			     hipIpcGetMemHandle(&mine->h, mc->sym_local) == hipSuccess;
-			if (!ok)
-				(void)hipGetLastError();
-			if (va_debug())
-				va_explain(ok ? "replacement exported" : "replacement refused",
-					   mc->sym_local, 2 * region + LFA_SIG_AREA_BYTES);
-		}
-		if (!ok) {
-			lfa_hip_note(why, hipErrorInvalidValue, "P2P workspace hipIpcGetMemHandle");
-			if (mc->sym_local) {
-				va_note('F', mc->sym_local, 0);
-				hipFree(mc->sym_local);
-				mc->sym_local = NULL;
-			}
-		}
-		for (int i = 0; i < nref; i++) {
-			va_note('F', refused[i], 0);
-			hipFree(refused[i]);
-		}
-	}
-	mine->ok = ok;
-	sym_free(mc, old_sym, old_local);
-}
-
-/* FNV-1a of an IPC handle (LFA_DEBUG lines). */
-static uint64_t handle_digest(const hipIpcMemHandle_t *h)
-{
-	const unsigned char *b = (const unsigned char *)h;
-	uint64_t x = 0xcbf29ce484222325ull;
-
-	for (size_t i = 0; i < sizeof(*h); i++)
-		x = (x ^ b[i]) * 0x100000001b3ull;
-	return x;
-}
-
-/* Every member's record in hand: map the peers' workspaces of 2·region + the
- * flag area, and read each one's identity word through the mapping — a
- * mapping onto any other memory fails the handshake on every member (the
- * agreement) instead of leaving its owner waiting for posts that land
- * elsewhere. */
-static int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, size_t region,
-		    int *why)
-{
-	int ret = 0;
-
-	for (int k = 0; k < mc->size && !ret; k++)
-		if (!recs[k].ok)
-			ret = -LFA_ENOMEM;
-	for (int k = 0; k < mc->size && !ret; k++) {
-		if (k == mc->rank) {
-			mc->sym[k] = mc->sym_local;
-		} else if (lfa_hip_note(why, hipIpcOpenMemHandle((void **)&mc->sym[k], recs[k].h,
-								  hipIpcMemLazyEnablePeerAccess),
-					"P2P hipIpcOpenMemHandle") != hipSuccess) {
-			mc->sym[k] = NULL;
-			ret = -LFA_EIO;
-		} else {
-			uint64_t id = 0;
-
-			va_note('I', mc->sym[k], 0);
-			/* on the endpoint's stream (idle here: the growth synchronised
-			 * it), not the null stream, which would wait for the
-			 * application's own queued work */
-			if (lfa_hip_note(why, hipMemcpyAsync(&id, mc->sym[k] + 2 * region +
-								     LFA_SIG_ID_OFF, sizeof(id),
-							     hipMemcpyDeviceToHost, mc->ep->stream),
-					 "P2P identity read") != hipSuccess ||
-			    lfa_hip_note(why, hipStreamSynchronize(mc->ep->stream),
-					 "P2P identity read sync") != hipSuccess) {
-				ret = -LFA_EIO;
-			} else if (id != recs[k].id) {
-				lfa_hip_note(why, hipErrorInvalidValue, "P2P workspace identity");
-				if (va_debug()) {
-					fprintf(stderr, "lfa: peer %d workspace mapped onto other memory: "
-						"identity %#llx, read %#llx; handle digest %#llx\n", k,
-						(unsigned long long)recs[k].id, (unsigned long long)id,
-						(unsigned long long)handle_digest(&recs[k].h));
-					va_explain("mismatched mapping", mc->sym[k],
-						   2 * region + LFA_SIG_AREA_BYTES);
-				}
-				ret = -LFA_EIO;
-			}
-		}
-	}
-	return ret;
-}
-
-static int host_start(struct lfa_coll_ep *ep, struct hop *h,
-		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
-		      const void *buf, void *result, size_t count, int root,
-		      enum lfa_datatype dt, enum lfa_op op, int dev,
-		      enum lfa_coll_algo algo);
-
-/* A handshake collective of hop `h` on its reserved seq (host buffers). */
-static int sub_start(struct lfa_coll_ep *ep, struct hop *h, enum lfa_collective_op coll,
-		     const void *buf, void *result, size_t count,
-		     enum lfa_datatype dt, enum lfa_op op, uint16_t seq)
-{
-	struct lfa_coll_mc *mc = h->r.mc;
-	int ret;
-
-	h->sub = calloc(1, sizeof(*h->sub));
-	if (!h->sub)
-		return -LFA_ENOMEM;
-	/* a fixed schedule: the handshake starts from progress, at a different
-	 * point of each member's calls, so the endpoint's algorithm then (the
-	 * caller may have selected another for later operations) can differ
-	 * between members */
-	ret = host_start(ep, h->sub, mc, coll, buf, result, count, -1, dt, op, 0,
-			 LFA_ALGO_TREE);
-	h->sub->r.cid = (uint64_t)mc->group_id << 16 | seq;
-	LFA_TRACE("hop cid %#x handshake %d on cid %#x (mc seq now %u)", (unsigned)h->r.cid,
-		  (int)coll, (unsigned)h->sub->r.cid, (unsigned)mc->seq);
-	return ret;
-}
-
-/* Run the current handshake collective: 1 done, 0 pending, <0 failed. */
-static int sub_advance(struct hop *h)
-{
-	int ret = xrun_advance(&h->sub->r);
-
-	if (ret) {
-		hop_free(h->sub);
-		h->sub = NULL;
-	}
-	return ret;
-}
-
-/*
- * The P2P prologue of a peer-domain hop, driven from progress calls like the
- * rest of it (nothing blocks inside a submit: the owner's transfers may only
- * move when the application drives progress).  WAIT_PRIOR: the operations
- * queued before this one share the symmetric workspace, so they finish
- * first — each ends with a barrier, so no peer still reads or writes it.
- * Then, if the workspace must grow, p2p_ensure's two agreements run as host
- * collectives on the seqs reserved at submit.
- */
-static int hop_prologue(struct lfa_coll_ep *ep, struct hop *h, size_t idx)
-{
-	struct lfa_coll_mc *mc = h->r.mc;
-	struct sym_rec *recs = ep->ctl_host;
-	int ret;
-
-	switch (h->phase) {
-	case HOP_WAIT_PRIOR:
-		for (size_t j = 0; j < idx; j++) {
-			struct hop *p = ep->q[(ep->qhead + j) % ep->qcap].hop;
-
-			if (p && p->err)
-				return p->err;
-			/* a device hop with every item on the stream is far enough:
-			 * this one's items queue behind it (a growth below first
-			 * synchronises the stream) */
-			if (p && !p->done && !p->issued)
-				return 0;
-		}
-		LFA_TRACE("hop cid %#x prologue: prior hops done or issued, need %zu have %zu",
-			  (unsigned)h->r.cid, h->sym_need, mc->sym_region);
-		if (h->sym_need <= mc->sym_region)
-			break;
-		h->sym_size = sym_grow(mc, h->sym_need);
-		sym_prepare(mc, h->sym_size,
-			    lfa_hip_note(&h->r.hip_err, hipStreamSynchronize(ep->stream),
-					 "P2P prologue stream sync") == hipSuccess,
-			    (struct sym_rec *)h->mine, &h->r.hip_err);
-		if (mc->size == 1) {
-			h->agree_in = h->agree_out = ((struct sym_rec *)h->mine)->ok;
-			recs[0] = *(struct sym_rec *)h->mine;
-			h->agree_out = h->agree_out &&
-				       sym_open(mc, recs, h->sym_size, &h->r.hip_err) == 0;
-			goto agreed;
-		}
-		ret = sub_start(ep, h, LFA_ALLGATHER, h->mine, recs, sizeof(struct sym_rec),
-				LFA_UINT8, LFA_NOOP, h->sub_seq);
-		if (ret)
-			return ret;
-		h->phase = HOP_SYM_GATHER;
-		LFA_TRACE("hop cid %#x workspace gather started (seq %u)", (unsigned)h->r.cid,
-			  (unsigned)h->sub_seq);
-		return 0;
-	case HOP_SYM_GATHER:
-		ret = sub_advance(h);
-		if (ret <= 0)
-			return ret;
-		h->agree_in = sym_open(mc, recs, h->sym_size, &h->r.hip_err) == 0;
-		ret = sub_start(ep, h, LFA_ALLREDUCE, &h->agree_in, &h->agree_out, 1,
-				LFA_INT32, LFA_MIN, (uint16_t)(h->sub_seq + 1));
-		if (ret)
-			return ret;
-		h->phase = HOP_SYM_AGREE;
-		LFA_TRACE("hop cid %#x workspace gathered, mapped=%d", (unsigned)h->r.cid,
-			  (int)h->agree_in);
-		return 0;
-	case HOP_SYM_AGREE:
-		ret = sub_advance(h);
-		if (ret <= 0)
-			return ret;
-agreed:
-		if (!h->agree_out) {
-			p2p_release(mc);
-			return -LFA_EIO;
-		}
-		mc->sym_region = h->sym_size;
-		break;
-	default:
-		return 0;
-	}
-	h->r.x.sym = mc->sym;
-	h->r.x.region = mc->sym_region;
-	h->phase = HOP_RUN;
-	LFA_TRACE("hop cid %#x runs on the workspace (%zu B)", (unsigned)h->r.cid,
-		  mc->sym_region);
-	return 0;
-}
-
-/* Device domains: the whole handshake, stream-ordered, over RCCL. */
-static int p2p_ensure(struct lfa_coll_mc *mc, size_t region)
-{
-	struct lfa_coll_ep *ep = mc->ep;
-	struct sym_rec *recs = ep->ctl_host;    /* nranks records, from ep open */
-	void *drec = ep->ctl_dev;
-	const size_t rb = sizeof(struct sym_rec);
-	int n = mc->size, ret = 0;
-
-	if (region <= mc->sym_region)
-		return 0;
-	region = sym_grow(mc, region);
-	/* the old workspace is released only after this rank's earlier
-	 * operations have completed — each of which ends with a barrier, so no
-	 * peer still touches it */
-	memset(recs, 0, (size_t)n * rb);
-	sym_prepare(mc, region, hipStreamSynchronize(ep->stream) == hipSuccess,
-		    &recs[mc->rank], NULL);
-	if (n > 1 &&
-	    (hipMemcpyAsync((char *)drec + (size_t)mc->rank * rb, &recs[mc->rank], rb,
-			    hipMemcpyHostToDevice, ep->stream) != hipSuccess ||
-	     ncclAllGather((char *)drec + (size_t)mc->rank * rb, drec, rb, ncclUint8,
-			   mc->comm, ep->stream) != ncclSuccess ||
-	     hipMemcpyAsync(recs, drec, (size_t)n * rb, hipMemcpyDeviceToHost,
-			    ep->stream) != hipSuccess ||
-	     hipStreamSynchronize(ep->stream) != hipSuccess))
-		ret = -LFA_EIO;
-	if (!ret)
-		ret = sym_open(mc, recs, region, NULL);
-	if (n > 1) {
-		/* agree that every member mapped every peer (MIN of the flags) */
-		int32_t all = ret == 0;
-
-		if (hipMemcpyAsync(drec, &all, sizeof(all), hipMemcpyHostToDevice,
-				   ep->stream) != hipSuccess ||
-		    ncclAllReduce(drec, drec, 1, ncclInt32, ncclMin, mc->comm,
-				  ep->stream) != ncclSuccess ||
-		    hipMemcpyAsync(&all, drec, sizeof(all), hipMemcpyDeviceToHost,
-				   ep->stream) != hipSuccess ||
-		    hipStreamSynchronize(ep->stream) != hipSuccess || !all)
-			ret = ret ? ret : -LFA_EIO;
-	}
-	if (ret) {
-		p2p_release(mc);
-		return ret;
-	}
-	mc->sym_region = region;
-	return 0;
-}
-
 static int rccl_type(enum lfa_datatype dt, ncclDataType_t *t)
 {
 	switch (dt) {
@@ -2439,86 +850,9 @@ static int cached_plan(struct lfa_coll_ep *ep, const struct plan **out,
 }
 
 /*
- * A small reducing collective of a one-member group (allreduce, reduce,
- * reduce_scatter: each a copy of the input) as one launch that ends in the
- * completion word, so the operation completes without an event (VERDICT r3
- * #4; the plan would be one COPY item plus an event record and query).
- */
-/* The direct queue for this endpoint's device, opened at first use. */
-static struct lfa_direct *direct_of(struct lfa_coll_ep *ep)
-{
-	const char *e;
-
-	if (ep->direct || ep->direct_tried)
-		return ep->direct;
-	ep->direct_tried = 1;
-	e = getenv("LFA_DIRECT");
-	if (e && e[0] == '0')
-		return NULL;
-	if (hipMalloc((void **)&ep->ddone_ctr, sizeof(uint32_t)) != hipSuccess ||
-	    hipMemset(ep->ddone_ctr, 0, sizeof(uint32_t)) != hipSuccess ||
-	    hipHostMalloc((void **)&ep->ddone_word, sizeof(uint64_t),
-			  hipHostMallocCoherent) != hipSuccess) {
-		(void)hipGetLastError();
-		return NULL;
-	}
-	*(volatile uint64_t *)ep->ddone_word = 0;
-	ep->direct = direct_acquire(ep->dom->device);
-	return ep->direct;
-}
-
-/* The largest world-1 reducing collective run_solo takes: LFA_ONESHOT_SOLO_BYTES
- * unless LFA_SOLO_BYTES says otherwise (a tuning knob). */
-static size_t solo_bytes(void)
-{
-	static long long v = -1;
-
-	if (v < 0) {
-		const char *e = getenv("LFA_SOLO_BYTES");
-		const long long x = e ? atoll(e) : -1;
-
-		v = x >= 0 && x <= (1ll << 30) ? x : (long long)LFA_ONESHOT_SOLO_BYTES;
-	}
-	return (size_t)v;
-}
-
-static int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
-		    enum lfa_datatype dt)
-{
-	int ret;
-
-	ep->op_done_w = NULL;
-	if (ep->allow_direct && count * lfa_datatype_size(dt) <= LFA_DIRECT_SOLO_BYTES &&
-	    direct_of(ep) && !lfa_direct_failed(ep->direct)) {
-		/* no HIP launch: ~3 us less host time */
-		ret = lfa_direct_solo_copy(ep->direct, result, buf, count * lfa_datatype_size(dt),
-					   ep->ddone_ctr, ep->ddone_word, ep->ddone_seq + 1);
-		if (!ret) {
-			ep->op_done_val = ++ep->ddone_seq;
-			ep->op_done_w = ep->ddone_word;
-			return 0;
-		}
-		if (ret != -LFA_EIO)
-			return ret;
-		/* the queue failed (nothing was enqueued): the HIP launch below;
-		 * the operations it still owes fail in word_overdue */
-	}
-
-	/* the one-shot kernel with n = 1 gives the same bytes; this kernel's
-	 * arguments are 48 bytes instead of ~700, about 1 us less from launch
-	 * to the word (tools/probe_solo_latency.py) */
-	ret = lfa_solo_copy_async(result, buf, count * lfa_datatype_size(dt), ep->done_ctr,
-				  ep->done_word, ep->done_seq + 1, ep->stream);
-	if (ret)
-		return ret;
-	ep->op_done_val = ++ep->done_seq;
-	return 0;
-}
-
-/*
  * One operation on device buffers, enqueued on ep->stream.
  */
-static int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+LFA_INTERNAL int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
 		      enum lfa_collective_op coll, const void *buf, void *result,
 		      size_t count, int root, enum lfa_datatype dt,
 		      enum lfa_op op, hipStream_t s, enum lfa_coll_algo algo)
@@ -2588,169 +922,6 @@ replan:
 	return ret;
 }
 
-int lfa_coll_host_chunk(enum lfa_collective_op coll, size_t count, int nranks,
-			size_t esz, size_t chunk_bytes, size_t idx,
-			struct lfa_host_chunk *c)
-{
-	const int rs = coll == LFA_REDUCE_SCATTER;
-	size_t nb, span, per, off;
-
-	if (!c || !esz || nranks < 1 ||
-	    !(coll == LFA_ALLREDUCE || coll == LFA_BROADCAST ||
-	      coll == LFA_REDUCE || rs) ||
-	    (rs && count % (size_t)nranks))
-		return -LFA_EINVAL;
-	nb = rs ? (size_t)nranks : 1;       /* blocks gathered per chunk */
-	span = count / nb;                  /* elements per block */
-	/* chunk_bytes 0: one chunk, the whole buffer.  Which chunk a member
-	 * uses is lfa_coll_member_chunk's rule: in a group of N > 1 only a
-	 * group-wide chunk, so every member issues the same device schedule
-	 * whatever its memory type (chunking is otherwise a local
-	 * choice the peers cannot see) */
-	per = chunk_bytes ? chunk_bytes / esz / nb : span;
-	if (!per)
-		per = 1;
-	if (per > span)
-		per = span;
-	if (!per || idx >= (span + per - 1) / per)
-		return 0;
-	off = idx * per;
-	c->src_off = off * esz;
-	c->src_pitch = span * esz;
-	c->width = (span - off < per ? span - off : per) * esz;
-	c->height = nb;
-	c->dev_count = nb * (c->width / esz);
-	c->dst_off = off * esz;
-	return 1;
-}
-
-/*
- * Host buffers: stream chunks through HBM on three streams: chunk c+1's H2D
- * (copy stream), chunk c's collective (executor stream) and chunk c-1's D2H
- * (d2h stream) run together, so both PCIe directions are busy at once; two
- * staging slots, ordered with events.  Valid for the element-wise collectives
- * (allreduce, reduce, broadcast), where chunks are independent, and for
- * reduce_scatter with equal blocks (count % N == 0): chunk c holds elements
- * [j, j+n) of EVERY rank's block (one 2-D H2D, height N), so the device
- * reduce_scatter of those N·n elements hands rank r elements [j, j+n) of its
- * own block.  Every element meets the same schedule as unchunked, so the
- * result is bit-identical to the whole-buffer form.
- */
-static int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
-			    enum lfa_collective_op coll, const void *buf,
-			    void *result, size_t count, int root,
-			    enum lfa_datatype dt, enum lfa_op op, size_t chunk)
-{
-	size_t esz = lfa_datatype_size(dt), in_slot, idx;
-	struct lfa_host_chunk c0, c;
-	hipEvent_t h2d[2], comp[2], done[2];
-	int ret, slot = 0;
-	const int out = coll != LFA_REDUCE || mc->rank == root;
-
-	ret = lfa_coll_host_chunk(coll, count, mc->size, esz, chunk, 0, &c0);
-	if (ret <= 0)
-		return ret < 0 ? ret : 0;
-	/* chunk 0 is the widest; the output half starts 256-byte aligned
-	 * (vector body of the kernels) */
-	in_slot = (c0.height * c0.width + 255) & ~(size_t)255;
-	if (grow_staging(ep, in_slot + c0.width))
-		return -LFA_ENOMEM;
-	ret = 0;
-	for (int i = 0; i < 2; i++) {
-		hipEventCreateWithFlags(&h2d[i], hipEventDisableTiming);
-		hipEventCreateWithFlags(&comp[i], hipEventDisableTiming);
-		hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
-		hipEventRecord(done[i], ep->stream);
-	}
-	for (idx = 0; !ret &&
-	     lfa_coll_host_chunk(coll, count, mc->size, esz, chunk, idx, &c) == 1;
-	     idx++) {
-		char *din = ep->hs[slot], *dout = din + in_slot;
-
-		/* slot reuse: wait until chunk c-2's D2H finished */
-		hipStreamWaitEvent(ep->copy_stream, done[slot], 0);
-		if (c.height > 1)
-			hipMemcpy2DAsync(din, c.width, (const char *)buf + c.src_off,
-					 c.src_pitch, c.width, c.height,
-					 hipMemcpyDefault, ep->copy_stream);
-		else if (coll != LFA_BROADCAST || mc->rank == root)
-			hipMemcpyAsync(din, (const char *)buf + c.src_off, c.width,
-				       hipMemcpyDefault, ep->copy_stream);
-		hipEventRecord(h2d[slot], ep->copy_stream);
-		hipStreamWaitEvent(ep->stream, h2d[slot], 0);
-		ret = run_device(ep, mc, coll, din,
-				 coll == LFA_BROADCAST ? din : dout, c.dev_count,
-				 root, dt, op, ep->stream, ep->algo);
-		hipEventRecord(comp[slot], ep->stream);
-		hipStreamWaitEvent(ep->d2h_stream, comp[slot], 0);
-		if (out)
-			hipMemcpyAsync((char *)result + c.dst_off,
-				       coll == LFA_BROADCAST ? din : dout,
-				       c.width, hipMemcpyDefault, ep->d2h_stream);
-		hipEventRecord(done[slot], ep->d2h_stream);
-		slot ^= 1;
-	}
-	/* the operation completes when the last D2H lands */
-	hipStreamWaitEvent(ep->stream, done[slot ^ 1], 0);
-	for (int i = 0; i < 2; i++) {
-		hipEventDestroy(h2d[i]);
-		hipEventDestroy(comp[i]);
-		hipEventDestroy(done[i]);
-	}
-	return ret;
-}
-
-/*
- * Device buffers under a group chunk: the chunks lfa_coll_host_chunk gives
- * the host members, run back to back on the caller's buffers — contiguous
- * chunks in place, reduce_scatter's 2-D chunks (elements [j, j+w) of every
- * block) through the staging pipeline, which moves them device to device.
- */
-static int run_device_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
-			      enum lfa_collective_op coll, const void *buf,
-			      void *result, size_t count, int root,
-			      enum lfa_datatype dt, enum lfa_op op, size_t chunk)
-{
-	struct lfa_host_chunk c;
-	int ret = 0;
-
-	if (coll == LFA_REDUCE_SCATTER)
-		return run_host_chunked(ep, mc, coll, buf, result, count, root, dt, op,
-					chunk);
-	for (size_t idx = 0; !ret &&
-	     lfa_coll_host_chunk(coll, count, mc->size, lfa_datatype_size(dt), chunk, idx,
-				 &c) == 1; idx++)
-		ret = run_device(ep, mc, coll, buf ? (const char *)buf + c.src_off : NULL,
-				 result ? (char *)result + c.dst_off : NULL, c.dev_count,
-				 root, dt, op, ep->stream, ep->algo);
-	return ret;
-}
-
-/* Host buffers for non-elementwise collectives: whole-buffer staging.
- * (Staging copies use hipMemcpyDefault: one side may be device memory when
- * the caller mixes a device buf with a host result.) */
-static int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
-			  enum lfa_collective_op coll, const void *buf,
-			  size_t in_bytes, void *result, size_t out_bytes,
-			  size_t count, int root, enum lfa_datatype dt,
-			  enum lfa_op op)
-{
-	char *din, *dout;
-	int ret;
-
-	if (grow_staging(ep, in_bytes + out_bytes + 32))
-		return -LFA_ENOMEM;
-	din = ep->hs[0];
-	dout = din + ((in_bytes + 15) & ~(size_t)15);
-	if (buf && in_bytes)
-		hipMemcpyAsync(din, buf, in_bytes, hipMemcpyDefault, ep->stream);
-	ret = run_device(ep, mc, coll, din, dout, count, root, dt, op, ep->stream, ep->algo);
-	if (!ret && result && out_bytes)
-		hipMemcpyAsync(result, dout, out_bytes, hipMemcpyDefault,
-			       ep->stream);
-	return ret;
-}
-
 LFA_INTERNAL int check_reduce_args(enum lfa_datatype dt, enum lfa_op op)
 {
 	if (op < LFA_MIN || op > LFA_BXOR)
@@ -2770,248 +941,9 @@ static int group_rank(struct lfa_coll_mc *mc, lfa_addr_t a)
 }
 
 /* Can this rank issue collectives on the group? */
-static int mc_member(const struct lfa_coll_mc *mc)
+LFA_INTERNAL int mc_member(const struct lfa_coll_mc *mc)
 {
 	return mc->rank >= 0 && (mc->ep->dom->host || mc->comm);
-}
-
-/* Schedule `h` for one collective on a host domain: the algorithm's plan
- * (P2P / RCCL run as TREE; TREE_COLL's collective items lowered to grouped
- * sends/receives) and its own TMP, so operations may overlap. */
-static int host_start(struct lfa_coll_ep *ep, struct hop *h,
-		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
-		      const void *buf, void *result, size_t count, int root,
-		      enum lfa_datatype dt, enum lfa_op op, int dev,
-		      enum lfa_coll_algo algo)
-{
-	size_t esz = lfa_datatype_size(dt);
-	/* this operation's sequence number, taken before a P2P handshake below
-	 * draws the next ones */
-	const uint16_t seq = (uint16_t)(mc->seq - 1);
-	struct plan raw;
-	int ret, sym;
-
-	h->ep = ep;
-	if (dev == 2) {
-		/* host buffers the GPU reaches (pinned, registered): the device
-		 * schedule runs on their mappings — this member's kernels alone
-		 * touch its buf and result (peers only see the symmetric
-		 * workspaces), so nothing is staged */
-		void *zb = buf ? zero_copy_of(buf, ep->dom->device) : NULL;
-		void *zr = result ? zero_copy_of(result, ep->dom->device) : NULL;
-
-		if ((!buf || zb) && (!result || zr)) {
-			buf = zb;
-			result = zr;
-			dev = 1;
-		} else if (count * esz <= LFA_BOUNCE_BYTES && (h->bounce = bounce_get(ep))) {
-			/* pageable buffers of a small operation: the input copied
-			 * into a pinned bounce block on the CPU, the schedule run on
-			 * the block's mapping, the result copied back when the hop
-			 * completes — no H2D / D2H copies and their events (2
-			 * processes, 4 KiB: DESIGN.md §7 round 5) */
-			char *bin = h->bounce, *bout = bin + LFA_BOUNCE_BYTES;
-			size_t moff, mlen;
-
-			lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
-			/* a non-root member of a reduce has no result: the kernels never
-			 * write the block's output half, so nothing is copied back
-			 * (the half still held an earlier operation's bytes,
-			 * and an in-place caller's input was overwritten with them) —
-			 * the staged path's out_bytes rule below */
-			if (coll == LFA_REDUCE && mc->rank != root)
-				result = NULL;
-			h->bounce_out = bout;
-			h->bounce_user = result;
-			h->bounce_bytes = !result ? 0 : coll == LFA_REDUCE_SCATTER ? mlen * esz :
-					  count * esz;
-			zb = zero_copy_of(bin, ep->dom->device);
-			zr = zero_copy_of(bout, ep->dom->device);
-			if (!zb || !zr) {
-				bounce_put(ep, h->bounce);
-				h->bounce = NULL;
-				h->bounce_bytes = 0;
-			} else {
-				memcpy(bin, buf, count * esz);
-				buf = zb;
-				result = result ? zr : NULL;
-				dev = 1;
-			}
-		}
-	}
-	/* P2P keeps its schedule on device buffers (the peers' symmetric
-	 * workspaces are IPC-mapped device memory; its barriers become zero-byte
-	 * messages); host buffers and RCCL run as TREE */
-	if ((algo == LFA_ALGO_P2P && !dev) || algo == LFA_ALGO_RCCL ||
-	    algo == LFA_ALGO_AUTO)
-		algo = LFA_ALGO_TREE;
-	ret = plan_make(&raw, coll, algo, mc->rank, mc->size, root, count, esz);
-	if (ret)
-		return ret;
-	sym = plan_uses_sym(raw.steps, raw.nsteps);
-	if (sym && dev) {
-		ret = sig_ready(mc);
-		if (ret) {
-			plan_free(&raw);
-			return ret;     /* epochs disagree since a timed-out wait */
-		}
-		h->r.x.ticket = ++mc->p2p_ticket;
-	}
-	/* a device hop's BARRIER stays: the flag kernel (sig_barrier) */
-	ret = lower_plan(&raw, mc->rank, mc->size, esz, &h->pl, sym && !dev, !dev);
-	plan_free(&raw);
-	if (ret)
-		return ret;
-	if (sym) {
-		/* the workspace is set up by hop_prologue, from progress; its two
-		 * possible handshakes get the next two seqs on every member */
-		h->phase = HOP_WAIT_PRIOR;
-		h->sym_need = plan_sym_need(h->pl.steps, h->pl.nsteps, mc->size,
-					    count, esz);
-		h->sub_seq = mc->seq;
-		mc->seq += 2;
-	}
-	h->dev = dev != 0;
-	h->r.stream = ep->stream;
-	if (dev == 1 && sym && h->pl.nsteps == 1 && h->pl.steps[0].type == LFA_STEP_ONESHOT &&
-	    ep->done_word) {
-		/* one kernel in place on device buffers: it ends in the
-		 * completion word, no event */
-		h->r.x.done_ctr = ep->done_ctr;
-		h->r.x.done_word = ep->done_word;
-		h->r.x.done_seq = &ep->done_seq;
-	}
-	if (dev) {
-		hipSetDevice(ep->dom->device);
-		if (h->pl.tmp && !(h->tmp = stage_get(ep, h->pl.tmp)))
-			return -LFA_ENOMEM;
-	} else if (h->pl.tmp && !(h->tmp = malloc(h->pl.tmp))) {
-		return -LFA_ENOMEM;
-	}
-	if (dev == 2) {
-		/* host buffers through device copies (reducing collectives) */
-		size_t moff, mlen, in_b = count * esz;
-
-		lfa_coll_block(count, mc->size, mc->rank, &moff, &mlen);
-		h->out_bytes = coll == LFA_REDUCE_SCATTER ? mlen * esz :
-			       coll == LFA_REDUCE && mc->rank != root ? 0 : count * esz;
-		h->user_out = result;
-		if (!(h->st_in = stage_get(ep, in_b)) ||
-		    !(h->st_out = stage_get(ep, h->out_bytes)))
-			return -LFA_ENOMEM;     /* hop_free releases what was made */
-		/* H2D on the copy stream now: a chunked operation's later chunks
-		 * upload while the earlier ones reduce (host_progress_all makes
-		 * the run wait for in_ev) */
-		if (!(h->in_ev = event_get(ep)))
-			return -LFA_EIO;
-		if (hipMemcpyAsync(h->st_in, buf, in_b, hipMemcpyHostToDevice,
-				   ep->copy_stream) != hipSuccess ||
-		    hipEventRecord(h->in_ev, ep->copy_stream) != hipSuccess)
-			return -LFA_EIO;
-		buf = h->st_in;
-		result = h->st_out;
-	}
-	h->r.xp = dev ? &xport_peer_dev : &xport_peer;
-	h->r.pl = &h->pl;
-	h->r.mc = mc;
-	h->r.op = op;
-	h->r.dt = dt;
-	h->r.cid = (uint64_t)mc->group_id << 16 | seq;
-	h->r.x.base[LFA_BUF_SEND] = coll == LFA_BROADCAST ? result : (void *)buf;
-	h->r.x.base[LFA_BUF_RESULT] = result;
-	h->r.x.base[LFA_BUF_TMP] = h->tmp;
-	return 0;
-}
-
-static int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
-		       enum lfa_collective_op coll, const void *buf,
-		       void *result, size_t count, int root,
-		       enum lfa_datatype dt, enum lfa_op op, void *context,
-		       int kind, struct lfa_coll_mc *jmc, int dev,
-		       enum lfa_coll_algo algo)
-{
-	struct hop *h = calloc(1, sizeof(*h));
-	const uint64_t t0 = mc->p2p_ticket;
-	int ret;
-
-	if (!h)
-		return -LFA_ENOMEM;
-	mc->seq++;                              /* coll_get_next_id :48-52 */
-	ret = host_start(ep, h, mc, coll, buf, result, count, root, dt, op, dev, algo);
-	LFA_TRACE("submit cid %#x coll %d count %zu dev %d algo %d phase %d sub_seq %u -> %d",
-		  (unsigned)h->r.cid, (int)coll, count, dev, (int)algo, h->phase,
-		  (unsigned)h->sub_seq, ret);
-	if (!ret)
-		ret = enqueue_host(ep, h, context, kind, jmc);
-	if (ret)
-		hop_free(h);
-	else
-		tag_p2p(ep, mc, t0);
-	return ret;
-}
-
-/*
- * The group chunk on a GPU peer domain.  Under LFA_ALGO_P2P
- * every member — host buffers staged, device buffers in place — runs the
- * one device schedule, so a group chunk splits an allreduce or reduce into
- * the same ⌈count / chunk⌉ P2P operations on every member: a rule of
- * (algorithm, collective, count, n, esz, chunk) only, never of the member's
- * buffer type.  Host members' chunks then pipeline: chunk c+1's H2D (copy
- * stream) and chunk c-1's D2H (d2h stream) overlap chunk c's kernels.
- * reduce_scatter keeps one operation (its chunks are 2-D).
- */
-static size_t peer_chunked(const struct lfa_coll_ep *ep, const struct lfa_coll_mc *mc,
-			   enum lfa_collective_op coll, size_t count, size_t esz)
-{
-	const size_t g = lfa_coll_group_chunk(ep->group_chunk, mc->size, count * esz);
-
-	return ep->algo == LFA_ALGO_P2P && g && ep->dom->device >= 0 &&
-	       mc->size > 1 && mc->size <= LFA_TREE_MAX && mc->size <= LFA_PUT_MAX &&
-	       (coll == LFA_ALLREDUCE || coll == LFA_REDUCE) &&
-	       count * esz > g ? g : 0;
-}
-
-static int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
-			       enum lfa_collective_op coll, const void *buf,
-			       void *result, size_t count, int root,
-			       enum lfa_datatype dt, enum lfa_op op, void *context,
-			       int dev, size_t chunk)
-{
-	const size_t esz = lfa_datatype_size(dt);
-	const uint64_t chain = ++ep->next_chain;
-	size_t per = chunk / esz;
-	int ret;
-
-	if (!per)
-		per = 1;
-	/* every chunk's queue slot before the first chunk is posted (ADVICE
-	 * r4): a full ring can then not stop the operation partway, which
-	 * would leave the members with different operations on the group */
-	ret = queue_reserve(ep, (count + per - 1) / per);
-	if (ret)
-		return ret;
-	for (size_t off = 0; off < count; off += per) {
-		const size_t n = count - off < per ? count - off : per;
-		const int last = off + n == count;
-		void *r = result ? (char *)result + off * esz : NULL;
-
-		ret = host_submit(ep, mc, coll, (const char *)buf + off * esz, r, n, root,
-				  dt, op, context, last ? 0 : 3, NULL, dev, ep->algo);
-
-		if (ret) {
-			/* the caller is told the operation never started: the
-			 * chunks already queued still run (their peers wait for
-			 * them) but reap silently.  The members have now issued
-			 * different operations on the group, so its later
-			 * collectives fail (P2P waits time out): close and
-			 * re-join it (lfa_coll.h) */
-			if (off)
-				ep->failed_chain = chain;
-			return ret;
-		}
-		ep->q[(ep->qhead + ep->qlen - 1) % ep->qcap].chain = chain;
-	}
-	return 0;
 }
 
 static ssize_t submit(struct lfa_coll_ep *ep, enum lfa_collective_op coll,
@@ -3306,319 +1238,6 @@ ssize_t lfa_barrier(struct lfa_coll_ep *ep, lfa_addr_t coll_addr, void *context)
 }
 
 /* ---------------------------------------------------------------------- */
-/* join                                                                    */
-/* ---------------------------------------------------------------------- */
-
-/*
- * A device domain's communicator for a group formed by its members alone
- * (lfa_join_members on a strict subset): the first member's RCCL unique id
- * reaches the others point-to-point over the parent's communicator — only
- * the members take part in those transfers — and the members then create
- * their communicator together.  The transfers are enqueued under ep->lock
- * (this rank's position in the parent's operation order); the waits run
- * outside it, so progress keeps reaping completions meanwhile.
- */
-static int members_comm(struct lfa_coll_ep *ep, struct lfa_coll_mc *parent,
-			const int *ranks, size_t n, int pos, ncclComm_t *out)
-{
-	ncclUniqueId uid;
-	hipEvent_t ev = NULL;
-	void *d = NULL;
-	int ret = 0;
-
-	memset(&uid, 0, sizeof(uid));
-	hipSetDevice(ep->dom->device);
-	if (pos == 0 && ncclGetUniqueId(&uid) != ncclSuccess)
-		ret = -LFA_EIO;         /* the others still get (and fail on) zeros */
-	if (hipMalloc(&d, sizeof(uid)) != hipSuccess ||
-	    hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-		if (d)
-			hipFree(d);
-		return -LFA_ENOMEM;
-	}
-	pthread_mutex_lock(&ep->lock);
-	if ((pos == 0 && hipMemcpyAsync(d, &uid, sizeof(uid), hipMemcpyHostToDevice,
-					ep->stream) != hipSuccess) ||
-	    ncclGroupStart() != ncclSuccess)
-		ret = -LFA_EIO;
-	for (size_t k = 1; k < n && pos == 0; k++)
-		if (ncclSend(d, sizeof(uid), ncclUint8, ranks[k], parent->comm,
-			     ep->stream) != ncclSuccess)
-			ret = -LFA_EIO;
-	if (pos != 0 && ncclRecv(d, sizeof(uid), ncclUint8, ranks[0], parent->comm,
-				 ep->stream) != ncclSuccess)
-		ret = -LFA_EIO;
-	if (ncclGroupEnd() != ncclSuccess ||
-	    hipMemcpyAsync(&uid, d, sizeof(uid), hipMemcpyDeviceToHost,
-			   ep->stream) != hipSuccess ||
-	    hipEventRecord(ev, ep->stream) != hipSuccess)
-		ret = -LFA_EIO;
-	pthread_mutex_unlock(&ep->lock);
-	if (hipEventSynchronize(ev) != hipSuccess)
-		ret = -LFA_EIO;
-	hipEventDestroy(ev);
-	hipFree(d);
-	{
-		/* a first member without an id sent zeros: everyone stops here */
-		static const ncclUniqueId none;
-
-		if (!memcmp(&uid, &none, sizeof(uid)))
-			return ret ? ret : -LFA_EIO;
-	}
-	pthread_mutex_lock(&ep->comm_lock);
-	if (ncclCommInitRank(out, (int)n, uid, pos) != ncclSuccess)
-		ret = ret ? ret : -LFA_EIO;
-	pthread_mutex_unlock(&ep->comm_lock);
-	return ret;
-}
-
-/* members_only: lfa_join_members — the agreement runs over the new group
- * itself, so only its members call (see lfa_coll.h). */
-static int join_impl(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
-		     const int *ranks, size_t nmembers, uint64_t flags,
-		     struct lfa_coll_mc **mcp, void *context, int members_only)
-{
-	struct lfa_coll_mc *parent, *mc;
-	int member = 0, pos = -1, ret = 0, host;
-	void *dmask;
-
-	if (!ep || !mcp)
-		return -LFA_EINVAL;
-	if (flags & ~LFA_COLLECTIVE)
-		return -LFA_EBADFLAGS;
-	host = ep->dom->host;
-	parent = mc_of(ep, coll_addr);
-	if (!mc_member(parent))
-		return -LFA_EINVAL;
-	if (members_only && !ranks)
-		return -LFA_EINVAL;
-	if (ranks) {
-		/* ranks[i] is the parent rank of group rank i, in any order: the
-		 * group numbers its members by their position in the joined set,
-		 * as prov/coll does (coll_find_local_rank, coll_coll.c:669-689:
-		 * local_rank = index in the av_set's fi_addr_array) */
-		uint8_t *seen;
-
-		if (!nmembers || nmembers > (size_t)parent->size)
-			return -LFA_EINVAL;
-		seen = calloc((size_t)parent->size / 8 + 1, 1);
-		if (!seen)
-			return -LFA_ENOMEM;
-		for (size_t i = 0; i < nmembers; i++) {
-			if (ranks[i] < 0 || ranks[i] >= parent->size ||
-			    (seen[ranks[i] / 8] & (1u << (ranks[i] % 8)))) {
-				free(seen);
-				return -LFA_EINVAL;     /* out of range or listed twice */
-			}
-			seen[ranks[i] / 8] |= (uint8_t)(1u << (ranks[i] % 8));
-			if (ranks[i] == parent->rank) {
-				member = 1;
-				pos = (int)i;
-			}
-		}
-		free(seen);
-	} else {
-		member = 1;
-		pos = parent->rank;
-		nmembers = (size_t)parent->size;
-	}
-	if (members_only) {
-		if (!member)
-			return -LFA_EINVAL;     /* only members call this form */
-		if (!host && nmembers == (size_t)parent->size)
-			members_only = 0;       /* the whole group: every rank calls */
-	}
-	mc = calloc(1, sizeof(*mc));
-	if (!mc)
-		return -LFA_ENOMEM;
-	mc->ep = ep;
-	mc->join_context = context;
-	mc->group_id = LFA_MAX_GROUP_ID;        /* none until the join completes */
-	if (!ranks) {
-		mc->comm = parent->comm;
-		mc->rank = parent->rank;
-		mc->size = parent->size;
-		if (host && parent->members) {
-			mc->members = malloc(nmembers * sizeof(*mc->members));
-			if (!mc->members)
-				ret = -LFA_ENOMEM;
-			else
-				memcpy(mc->members, parent->members,
-				       nmembers * sizeof(*mc->members));
-		}
-	} else if (host) {
-		/* prov/coll's av_set: group rank -> the owner's address (here
-		 * the domain rank) */
-		mc->rank = pos;
-		mc->size = (int)nmembers;
-		mc->members = malloc(nmembers * sizeof(*mc->members));
-		if (!mc->members)
-			ret = -LFA_ENOMEM;
-		for (size_t i = 0; !ret && i < nmembers; i++)
-			mc->members[i] = world_rank(parent, ranks[i]);
-	} else if (members_only) {
-		/* a strict subset formed by its members alone: no split (that
-		 * needs every parent rank) but a communicator of its own */
-		ret = members_comm(ep, parent, ranks, nmembers, pos, &mc->comm);
-		mc->owns_comm = !ret;
-		mc->rank = pos;
-		mc->size = (int)nmembers;
-	} else {
-		/*
-		 * Every parent rank takes part in the split (non-members with
-		 * NCCL_SPLIT_NOCOLOR).  The split is a blocking rendezvous of the
-		 * parent's members; it is issued under comm_lock, in this rank's
-		 * call order, and NOT under ep->lock, so completions keep being
-		 * reaped (lfa_cq_read, e.g. from off_lfa's progress thread)
-		 * while the members meet (DESIGN.md §6 "ordering").
-		 */
-		ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-
-		pthread_mutex_lock(&ep->comm_lock);
-		hipSetDevice(ep->dom->device);
-		/* key = the position in the set: RCCL numbers the new
-		 * communicator by key, so its rank is the group rank */
-		if (ncclCommSplit(parent->comm, member ? 0 : NCCL_SPLIT_NOCOLOR,
-				  member ? pos : parent->rank, &mc->comm, &cfg) != ncclSuccess)
-			ret = -LFA_EIO;
-		pthread_mutex_unlock(&ep->comm_lock);
-		mc->owns_comm = !ret;
-		mc->rank = pos;
-		mc->size = (int)nmembers;
-	}
-	/*
-	 * A non-member (every parent rank calls join, as every rank of the
-	 * reference's parent group takes part in the join allreduce) gets a
-	 * handle with no communicator: it completes the join like the members
-	 * but cannot issue collectives on it (-LFA_EINVAL).
-	 */
-	if (!member) {
-		mc->comm = NULL;
-		mc->rank = -1;
-		mc->size = (int)nmembers;
-	}
-	pthread_mutex_lock(&ep->lock);
-	/* agree on the group id: BAND of the free-id masks over the PARENT
-	 * group (coll_join_collective, coll_coll.c:969-973), UINT8 x 32 — or,
-	 * members_only, over the new group itself under the reserved id
-	 * LFA_MAX_GROUP_ID (the av_set's own coll_mc as the parent) */
-	if (!ret && host) {
-		mc->mask_host = malloc(2 * LFA_CID_BYTES);
-		if (!mc->mask_host)
-			ret = -LFA_ENOMEM;
-		if (!ret) {
-			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
-			ret = host_submit(ep, members_only ? mc : parent, LFA_ALLREDUCE,
-					  mc->mask_host + LFA_CID_BYTES, mc->mask_host,
-					  LFA_CID_BYTES, -1, LFA_UINT8, LFA_BAND,
-					  context, 1, mc, 0, LFA_ALGO_TREE);
-		}
-	} else if (!ret) {
-		struct lfa_coll_mc *over = members_only ? mc : parent;
-		const uint64_t t0 = over->p2p_ticket;
-
-		hipSetDevice(ep->dom->device);
-		ret = hipHostMalloc((void **)&mc->mask_host, 2 * LFA_CID_BYTES, 0) ==
-		      hipSuccess ? 0 : -LFA_ENOMEM;
-		if (!ret && grow_staging(ep, 4 * LFA_CID_BYTES))
-			ret = -LFA_ENOMEM;
-		if (!ret) {
-			dmask = ep->hs[0];
-			memcpy(mc->mask_host + LFA_CID_BYTES, ep->cid_mask, LFA_CID_BYTES);
-			hipMemcpyAsync(dmask, mc->mask_host + LFA_CID_BYTES, LFA_CID_BYTES,
-				       hipMemcpyHostToDevice, ep->stream);
-			/* the join's own agreement: a fixed schedule, whatever
-			 * algorithm each member has selected for its collectives */
-			ret = run_device(ep, over, LFA_ALLREDUCE, dmask,
-					 (char *)dmask + LFA_CID_BYTES, LFA_CID_BYTES, -1,
-					 LFA_UINT8, LFA_BAND, ep->stream, LFA_ALGO_TREE);
-			if (!ret)
-				hipMemcpyAsync(mc->mask_host, (char *)dmask + LFA_CID_BYTES,
-					       LFA_CID_BYTES, hipMemcpyDeviceToHost, ep->stream);
-		}
-		if (!ret)
-			ret = enqueue_completion(ep, ep->stream, context, 1, mc, 0, NULL);
-		if (!ret)
-			tag_p2p(ep, over, t0);
-	}
-	if (ret)
-		free_mask(ep, mc);
-	pthread_mutex_unlock(&ep->lock);
-	if (ret) {
-		if (mc->owns_comm && mc->comm) {
-			pthread_mutex_lock(&ep->comm_lock);
-			ncclCommDestroy(mc->comm);
-			pthread_mutex_unlock(&ep->comm_lock);
-		}
-		free(mc->members);
-		free(mc);
-		return ret;
-	}
-	*mcp = mc;
-	return 0;
-}
-
-int lfa_join_collective(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
-			const int *ranks, size_t nmembers, uint64_t flags,
-			struct lfa_coll_mc **mcp, void *context)
-{
-	return join_impl(ep, coll_addr, ranks, nmembers, flags, mcp, context, 0);
-}
-
-int lfa_join_members(struct lfa_coll_ep *ep, lfa_addr_t coll_addr,
-		     const int *ranks, size_t nmembers, uint64_t flags,
-		     struct lfa_coll_mc **mcp, void *context)
-{
-	return join_impl(ep, coll_addr, ranks, nmembers, flags, mcp, context, 1);
-}
-
-int lfa_mc_close(struct lfa_coll_mc *mc)
-{
-	struct lfa_coll_ep *ep;
-
-	if (!mc)
-		return -LFA_EINVAL;
-	if (mc->is_world)
-		return -LFA_EINVAL;
-	ep = mc->ep;
-	lfa_coll_ep_flush(ep);
-	/* a join still queued for this handle completes without it */
-	pthread_mutex_lock(&ep->lock);
-	for (size_t i = 0; i < ep->qlen; i++) {
-		struct pending *p = &ep->q[(ep->qhead + i) % ep->qcap];
-
-		if (p->kind == 1 && p->mc == mc) {
-			p->kind = 2;
-			p->mc = NULL;
-		}
-		if (p->pmc == mc) {
-			/* the stream has drained (flush above): the word is final */
-			p->timed_out = p2p_timed_out(p);
-			p->pmc = NULL;
-		}
-	}
-	free_mask(ep, mc);
-	/* release the group id only if the join assigned one (a
-	 * never-completed join must not free the world's reserved id 0) */
-	if (mc->group_id < LFA_MAX_GROUP_ID)
-		ep->cid_mask[mc->group_id / 8] |= (uint8_t)(1u << (mc->group_id % 8));
-	pthread_mutex_unlock(&ep->lock);
-	if (!ep->dom->host) {
-		pthread_mutex_lock(&ep->comm_lock);
-		p2p_release(mc);
-		if (mc->owns_comm && mc->comm)
-			ncclCommDestroy(mc->comm);
-		pthread_mutex_unlock(&ep->comm_lock);
-	} else {
-		p2p_release(mc);        /* a peer domain's device workspace */
-	}
-	sig_word_free(mc);
-	free(mc->members);
-	free(mc);
-	return 0;
-}
-
-/* ---------------------------------------------------------------------- */
 /* query (coll_query_collective, coll_coll.c:1267-1318)                     */
 /* ---------------------------------------------------------------------- */
 
@@ -3662,10 +1281,3 @@ int lfa_query_collective(struct lfa_coll_domain *domain,
 	attr->max_members = ~(0x80000000u);
 	return 0;
 }
-
-/*
- * Rewrite ALLTOALL / ALLGATHER items as the equivalent grouped SEND/RECV +
- * COPY items, for executors without RCCL collectives (the loopback below;
- * tests/_plansim.py does the same in Python).
- */
-

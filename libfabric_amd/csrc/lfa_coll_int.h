@@ -337,4 +337,143 @@ LFA_INTERNAL extern const struct xport xport_peer, xport_peer_dev;
 /* lfa_coll.c */
 LFA_INTERNAL int check_reduce_args(enum lfa_datatype dt, enum lfa_op op);
 
+/* One member's record in the P2P workspace handshake (lfa_coll_ws.c): its
+ * export succeeded, the IPC handle, the workspace's identity word. */
+struct sym_rec {
+	int32_t ok;
+	int32_t pad;
+	hipIpcMemHandle_t h;
+	uint64_t id;            /* the workspace's identity word (LFA_SIG_ID_OFF) */
+};
+
+
+/*
+ * One collective on a host domain: prov/coll's util_coll_operation and its
+ * work queue (ofi_coll.h:146-163) — the schedule, its own TMP, and the run.
+ */
+struct hop {
+	struct xrun r;
+	struct plan pl;
+	void *tmp;              /* host, or device memory for a device hop */
+	int done, err;
+	int dev;                /* device buffers (xport_peer_dev) */
+	hipEvent_t fin;         /* device hop: the stream reached the end */
+	/* host buffers run as a device hop (LFA_ALGO_P2P on a GPU peer domain:
+	 * every member must follow the one schedule): staged copies, H2D on the
+	 * endpoint's copy stream (in_ev: the run's first item waits for it), D2H
+	 * on its d2h stream after the run (out_ev ends the hop) */
+	void *st_in, *st_out, *user_out;
+	size_t out_bytes;
+	hipEvent_t in_ev, out_ev;
+	int in_waited;
+	/* pageable host buffers of a small operation: a pinned bounce block
+	 * (ep->bounce) holds the input and the result; the result is copied to
+	 * bounce_user on the CPU when the hop completes (bounce_finish) */
+	void *bounce, *bounce_out, *bounce_user;
+	size_t bounce_bytes;
+	/* a device hop whose every item is on the stream: a later P2P hop may
+	 * enqueue behind it (stream order) without waiting for it to finish */
+	int issued;
+	struct word_wait ww;    /* a hop ending in the completion word */
+	/* LFA_ALGO_P2P prologue (hop_prologue): wait for the earlier operations
+	 * (they share the symmetric workspace), then grow it if needed through
+	 * two handshake collectives on the reserved seqs sub_seq, sub_seq + 1 */
+	int phase;
+	size_t sym_need, sym_size;
+	struct hop *sub;
+	uint16_t sub_seq;
+	int32_t agree_in, agree_out;
+	unsigned char mine[LFA_SYM_REC_BYTES];
+	uint64_t scratch[2];    /* barrier word and its result */
+	struct lfa_coll_ep *ep;
+};
+
+enum { HOP_RUN, HOP_WAIT_PRIOR, HOP_SYM_GATHER, HOP_SYM_AGREE };
+
+/* host-buffer chunk (bench.py --only-extra host_rs, 256 MiB float allreduce:
+ * 8 MiB 9.49 ms, 16 MiB 6.57, 32 MiB 6.49, 64 MiB 6.81, 128 MiB 7.63) */
+#define LFA_DEFAULT_CHUNK (32u << 20)
+
+/* Internal entry points shared by the provider's translation units. */
+/* lfa_coll.c */
+LFA_INTERNAL struct lfa_coll_mc *mc_of(struct lfa_coll_ep *ep, lfa_addr_t a);
+LFA_INTERNAL void release_event(struct lfa_coll_ep *ep, hipEvent_t ev);
+LFA_INTERNAL hipEvent_t event_get(struct lfa_coll_ep *ep);
+LFA_INTERNAL int queue_reserve(struct lfa_coll_ep *ep, size_t n);
+LFA_INTERNAL struct pending *queue_slot(struct lfa_coll_ep *ep);
+LFA_INTERNAL int enqueue_completion(struct lfa_coll_ep *ep, hipStream_t s,
+			      void *context, int kind, struct lfa_coll_mc *mc,
+			      uint64_t done_val, const uint64_t *done_w);
+LFA_INTERNAL int run_device(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+		      enum lfa_collective_op coll, const void *buf, void *result,
+		      size_t count, int root, enum lfa_datatype dt,
+		      enum lfa_op op, hipStream_t s, enum lfa_coll_algo algo);
+LFA_INTERNAL int mc_member(const struct lfa_coll_mc *mc);
+/* lfa_coll_word.c */
+LFA_INTERNAL int word_overdue(const struct lfa_coll_ep *ep, const uint64_t *w, hipStream_t s,
+			struct word_wait *ww, int *perr);
+LFA_INTERNAL int done_word_init(struct lfa_coll_ep *ep);
+LFA_INTERNAL void done_word_free(struct lfa_coll_ep *ep, int stream_ok);
+LFA_INTERNAL size_t solo_bytes(void);
+LFA_INTERNAL int run_solo(struct lfa_coll_ep *ep, const void *buf, void *result, size_t count,
+		    enum lfa_datatype dt);
+/* lfa_coll_ws.c */
+LFA_INTERNAL void sig_word_free(struct lfa_coll_mc *mc);
+LFA_INTERNAL int sig_ready(struct lfa_coll_mc *mc);
+LFA_INTERNAL void tag_p2p(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc, uint64_t t0);
+LFA_INTERNAL int p2p_timed_out(const struct pending *p);
+LFA_INTERNAL void ws_domain_ref(int delta);
+LFA_INTERNAL void p2p_release(struct lfa_coll_mc *mc);
+LFA_INTERNAL size_t sym_grow(const struct lfa_coll_mc *mc, size_t region);
+LFA_INTERNAL void sym_prepare(struct lfa_coll_mc *mc, size_t region, int ok,
+			struct sym_rec *mine, int *why);
+LFA_INTERNAL int sym_open(struct lfa_coll_mc *mc, const struct sym_rec *recs, size_t region,
+		    int *why);
+LFA_INTERNAL int p2p_ensure(struct lfa_coll_mc *mc, size_t region);
+/* lfa_coll_host.c */
+LFA_INTERNAL int is_device_ptr(const void *p);
+LFA_INTERNAL void *zero_copy_of(const void *p, int dev);
+LFA_INTERNAL int grow_staging(struct lfa_coll_ep *ep, size_t need);
+LFA_INTERNAL void stage_trim(struct lfa_coll_ep *ep, size_t keep);
+LFA_INTERNAL void *bounce_get(struct lfa_coll_ep *ep);
+LFA_INTERNAL void bounce_put(struct lfa_coll_ep *ep, void *p);
+LFA_INTERNAL void bounce_free_all(struct lfa_coll_ep *ep, int drained);
+LFA_INTERNAL void hop_free(struct hop *h);
+LFA_INTERNAL void host_progress_all(struct lfa_coll_ep *ep);
+LFA_INTERNAL int enqueue_host(struct lfa_coll_ep *ep, struct hop *h, void *context,
+			int kind, struct lfa_coll_mc *mc);
+LFA_INTERNAL int run_host_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			    enum lfa_collective_op coll, const void *buf,
+			    void *result, size_t count, int root,
+			    enum lfa_datatype dt, enum lfa_op op, size_t chunk);
+LFA_INTERNAL int run_device_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			      enum lfa_collective_op coll, const void *buf,
+			      void *result, size_t count, int root,
+			      enum lfa_datatype dt, enum lfa_op op, size_t chunk);
+LFA_INTERNAL int run_host_whole(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			  enum lfa_collective_op coll, const void *buf,
+			  size_t in_bytes, void *result, size_t out_bytes,
+			  size_t count, int root, enum lfa_datatype dt,
+			  enum lfa_op op);
+LFA_INTERNAL int host_start(struct lfa_coll_ep *ep, struct hop *h,
+		      struct lfa_coll_mc *mc, enum lfa_collective_op coll,
+		      const void *buf, void *result, size_t count, int root,
+		      enum lfa_datatype dt, enum lfa_op op, int dev,
+		      enum lfa_coll_algo algo);
+LFA_INTERNAL int host_submit(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+		       enum lfa_collective_op coll, const void *buf,
+		       void *result, size_t count, int root,
+		       enum lfa_datatype dt, enum lfa_op op, void *context,
+		       int kind, struct lfa_coll_mc *jmc, int dev,
+		       enum lfa_coll_algo algo);
+LFA_INTERNAL size_t peer_chunked(const struct lfa_coll_ep *ep, const struct lfa_coll_mc *mc,
+			   enum lfa_collective_op coll, size_t count, size_t esz);
+LFA_INTERNAL int peer_submit_chunked(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc,
+			       enum lfa_collective_op coll, const void *buf,
+			       void *result, size_t count, int root,
+			       enum lfa_datatype dt, enum lfa_op op, void *context,
+			       int dev, size_t chunk);
+/* lfa_coll_group.c */
+LFA_INTERNAL void join_finish(struct lfa_coll_ep *ep, struct lfa_coll_mc *mc);
+
 #endif

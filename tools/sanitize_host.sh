@@ -1,6 +1,6 @@
 #!/bin/bash
 # Host-code sanitizer runs (CPU only, no GPU): the collective provider
-# (lfa_coll.c), the off_lfa provider and the multi-process peer-transport owner
+# (lfa_coll*.c), the off_lfa provider and the multi-process peer-transport owner
 # rebuilt with ASan+UBSan and with TSan, then examples/off_lfa_peer run with
 # 2-3 ranks, owner-driven and progress-thread modes.  Kernels are not involved
 # (the peer transport reduces on the host); liblfa.so is the normal build.
@@ -14,7 +14,7 @@ for kind in asan tsan; do
   if [ $kind = asan ]; then SAN="-fsanitize=address,undefined -fno-omit-frame-pointer -g -O1"
   else SAN="-fsanitize=thread -g -O1"; fi
   gcc $SAN -fPIC -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I"$R/include" -I/opt/rocm/include \
-      -shared -o "$d/liblfa_coll.so" "$R/libfabric_amd/csrc/lfa_coll.c" "$R/libfabric_amd/csrc/lfa_coll_exec.c" "$R/libfabric_amd/csrc/lfa_coll_plan.c" "$R/libfabric_amd/csrc/lfa_coll_loopback.c" -L"$R/libfabric_amd" -llfa \
+      -shared -o "$d/liblfa_coll.so" $(for f in lfa_coll lfa_coll_word lfa_coll_ws lfa_coll_host lfa_coll_group lfa_coll_exec; do echo "$R/libfabric_amd/csrc/$f.c"; done) "$R/libfabric_amd/csrc/lfa_coll_plan.c" "$R/libfabric_amd/csrc/lfa_coll_loopback.c" -L"$R/libfabric_amd" -llfa \
       -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,"$R/libfabric_amd" -Wl,-soname,liblfa_coll.so
   gcc $SAN -fPIC -std=gnu11 -Wall -I"$R/include" -I"$FAB" -shared -o "$d/liboff_lfa-fi.so" \
       "$R/libfabric_amd/csrc/off_lfa.c" -L"$d" -llfa_coll -lpthread -Wl,-rpath,'$ORIGIN'
