@@ -15,6 +15,10 @@
  *   off_lfa_host <provider.so> avset          av_set union / intersect /
  *                                             diff on sets read from stdin,
  *                                             result order printed (CPU)
+ *   off_lfa_host <provider.so> params [LFA_X...]  the parameters the
+ *                                             provider defined (fi_info -e
+ *                                             style), then the values liblfa
+ *                                             sees for the named knobs (CPU)
  *
  * Sequence mirrored from rxm: rxm_fabric.c:85-121 (getinfo with
  * FI_PEER_TRANSFER, fi_fabric), rxm_domain.c:944-953 (fi_domain2 FI_PEER),
@@ -46,6 +50,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "off_lfa.h"
+#include "fi_param_stub.h"
 
 static int failures;
 #define CHECK(cond, ...)                                                  \
@@ -384,6 +389,16 @@ int main(int argc, char **argv)
 	CHECK(prov && !strncmp(prov->name, "off_", 4), "offload prefix");
 	CHECK(!strcmp(prov->name, OFF_LFA_PROV_NAME), "name %s", prov->name);
 	CHECK(FI_MAJOR(prov->fi_version) == FI_MAJOR_VERSION, "fi_version");
+	if (!strcmp(argv[2], "params")) {
+		typedef const char *(*param_fn)(const char *);
+		param_fn lp = (param_fn)dlsym(dl, "lfa_param");
+
+		stub_print_params(stdout);
+		for (int i = 3; i < argc && lp; i++)
+			printf("LFA %s=%s\n", argv[i], lp(argv[i]) ? lp(argv[i]) : "(unset)");
+		fflush(stdout);
+		return failures || !lp ? 1 : 0;
+	}
 
 	/* getinfo: FI_PEER_TRANSFER required (coll_init.c:39-43) */
 	hints = calloc(1, sizeof(*hints));

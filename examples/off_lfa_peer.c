@@ -56,6 +56,7 @@
 #include <rdma/providers/fi_prov.h>
 
 #include "off_lfa.h"
+#include "fi_param_stub.h"
 
 #define MAXR 16
 static int failures, me, nranks;

@@ -195,6 +195,20 @@ size_t lfa_host_small_bytes(void);
 /* Version string of the kernel library (build id, target arch). */
 const char *lfa_version(void);
 
+/*
+ * Tuning parameters.  Every knob of liblfa.so and liblfa_coll.so (LFA_*,
+ * DESIGN.md §5b's table) is read through lfa_param(name): a value set with
+ * lfa_param_set, else the environment variable of that name.  The off_lfa
+ * provider registers the deployer-facing ones with libfabric's parameter
+ * system (fi_param_define, src/var.c:188-231) as FI_OFF_LFA_<NAME> — so they
+ * show in `fi_info -e` — and hands what fi_param_get returns to
+ * lfa_param_set before it opens a domain.  Most knobs are read once, at first
+ * use: set them before the first collective of the process.
+ * lfa_param_set: value NULL removes the setting; 0 or -LFA_EINVAL / -LFA_ENOMEM.
+ */
+const char *lfa_param(const char *name);
+int lfa_param_set(const char *name, const char *value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -241,17 +241,20 @@ def build_off_lfa(verbose: bool = False) -> str | None:
               "-Wl,-rpath,$ORIGIN", "-Wl,-soname,liboff_lfa-fi.so"])
         if verbose:
             print(f"built {LIB_OFF}")
-    if _newer(OFF_HOST, [host, os.path.join(INC, "off_lfa.h")]):
+    stub = os.path.join(ROOT, "examples", "fi_param_stub.h")
+    if _newer(OFF_HOST, [host, os.path.join(INC, "off_lfa.h"), stub]):
+        # -rdynamic: the provider's fi_param_* references resolve to the
+        # owner's stubs (examples/fi_param_stub.h), as to libfabric's core
         _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Wno-unused-parameter",
-              "-D__HIP_PLATFORM_AMD__", "-I" + INC, "-I" + FABRIC_INC,
+              "-rdynamic", "-D__HIP_PLATFORM_AMD__", "-I" + INC, "-I" + FABRIC_INC,
               "-I" + os.path.join(ROCM, "include"), "-o", OFF_HOST, host,
               "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-ldl"])
         if verbose:
             print(f"built {OFF_HOST}")
-    if _newer(OFF_PEER, [OFF_PEER + ".c", os.path.join(INC, "off_lfa.h")]):
+    if _newer(OFF_PEER, [OFF_PEER + ".c", os.path.join(INC, "off_lfa.h"), stub]):
         # the multi-process owner with its own tagged transport: no HIP
         _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Wno-unused-parameter",
-              "-I" + INC, "-I" + FABRIC_INC, "-o", OFF_PEER, OFF_PEER + ".c", "-ldl",
+              "-rdynamic", "-I" + INC, "-I" + FABRIC_INC, "-o", OFF_PEER, OFF_PEER + ".c", "-ldl",
               "-lpthread"])
         if verbose:
             print(f"built {OFF_PEER}")

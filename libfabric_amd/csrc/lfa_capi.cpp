@@ -10,6 +10,7 @@
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/lfa_atomic.h"
 #include "lfa_signal.h"
@@ -436,7 +437,7 @@ int staging_acquire(StagingCtx &c, size_t bytes) {
 }
 
 bool zero_copy_on() {
-  const char *e = getenv("LFA_HOST_ZERO_COPY");
+  const char *e = lfa_param("LFA_HOST_ZERO_COPY");
   return !e || strtol(e, nullptr, 0);
 }
 
@@ -514,9 +515,10 @@ void *register_for_call(const void *p, size_t bytes) {
 
 // A temporary registration of exactly [p, p + bytes) for this call: a READY
 // one shared (refs + 1), else a new one; its index and device address, or -1
-// (the pages overlap another call's registration, the table is full, or the
-// runtime refused): the caller stages.
-int temp_take(const void *p, size_t bytes, void **d) {
+// (the pages overlap another call's registration, another call holds one —
+// `mine`, this call's other operand's, aside — or the runtime refused): the
+// caller stages.
+int temp_take(const void *p, size_t bytes, void **d, int mine) {
   pthread_mutex_lock(&g_reg_lock);
   int i = temp_find(p, bytes);
   if (i >= 0) {
@@ -529,9 +531,16 @@ int temp_take(const void *p, size_t bytes, void **d) {
     pthread_mutex_unlock(&g_reg_lock);
     return share ? i : -1;
   }
+  // one call registers at a time: hipHostRegister / hipHostUnregister from
+  // several threads at once slow each other down (4 threads of pageable
+  // 2 MiB combines: 29x one call, against 3.7x when they stage;
+  // profiles/r06_threads_probe.jsonl), so while another call holds or makes
+  // a registration this one takes the staged pipeline, which overlaps
+  int busy = 0;
+  for (int k = 0; k < kTempRegs; k++) busy += k != mine && g_temp[k].state != kRegFree;
   for (i = 0; i < kTempRegs && g_temp[i].state != kRegFree; i++) {
   }
-  if (i == kTempRegs) {
+  if (busy || i == kTempRegs) {
     pthread_mutex_unlock(&g_reg_lock);
     return -1;
   }
@@ -549,6 +558,19 @@ int temp_take(const void *p, size_t bytes, void **d) {
   pthread_mutex_unlock(&g_reg_lock);
   *d = dp;
   return dp ? i : -1;
+}
+
+// Calls in the staged pipeline right now: a call does not register its
+// pageable operands while any is (lfa_atomic_write_staged).
+int g_staged_calls;
+
+// Pageable buckets below this stage instead of registering for the call
+// (LFA_HOST_REGISTER_BYTES, default 64 MiB): below it the gain is a few
+// hundred microseconds, and a registration stalls concurrent callers.
+size_t register_min_bytes() {
+  // read per call (a call this size costs milliseconds): tests move it
+  const char *e = lfa_param("LFA_HOST_REGISTER_BYTES");
+  return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)64 << 20;
 }
 
 // This call is done with registration i: the last user unregisters it (the
@@ -596,14 +618,19 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     zd = zero_copy_addr(dst, bytes, devno, &pd);
     zs = zero_copy_addr(src, bytes, devno, &ps);
     pthread_mutex_unlock(&g_reg_lock);
-    if ((zd || pd) && (zs || ps) && (pd || ps)) {
-      // pageable operands are pinned for the call: registration + the
-      // zero-copy combine beats the runtime's staging of pageable memory
-      // (4 MiB 0.419 -> 0.256 ms, 256 MiB 15.4 -> 11.5 ms,
-      // profiles/r05_zero_copy_pageable.log)
-      if (pd) reg[0] = temp_take(dst, bytes, &zd);
+    if ((zd || pd) && (zs || ps) && (pd || ps) && bytes >= register_min_bytes() &&
+        !__atomic_load_n(&g_staged_calls, __ATOMIC_RELAXED)) {
+      // large pageable operands of a call that is alone are pinned for the
+      // call: registration + the zero-copy combine beats the runtime's
+      // staging of pageable memory (256 MiB 15.4 -> 11.5 ms,
+      // profiles/r05_zero_copy_pageable.log).  Not below
+      // LFA_HOST_REGISTER_BYTES, and not while another call is staging:
+      // registering and unregistering stall every other caller's copies and
+      // kernels (4 threads of 2 MiB: 29x one call registering, 3.7x
+      // staging; profiles/r06_threads_probe_*.jsonl)
+      if (pd) reg[0] = temp_take(dst, bytes, &zd, -1);
       if (ps && src == dst) zs = zd;
-      else if (ps) reg[1] = temp_take(src, bytes, &zs);
+      else if (ps) reg[1] = temp_take(src, bytes, &zs, reg[0]);
     }
     if (!zd || !zs) {
       // stage instead
@@ -611,6 +638,8 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
       for (int &i : reg) temp_drop(i), i = -1;
     }
   }
+  const bool staged = !(zd && zs);
+  if (staged) __atomic_add_fetch(&g_staged_calls, 1, __ATOMIC_RELAXED);
   StagingCtx &c = staging_lock(devno);
   if (zd && zs) {
     // every operand reachable from the device: one combine over the mapped
@@ -644,6 +673,7 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     if (hipStreamSynchronize(c.s_in) != hipSuccess && !ret) ret = -LFA_EIO;
   }
   pthread_mutex_unlock(&c.lock);
+  if (staged) __atomic_sub_fetch(&g_staged_calls, 1, __ATOMIC_RELAXED);
   return ret;
 }
 
@@ -666,10 +696,58 @@ int lfa__temp_registrations(void) {
 
 size_t lfa_host_small_bytes(void) {
   static size_t v = [] {
-    const char *e = getenv("LFA_HOST_SMALL_BYTES");
+    const char *e = lfa_param("LFA_HOST_SMALL_BYTES");
     return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)LFA_HOST_SMALL_DEFAULT;
   }();
   return v;
+}
+
+namespace {
+constexpr int kParams = 64;
+struct ParamSlot {
+  char name[48];
+  char value[80];
+  bool set;
+};
+ParamSlot g_params[kParams];
+pthread_mutex_t g_param_lock = PTHREAD_MUTEX_INITIALIZER;
+}  // namespace
+
+const char *lfa_param(const char *name) {
+  if (!name) return nullptr;
+  const char *v = nullptr;
+  pthread_mutex_lock(&g_param_lock);
+  for (const ParamSlot &p : g_params)
+    if (p.set && !strcmp(p.name, name)) v = p.value;
+  pthread_mutex_unlock(&g_param_lock);
+  // a set value lives until the process ends (slots are never reused for
+  // another name), so the pointer stays valid after the lock
+  return v ? v : getenv(name);
+}
+
+int lfa_param_set(const char *name, const char *value) {
+  if (!name || !*name || strlen(name) >= sizeof(ParamSlot::name) ||
+      (value && strlen(value) >= sizeof(ParamSlot::value)))
+    return -LFA_EINVAL;
+  int ret = -LFA_ENOMEM;
+  pthread_mutex_lock(&g_param_lock);
+  ParamSlot *slot = nullptr;
+  for (ParamSlot &p : g_params)
+    if (p.name[0] && !strcmp(p.name, name)) slot = &p;
+  if (!slot)
+    for (ParamSlot &p : g_params)
+      if (!p.name[0]) {
+        slot = &p;
+        strcpy(p.name, name);
+        break;
+      }
+  if (slot) {
+    slot->set = value != nullptr;
+    if (value) strcpy(slot->value, value);
+    ret = 0;
+  }
+  pthread_mutex_unlock(&g_param_lock);
+  return ret;
 }
 
 const char *lfa_version(void) {

@@ -177,16 +177,16 @@ int lfa_coll_ep_open(struct lfa_coll_domain *d, struct lfa_coll_ep **out)
 	ep->chunk = LFA_DEFAULT_CHUNK;
 	ep->solo_max = solo_bytes();
 	{
-		const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+		const char *e = lfa_param("LFA_SIG_TIMEOUT_MS");
 		const long ms = e ? atol(e) : 0;
 
 		ep->word_timeout_ns = (uint64_t)(ms > 0 ? ms : 20000) * 1000000ull;
 	}
 	{
-		const char *e = getenv("LFA_GROUP_CHUNK_BYTES");
+		const char *e = lfa_param("LFA_GROUP_CHUNK_BYTES");
 
 		ep->group_chunk = e ? (size_t)strtoull(e, NULL, 0) : LFA_GROUP_CHUNK_AUTO;
-		e = getenv("LFA_STAGE_POOL_BYTES");
+		e = lfa_param("LFA_STAGE_POOL_BYTES");
 		ep->stage_cap = e ? (size_t)strtoull(e, NULL, 0) : LFA_STAGE_POOL_BYTES;
 	}
 	/* the P2P workspace exchange needs these on every member even when a

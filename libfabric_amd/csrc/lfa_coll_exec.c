@@ -24,7 +24,7 @@ LFA_INTERNAL hipError_t lfa_hip_note(int *slot, hipError_t e, const char *what)
 		(void)hipGetLastError();
 		if (slot && !*slot)
 			*slot = (int)e;
-		if (getenv("LFA_DEBUG"))
+		if (lfa_param("LFA_DEBUG"))
 			fprintf(stderr, "lfa: %s failed: %s (%d)\n", what,
 				hipGetErrorString(e), (int)e);
 	}
@@ -160,7 +160,7 @@ static uint64_t sig_timeout_us(void)
 	static uint64_t us;
 
 	if (!us) {
-		const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+		const char *e = lfa_param("LFA_SIG_TIMEOUT_MS");
 		long ms = e ? atol(e) : 0;
 
 		us = (uint64_t)(ms > 0 ? ms : 20000) * 1000;

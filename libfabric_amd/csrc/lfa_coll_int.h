@@ -297,7 +297,7 @@ static int lfa_trace_on __attribute__((unused)) = -1;
 #define LFA_TRACE(...)                                                        \
 	do {                                                                  \
 		if (lfa_trace_on < 0)                                         \
-			lfa_trace_on = getenv("LFA_TRACE") != NULL;            \
+			lfa_trace_on = lfa_param("LFA_TRACE") != NULL;            \
 		if (lfa_trace_on) {                                           \
 			struct timespec ts_;                                  \
 			clock_gettime(CLOCK_MONOTONIC, &ts_);                 \

@@ -502,7 +502,7 @@ size_t lfa_os_ag_bytes(void)
 	static long long v = -1;
 
 	if (v < 0) {
-		const char *e = getenv("LFA_OS_AG_BYTES");
+		const char *e = lfa_param("LFA_OS_AG_BYTES");
 		const long long x = e ? atoll(e) : 0;
 
 		v = x > 0 && x <= (1ll << 30) ? x : (long long)LFA_OS_AG_BYTES_DEFAULT;
@@ -515,7 +515,7 @@ size_t lfa_os_rs_bytes(void)
 	static long long v = -1;
 
 	if (v < 0) {
-		const char *e = getenv("LFA_OS_RS_BYTES");
+		const char *e = lfa_param("LFA_OS_RS_BYTES");
 		const long long x = e ? atoll(e) : 0;
 
 		v = x > 0 && x <= (1ll << 30) ? x : (long long)LFA_OS_RS_BYTES;

@@ -255,7 +255,7 @@ static struct lfa_direct *direct_of(struct lfa_coll_ep *ep)
 	if (ep->direct || ep->direct_tried)
 		return ep->direct;
 	ep->direct_tried = 1;
-	e = getenv("LFA_DIRECT");
+	e = lfa_param("LFA_DIRECT");
 	if (e && e[0] == '0')
 		return NULL;
 	if (hipMalloc((void **)&ep->ddone_ctr, sizeof(uint32_t)) != hipSuccess ||
@@ -277,7 +277,7 @@ LFA_INTERNAL size_t solo_bytes(void)
 	static long long v = -1;
 
 	if (v < 0) {
-		const char *e = getenv("LFA_SOLO_BYTES");
+		const char *e = lfa_param("LFA_SOLO_BYTES");
 		const long long x = e ? atoll(e) : -1;
 
 		v = x >= 0 && x <= (1ll << 30) ? x : (long long)LFA_ONESHOT_SOLO_BYTES;

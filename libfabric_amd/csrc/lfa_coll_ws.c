@@ -164,7 +164,7 @@ static int va_debug(void)
 	static int on = -1;
 
 	if (on < 0)
-		on = getenv("LFA_DEBUG") != NULL;
+		on = lfa_param("LFA_DEBUG") != NULL;
 	return on;
 }
 
@@ -262,7 +262,7 @@ static pthread_mutex_t ws_lock = PTHREAD_MUTEX_INITIALIZER;
 
 static size_t env_bytes(const char *name, long long dflt)
 {
-	const char *e = getenv(name);
+	const char *e = lfa_param(name);
 	long long v = e ? atoll(e) : dflt;
 
 	return v < 0 ? 0 : (size_t)v;
@@ -501,7 +501,7 @@ int lfa_coll_ws_mem(void)
 	static int f = -1;
 
 	if (f < 0) {
-		const char *e = getenv("LFA_WS_MEM");
+		const char *e = lfa_param("LFA_WS_MEM");
 
 		f = !e || !*e || !strcmp(e, "uncached") ? hipDeviceMallocUncached :
 		    !strcmp(e, "fine") ? hipDeviceMallocFinegrained :

@@ -26,6 +26,7 @@
 #include <time.h>
 
 #include "lfa_fabric.h"
+#include "lfa_atomic.h"
 #include "lfa_signal.h"
 
 extern "C" const unsigned char lfa_direct_co[], lfa_direct_co_pl[];
@@ -127,7 +128,7 @@ uint64_t now_ns() {
 // The ring's bound: LFA_SIG_TIMEOUT_MS, the provider's bound on every GPU
 // wait (default 20 s).
 uint64_t ring_timeout_ns() {
-  const char *e = getenv("LFA_SIG_TIMEOUT_MS");
+  const char *e = lfa_param("LFA_SIG_TIMEOUT_MS");
   const long ms = e ? atol(e) : 0;
   return (uint64_t)(ms > 0 ? ms : 20000) * 1000000ull;
 }
@@ -260,7 +261,7 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
   ok = ok && hsa_agent_iterate_regions(d->gpu, find_kernarg, &karg) == HSA_STATUS_INFO_BREAK;
   // LFA_DIRECT_PRELOAD=1: the build whose arguments the packet processor
   // preloads into SGPRs (lfa_direct_k.hip)
-  const char *pe = getenv("LFA_DIRECT_PRELOAD");
+  const char *pe = lfa_param("LFA_DIRECT_PRELOAD");
   const bool pl = pe && pe[0] == '1';
   ok = ok && hsa_code_object_reader_create_from_memory(lfa_direct_co, lfa_direct_co_size,
                                                        &d->reader) == HSA_STATUS_SUCCESS;
@@ -306,7 +307,7 @@ extern "C" struct lfa_direct *lfa_direct_open(int device) {
   // needs; at system scope it is a cache writeback that the next packet (the
   // barrier bit) waits for.  LFA_DIRECT_FENCE: two letters, acquire then
   // release, s(ystem) / a(gent) / n(one); default "an".
-  const char *fe = getenv("LFA_DIRECT_FENCE");
+  const char *fe = lfa_param("LFA_DIRECT_FENCE");
   auto scope = [](char c) {
     return c == 's' ? HSA_FENCE_SCOPE_SYSTEM : c == 'a' ? HSA_FENCE_SCOPE_AGENT
                                                         : HSA_FENCE_SCOPE_NONE;

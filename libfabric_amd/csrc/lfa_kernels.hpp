@@ -1689,7 +1689,7 @@ static int launch_tree_put(void *const *dsts, int ndst, const void *const *srcs,
 static inline bool ll_enabled() {
   static int on = -1;
   if (on < 0) {
-    const char *e = getenv("LFA_OS_LL");
+    const char *e = lfa_param("LFA_OS_LL");
     on = e && e[0] == '1';
   }
   return on;
@@ -1701,7 +1701,7 @@ static inline bool ll_enabled() {
 static inline size_t os_min_chunk() {
   static long c = -1;
   if (c < 0) {
-    const char *e = getenv("LFA_OS_MIN_CHUNK");
+    const char *e = lfa_param("LFA_OS_MIN_CHUNK");
     const long v = e ? atol(e) : 0;
     c = v >= 16 && v <= (1l << 20) ? (v + 15) & ~15l : 4096;
   }

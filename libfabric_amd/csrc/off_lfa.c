@@ -76,12 +76,138 @@
 #define olfa_container_of(ptr, type, field) \
 	((type *)((char *)(ptr) - offsetof(type, field)))
 
+/* ---------------------------------------------------------- parameters -- */
+
+/*
+ * Provider parameters, registered the libfabric way:
+ * fi_param_define at fi_prov_ini makes each one FI_OFF_LFA_<NAME> and lists
+ * it with its help in `fi_info -e` (src/var.c:188-231; rxm does the same,
+ * prov/rxm/src/rxm_init.c:633-671); fi_param_get reads it.  The provider's
+ * own knobs are kept here; the kernel and executor knobs (LFA_*) go to
+ * liblfa through lfa_param_set, before any domain opens.  A host without
+ * libfabric's core (the test owners, an embedder) may leave fi_param_* out:
+ * they are weak here, and then the raw names (OFF_LFA_*, LFA_*) are read
+ * from the environment, as before round 6.  "provisional" marks defaults
+ * tuned with 2-4 processes time-sharing ONE MI355X, not on
+ * the 8-GPU xGMI topology.
+ */
+#pragma weak fi_param_define
+#pragma weak fi_param_get
+
+static const struct olfa_param {
+	const char *name;       /* FI_OFF_LFA_<NAME> */
+	enum fi_param_type type;
+	const char *raw;        /* the environment name it replaces, and for
+				 * LFA_* the liblfa knob it sets */
+	const char *help;
+} olfa_params[] = {
+	{ "transport", FI_PARAM_STRING, "OFF_LFA_TRANSPORT",
+	  "group transport: rccl (default: RCCL over xGMI) or peer (the owner's tagged messages)" },
+	{ "progress", FI_PARAM_STRING, "OFF_LFA_PROGRESS",
+	  "auto (a progress thread per endpoint, FI_PROGRESS_AUTO) or manual" },
+	{ "algo", FI_PARAM_INT, "OFF_LFA_ALGO",
+	  "enum lfa_coll_algo: 0 tree, 1 recursive doubling, 2 rccl, 3 tree over RCCL collectives, 4 p2p, 5 auto (default)" },
+	{ "device", FI_PARAM_INT, "OFF_LFA_DEVICE",
+	  "HIP device ordinal (default $LOCAL_RANK, else 0; -1 with the peer transport: host buffers only)" },
+	{ "bootstrap_dir", FI_PARAM_STRING, "OFF_LFA_BOOTSTRAP_DIR",
+	  "directory of the file rendezvous for the RCCL unique id (without fi_setopt)" },
+	{ "bootstrap_key", FI_PARAM_STRING, "OFF_LFA_BOOTSTRAP_KEY",
+	  "file rendezvous key (default world)" },
+	{ "bootstrap_timeout", FI_PARAM_INT, "OFF_LFA_BOOTSTRAP_TIMEOUT",
+	  "seconds to wait at the file rendezvous (default 120)" },
+	{ "debug", FI_PARAM_BOOL, "OFF_LFA_DEBUG", "warnings on stderr" },
+	{ "sig_timeout_ms", FI_PARAM_INT, "LFA_SIG_TIMEOUT_MS",
+	  "bound of every GPU-side wait (flag barrier, one-shot, completion word), ms (default 20000)" },
+	{ "oneshot_allreduce_bytes", FI_PARAM_SIZE_T, "LFA_OS_AG_BYTES",
+	  "allreduce/reduce buckets up to this many bytes summed over the members run as one one-shot kernel (default 2 MiB; provisional)" },
+	{ "oneshot_rs_bytes", FI_PARAM_SIZE_T, "LFA_OS_RS_BYTES",
+	  "reduce_scatter buckets up to this many bytes per member run as one one-shot kernel (default 4 MiB; provisional)" },
+	{ "group_chunk_bytes", FI_PARAM_SIZE_T, "LFA_GROUP_CHUNK_BYTES",
+	  "chunk every member of a group splits large operations into (0 off; default: 32 MiB chunks from 64 MiB per member)" },
+	{ "stage_pool_bytes", FI_PARAM_SIZE_T, "LFA_STAGE_POOL_BYTES",
+	  "idle device staging bytes a peer domain keeps (default 1 GiB)" },
+	{ "ws_mem", FI_PARAM_STRING, "LFA_WS_MEM",
+	  "P2P workspace memory: uncached (default), fine or coarse" },
+	{ "ws_cache_bytes", FI_PARAM_SIZE_T, "LFA_WS_CACHE_BYTES",
+	  "released P2P workspaces kept for reuse per process (default 4 GiB)" },
+	{ "ws_quarantine_bytes", FI_PARAM_SIZE_T, "LFA_WS_QUARANTINE_BYTES",
+	  "released P2P workspaces held, never reused, per process (default 4 GiB)" },
+	{ "host_zero_copy", FI_PARAM_BOOL, "LFA_HOST_ZERO_COPY",
+	  "combine pinned/registered host buffers on their device mappings (default 1)" },
+	{ "host_small_bytes", FI_PARAM_SIZE_T, "LFA_HOST_SMALL_BYTES",
+	  "host buckets up to this size combine in the host loop (default 1 MiB)" },
+	{ "host_register_bytes", FI_PARAM_SIZE_T, "LFA_HOST_REGISTER_BYTES",
+	  "pageable host buckets from this size are registered for the call when no other call is staging (default 64 MiB)" },
+	{ "direct", FI_PARAM_BOOL, "LFA_DIRECT",
+	  "one-member small collectives through liblfa's own HSA queue (default 1)" },
+};
+#define OLFA_NPARAMS (sizeof(olfa_params) / sizeof(olfa_params[0]))
+/* the provider's own knobs as read at fi_prov_ini (string form) */
+static char olfa_param_val[OLFA_NPARAMS][256];
+static int olfa_param_isset[OLFA_NPARAMS];
+
+/* Register and read every parameter once (fi_prov_ini). */
+static void olfa_params_init(struct fi_provider *prov)
+{
+	static int done;
+
+	if (done++)
+		return;
+	for (size_t i = 0; i < OLFA_NPARAMS; i++) {
+		const struct olfa_param *p = &olfa_params[i];
+		char buf[256];
+		int have = 0;
+
+		if (fi_param_define && fi_param_get) {
+			union { char *s; int i; size_t z; } v;
+
+			memset(&v, 0, sizeof(v));
+			fi_param_define(prov, p->name, p->type, "%s", p->help);
+			if (fi_param_get(prov, p->name, &v) == FI_SUCCESS) {
+				have = 1;
+				if (p->type == FI_PARAM_STRING)
+					snprintf(buf, sizeof(buf), "%s", v.s ? v.s : "");
+				else if (p->type == FI_PARAM_SIZE_T)
+					snprintf(buf, sizeof(buf), "%zu", v.z);
+				else
+					snprintf(buf, sizeof(buf), "%d", v.i);
+			}
+		}
+		if (!have && getenv(p->raw)) {
+			have = 1;
+			snprintf(buf, sizeof(buf), "%s", getenv(p->raw));
+		}
+		if (!have)
+			continue;
+		olfa_param_isset[i] = 1;
+		snprintf(olfa_param_val[i], sizeof(olfa_param_val[i]), "%s", buf);
+		if (!strncmp(p->raw, "LFA_", 4))
+			lfa_param_set(p->raw, buf);
+	}
+}
+
+/* The provider's own knob `name` (its string), or NULL when unset. */
+static const char *olfa_param(const char *name)
+{
+	for (size_t i = 0; i < OLFA_NPARAMS; i++)
+		if (!strcmp(olfa_params[i].name, name))
+			return olfa_param_isset[i] ? olfa_param_val[i] : NULL;
+	return NULL;
+}
+
+static int olfa_param_int(const char *name, int dflt)
+{
+	const char *v = olfa_param(name);
+
+	return v && *v ? atoi(v) : dflt;
+}
+
 static int olfa_debug = -1;
 
 static void olfa_warn(const char *fmt, const char *arg, long v)
 {
 	if (olfa_debug < 0)
-		olfa_debug = getenv("OFF_LFA_DEBUG") != NULL;
+		olfa_debug = olfa_param("debug") && strcmp(olfa_param("debug"), "0");
 	if (olfa_debug)
 		fprintf(stderr, "off_lfa: %s %s (%ld)\n", fmt, arg ? arg : "", v);
 }
@@ -496,9 +622,9 @@ static void *olfa_progress_thread(void *arg)
 
 static int olfa_uid_rendezvous(int rank, unsigned char *id)
 {
-	const char *dir = getenv("OFF_LFA_BOOTSTRAP_DIR");
-	const char *key = getenv("OFF_LFA_BOOTSTRAP_KEY");
-	int timeout = olfa_env_int("OFF_LFA_BOOTSTRAP_TIMEOUT", 120);
+	const char *dir = olfa_param("bootstrap_dir");
+	const char *key = olfa_param("bootstrap_key");
+	int timeout = olfa_param_int("bootstrap_timeout", 120);
 	char path[4096], tmp[4200];
 	const struct timespec nap = { 0, 10000000 };
 	struct timespec t0, t;
@@ -1385,14 +1511,12 @@ static int olfa_endpoint(struct fid_domain *domain, struct fi_info *info,
 	pc->peer_ops = &olfa_peer_xfer_ops;
 	pthread_mutex_init(&ep->lock, NULL);
 	pthread_mutex_init(&ep->plock, NULL);
-	ep->device = olfa_env_int("OFF_LFA_DEVICE", olfa_env_int("LOCAL_RANK", 0));
-	ep->device_set = getenv("OFF_LFA_DEVICE") != NULL;
-	algo = getenv("OFF_LFA_ALGO");
+	ep->device = olfa_param_int("device", olfa_env_int("LOCAL_RANK", 0));
+	ep->device_set = olfa_param("device") != NULL;
+	algo = olfa_param("algo");
 	ep->algo = algo && *algo ? atoi(algo) : -1;
-	ep->manual_progress = getenv("OFF_LFA_PROGRESS") &&
-			      !strcmp(getenv("OFF_LFA_PROGRESS"), "manual");
-	ep->peer_xport = getenv("OFF_LFA_TRANSPORT") &&
-			 !strcmp(getenv("OFF_LFA_TRANSPORT"), "peer");
+	ep->manual_progress = olfa_param("progress") && !strcmp(olfa_param("progress"), "manual");
+	ep->peer_xport = olfa_param("transport") && !strcmp(olfa_param("transport"), "peer");
 	*ep_fid = &ep->util.ep_fid;
 	return 0;
 }
@@ -2097,6 +2221,7 @@ static struct fi_provider olfa_prov = {
 
 FI_EXT_INI
 {
+	olfa_params_init(&olfa_prov);
 	return &olfa_prov;
 }
 

@@ -626,16 +626,18 @@ def test_staged_host_buffers(lfa):
              rng.integers(-2**62, 2**62, n)).astype(nd)
         want = a.copy()
         oracle.write(op, dt, want, b)
-        # pageable numpy buffers: registered for the call (zero-copy), then
-        # the staged pipeline in 1 MiB chunks (many pipeline steps)
+        # pageable numpy buffers: registered for the call (zero-copy, from
+        # 0 bytes here), then the staged pipeline in 1 MiB chunks
         for zero_copy in ("1", "0"):
             os.environ["LFA_HOST_ZERO_COPY"] = zero_copy
+            os.environ["LFA_HOST_REGISTER_BYTES"] = "0"
             try:
                 d = a.copy()
                 assert L.lfa_atomic_write_staged(op, dt, d.ctypes.data, b.ctypes.data, n,
                                                  1 << 20) == 0
             finally:
                 del os.environ["LFA_HOST_ZERO_COPY"]
+                del os.environ["LFA_HOST_REGISTER_BYTES"]
             assert d.tobytes() == want.tobytes(), f"pageable zero-copy={zero_copy}"
         # pinned buffers, default chunk: zero-copy, then the staged pipeline
         for zero_copy in ("1", "0"):
@@ -650,11 +652,13 @@ def test_staged_host_buffers(lfa):
     assert L.lfa_atomic_write_staged(6, 8, None, None, 4, 0) == -95
 
 
-def test_pageable_operands_sharing_pages(lfa):
+def test_pageable_operands_sharing_pages(lfa, monkeypatch):
     """Pageable dst and src in ONE allocation (dst's last page is src's
     first): the second registration is refused, so the call stages; and the
     in-place form (src == dst, registered once).  Bit-exact, and the pages are
-    left unregistered (a second call registers them again)."""
+    left unregistered (a second call registers them again).  Registration
+    from 0 bytes (LFA_HOST_REGISTER_BYTES; 64 MiB by default)."""
+    monkeypatch.setenv("LFA_HOST_REGISTER_BYTES", "0")
     from libfabric_amd import _native
     L = _native.lib()
     rng = np.random.default_rng(29)
@@ -673,12 +677,14 @@ def test_pageable_operands_sharing_pages(lfa):
     assert x.tobytes() == want.tobytes()
 
 
-def test_pageable_registration_concurrent_callers(lfa):
+def test_pageable_registration_concurrent_callers(lfa, monkeypatch):
     """Four threads combine into their own pageable dst from ONE shared
     pageable src, 12 calls each (ctypes drops the GIL, so the calls
     overlap): a thread must never run on another call's temporary
     registration of src after that call unregistered it — every result
-    bit-exact."""
+    bit-exact.  Registration from 0 bytes (LFA_HOST_REGISTER_BYTES), so
+    calls that find no other call staging register, the others stage."""
+    monkeypatch.setenv("LFA_HOST_REGISTER_BYTES", "0")
     import threading
     from libfabric_amd import _native
     L = _native.lib()
@@ -909,9 +915,9 @@ def test_host_combines_from_threads_overlap(lfa):
     """the provider advertises FI_THREAD_SAFE, so host-buffer
     combines from several threads must not serialise behind one caller's
     lock.  Four threads each run a pageable float SUM through the
-    synchronous table at once (each registers its operands for the call —
-    a refcounted registry, no process-wide lock across the combine — and
-    takes its own staging slot): every result exact, at 2 and 32 MiB.  The
+    synchronous table at once (each takes its own staging slot; below
+    LFA_HOST_REGISTER_BYTES pageable operands stage, and no call registers
+    while another stages): every result exact, at 2 and 32 MiB.  The
     four calls share one PCIe link, so at 32 MiB (PCIe-bound: ~96 MiB over
     the link per call) their wall time is the link's, not below one call;
     what must not happen is losing aggregate rate to contention.  Then,
@@ -999,7 +1005,10 @@ def test_host_combines_from_threads_overlap(lfa):
     if os.path.isdir("gpurun_out"):
         with open("gpurun_out/threads_overlap.json", "a") as f:
             f.write(json.dumps(rec) + "\n")
-    # no aggregate rate lost to contention: four calls within 4.6x one
-    assert rec["32mib"]["ratio_to_one"] < 4.6, rec
-    assert rec["2mib"]["ratio_to_one"] < 4.6, rec
+    # the combine is PCIe-bound from ~1 MiB (2 MiB pinned: 6 MiB over the
+    # link in 0.13 ms), so four calls need about four times the link time;
+    # what must not happen is contention on top of it (round 5: one lock;
+    # concurrent per-call registrations: 29x at 2 MiB, tools/probe_threads.py)
+    assert rec["32mib"]["ratio_to_one"] < 5.0, rec
+    assert rec["2mib"]["ratio_to_one"] < 5.0, rec
     assert len(lat) > 10 and max(lat) < 0.1 * big_s, rec

@@ -54,6 +54,58 @@ def test_provider_exports():
     assert os.path.basename(lib) == "liboff_lfa-fi.so"     # lib<name>-fi.so
 
 
+def _params(env_extra, knobs):
+    lib, exe = _binaries()
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("FI_OFF_LFA_", "OFF_LFA_", "LFA_"))}
+    env.update(env_extra)
+    r = subprocess.run([exe, lib, "params", *knobs], capture_output=True, text=True,
+                       timeout=60, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    params = {}
+    seen = {}
+    for line in r.stdout.splitlines():
+        if line.startswith("PARAM "):
+            name, rest = line[6:].split(" ", 1)
+            params[name] = rest
+        elif line.startswith("LFA "):
+            k, v = line[4:].split("=", 1)
+            seen[k] = v
+    return params, seen
+
+
+def test_provider_parameters_through_fi_param():
+    """the provider registers its knobs with libfabric's
+    parameter system (fi_param_define at fi_prov_ini, src/var.c:188-231, as
+    rxm does, prov/rxm/src/rxm_init.c:633-671) — FI_OFF_LFA_<NAME>, listed
+    with type and help like `fi_info -e` — and what fi_param_get returns for
+    the executor's and kernels' knobs reaches liblfa (lfa_param).  The raw
+    names still work when FI_OFF_LFA_* is unset; FI_OFF_LFA_* wins over them.
+    The owner stands in for libfabric's core (examples/fi_param_stub.h)."""
+    want = {"FI_OFF_LFA_TRANSPORT", "FI_OFF_LFA_PROGRESS", "FI_OFF_LFA_ALGO",
+            "FI_OFF_LFA_DEVICE", "FI_OFF_LFA_SIG_TIMEOUT_MS",
+            "FI_OFF_LFA_ONESHOT_ALLREDUCE_BYTES", "FI_OFF_LFA_ONESHOT_RS_BYTES",
+            "FI_OFF_LFA_GROUP_CHUNK_BYTES", "FI_OFF_LFA_WS_MEM", "FI_OFF_LFA_HOST_ZERO_COPY",
+            "FI_OFF_LFA_DIRECT", "FI_OFF_LFA_STAGE_POOL_BYTES"}
+    knobs = ["LFA_SIG_TIMEOUT_MS", "LFA_OS_AG_BYTES", "LFA_OS_RS_BYTES", "LFA_DIRECT",
+             "LFA_WS_MEM", "LFA_HOST_SMALL_BYTES"]
+    params, seen = _params({}, knobs)
+    assert want <= set(params), sorted(want - set(params))
+    assert params["FI_OFF_LFA_ONESHOT_ALLREDUCE_BYTES"].startswith("size_t:")
+    assert "provisional" in params["FI_OFF_LFA_ONESHOT_ALLREDUCE_BYTES"]
+    assert params["FI_OFF_LFA_DIRECT"].startswith("Boolean")
+    assert all(v == "(unset)" for v in seen.values()), seen
+    params, seen = _params({"FI_OFF_LFA_SIG_TIMEOUT_MS": "1234",
+                            "FI_OFF_LFA_ONESHOT_RS_BYTES": "0x10000",
+                            "FI_OFF_LFA_DIRECT": "off", "FI_OFF_LFA_WS_MEM": "fine",
+                            "LFA_OS_AG_BYTES": "777",              # raw name, no FI_ one
+                            "LFA_HOST_SMALL_BYTES": "5",
+                            "FI_OFF_LFA_HOST_SMALL_BYTES": "4096"}, knobs)
+    assert seen == {"LFA_SIG_TIMEOUT_MS": "1234", "LFA_OS_AG_BYTES": "777",
+                    "LFA_OS_RS_BYTES": "65536", "LFA_DIRECT": "0", "LFA_WS_MEM": "fine",
+                    "LFA_HOST_SMALL_BYTES": "4096"}, seen
+
+
 @pytest.mark.parametrize("mode", [[], ["manual"]])
 def test_host_driver_cpu(mode):
     assert _run("cpu", *mode).startswith("OK cpu")

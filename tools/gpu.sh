@@ -176,6 +176,10 @@ for stage in "$@"; do
         LFA_WS_MEM=$kind $S "wsmem_$kind" 300 python3 -u tools/probe_p2p_latency.py --world 2 \
           --reps "${WSMEM_REPS:-300}" --only "p2p:${WSMEM_SIZES:-4096,65536,1048576,16777216,67108864}" || exit 99
       done ;;
+    threads)
+      # host-buffer combines from 4 threads: zero-copy (default), then staged
+      $S threads_zc 200 python3 -u tools/probe_threads.py && \
+      LFA_HOST_ZERO_COPY=0 $S threads_staged 200 python3 -u tools/probe_threads.py || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac
