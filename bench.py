@@ -118,7 +118,8 @@ _CHILD = None                          # the running isolated child (watchdog ki
 _ISO_SEQ = [0]
 
 
-def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float) -> dict:
+def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float,
+                 env_extra: dict | None = None) -> dict:
     """Run `cmd` as this rank's member of a NEW N-rank job (fresh rendezvous
     port, same RANK / LOCAL_RANK / WORLD_SIZE) in a child process, and return
     rank 0's last JSON line from it.
@@ -144,6 +145,7 @@ def run_isolated(cmd: list[str], rank: int, world: int, budget_s: float) -> dict
     env.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=port, LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)),
                HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.update(env_extra or {})
     status = "ok"
     with tempfile.TemporaryFile("w+") as out:
         p = _CHILD = subprocess.Popen(cmd, env=env, stdout=out)
@@ -633,9 +635,11 @@ def extra_fetch_tables(dev, stream):
             ("swap_float_cswap", 5 * S_BYTES,
              lambda i: atomic.swap(12, FI_FLOAT, sets[i % 2][0], sets[i % 2][1],
                                    sets[i % 2][3], sets[i % 2][2], COUNT, stream))):
-        for i in range(4):
-            fn(i)
-        ms = _kernel_events(fn, 20, stream)
+        # steady clocks first, as for the headline (round 5 timed 20 launches
+        # after 4 and measured the clock ramp with them: 170.2 / 219.3 us
+        # against 163-168 / 210 us after a prewarm)
+        prewarm(fn, 0.1)
+        ms = _kernel_events(fn, 40, stream)
         gbps = nb / (ms * 1e-3) / 1e9
         out[name] = {"kernel_us": round(ms * 1e3, 1), "achieved_gbs": round(gbps, 1),
                      "frac": round(gbps / PEAK_GBPS, 4)}
@@ -1327,6 +1331,91 @@ def _allreduce_sweep(ep, world, algos, out=None):
     return out
 
 
+OS_CROSSOVER_BOUND = 1 << 30     # one-shot bounds in the crossover child
+
+
+def _provider_ep(rank, world):
+    """The endpoint the N > 1 provider extras use: a device domain over RCCL,
+    or in a rehearsal (ranks sharing a GPU, which RCCL refuses) a GPU peer
+    domain whose transfers gloo carries."""
+    from libfabric_amd import coll
+    if REHEARSE and world > 1:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from gloo_xfer import GlooXfer
+        return coll.HostEndpoint(rank, world, GlooXfer(), device=torch.cuda.current_device())
+    return coll.Endpoint.from_torch_dist()
+
+
+def extra_oneshot_crossover(rank, world, emit=None):
+    """where the one-shot kernel stops beating the tree, per
+    bucket, on THIS topology — so the first 8-GPU run retunes LFA_OS_AG_BYTES
+    / LFA_OS_RS_BYTES (FI_OFF_LFA_ONESHOT_*) from data.  Runs in its own
+    child with both bounds at OS_CROSSOVER_BOUND, so LFA_ALGO_P2P plans the
+    one-shot at every size here; TREE beside it.  Float SUM allreduce and
+    double PROD reduce_scatter, batches in flight, max over ranks.  Reports
+    per size both times, and the largest bucket where the one-shot wins —
+    the bound to set (allreduce: summed over the members, as the knob is)."""
+    from libfabric_amd import coll
+    emit = emit or (lambda _o: None)
+    out = {"bounds_in_this_child": {"LFA_OS_AG_BYTES": os.environ.get("LFA_OS_AG_BYTES"),
+                                    "LFA_OS_RS_BYTES": os.environ.get("LFA_OS_RS_BYTES")},
+           "defaults": {"LFA_OS_AG_BYTES": 2 << 20, "LFA_OS_RS_BYTES": 4 << 20},
+           "tuned_on": "2-4 processes sharing one MI355X (DESIGN.md §5b)"}
+    ep = _provider_ep(rank, world)
+    try:
+        for coll_name, sizes in (("allreduce", (16 << 10, 64 << 10, 256 << 10, 1 << 20,
+                                                4 << 20)),
+                                 ("reduce_scatter", (64 << 10, 256 << 10, 1 << 20, 4 << 20,
+                                                     16 << 20))):
+            rows, win = {}, 0
+            for nbytes in sizes:
+                if coll_name == "allreduce":
+                    n = nbytes // 4
+                    x = torch.rand(n, device="cuda")
+                    y = torch.empty_like(x)
+
+                    def op():
+                        return ep.allreduce(x, y, n, 8, 2)
+                else:
+                    n = nbytes // 8
+                    x = torch.rand(n, device="cuda", dtype=torch.float64) * 0.2 + 0.9
+                    y = torch.empty(max(coll.block(n, world, rank)[1], 1), device="cuda",
+                                    dtype=torch.float64)
+
+                    def op():
+                        return ep.reduce_scatter(x, y, n, 9, 3)
+                torch.cuda.synchronize()
+                row = {}
+                reps = 30 if nbytes <= (1 << 20) else 10
+                for name, algo in (("tree", coll.ALGO_TREE), ("oneshot", coll.ALGO_P2P)):
+                    try:
+                        ep.set_algo(algo)
+                        ep.wait(op())
+                        barrier(world)
+                        t0 = time.perf_counter()
+                        ctxs = [op() for _ in range(reps)]
+                        ep.wait(ctxs[-1])
+                        row[name + "_us"] = round(
+                            max_over_ranks(time.perf_counter() - t0, world) / reps * 1e6, 1)
+                    except Exception as e:  # noqa: BLE001
+                        row[name + "_error"] = f"{e}"[:120]
+                if row.get("oneshot_us", 1e30) < row.get("tree_us", 0.0):
+                    win = nbytes
+                rows[str(nbytes)] = row
+            ep.set_algo(coll.ALGO_TREE)
+            c = ep.counters()
+            out[coll_name] = {"by_bucket_bytes_per_rank": rows,
+                              "oneshot_wins_up_to_bytes_per_rank": win,
+                              "suggested_bound": win * world if coll_name == "allreduce" else win,
+                              "knob": ("LFA_OS_AG_BYTES (summed over the members)"
+                                       if coll_name == "allreduce" else "LFA_OS_RS_BYTES")}
+            out["counters"] = c
+            emit(out)
+    finally:
+        ep.close()
+    return out
+
+
 def extra_collectives(rank, world, stream, emit=None):
     """BASELINE configs[3]/[4] at N>1: float SUM allreduce of 256 MiB per rank
     and a double PROD reduce_scatter bucket sweep, through the C provider
@@ -1854,7 +1943,8 @@ def main() -> None:
                     help="--tune-treeput: separate allocations or one skewed pool")
     ap.add_argument("--skews", default="", help="comma list of byte skews")
     ap.add_argument("--sweep-ops", action="store_true")
-    ap.add_argument("--only-extra", default="", help="run one extra: tree_put, host_rs, config3, sizes (dev); "
+    ap.add_argument("--only-extra", default="", help="run one extra: tree_put, host_rs, config3, sizes, fetch, buckets (dev); "
+                    "crossover (the one-shot / tree crossover child), "
                     "coll (the isolated N>1 provider extras, started by run_isolated)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-extras-coll", action="store_true",
@@ -1902,6 +1992,16 @@ def main() -> None:
                                                torch.cuda.current_stream(),
                                                args.sizes_reps, args.prewarm_s)}))
         return
+    if args.only_extra == "fetch":
+        torch.cuda.set_device(0)
+        print(json.dumps({"fetch": extra_fetch_tables(torch.device("cuda", 0),
+                                                      torch.cuda.current_stream())}))
+        return
+    if args.only_extra == "buckets":
+        torch.cuda.set_device(0)
+        print(json.dumps({"buckets_two_streams": extra_two_streams(
+            torch.device("cuda", 0), [COUNT // 8])}))
+        return
     if args.only_extra == "tree_put":
         torch.cuda.set_device(0)
         print(json.dumps({"tree_put": extra_tree_put(torch.device("cuda", 0),
@@ -1917,14 +2017,18 @@ def main() -> None:
     lib()  # no fallback: raises if liblfa.so is missing
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
-    if args.only_extra == "coll":
+    if args.only_extra in ("coll", "crossover"):
         # the isolated child of run_isolated: the provider extras only
         def show(o):
             if rank == 0:
                 print(json.dumps(o), flush=True)
                 log(f"bench.py: provider extras rows so far: {len(o)}")
         try:
-            extra_collectives(rank, world, stream, show)
+            if args.only_extra == "crossover":
+                show({"oneshot_crossover": extra_oneshot_crossover(
+                    rank, world, lambda o: show({"oneshot_crossover": o}))})
+            else:
+                extra_collectives(rank, world, stream, show)
         except Exception as e:  # noqa: BLE001
             show({"error": f"{type(e).__name__}: {e}"[:300]})
         finally:
@@ -1997,6 +2101,28 @@ def main() -> None:
                           "(profiles/r02_probe_hbm_access_mix.log)"},
         },
     }
+    if world > 1:
+        # Strong scaling beside the weak headline, with equal prominence
+        # (ADVICE r5): ONE 256 MiB pair per step split into N contiguous
+        # 4 KiB-aligned shards (BASELINE configs[3]'s "8 GPUs
+        # each combine S/8").  Rounds 1-4 reported THIS as `value`; since
+        # round 5 `value` is the weak form (the tier's rule for a path that
+        # partitions), so compare rounds on the matching field.
+        off, scnt = shard_of(COUNT, world, rank)
+        w = timed_combine(dev, stream, scnt, 2000 + rank, args, world)
+        line["strong_scaling"] = {
+            "value": round(3 * S_BYTES * args.steps / w["elapsed"] / 2**30, 2),
+            "unit": "GiB/s", "scaling": "strong",
+            "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
+            "workload": "one 256 MiB float32 pair per step, sharded over the N GPUs",
+            "shard_bytes_per_gpu": scnt * 4,
+            "kernel_us": round(w["kern_ms"] * 1e3, 2),
+            "frac": round(3 * scnt * 4 / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4),
+            "traffic": read_traffic_shard(scnt * 4)[0]}
+        line["scaling_note"] = ("value: weak (every GPU its own 256 MiB pair per step) since "
+                                "round 5; rounds 1-4 reported the strong form, now "
+                                "strong_scaling.value")
+        torch.cuda.empty_cache()
     if REHEARSE:
         line["rehearsal"] = "LFA_BENCH_REHEARSE: ranks share GPUs; not a measurement"
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -2027,19 +2153,6 @@ def main() -> None:
         wd.start()
         ex = line.setdefault("extras", {})
         try:
-            if world > 1:
-                # strong scaling beside the weak headline: ONE 256 MiB pair
-                # split into N contiguous 4 KiB-aligned shards
-                off, scnt = shard_of(COUNT, world, rank)
-                w = timed_combine(dev, stream, scnt, 2000 + rank, args, world)
-                ex["strong_scaling_one_256mib_pair_sharded"] = {
-                    "value": round(3 * S_BYTES * args.steps / w["elapsed"] / 2**30, 2),
-                    "unit": "GiB/s", "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
-                    "shard_bytes_per_gpu": scnt * 4,
-                    "kernel_us": round(w["kern_ms"] * 1e3, 2),
-                    "frac": round(3 * scnt * 4 / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4),
-                    "traffic": read_traffic_shard(scnt * 4)[0]}
-                torch.cuda.empty_cache()
             # independent buckets two streams at a time, at this rank's
             # shard (and at N = 1 at the N = 8 shard, 32 MiB) — only below
             # 192 MiB per operand: at 256 MiB two streams contend and lose
@@ -2064,7 +2177,19 @@ def main() -> None:
                 budget = args.extras_timeout - (time.time() - t_extras) - 20.0
                 ex.update(run_isolated(
                     [sys.executable, os.path.abspath(__file__), "--gpus", str(world),
-                     "--only-extra", "coll"], rank, world, max(budget, 10.0)))
+                     "--only-extra", "coll"], rank, world, max(budget - 60.0, 10.0)))
+                # the one-shot / tree crossover per bucket, with the one-shot
+                # bounds lifted in that child only
+                budget = args.extras_timeout - (time.time() - t_extras) - 20.0
+                if budget > 20.0:
+                    res = run_isolated(
+                        [sys.executable, os.path.abspath(__file__), "--gpus", str(world),
+                         "--only-extra", "crossover"], rank, world, budget,
+                        {"LFA_OS_AG_BYTES": str(OS_CROSSOVER_BOUND),
+                         "LFA_OS_RS_BYTES": str(OS_CROSSOVER_BOUND)})
+                    ex["oneshot_crossover"] = res.get("oneshot_crossover", res)
+                    if "isolated_status" in res:
+                        ex["oneshot_crossover"]["isolated_status"] = res["isolated_status"]
             elif not args.no_extras_coll:
                 ex.update(extra_collectives(rank, world, stream))
         except Exception as e:  # noqa: BLE001 — extras must not hide the metric

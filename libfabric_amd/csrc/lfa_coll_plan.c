@@ -610,7 +610,15 @@ int lfa_coll_plan(enum lfa_collective_op coll, enum lfa_coll_algo algo,
 	if (algo == LFA_ALGO_P2P) {
 		/* reducing collectives over the symmetric workspace; the rest
 		 * (pure transport) keep the RCCL schedules */
-		if (n > 1 && n <= LFA_TREE_MAX && n <= LFA_PUT_MAX &&
+		/* n = 1: only a one-shot-sized bucket — the one-shot kernel's
+		 * degenerate group, one copy launch ending in the completion
+		 * word (a one-member endpoint runs it when its solo copy is
+		 * turned off, lfa_coll_ep_test_solo) */
+		const int os1 = n == 1 &&
+				(coll == LFA_REDUCE_SCATTER ? bytes <= lfa_os_rs_bytes() :
+							       bytes <= lfa_os_ag_bytes());
+
+		if ((n > 1 || os1) && n <= LFA_TREE_MAX && n <= LFA_PUT_MAX &&
 		    (coll == LFA_ALLREDUCE || coll == LFA_REDUCE_SCATTER ||
 		     coll == LFA_REDUCE)) {
 			int ret = plan_p2p(&p, coll, r, n, root, count, esz);

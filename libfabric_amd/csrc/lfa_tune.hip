@@ -1004,6 +1004,107 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
 }
 
 // ---------------------------------------------------------------------------
+// Compare body with its third input in registers: CSWAP's
+// fetch_lds stages dst, src and cmp through LDS — 48 KiB per workgroup at
+// U = 4, so 3 workgroups (12 waves, 144 KiB of loads in flight) per CU
+// against the write body's 5 (160 KiB).  Here dst and src go HBM -> LDS and
+// cmp into VGPRs (nt global loads issued right after), 32 KiB of LDS per
+// workgroup: 5 per CU, 240 KiB in flight.  SAUX: the stores' cache policy.
+namespace lfa {
+template <int U, int SAUX, typename F>
+__global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds3r(F f, size_t nvec) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id(), l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+    u32x4 c[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      __builtin_amdgcn_global_load_lds((const void *)(f.dv + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(f.sv + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) c[u] = ld<true>(f.cv + base + u * 64 + l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u32x4 a = lds[0][w][u][l], b = lds[1][w][u][l];
+      const unsigned off = (unsigned)(u * 64 + l) * 16;
+      if constexpr (SAUX == kStoreNt) {
+        st<true>(f.rv + base + u * 64 + l, a);
+        st<true>(f.dv + base + u * 64 + l, f.op(a, b, c[u]));
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
+        __builtin_amdgcn_raw_buffer_store_b128(f.op(a, b, c[u]), rd, off, 0, SAUX);
+      }
+    }
+  } else {
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec) f.vec(i);
+    }
+  }
+}
+
+// The same, drained step by step (fetch_drain's scheme): loads issue per step
+// u as dst u, src u (LDS) and cmp u (VGPRs), so step u waits only until its
+// three have landed — 3·(U-1-u) younger loads and the 2·u stores of the
+// earlier steps may still be in flight.
+template <int U, int SAUX, typename F, int u>
+__device__ __forceinline__ void swap3r_drain(const F &f, u32x4 (*lds)[kLdsWaves][U][64],
+                                             const u32x4 *c, unsigned w, unsigned l,
+                                             size_t base, __amdgpu_buffer_rsrc_t rr,
+                                             __amdgpu_buffer_rsrc_t rd) {
+  if constexpr (u < U) {
+    wait_vmcnt<3 * (U - 1 - u) + 2 * u>();
+    const u32x4 a = lds[0][w][u][l], b = lds[1][w][u][l];
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    if constexpr (SAUX == kStoreNt) {
+      st<true>(f.rv + base + u * 64 + l, a);
+      st<true>(f.dv + base + u * 64 + l, f.op(a, b, c[u]));
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
+      __builtin_amdgcn_raw_buffer_store_b128(f.op(a, b, c[u]), rd, off, 0, SAUX);
+    }
+    swap3r_drain<U, SAUX, F, u + 1>(f, lds, c, w, l, base, rr, rd);
+  }
+}
+
+template <int U, int SAUX, typename F>
+__global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds3r_drain(F f, size_t nvec) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id(), l = threadIdx.x % 64;
+  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+  if (base + 64 * U <= nvec) {
+    u32x4 c[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      __builtin_amdgcn_global_load_lds((const void *)(f.dv + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(f.sv + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+      c[u] = __builtin_nontemporal_load(f.cv + base + u * 64 + l);
+    }
+    swap3r_drain<U, SAUX, F, 0>(
+        f, lds, c, w, l, base,
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000),
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000));
+  } else {
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec) f.vec(i);
+    }
+  }
+}
+}  // namespace lfa
+
+// ---------------------------------------------------------------------------
 // fetch / compare table bodies (tools/probe_fetch.py --tune): float SUM
 // readwrite (swap = 0) or float CSWAP (swap = 1) over nvec co-aligned 16-B
 // vectors.  0 = the round-1 register form (fetch_vec, 2 vectors per lane),
@@ -1044,6 +1145,33 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
       case 5: lds(I2(), SC1(), NO()); break;
       case 6: lds(I4(), SC1(), YES()); break;  // drained steps (combine_drain's scheme)
       case 7: lds(I4(), NT(), YES()); break;
+      case 8: case 9: case 10: case 11:   // compare: cmp in registers
+        if constexpr (FF::kIn == 3) {
+          auto r3 = [&](auto u, auto aux) {
+            constexpr int U = decltype(u)::value, A = decltype(aux)::value;
+            hipLaunchKernelGGL((fetch_lds3r<U, A, FF>),
+                               dim3(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu)),
+                               dim3(kLdsWaves * 64), 0, s, f, nvec);
+          };
+          if (variant == 8) r3(I4(), SC1());
+          else if (variant == 9) r3(I4(), NT());
+          else if (variant == 10) r3(I2(), SC1());
+          else r3(I2(), NT());
+          break;
+        }
+        return -LFA_EINVAL;
+      case 12: case 13:   // compare: cmp in registers, drained
+        if constexpr (FF::kIn == 3) {
+          const dim3 g(grid_for(nvec, (size_t)kLdsWaves * 64 * 4, 0x7fffffffu));
+          if (variant == 12)
+            hipLaunchKernelGGL((fetch_lds3r_drain<4, kStoreNt, FF>), g, dim3(kLdsWaves * 64),
+                               0, s, f, nvec);
+          else
+            hipLaunchKernelGGL((fetch_lds3r_drain<4, kStoreSc1, FF>), g, dim3(kLdsWaves * 64),
+                               0, s, f, nvec);
+          break;
+        }
+        return -LFA_EINVAL;
       default: return -LFA_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : -LFA_EIO;
@@ -1457,6 +1585,81 @@ static void launch_taper(u32x4 *d, const u32x4 *v, size_t nvec, unsigned tail_di
                        dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
 }
 
+// Statically balanced resident grid: exactly one round of
+// workgroups (the occupancy limit per CU times the CUs, so the dispatcher
+// gives every CU the same number), each wave owning a contiguous run of
+// 1-KiB units (64 vectors) whose length differs by at most one unit between
+// waves, walked U units per LDS-DMA step.  Every CU then carries the same
+// bytes and no second, partial round of waves drains after the first — the
+// fixed cost the per-wave stamps put at 2.37 us of a 32 MiB launch.  The
+// last vectors past a whole unit go to the last wave's guarded path.
+template <int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_static(u32x4 *__restrict__ dst,
+                                                                const u32x4 *__restrict__ src,
+                                                                size_t nvec) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t nw = (size_t)gridDim.x * kLdsWaves;
+  const size_t gw = (size_t)blockIdx.x * kLdsWaves + w;
+  const size_t units = nvec / 64;
+  // balanced split: wave gw owns units [gw*units/nw, (gw+1)*units/nw)
+  size_t ub = gw * units / nw;
+  const size_t ue = (gw + 1) * units / nw;
+  while (ub < ue) {
+    const unsigned k = (unsigned)(ue - ub < (size_t)U ? ue - ub : (size_t)U);
+    const size_t base = ub * 64;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if ((unsigned)u < k) {
+        __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                         (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+        __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                         (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if ((unsigned)u < k) {
+        u32x4 v = apply_vec<OP_SUM, float>(lds[0][w][u][l], lds[1][w][u][l]);
+        if constexpr (SAUX == kStoreNt)
+          st<true>(dst + base + u * 64 + l, v);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+      }
+    ub += k;
+  }
+  if (gw == nw - 1) {
+    const size_t i = units * 64 + l;
+    if (i < nvec)
+      st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+  }
+}
+
+template <int U>
+static void launch_static(u32x4 *d, const u32x4 *v, size_t nvec, int grid_mult,
+                          hipStream_t s) {
+  int per_cu = 0, dev = 0, cus = 0;
+  const bool nt = nvec * 16 >= kSc1Bytes;
+  if ((nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreNt>,
+                                                          kLdsWaves * 64, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreSc1>,
+                                                          kLdsWaves * 64, 0)) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return;
+  size_t g = (size_t)per_cu * cus * grid_mult;
+  const size_t waves_needed = (nvec / 64 + 1 + kLdsWaves - 1) / kLdsWaves;
+  if (g > waves_needed) g = waves_needed ? waves_needed : 1;
+  if (nt)
+    hipLaunchKernelGGL((combine_static<U, kStoreNt>), dim3((unsigned)g), dim3(kLdsWaves * 64), 0,
+                       s, d, v, nvec);
+  else
+    hipLaunchKernelGGL((combine_static<U, kStoreSc1>), dim3((unsigned)g), dim3(kLdsWaves * 64), 0,
+                       s, d, v, nvec);
+}
+
 }  // namespace lfa
 
 extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_t nvec,
@@ -1488,6 +1691,12 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 84: lfa::launch_dyn<8, lfa::kStoreSc1, true>(d, v, nvec, s); break;
     // tapered tail: head tiles 4 KiB per wave, the last 1/div of the data in
     // UT-KiB tiles
+    // statically balanced resident grid: U-KiB steps, one (or two) rounds
+    case 90: lfa::launch_static<4>(d, v, nvec, 1, s); break;
+    case 91: lfa::launch_static<2>(d, v, nvec, 1, s); break;
+    case 92: lfa::launch_static<8>(d, v, nvec, 1, s); break;
+    case 93: lfa::launch_static<4>(d, v, nvec, 2, s); break;
+    case 94: lfa::launch_static<1>(d, v, nvec, 1, s); break;
     case 85: lfa::launch_taper<4, 2>(d, v, nvec, 8, s); break;
     case 86: lfa::launch_taper<4, 2>(d, v, nvec, 4, s); break;
     case 87: lfa::launch_taper<4, 1>(d, v, nvec, 8, s); break;

@@ -229,7 +229,7 @@ def test_word_bound_starts_at_the_head_of_the_queue(coll, monkeypatch):
         torch.cuda.synchronize()
         per_s = 50_000_000 / max(time.monotonic() - t0, 1e-4)
         e.test_word(timeout_ms=300)
-        s = torch.cuda.ExternalStream(e.stream_handle(), device=torch.device(DEV))
+        s = torch.cuda.ExternalStream(e.stream_handle, device=torch.device(DEV))
         w0 = e.word_ops()
         t0 = time.monotonic()
         with torch.cuda.stream(s):

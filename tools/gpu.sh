@@ -180,6 +180,13 @@ for stage in "$@"; do
       # host-buffer combines from 4 threads: zero-copy (default), then staged
       $S threads_zc 200 python3 -u tools/probe_threads.py && \
       LFA_HOST_ZERO_COPY=0 $S threads_staged 200 python3 -u tools/probe_threads.py || exit 99 ;;
+    fetchx)
+      # the fetch / compare table extra (prewarmed), three times
+      for i in 1 2 3; do $S "fetch_extra_$i" 200 python3 -u bench.py --only-extra fetch || exit 99; done ;;
+    fetchtune)
+      FETCH_VARIANTS="${FETCH_VARIANTS:-4,6,7,8,9,10,11}" $S fetch_tune 400 python3 -u tools/probe_fetch.py --tune || exit 99 ;;
+    bucketsx)
+      $S buckets_extra 200 python3 -u bench.py --only-extra buckets || exit 99 ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac

@@ -69,14 +69,16 @@ def tune():
     n = S // 4
     nvec = n // 4
     variants = [int(v) for v in os.environ.get("FETCH_VARIANTS", "0,1,2,3,4,5,6,7").split(",")]
+    # 8..11: the compare body with cmp in registers (U 4 sc1 / 4 nt / 2 sc1 / 2 nt)
     for swap, nbytes in ((0, 4 * S), (1, 5 * S)):
         g = torch.Generator(device="cuda").manual_seed(3)
         sets = [[torch.rand(n, device="cuda", generator=g) for _ in range(4)]
                 for _ in range(2)]
         for t in sets:                      # cmp == dst on half the lanes
             t[3][::2] = t[0][::2]
+        vs = [v for v in variants if swap or v < 8]    # 8..11: compare only
         ref = None
-        for v in variants:                  # correctness on a fresh copy
+        for v in vs:                        # correctness on a fresh copy
             d, sr, c, r = (x.clone() for x in sets[0])
             assert L.lfa__tune_fetch_f32(v, swap, d.data_ptr(), sr.data_ptr(), c.data_ptr(),
                                          r.data_ptr(), nvec, h) == 0
@@ -86,9 +88,9 @@ def tune():
             elif not (torch.equal(ref[0], d) and torch.equal(ref[1], r)):
                 raise SystemExit(f"fetch variant {v} swap={swap} WRONG")
         del ref
-        times = {v: [] for v in variants}
+        times = {v: [] for v in vs}
         for _ in range(8):
-            for v in variants:
+            for v in vs:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for i in range(10):
@@ -98,7 +100,7 @@ def tune():
                 b.record()
                 torch.cuda.synchronize()
                 times[v].append(a.elapsed_time(b) / 10)
-        for v in variants:
+        for v in vs:
             t = statistics.median(times[v][2:])
             print(json.dumps({"tune_fetch": "cswap" if swap else "readwrite_sum", "variant": v,
                               "us": round(t * 1e3, 1),

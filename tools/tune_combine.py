@@ -43,7 +43,7 @@ def main():
 
     def fn(v):
         return (L.lfa__tune_sum_f32 if v < 12 or v == 30 else
-                L.lfa__tune3_sum_f32 if 70 <= v < 90 else L.lfa__tune2_sum_f32)
+                L.lfa__tune3_sum_f32 if 70 <= v < 100 else L.lfa__tune2_sum_f32)
 
     # correctness first, odd size (partial last tile)
     n = (1 << 20) + 77
