@@ -1883,16 +1883,19 @@ static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
     // to back, profiles/r03_tune_fetch*.log).  The three-input compare body
     // gains nothing measurable either way (212.5 - 217.6 us over every form)
     // and keeps round 2's.
+    // Round 6: the three-input compare body takes the nt-drained form from
+    // kSc1Bytes too — 256 MiB float CSWAP 212.5 us (79.0 %) against 215.2 us
+    // for the sc1 body on one box, 167.0-167.9 / 173.8-175.8 us for the
+    // readwrite pair (tools/probe_fetch.py --tune, profiles/r06_tune_fetch_*.jsonl);
+    // cmp loaded into VGPRs instead of LDS (5 workgroups per CU instead of 3)
+    // measured 213.7 us, no better.
     constexpr int U = 4;
     constexpr bool D = FF::kIn == 2;
     const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu));
-    bool nt = false;
-    if constexpr (D) {
-      nt = nvec * 16 >= kSc1Bytes;
-      if (nt)
-        hipLaunchKernelGGL((fetch_lds<U, kStoreNt, FF, true>), grid, dim3(kLdsWaves * 64), 0,
-                           s, f, nvec);
-    }
+    const bool nt = nvec * 16 >= kSc1Bytes;
+    if (nt)
+      hipLaunchKernelGGL((fetch_lds<U, kStoreNt, FF, true>), grid, dim3(kLdsWaves * 64), 0, s,
+                         f, nvec);
     if (nvec && !nt)
       hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF, D>), grid, dim3(kLdsWaves * 64), 0, s,
                          f, nvec);

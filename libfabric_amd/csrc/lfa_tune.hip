@@ -1052,56 +1052,6 @@ __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds3r(F f, size_t nvec) 
   }
 }
 
-// The same, drained step by step (fetch_drain's scheme): loads issue per step
-// u as dst u, src u (LDS) and cmp u (VGPRs), so step u waits only until its
-// three have landed — 3·(U-1-u) younger loads and the 2·u stores of the
-// earlier steps may still be in flight.
-template <int U, int SAUX, typename F, int u>
-__device__ __forceinline__ void swap3r_drain(const F &f, u32x4 (*lds)[kLdsWaves][U][64],
-                                             const u32x4 *c, unsigned w, unsigned l,
-                                             size_t base, __amdgpu_buffer_rsrc_t rr,
-                                             __amdgpu_buffer_rsrc_t rd) {
-  if constexpr (u < U) {
-    wait_vmcnt<3 * (U - 1 - u) + 2 * u>();
-    const u32x4 a = lds[0][w][u][l], b = lds[1][w][u][l];
-    const unsigned off = (unsigned)(u * 64 + l) * 16;
-    if constexpr (SAUX == kStoreNt) {
-      st<true>(f.rv + base + u * 64 + l, a);
-      st<true>(f.dv + base + u * 64 + l, f.op(a, b, c[u]));
-    } else {
-      __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
-      __builtin_amdgcn_raw_buffer_store_b128(f.op(a, b, c[u]), rd, off, 0, SAUX);
-    }
-    swap3r_drain<U, SAUX, F, u + 1>(f, lds, c, w, l, base, rr, rd);
-  }
-}
-
-template <int U, int SAUX, typename F>
-__global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds3r_drain(F f, size_t nvec) {
-  __shared__ u32x4 lds[2][kLdsWaves][U][64];
-  const unsigned w = wave_id(), l = threadIdx.x % 64;
-  const size_t base = (size_t)blockIdx.x * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
-  if (base + 64 * U <= nvec) {
-    u32x4 c[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      __builtin_amdgcn_global_load_lds((const void *)(f.dv + base + u * 64 + l),
-                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
-      __builtin_amdgcn_global_load_lds((const void *)(f.sv + base + u * 64 + l),
-                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
-      c[u] = __builtin_nontemporal_load(f.cv + base + u * 64 + l);
-    }
-    swap3r_drain<U, SAUX, F, 0>(
-        f, lds, c, w, l, base,
-        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000),
-        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000));
-  } else {
-    for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * 64 + l;
-      if (i < nvec) f.vec(i);
-    }
-  }
-}
 }  // namespace lfa
 
 // ---------------------------------------------------------------------------
@@ -1157,18 +1107,6 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
           else if (variant == 9) r3(I4(), NT());
           else if (variant == 10) r3(I2(), SC1());
           else r3(I2(), NT());
-          break;
-        }
-        return -LFA_EINVAL;
-      case 12: case 13:   // compare: cmp in registers, drained
-        if constexpr (FF::kIn == 3) {
-          const dim3 g(grid_for(nvec, (size_t)kLdsWaves * 64 * 4, 0x7fffffffu));
-          if (variant == 12)
-            hipLaunchKernelGGL((fetch_lds3r_drain<4, kStoreNt, FF>), g, dim3(kLdsWaves * 64),
-                               0, s, f, nvec);
-          else
-            hipLaunchKernelGGL((fetch_lds3r_drain<4, kStoreSc1, FF>), g, dim3(kLdsWaves * 64),
-                               0, s, f, nvec);
           break;
         }
         return -LFA_EINVAL;

@@ -381,6 +381,50 @@ def test_nt_store_path_every_op_family(lfa, op, dt):
         assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
 
 
+@pytest.mark.parametrize("table,op,dt", [("rw", 2, 8), ("rw", 10, 9), ("rw", 7, 6),
+                                         ("swap", 12, 8), ("swap", 16, 9), ("swap", 18, 6)])
+def test_fetch_compare_nt_path(lfa, table, op, dt):
+    """From 192 MiB per operand the fetch and the compare tables run the
+    nt-store drained body (round 6 moved the three-input compare there too):
+    float SUM / double ATOMIC_READ / int64 BAND readwrite and float CSWAP /
+    double CSWAP_GE / int64 MSWAP at 200 MiB + a ragged tail, against the
+    oracle on windows at both ends, the middle and across the last tile.
+    cmp equals dst on half the lanes, so both outcomes of every compare run."""
+    nd = oracle.DT_NP[dt]
+    e = nd.itemsize
+    n = ((200 << 20) + 4 * 1000 + e * 3) // e
+    g = torch.Generator(device=DEV).manual_seed(op * 11 + dt)
+    tdt = {4: torch.float32, 8: torch.float64}.get(e) if nd.kind == "f" else torch.int64
+
+    def rnd():
+        if nd.kind == "f":
+            return torch.rand(n, device=DEV, generator=g, dtype=tdt) + 0.5
+        return torch.randint(-2**62, 2**62, (n,), device=DEV, generator=g, dtype=torch.int64)
+    d0, sv, cm = rnd(), rnd(), rnd()
+    cm[::2] = d0[::2]
+    d, res = d0.clone(), torch.empty_like(d0)
+    torch.cuda.synchronize()
+    if table == "rw":
+        lfa.readwrite(op, dt, d, None if op == 10 else sv, res, n)
+    else:
+        lfa.swap(op, dt, d, sv, cm, res, n)
+    torch.cuda.synchronize()
+    tile = 16 * 1024 // e
+    for lo in (0, n // 2, (n // tile - 1) * tile - 777, n - 5000):
+        hi = min(n, lo + 5000)
+        wd = d0[lo:hi].cpu().numpy().copy()
+        wr = np.empty_like(wd)
+        if table == "rw":
+            oracle.readwrite(op, dt, wd, sv[lo:hi].cpu().numpy().copy(), wr)
+        else:
+            oracle.swap(op, dt, wd, sv[lo:hi].cpu().numpy().copy(),
+                        cm[lo:hi].cpu().numpy().copy(), wr)
+        assert_parity(dt, res[lo:hi].cpu().numpy().view(np.uint8), wr.view(np.uint8),
+                      f"res [{lo},{hi})")
+        assert_parity(dt, d[lo:hi].cpu().numpy().view(np.uint8), wd.view(np.uint8),
+                      f"dst [{lo},{hi})")
+
+
 @pytest.mark.parametrize("op,dt", [(0, 8), (1, 6), (3, 9), (6, 5), (11, 4), (8, 1), (9, 7)])
 @pytest.mark.parametrize("mib", [32, 100])
 def test_tapered_tail_every_op_family(lfa, op, dt, mib):
