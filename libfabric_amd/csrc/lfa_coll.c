@@ -538,13 +538,21 @@ static int pending_state(const struct lfa_coll_ep *ep, struct pending *p,
 	return 0;
 }
 
-static void pending_release(struct lfa_coll_ep *ep, struct pending *p)
+/* failed: the operation was reaped in error (a word timeout, a failed queue
+ * or stream) — its kernel may still run later and read or write its bounce
+ * block, so the block leaves the pool for good instead of going back to be
+ * refilled by the next submit (done_word_free keeps owed words
+ * the same way).  A hop's own free synchronises its stream first. */
+static void pending_release(struct lfa_coll_ep *ep, struct pending *p, int failed)
 {
 	if (p->hop)
 		hop_free(p->hop);
 	else if (p->ev)
 		release_event(ep, p->ev);
-	bounce_put(ep, p->bounce);
+	if (failed && !p->hop)
+		bounce_retire(ep, p->bounce);
+	else
+		bounce_put(ep, p->bounce);
 	p->hop = NULL;
 	p->ev = NULL;
 	p->bounce = NULL;
@@ -610,7 +618,7 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 		}
 		if (st == 0 && p->done_val)
 			ep->word_ops++;
-		pending_release(ep, p);
+		pending_release(ep, p, st < 0);
 		ep->qhead = (ep->qhead + 1) % ep->qcap;
 		ep->qlen--;
 	}

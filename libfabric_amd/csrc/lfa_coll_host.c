@@ -210,6 +210,20 @@ LFA_INTERNAL void bounce_put(struct lfa_coll_ep *ep, void *p)
 			ep->bounce[i].busy = 0;
 }
 
+/* A block a failed operation's kernel may still touch: out of the pool for
+ * good (its pinned memory is left allocated, with a line on stderr). */
+LFA_INTERNAL void bounce_retire(struct lfa_coll_ep *ep, void *p)
+{
+	for (int i = 0; p && i < LFA_BOUNCE_POOL; i++)
+		if (ep->bounce[i].p == p) {
+			ep->bounce[i].p = NULL;
+			ep->bounce[i].busy = 0;
+			ep->bounce_retired++;
+			fprintf(stderr, "lfa: a failed operation's bounce block (%p) is kept "
+				"out of the pool: its kernel may still run\n", p);
+		}
+}
+
 /* Endpoint close: the pinned bounce blocks back to the runtime, or, when
  * the endpoint did not drain (a kernel may still write one), kept. */
 LFA_INTERNAL void bounce_free_all(struct lfa_coll_ep *ep, int drained)

@@ -180,6 +180,7 @@ struct lfa_coll_ep {
 		void *p;
 		int busy;
 	} bounce[LFA_BOUNCE_POOL];
+	int bounce_retired;         /* blocks kept out after failed operations */
 	size_t stage_cap;           /* idle staging bytes kept */
 	int stage_trim_due;         /* idle bytes passed the cap: trim when the
 				     * queue has drained */
@@ -437,6 +438,7 @@ LFA_INTERNAL int grow_staging(struct lfa_coll_ep *ep, size_t need);
 LFA_INTERNAL void stage_trim(struct lfa_coll_ep *ep, size_t keep);
 LFA_INTERNAL void *bounce_get(struct lfa_coll_ep *ep);
 LFA_INTERNAL void bounce_put(struct lfa_coll_ep *ep, void *p);
+LFA_INTERNAL void bounce_retire(struct lfa_coll_ep *ep, void *p);
 LFA_INTERNAL void bounce_free_all(struct lfa_coll_ep *ep, int drained);
 LFA_INTERNAL void hop_free(struct hop *h);
 LFA_INTERNAL void host_progress_all(struct lfa_coll_ep *ep);

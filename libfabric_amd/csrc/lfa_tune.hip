@@ -1095,6 +1095,8 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
       case 5: lds(I2(), SC1(), NO()); break;
       case 6: lds(I4(), SC1(), YES()); break;  // drained steps (combine_drain's scheme)
       case 7: lds(I4(), NT(), YES()); break;
+      case 12: lds(I2(), NT(), YES()); break;   // drained nt, U = 2 / 3
+      case 13: lds(std::integral_constant<int, 3>(), NT(), YES()); break;
       case 8: case 9: case 10: case 11:   // compare: cmp in registers
         if constexpr (FF::kIn == 3) {
           auto r3 = [&](auto u, auto aux) {

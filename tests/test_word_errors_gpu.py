@@ -245,3 +245,33 @@ def test_word_bound_starts_at_the_head_of_the_queue(coll, monkeypatch):
         assert torch.equal(big_out, big) and torch.equal(y, x)
     finally:
         e.close()
+
+
+def test_lost_word_on_a_bounced_operation(coll, monkeypatch):
+    """a one-member group's small operation on PAGEABLE host
+    buffers runs through a pinned bounce block and completes through the
+    word.  When that word is lost the operation fails once (ETIMEDOUT) and
+    its block leaves the pool — its kernel may still run — so the operations
+    after it, which take other blocks, keep their own results."""
+    import numpy as np
+    monkeypatch.setenv("LFA_DIRECT", "0")
+    e = coll.Endpoint(0, 1, 0, coll.Endpoint.unique_id())
+    try:
+        xs = [np.arange(1024, dtype=np.float32) + 1000 * k for k in range(12)]
+        ys = [np.zeros(1024, np.float32) for _ in range(12)]
+        e.wait(e.allreduce(xs[0], ys[0], 1024, FLOAT, SUM))
+        assert np.array_equal(ys[0], xs[0])
+        e.test_word(drop_next=1, timeout_ms=300)
+        ctxs = [e.allreduce(xs[k], ys[k], 1024, FLOAT, SUM) for k in range(1, 12)]
+        ok, errs = _drain(e, 10, timeout_s=10.0)
+        assert ok == ctxs[1:]
+        assert [(x[0], x[2]) for x in errs] == [(errno.ETIMEDOUT, ctxs[0])]
+        for k in range(2, 12):
+            assert np.array_equal(ys[k], xs[k]), k
+        # the pool goes on with the blocks it has left
+        for k in range(12):
+            ys[k][:] = 0
+            e.wait(e.allreduce(xs[k], ys[k], 1024, FLOAT, SUM))
+            assert np.array_equal(ys[k], xs[k]), k
+    finally:
+        e.close()
