@@ -78,14 +78,15 @@ enum lfa_coll_algo {
 	 * (pushes) the result block into every rank's workspace in the same
 	 * pass; two stream-ordered barriers per operation, each a one-wave
 	 * flag kernel on the workspace (no RCCL collective).  Small buckets
-	 * (allreduce / reduce <= 256 KiB over all members, reduce_scatter <=
-	 * 1 MiB, 2..8 members) are ONE kernel: push into the peers' slots,
+	 * (allreduce / reduce <= 2 MiB over all members, reduce_scatter <=
+	 * 4 MiB per member, 2..8 members; LFA_OS_AG_BYTES / LFA_OS_RS_BYTES,
+	 * FI_OFF_LFA_ONESHOT_*) are ONE kernel: push into the peers' slots,
 	 * flags, tree.  No intermediate transport copies, xGMI in and out
 	 * directions busy at once. */
 	LFA_ALGO_P2P = 4,
 	/* the default on device domains: per operation, LFA_ALGO_P2P's
-	 * one-kernel path for small buckets (allreduce / reduce of <= 256 KiB
-	 * summed over the members, reduce_scatter of <= 1 MiB, 2..8 members)
+	 * one-kernel path for small buckets (allreduce / reduce of <= 2 MiB
+	 * summed over the members, reduce_scatter of <= 4 MiB, 2..8 members)
 	 * and LFA_ALGO_TREE above.  The choice depends only on (collective,
 	 * count, members, datatype size) — lfa_coll_auto_algo — and on the
 	 * group's P2P state, itself agreed by every member: the first small
