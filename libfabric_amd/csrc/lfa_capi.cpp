@@ -646,7 +646,7 @@ int lfa_atomic_write_staged(enum lfa_op op, enum lfa_datatype dt, void *dst,
     // buffers, no HBM round trip (256 MiB float SUM, both pinned: 9.96 ms
     // against 11.22 ms staged, profiles/r05_zero_copy.log)
     int ret = staging_acquire(c, 0);
-    if (!ret) ret = kWrite[op](dt, zd, zs, cnt, c.s_out);
+    if (!ret) ret = kWrite[op](dt | LFA_WRITE_MAPPED, zd, zs, cnt, c.s_out);
     if (hipStreamSynchronize(c.s_out) != hipSuccess && !ret) ret = -LFA_EIO;
     pthread_mutex_unlock(&c.lock);
     for (int i : reg) temp_drop(i);

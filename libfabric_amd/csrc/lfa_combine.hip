@@ -94,9 +94,11 @@ static int by_type(int dt, F &&f) {
 extern "C" int LFA_CAT(lfa__write_op, LFA_OP)(int dt, void *dst,
                                               const void *src, size_t cnt,
                                               void *stream) {
-  return lfa::by_type<LFA_OP>(dt, [&](auto *tag) {
+  // dt | LFA_WRITE_MAPPED: operands on their host mappings (lfa_capi.cpp)
+  const bool mapped = (dt & LFA_WRITE_MAPPED) != 0;
+  return lfa::by_type<LFA_OP>(dt & ~LFA_WRITE_MAPPED, [&](auto *tag) {
     typedef typename std::remove_pointer<decltype(tag)>::type T;
-    return lfa::launch_write<LFA_OP, T>(dst, src, cnt, (hipStream_t)stream);
+    return lfa::launch_write<LFA_OP, T>(dst, src, cnt, (hipStream_t)stream, mapped);
   });
 }
 #endif

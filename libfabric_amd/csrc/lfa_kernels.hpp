@@ -1300,7 +1300,7 @@ constexpr unsigned kElemGridCap = 256 * 8;  // 8 workgroups per CU, grid-stride
 
 template <int OP, typename T>
 static int launch_write(void *dst, const void *src, size_t cnt,
-                        hipStream_t s) {
+                        hipStream_t s, bool mapped = false) {
   if constexpr (!supported<OP, T>()) {
     return -LFA_EOPNOTSUPP;
   } else {
@@ -1322,7 +1322,14 @@ static int launch_write(void *dst, const void *src, size_t cnt,
         u32x4 *d = (u32x4 *)((char *)dst + head * E);
         const u32x4 *v = (const u32x4 *)((const char *)src + head * E);
         const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * kUnroll, 0x7fffffffu));
-        if (nvec * 16 >= kTaperBytes && nvec * 16 < kSc1Bytes) {
+        if (mapped) {
+          // host-mapped operands (lfa_atomic_write_staged's zero-copy form):
+          // PCIe-bound, so the tiling does not matter; the plain write-through
+          // body at every size keeps these ~10 ms launches out of the device
+          // kernels' instantiations in traces (rocprofv3 stats per kernel)
+          hipLaunchKernelGGL((combine_lds<OP, T, kUnroll, kStoreSc1>), grid,
+                             dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+        } else if (nvec * 16 >= kTaperBytes && nvec * 16 < kSc1Bytes) {
           // the last 1/kTaperDiv of the vectors in 1-KiB tiles
           const size_t hv = (size_t)kLdsWaves * 64 * kUnroll;
           size_t split = nvec - nvec / kTaperDiv;

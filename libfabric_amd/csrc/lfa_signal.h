@@ -139,6 +139,9 @@ int lfa_oneshot_reduce_async(int op, int datatype, const struct lfa_oneshot *a,
  * device's, or LFA_HOST_ZERO_COPY=0.  Never a registration lfa_atomic_write_staged
  * made for one call of its own. */
 void *lfa_zero_copy_addr(const void *p, int device);
+/* Flag on the datatype argument of liblfa's internal per-op write entries
+ * (lfa__write_op<N>): the operands are host memory on its device mapping. */
+#define LFA_WRITE_MAPPED 0x10000
 /* Temporary registrations lfa_atomic_write_staged holds right now (tests:
  * 0 once every call has returned). */
 int lfa__temp_registrations(void);
