@@ -2101,28 +2101,6 @@ def main() -> None:
                           "(profiles/r02_probe_hbm_access_mix.log)"},
         },
     }
-    if world > 1:
-        # Strong scaling beside the weak headline, with equal prominence
-        # (ADVICE r5): ONE 256 MiB pair per step split into N contiguous
-        # 4 KiB-aligned shards (BASELINE configs[3]'s "8 GPUs
-        # each combine S/8").  Rounds 1-4 reported THIS as `value`; since
-        # round 5 `value` is the weak form (the tier's rule for a path that
-        # partitions), so compare rounds on the matching field.
-        off, scnt = shard_of(COUNT, world, rank)
-        w = timed_combine(dev, stream, scnt, 2000 + rank, args, world)
-        line["strong_scaling"] = {
-            "value": round(3 * S_BYTES * args.steps / w["elapsed"] / 2**30, 2),
-            "unit": "GiB/s", "scaling": "strong",
-            "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
-            "workload": "one 256 MiB float32 pair per step, sharded over the N GPUs",
-            "shard_bytes_per_gpu": scnt * 4,
-            "kernel_us": round(w["kern_ms"] * 1e3, 2),
-            "frac": round(3 * scnt * 4 / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4),
-            "traffic": read_traffic_shard(scnt * 4)[0]}
-        line["scaling_note"] = ("value: weak (every GPU its own 256 MiB pair per step) since "
-                                "round 5; rounds 1-4 reported the strong form, now "
-                                "strong_scaling.value")
-        torch.cuda.empty_cache()
     if REHEARSE:
         line["rehearsal"] = "LFA_BENCH_REHEARSE: ranks share GPUs; not a measurement"
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -2153,6 +2131,8 @@ def main() -> None:
         wd.start()
         ex = line.setdefault("extras", {})
         try:
+            if world > 1:
+                strong_scaling(line, dev, stream, args, world, rank)
             # independent buckets two streams at a time, at this rank's
             # shard (and at N = 1 at the N = 8 shard, 32 MiB) — only below
             # 192 MiB per operand: at 256 MiB two streams contend and lose
@@ -2203,6 +2183,32 @@ def main() -> None:
         bye.daemon = True
         bye.start()
         dist.destroy_process_group()
+
+
+def strong_scaling(line, dev, stream, args, world, rank) -> None:
+    """Strong scaling beside the weak headline, with equal prominence
+    (ADVICE r5), at the top level of the line.  Timed first among the
+    extras, under their watchdog, so a stalled rank cannot keep the line from
+    printing.  ONE 256 MiB pair per step split into N contiguous 4 KiB-aligned
+    shards (BASELINE configs[3]'s "8 GPUs each combine S/8").
+    Rounds 1-4 reported THIS as `value`; since round 5 `value` is the weak
+    form (the tier's rule for a path that partitions), so rounds compare on
+    the matching field."""
+    off, scnt = shard_of(COUNT, world, rank)
+    w = timed_combine(dev, stream, scnt, 2000 + rank, args, world)
+    line["strong_scaling"] = {
+        "value": round(3 * S_BYTES * args.steps / w["elapsed"] / 2**30, 2),
+        "unit": "GiB/s", "scaling": "strong",
+        "ms_per_step": round(w["elapsed"] / args.steps * 1e3, 4),
+        "workload": "one 256 MiB float32 pair per step, sharded over the N GPUs",
+        "shard_bytes_per_gpu": scnt * 4,
+        "kernel_us": round(w["kern_ms"] * 1e3, 2),
+        "frac": round(3 * scnt * 4 / (w["kern_ms"] * 1e-3) / 1e9 / PEAK_GBPS, 4),
+        "traffic": read_traffic_shard(scnt * 4)[0]}
+    line["scaling_note"] = ("value: weak (every GPU its own 256 MiB pair per step) since "
+                            "round 5; rounds 1-4 reported the strong form, now "
+                            "strong_scaling.value")
+    torch.cuda.empty_cache()
 
 
 def timed_combine(dev, stream, count: int, seed: int, args, world: int) -> dict:
