@@ -1367,7 +1367,7 @@ def extra_oneshot_crossover(rank, world, emit=None):
                                                 4 << 20)),
                                  ("reduce_scatter", (64 << 10, 256 << 10, 1 << 20, 4 << 20,
                                                      16 << 20))):
-            rows, win = {}, 0
+            rows, win, lost = {}, 0, False
             for nbytes in sizes:
                 if coll_name == "allreduce":
                     n = nbytes // 4
@@ -1399,8 +1399,12 @@ def extra_oneshot_crossover(rank, world, emit=None):
                             max_over_ranks(time.perf_counter() - t0, world) / reps * 1e6, 1)
                     except Exception as e:  # noqa: BLE001
                         row[name + "_error"] = f"{e}"[:120]
-                if row.get("oneshot_us", 1e30) < row.get("tree_us", 0.0):
+                # the bound: the largest bucket up to which the one-shot wins
+                # at every size measured
+                if not lost and row.get("oneshot_us", 1e30) < row.get("tree_us", 0.0):
                     win = nbytes
+                else:
+                    lost = True
                 rows[str(nbytes)] = row
             ep.set_algo(coll.ALGO_TREE)
             c = ep.counters()
