@@ -100,3 +100,33 @@ def test_async_argument_errors():
 def test_version_string():
     L = _lib_or_skip("lfa")
     assert b"gfx950" in L.lfa_version()
+
+
+def test_param_layer():
+    """lfa_param / lfa_param_set (include/lfa_atomic.h): a set value wins over
+    the environment, NULL removes it (the environment shows through again),
+    names and values past the slot sizes are -EINVAL.  The off_lfa provider
+    feeds fi_param_get's values through this (tests/test_off_lfa.py)."""
+    import errno
+    L = _lib_or_skip("lfa")
+    L.lfa_param.restype = ctypes.c_char_p
+    L.lfa_param.argtypes = [ctypes.c_char_p]
+    L.lfa_param_set.restype = ctypes.c_int
+    L.lfa_param_set.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    name = b"LFA_TEST_PARAM_LAYER"
+    os.environ.pop(name.decode(), None)
+    assert L.lfa_param(name) is None
+    os.environ[name.decode()] = "from-env"
+    try:
+        assert L.lfa_param(name) == b"from-env"
+        assert L.lfa_param_set(name, b"12345") == 0
+        assert L.lfa_param(name) == b"12345"
+        assert L.lfa_param_set(name, b"678") == 0
+        assert L.lfa_param(name) == b"678"
+        assert L.lfa_param_set(name, None) == 0
+        assert L.lfa_param(name) == b"from-env"
+    finally:
+        del os.environ[name.decode()]
+    assert L.lfa_param_set(b"", b"x") == -errno.EINVAL
+    assert L.lfa_param_set(b"L" * 64, b"x") == -errno.EINVAL
+    assert L.lfa_param_set(name, b"v" * 200) == -errno.EINVAL

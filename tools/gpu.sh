@@ -183,6 +183,10 @@ for stage in "$@"; do
     fetchx)
       # the fetch / compare table extra (prewarmed), three times
       for i in 1 2 3; do $S "fetch_extra_$i" 200 python3 -u bench.py --only-extra fetch || exit 99; done ;;
+    threads2)
+      # the 2 MiB pageable case fresh and with device memory held first
+      $S threads_fresh 200 python3 -u tools/probe_threads.py --sizes 2,8 --kinds pageable && \
+      $S threads_hold 200 python3 -u tools/probe_threads.py --sizes 2,8 --kinds pageable --pre-alloc-gib 64 || exit 99 ;;
     fetchtune)
       FETCH_VARIANTS="${FETCH_VARIANTS:-4,6,7,8,9,10,11}" $S fetch_tune 400 python3 -u tools/probe_fetch.py --tune || exit 99 ;;
     bucketsx)

@@ -25,17 +25,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="2,8,32")
     ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--pre-alloc-gib", type=int, default=0,
+                    help="hold this much device memory first (torch), as a test process does")
+    ap.add_argument("--kinds", default="pageable,pinned")
     a = ap.parse_args()
     import numpy as np
     import torch
     from libfabric_amd import atomic, lib
     lib()
     torch.cuda.init()
+    hold = (torch.empty(a.pre_alloc_gib << 30, dtype=torch.uint8, device="cuda")
+            if a.pre_alloc_gib else None)
     fn = atomic.write_handler(2, 8)
     T = a.threads
     for mib in (int(x) for x in a.sizes.split(",")):
         n = (mib << 20) // 4
-        for kind in ("pageable", "pinned"):
+        for kind in a.kinds.split(","):
             if kind == "pinned":
                 bufs = [(torch.rand(n).pin_memory().numpy(), torch.rand(n).pin_memory().numpy())
                         for _ in range(T)]
@@ -79,6 +84,8 @@ def main():
                               "threads_wall_ms": round(wm * 1e3, 3),
                               "slowest_thread_call_ms": round(statistics.median(per) * 1e3, 3),
                               "ratio_to_one": round(wm / s1, 2),
+                              "walls_ms": [round(w * 1e3, 3) for w in walls],
+                              "pre_alloc_gib": a.pre_alloc_gib,
                               "zero_copy": os.environ.get("LFA_HOST_ZERO_COPY", "1")}),
                   flush=True)
 
