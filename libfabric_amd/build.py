@@ -52,6 +52,7 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     kern = os.path.join(CSRC, "lfa_combine.hip")
     hdrs = [os.path.join(CSRC, "lfa_ops.hpp"), os.path.join(CSRC, "lfa_kernels.hpp"),
+            *(os.path.join(CSRC, f"lfa_k_{p}.hpp") for p in ("tree", "oneshot", "fetch", "launch")),
             os.path.join(INC, "lfa_atomic.h"), os.path.join(INC, "lfa_fabric.h")]
     steps = []
     objs = []
@@ -61,14 +62,17 @@ def build_lfa(jobs: int = 8, verbose: bool = False) -> str:
         if _newer(o, [kern] + hdrs):
             steps.append([HIPCC, *HIP_FLAGS, f"-DLFA_OP={op}", "-c", kern, "-o", o])
     # tuning-only kernel forms (bench.py --tune*): their own library
-    tune = os.path.join(CSRC, "lfa_tune.hip")
-    tune_o = os.path.join(BUILD, "lfa_tune.o")
-    if _newer(tune_o, [tune] + hdrs):
-        steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", tune_o])
+    tune_objs = []
+    for name in ("lfa_tune", "lfa_tune_b"):
+        tune = os.path.join(CSRC, name + ".hip")
+        tune_o = os.path.join(BUILD, name + ".o")
+        tune_objs.append(tune_o)
+        if _newer(tune_o, [tune] + hdrs):
+            steps.append([HIPCC, *HIP_FLAGS, "-c", tune, "-o", tune_o])
     # the tree_put register-pressure probe (tools/probe_treeput_narrow.py)
     probe = os.path.join(CSRC, "lfa_probe.hip")
     probe_o = os.path.join(BUILD, "lfa_probe.o")
-    tune_objs = [tune_o, probe_o]
+    tune_objs.append(probe_o)
     if _newer(probe_o, [probe] + hdrs):
         steps.append([HIPCC, *HIP_FLAGS, "-c", probe, "-o", probe_o])
     # op-independent device code: the P2P flag barrier
@@ -227,17 +231,19 @@ def build_off_lfa(verbose: bool = False) -> str | None:
     """libfabric offload-collective provider (liboff_lfa-fi.so) over
     liblfa_coll.so, plus the rxm-shaped host driver examples/off_lfa_host."""
     src = os.path.join(CSRC, "off_lfa.c")
+    srcs = [src, os.path.join(CSRC, "off_lfa_ep.c")]
     host = OFF_HOST + ".c"
     if not have_fabric_headers():
         if verbose:
             print("libfabric headers absent: off_lfa not rebuilt "
                   f"({'prebuilt present' if os.path.exists(LIB_OFF) else 'missing'})")
         return LIB_OFF if os.path.exists(LIB_OFF) else None
-    hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "off_lfa.h"), LIB_COLL]
-    if _newer(LIB_OFF, [src] + hdrs):
+    hdrs = [os.path.join(INC, "lfa_coll.h"), os.path.join(INC, "off_lfa.h"),
+            os.path.join(CSRC, "off_lfa_int.h"), LIB_COLL]
+    if _newer(LIB_OFF, srcs + hdrs):
         _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra",
               "-Wno-unused-parameter", "-I" + INC, "-I" + FABRIC_INC, "-shared",
-              "-o", LIB_OFF, src, "-L" + PKG, "-llfa_coll", "-lpthread",
+              "-o", LIB_OFF, *srcs, "-L" + PKG, "-llfa_coll", "-llfa", "-lpthread",
               "-Wl,-rpath,$ORIGIN", "-Wl,-soname,liboff_lfa-fi.so"])
         if verbose:
             print(f"built {LIB_OFF}")

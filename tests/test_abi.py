@@ -108,7 +108,7 @@ def test_util_ep_prefix_matches_reference_layout():
         else:
             ref_struct.append(f"  {f};")
     ref_struct.append("};")
-    off = open(os.path.join(ROOT, "libfabric_amd", "csrc", "off_lfa.c")).read()
+    off = open(os.path.join(ROOT, "libfabric_amd", "csrc", "off_lfa_int.h")).read()
     ours = re.search(r"(#define OLFA_UTIL_CNTR_CNT.*?\nstruct olfa_util_ep_prefix \{.*?\n\};)",
                      off, re.S).group(1)
     src = "\n".join(["#include <stddef.h>", "#include <stdint.h>", "#include <rdma/fabric.h>",

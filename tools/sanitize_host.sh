@@ -17,7 +17,7 @@ for kind in asan tsan; do
       -shared -o "$d/liblfa_coll.so" $(for f in lfa_coll lfa_coll_word lfa_coll_ws lfa_coll_host lfa_coll_group lfa_coll_exec; do echo "$R/libfabric_amd/csrc/$f.c"; done) "$R/libfabric_amd/csrc/lfa_coll_plan.c" "$R/libfabric_amd/csrc/lfa_coll_loopback.c" -L"$R/libfabric_amd" -llfa \
       -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,"$R/libfabric_amd" -Wl,-soname,liblfa_coll.so
   gcc $SAN -fPIC -std=gnu11 -Wall -I"$R/include" -I"$FAB" -shared -o "$d/liboff_lfa-fi.so" \
-      "$R/libfabric_amd/csrc/off_lfa.c" -L"$d" -llfa_coll -lpthread -Wl,-rpath,'$ORIGIN'
+      "$R/libfabric_amd/csrc/off_lfa.c" "$R/libfabric_amd/csrc/off_lfa_ep.c" -L"$d" -llfa_coll -L"$R/libfabric_amd" -llfa -lpthread -Wl,-rpath,'$ORIGIN'
   gcc $SAN -std=gnu11 -I"$R/include" -I"$FAB" -o "$d/peer" "$R/examples/off_lfa_peer.c" -ldl -lpthread
   for args in "3 manual" "3" "2 latency" "5 core" "4 core manual"; do
     set -- $args
