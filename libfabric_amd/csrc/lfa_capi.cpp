@@ -534,7 +534,7 @@ int temp_take(const void *p, size_t bytes, void **d, int mine) {
   // one call registers at a time: hipHostRegister / hipHostUnregister from
   // several threads at once slow each other down (4 threads of pageable
   // 2 MiB combines: 29x one call, against 3.7x when they stage;
-  // profiles/r06_threads_probe.jsonl), so while another call holds or makes
+  // profiles/r06_threads_probe_before.jsonl), so while another call holds or makes
   // a registration this one takes the staged pipeline, which overlaps
   int busy = 0;
   for (int k = 0; k < kTempRegs; k++) busy += k != mine && g_temp[k].state != kRegFree;

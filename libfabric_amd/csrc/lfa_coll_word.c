@@ -37,8 +37,9 @@ static uint64_t mono_ns(void)
  * completion of the endpoint (they are reaped in issue order).  So at most
  * every LFA_WORD_CHECK_NS a poll also asks the direct queue whether it has
  * failed, or the stream whether it reports an error, and past the deadline
- * (LFA_SIG_TIMEOUT_MS after the submit, the bound of every other GPU wait of
- * the provider) the operation fails with ETIMEDOUT.  The failing operation
+ * (LFA_SIG_TIMEOUT_MS, the bound of every other GPU wait of the provider,
+ * counted from the first poll that finds the operation at the head of the
+ * queue: since round 6) the operation fails with ETIMEDOUT.  The failing operation
  * is reaped once, as an error entry; the word's later arrival is harmless,
  * the words only ever grow.
  */
