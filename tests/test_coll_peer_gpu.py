@@ -1463,3 +1463,48 @@ def test_rejoin_after_timeout_does_not_reuse_the_timed_out_workspace():
     operations are exact.  Every kept workspace is freed with the last GPU
     domain."""
     _spawn(_late_member_worker, 2)
+
+
+def _world1_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LFA_DEBUG="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gloo_xfer import GlooXfer
+        from libfabric_amd import coll
+        ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+        try:
+            ep.set_algo(coll.ALGO_P2P)
+            # a one-member GPU peer domain under P2P: one-shot-sized buckets
+            # plan the n = 1 one-shot (round 6), larger ones the two-barrier
+            # schedule; each is a copy of the input
+            for n in (1, 1000, 70_001, (3 << 20) + 5):
+                x = torch.rand(n, device="cuda")
+                for kind in ("allreduce", "reduce_scatter", "reduce"):
+                    y = torch.full_like(x, -1.0)
+                    _ready()
+                    if kind == "allreduce":
+                        ep.wait(ep.allreduce(x, y, n, 8, 2))
+                    elif kind == "reduce_scatter":
+                        ep.wait(ep.reduce_scatter(x, y, n, 8, 2))
+                    else:
+                        ep.wait(ep.reduce(x, y, n, 0, 8, 2))
+                    assert torch.equal(x, y), f"{kind} n={n}"
+            c = ep.counters()
+            assert c["oneshot"] >= 9 and not c["timed_out"], c
+        finally:
+            ep.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_p2p_one_member_peer_domain():
+    """LFA_ALGO_P2P on a one-member GPU peer domain: the n = 1 one-shot the
+    planner emits for one-shot-sized buckets since round 6 (the workspace
+    handshake of a group of one, the kernel's degenerate copy, the
+    completion word) and the two-barrier schedule above; allreduce,
+    reduce_scatter and reduce give the input back."""
+    _spawn(_world1_worker, 1)
