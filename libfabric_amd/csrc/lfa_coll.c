@@ -580,6 +580,13 @@ static void progress(struct lfa_coll_ep *ep, struct lfa_cq_entry *out,
 				p->pmc->sig_failed = 1;
 			st = -1;
 			perr = ETIMEDOUT;
+		} else if (st < 0 && p->pmc) {
+			/* a P2P operation reaped as failed for another cause (its
+			 * word's bound, a failed queue or stream): its kernel may
+			 * still run and post into the workspace, so the group takes
+			 * no further P2P operation and its workspace goes to the
+			 * quarantine at close, as after a timed-out wait */
+			p->pmc->sig_failed = 1;
 		}
 		if (st == 0 && p->bounce_bytes) {
 			/* a bounced operation's result to the caller's buffer */

@@ -1308,6 +1308,9 @@ def _word_drop_worker(rank, world, port, q):
         import oracle
         from gloo_xfer import GlooXfer
         from libfabric_amd import coll
+        # a second GPU domain keeps the workspace cache and quarantine alive
+        # across the re-join
+        anchor = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
         ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
         msg = "ok"
         try:
@@ -1347,14 +1350,31 @@ def _word_drop_worker(rank, world, port, q):
             want_words = 1 if rank == 0 else 2      # the lost word is not one
             if msg == "ok" and ep.word_ops() - before != want_words:
                 msg = f"word operations {ep.word_ops() - before}, want {want_words}"
-            # the group goes on: the kernels ran, only the word was lost
+            # the member whose operation failed cannot know its
+            # kernel finished, so its group refuses further P2P operations
+            # and its workspace goes to the quarantine at close, as after a
+            # timed-out wait; the members close and re-join
+            quar0 = coll.ws_quarantined_bytes()
+            if rank == 0:
+                try:
+                    ep.allreduce(xs[0], rs[0], 4096, 8, 2)
+                    msg = msg if msg != "ok" else "a P2P submit on the failed group"
+                except coll.CollError as e:
+                    if e.rc != -coll.EIO and msg == "ok":
+                        msg = f"refused with {e.rc}"
+            ep.close()
+            if msg == "ok" and rank == 0 and not coll.ws_quarantined_bytes() > quar0:
+                msg = "the failed group's workspace was not quarantined"
+            ep = coll.HostEndpoint(rank, world, GlooXfer(), device=0)
+            ep.set_algo(coll.ALGO_P2P)
             rs[0].zero_()
             _ready()
             ep.wait(ep.allreduce(xs[0], rs[0], 4096, 8, 2))
             if msg == "ok" and rs[0].cpu().numpy().tobytes() != wants[0].tobytes():
-                msg = "allreduce after the lost word wrong"
+                msg = "allreduce after the re-join wrong"
         finally:
             ep.close()
+            anchor.close()
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, msg))
@@ -1368,7 +1388,10 @@ def test_lost_one_shot_word_fails_that_operation_once():
     member's one-shot waits for a completion-word value its kernel never
     stores.  That operation is reaped once, as an ETIMEDOUT error entry,
     after the bound; the one queued behind it completes normally on both
-    members; every result is exact and the group keeps working."""
+    members and every result is exact.  That member's group then refuses
+    P2P operations (EIO) and its workspace is quarantined at close (ADVICE
+    r5: the failed operation's kernel may still post into it); the re-made
+    group is exact."""
     _spawn(_word_drop_worker, 2)
 
 

@@ -202,6 +202,12 @@ def test_device_domain_one_shot_reaps_through_the_word(coll):
         assert e.cq_readerr() is None
         torch.cuda.synchronize()
         assert torch.equal(out[:2], src[:2])
+        # a P2P operation reaped as failed leaves the group
+        # refusing P2P operations (its kernel may still post into the
+        # workspace), as after a timed-out wait: close and re-join
+        with pytest.raises(coll.CollError) as ei:
+            e.allreduce(src[2], out[2], 1024, FLOAT, SUM)
+        assert ei.value.rc == -coll.EIO
     finally:
         e.close()
 
