@@ -34,6 +34,7 @@
 #   ramp         per-wave timestamps of one combine launch (ramp / drain)
 #   solo         launch -> completion word of one small kernel, by part
 #   tunecomb     back-to-back combine forms at 32/64/256 MiB (COMBINE_VARIANTS)
+#   tablepmc     fetch / compare tables and 32 MiB buckets: kernel trace + PMC
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -191,6 +192,16 @@ for stage in "$@"; do
       FETCH_VARIANTS="${FETCH_VARIANTS:-4,6,7,8,9,10,11}" $S fetch_tune 400 python3 -u tools/probe_fetch.py --tune || exit 99 ;;
     bucketsx)
       $S buckets_extra 200 python3 -u bench.py --only-extra buckets || exit 99 ;;
+    tablepmc)
+      # the fetch / compare tables (256 MiB) and the 32 MiB buckets under
+      # --kernel-trace --stats, then FETCH_SIZE and WRITE_SIZE in their own passes
+      for x in fetch buckets; do
+        $S "prof_$x" 300 $P -d "gpurun_out/prof_$x" -o run -- python3 bench.py --only-extra $x && \
+        $S "pmc_${x}_fetch" 200 timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+          -d "gpurun_out/pmc_${x}_fetch" -o run -- python3 bench.py --only-extra $x && \
+        $S "pmc_${x}_write" 200 timeout -s KILL 190 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+          -d "gpurun_out/pmc_${x}_write" -o run -- python3 bench.py --only-extra $x || exit 99
+      done ;;
     *)
       echo "unknown stage $stage"; exit 2 ;;
   esac
