@@ -588,16 +588,22 @@ __global__ __launch_bounds__(kLdsWaves * 64) void combine_static(u32x4 *__restri
 template <int U>
 static void launch_static(u32x4 *d, const u32x4 *v, size_t nvec, int grid_mult,
                           hipStream_t s) {
-  int per_cu = 0, dev = 0, cus = 0;
+  // the occupancy query once per store policy (round 6: variants 90-94 were
+  // first measured with it on every launch)
+  static int slots[2];
   const bool nt = nvec * 16 >= kSc1Bytes;
-  if ((nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreNt>,
-                                                          kLdsWaves * 64, 0)
-          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreSc1>,
-                                                          kLdsWaves * 64, 0)) != hipSuccess ||
-      hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return;
-  size_t g = (size_t)per_cu * cus * grid_mult;
+  if (!slots[nt]) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if ((nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreNt>,
+                                                            kLdsWaves * 64, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, combine_static<U, kStoreSc1>,
+                                                            kLdsWaves * 64, 0)) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return;
+    slots[nt] = per_cu * cus;
+  }
+  size_t g = (size_t)slots[nt] * grid_mult;
   const size_t waves_needed = (nvec / 64 + 1 + kLdsWaves - 1) / kLdsWaves;
   if (g > waves_needed) g = waves_needed ? waves_needed : 1;
   if (nt)
@@ -606,6 +612,117 @@ static void launch_static(u32x4 *d, const u32x4 *v, size_t nvec, int grid_mult,
   else
     hipLaunchKernelGGL((combine_static<U, kStoreSc1>), dim3((unsigned)g), dim3(kLdsWaves * 64), 0,
                        s, d, v, nvec);
+}
+
+// The static grid above, software-pipelined (round 6): each wave's steps of U
+// units are double-buffered in LDS, and step j+1's LDS-DMA loads are issued
+// before step j is combined and stored, so a wave always has a step's loads
+// in flight — variants 90-94 waited vmcnt(0) between every step's loads and
+// its stores, and lost 3-7 % to those serial phases.  LDS per wave equals the
+// product's at U = 2 (2 buffers x 2 operands x 2 KiB = 8 KiB), so the same 5
+// workgroups fit per CU.  vmcnt counts loads and stores together in issue
+// order: with stores(j-1) and loads(j+1) behind loads(j), loads(j) have
+// landed at vmcnt(3U) (2U at the first step, U at the last).  Buffer reuse:
+// loads(j+1) overwrite the buffer step j-1 read, and are issued after step
+// j-1's stores, which consumed those reads.  A wave's units past its last
+// whole step take the guarded register path after the pipeline.
+template <int U, int SAUX>
+__device__ __forceinline__ void pipe_issue(const u32x4 *__restrict__ dst,
+                                           const u32x4 *__restrict__ src, size_t base,
+                                           u32x4 (*buf)[kLdsWaves][U][64], unsigned w,
+                                           unsigned l) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                     (lds_void *)&buf[0][w][u][0], 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                     (lds_void *)&buf[1][w][u][0], 16, 0, 2);
+  }
+}
+
+template <int U, int SAUX>
+__device__ __forceinline__ void pipe_store(u32x4 *__restrict__ dst, size_t base,
+                                           u32x4 (*buf)[kLdsWaves][U][64], unsigned w,
+                                           unsigned l) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    u32x4 v = apply_vec<OP_SUM, float>(buf[0][w][u][l], buf[1][w][u][l]);
+    if constexpr (SAUX == kStoreNt)
+      st<true>(dst + base + u * 64 + l, v);
+    else
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(u * 64 + l) * 16, 0, SAUX);
+  }
+}
+
+template <int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_static_pipe(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec) {
+  __shared__ u32x4 lds[2][2][kLdsWaves][U][64];  // [buffer][dst, src][wave][u][lane]
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const size_t nw = (size_t)gridDim.x * kLdsWaves;
+  const size_t gw = (size_t)blockIdx.x * kLdsWaves + w;
+  const size_t units = nvec / 64;
+  const size_t ub = gw * units / nw, ue = (gw + 1) * units / nw;
+  const size_t nsteps = (ue - ub) / U;
+  if (nsteps) {
+    pipe_issue<U, SAUX>(dst, src, ub * 64, lds[0], w, l);
+    if (nsteps > 1) {
+      pipe_issue<U, SAUX>(dst, src, (ub + U) * 64, lds[1], w, l);
+      wait_vmcnt<2 * U>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    pipe_store<U, SAUX>(dst, ub * 64, lds[0], w, l);
+    for (size_t j = 1; j < nsteps; j++) {
+      const size_t base = (ub + j * U) * 64;
+      if (j + 1 < nsteps) {
+        pipe_issue<U, SAUX>(dst, src, base + U * 64, lds[(j + 1) & 1], w, l);
+        wait_vmcnt<3 * U>();
+      } else {
+        wait_vmcnt<U>();
+      }
+      pipe_store<U, SAUX>(dst, base, lds[j & 1], w, l);
+    }
+  }
+  // units past the last whole step, then the vectors past the last unit
+  for (size_t i = (ub + nsteps * U) * 64 + l; i < ue * 64; i += 64)
+    st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+  if (gw == nw - 1) {
+    const size_t i = units * 64 + l;
+    if (i < nvec)
+      st<true>(dst + i, apply_vec<OP_SUM, float>(ld<true>(dst + i), ld<true>(src + i)));
+  }
+}
+
+template <int U>
+static void launch_static_pipe(u32x4 *d, const u32x4 *v, size_t nvec, int grid_mult,
+                               hipStream_t s) {
+  // one occupancy query per form and store policy (not one per launch: the
+  // host must stay ahead of a 16 us kernel)
+  static int slots[2];
+  const bool nt = nvec * 16 >= kSc1Bytes;
+  if (!slots[nt]) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if ((nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &per_cu, combine_static_pipe<U, kStoreNt>, kLdsWaves * 64, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &per_cu, combine_static_pipe<U, kStoreSc1>, kLdsWaves * 64, 0)) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return;
+    slots[nt] = per_cu * cus;
+  }
+  size_t g = (size_t)slots[nt] * grid_mult;
+  const size_t waves_needed = (nvec / 64 + 1 + kLdsWaves - 1) / kLdsWaves;
+  if (g > waves_needed) g = waves_needed ? waves_needed : 1;
+  if (nt)
+    hipLaunchKernelGGL((combine_static_pipe<U, kStoreNt>), dim3((unsigned)g),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec);
+  else
+    hipLaunchKernelGGL((combine_static_pipe<U, kStoreSc1>), dim3((unsigned)g),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec);
 }
 
 }  // namespace lfa
@@ -645,6 +762,10 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 92: lfa::launch_static<8>(d, v, nvec, 1, s); break;
     case 93: lfa::launch_static<4>(d, v, nvec, 2, s); break;
     case 94: lfa::launch_static<1>(d, v, nvec, 1, s); break;
+    // the same, software-pipelined (round 6): U = 2 / 4 / 1 KiB steps
+    case 95: lfa::launch_static_pipe<2>(d, v, nvec, 1, s); break;
+    case 96: lfa::launch_static_pipe<4>(d, v, nvec, 1, s); break;
+    case 97: lfa::launch_static_pipe<1>(d, v, nvec, 1, s); break;
     case 85: lfa::launch_taper<4, 2>(d, v, nvec, 8, s); break;
     case 86: lfa::launch_taper<4, 2>(d, v, nvec, 4, s); break;
     case 87: lfa::launch_taper<4, 1>(d, v, nvec, 8, s); break;

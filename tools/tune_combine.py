@@ -80,6 +80,15 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 per[v].append(e0.elapsed_time(e1) * 1e3 / args.k)
+        # exactness at this size too (every form's whole-step / remainder split)
+        d0, s0 = sets[0]
+        for v in variants:
+            a = d0.clone()
+            assert fn(v)(v, a.data_ptr(), s0.data_ptr(), nvec, h) == 0
+            torch.cuda.synchronize()
+            if not torch.equal(a, d0 + s0):
+                raise SystemExit(f"variant {v} is WRONG at {mib} MiB")
+            del a
         for v in variants:
             us = statistics.median(per[v])
             row = {"variant": v, "mib": mib, "us": round(us, 3),
