@@ -205,6 +205,8 @@ const char *lfa_version(void);
  * lfa_param_set before it opens a domain.  Most knobs are read once, at first
  * use: set them before the first collective of the process.
  * lfa_param_set: value NULL removes the setting; 0 or -LFA_EINVAL / -LFA_ENOMEM.
+ * Both are thread-safe; a string lfa_param returned from a set value is never
+ * changed or freed (a later set of the same name makes a new one).
  */
 const char *lfa_param(const char *name);
 int lfa_param_set(const char *name, const char *value);

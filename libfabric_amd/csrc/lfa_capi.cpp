@@ -704,10 +704,15 @@ size_t lfa_host_small_bytes(void) {
 
 namespace {
 constexpr int kParams = 64;
+constexpr size_t kParamValueMax = 80;
+// A value, once set, is never written again: a new value of the same name
+// is a new string and the old one is kept (a caller may still be parsing it
+// on another thread), so every pointer lfa_param returned stays valid and
+// unchanged for the life of the process.  Sets are rare (provider init,
+// tests), so what is kept stays small.
 struct ParamSlot {
   char name[48];
-  char value[80];
-  bool set;
+  const char *value;  // null: not set (the environment shows through)
 };
 ParamSlot g_params[kParams];
 pthread_mutex_t g_param_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -718,17 +723,17 @@ const char *lfa_param(const char *name) {
   const char *v = nullptr;
   pthread_mutex_lock(&g_param_lock);
   for (const ParamSlot &p : g_params)
-    if (p.set && !strcmp(p.name, name)) v = p.value;
+    if (p.value && !strcmp(p.name, name)) v = p.value;
   pthread_mutex_unlock(&g_param_lock);
-  // a set value lives until the process ends (slots are never reused for
-  // another name), so the pointer stays valid after the lock
   return v ? v : getenv(name);
 }
 
 int lfa_param_set(const char *name, const char *value) {
   if (!name || !*name || strlen(name) >= sizeof(ParamSlot::name) ||
-      (value && strlen(value) >= sizeof(ParamSlot::value)))
+      (value && strlen(value) >= kParamValueMax))
     return -LFA_EINVAL;
+  char *copy = value ? strdup(value) : nullptr;
+  if (value && !copy) return -LFA_ENOMEM;
   int ret = -LFA_ENOMEM;
   pthread_mutex_lock(&g_param_lock);
   ParamSlot *slot = nullptr;
@@ -742,11 +747,12 @@ int lfa_param_set(const char *name, const char *value) {
         break;
       }
   if (slot) {
-    slot->set = value != nullptr;
-    if (value) strcpy(slot->value, value);
+    slot->value = copy;  // the previous string, if any, is kept (above)
+    copy = nullptr;
     ret = 0;
   }
   pthread_mutex_unlock(&g_param_lock);
+  free(copy);
   return ret;
 }
 
