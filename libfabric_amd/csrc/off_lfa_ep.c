@@ -60,7 +60,61 @@ OLFA_INTERNAL void olfa_mc_unregister(struct olfa_ep *ep, struct olfa_mc *m)
 	m->next = NULL;
 }
 
+/* Test knob (LFA_TEST_JOIN_DELAY_US, never a deployer parameter): a pause
+ * between a join's lfa_join_* call and its registration, which widens the
+ * window olfa_post_join covers (tests/test_off_lfa.py). */
+static void olfa_test_join_delay(void)
+{
+	const char *v = lfa_param("LFA_TEST_JOIN_DELAY_US");
+	long us = v ? strtol(v, NULL, 0) : 0;
+
+	if (us > 0) {
+		struct timespec t = { us / 1000000, (us % 1000000) * 1000 };
+
+		nanosleep(&t, NULL);
+	}
+}
+
 /* ------------------------------------------------------------ progress -- */
+
+static void olfa_emit_join(struct olfa_ep *ep, struct olfa_mc *m,
+			   const struct lfa_eq_entry *lev)
+{
+	struct fi_eq_entry e;
+
+	memset(&e, 0, sizeof(e));
+	e.fid = m ? &m->mc_fid.fid : NULL;
+	e.context = lev->context;
+	e.data = lev->data;
+	if (ep->eq)
+		fi_eq_write(ep->eq->peer_eq, FI_JOIN_COMPLETE, &e, sizeof(e), 0);
+	else
+		olfa_warn("join completed with no EQ bound", NULL, 0);
+}
+
+/* A join event to the owner's EQ with the fid of its registered group;
+ * -FI_EAGAIN when the group is not registered yet but a join is between
+ * its lfa_join_* call and its registration (the event may be its own: a
+ * one-member join completes inside the call).  The count is read before the
+ * registry, so a miss with a join counted means that join's registration,
+ * which comes before its decrement, had not happened.  An event whose group
+ * is gone (closed before its event was read) goes out without a fid, as
+ * before. */
+static int olfa_post_join(struct olfa_ep *ep, const struct lfa_eq_entry *lev)
+{
+	const int joining = atomic_load(&ep->joins_in_flight);
+	struct olfa_mc *m;
+
+	pthread_mutex_lock(&ep->lock);
+	for (m = ep->mcs; m; m = m->next)
+		if (m->lmc && (void *)m->lmc == lev->fid)
+			break;
+	pthread_mutex_unlock(&ep->lock);
+	if (!m && joining)
+		return -FI_EAGAIN;
+	olfa_emit_join(ep, m, lev);
+	return 0;
+}
 
 /* Moves finished collectives and joins to the owner: CQ entries through
  * the peer CQ's owner_ops (coll_coll.c:725-733), join events through the
@@ -69,7 +123,6 @@ OLFA_INTERNAL int olfa_progress(struct olfa_ep *ep)
 {
 	struct lfa_cq_entry ent[16];
 	struct lfa_cq_err_entry lerr;
-	struct lfa_eq_entry lev;
 	uint32_t event;
 	ssize_t n;
 	int moved = 0;
@@ -113,23 +166,17 @@ OLFA_INTERNAL int olfa_progress(struct olfa_ep *ep)
 		}
 		break;
 	}
-	while (lfa_eq_read(ep->le, &event, &lev) > 0) {
-		struct olfa_mc *m;
-		struct fi_eq_entry e;
-
-		pthread_mutex_lock(&ep->lock);
-		for (m = ep->mcs; m; m = m->next)
-			if (m->lmc && (void *)m->lmc == lev.fid)
+	/* join events in order; one whose group is still being registered is
+	 * held (and the ones behind it wait) until a later pass */
+	for (;;) {
+		if (!ep->have_held) {
+			if (lfa_eq_read(ep->le, &event, &ep->held) <= 0)
 				break;
-		pthread_mutex_unlock(&ep->lock);
-		memset(&e, 0, sizeof(e));
-		e.fid = m ? &m->mc_fid.fid : NULL;
-		e.context = lev.context;
-		e.data = lev.data;
-		if (ep->eq)
-			fi_eq_write(ep->eq->peer_eq, FI_JOIN_COMPLETE, &e, sizeof(e), 0);
-		else
-			olfa_warn("join completed with no EQ bound", NULL, 0);
+			ep->have_held = 1;
+		}
+		if (olfa_post_join(ep, &ep->held) < 0)
+			break;
+		ep->have_held = 0;
 		moved++;
 	}
 	pthread_mutex_unlock(&ep->plock);
@@ -413,14 +460,17 @@ static int olfa_join_self(struct olfa_ep *ep, struct olfa_av_set *set,
 	for (size_t i = 0; i < n; i++)
 		m->members[i] = set->addr[i];   /* lfa_join_members rejects repeats */
 	m->nmembers = n;
+	atomic_fetch_add(&ep->joins_in_flight, 1);    /* olfa_post_join */
 	ret = lfa_join_members(ep->le, lfa_coll_world_addr(ep->le), ranks, n, flags,
 			       &m->lmc, context);
+	olfa_test_join_delay();
 	if (!ret) {
 		pthread_mutex_lock(&ep->lock);
 		m->laddr = lfa_mc_addr(m->lmc);
 		olfa_mc_register(ep, m);
 		pthread_mutex_unlock(&ep->lock);
 	}
+	atomic_fetch_sub(&ep->joins_in_flight, 1);
 out:
 	free(ranks);
 	if (ret) {
@@ -498,8 +548,10 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 		set->set_mc.nmembers = n;
 		/* not under the registry lock: the join's communicator work must
 		 * not hold up the progress thread's EQ hand-off */
+		atomic_fetch_add(&ep->joins_in_flight, 1);    /* olfa_post_join */
 		ret = lfa_join_collective(ep->le, LFA_ADDR_NOTAVAIL, NULL, 0, flags,
 					  &m->lmc, context);
+		olfa_test_join_delay();
 		pthread_mutex_lock(&ep->lock);
 		if (!ret) {
 			m->laddr = lfa_mc_addr(m->lmc);
@@ -510,6 +562,7 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 			olfa_mc_register(ep, &set->set_mc);
 		}
 		pthread_mutex_unlock(&ep->lock);
+		atomic_fetch_sub(&ep->joins_in_flight, 1);
 		if (ret)
 			goto err;
 		*mc_fid = &m->mc_fid;
@@ -552,13 +605,16 @@ static int olfa_join(struct fid_ep *ep_fid, const void *addr, uint64_t flags,
 	}
 	m->nmembers = n;
 	pthread_mutex_unlock(&ep->lock);
+	atomic_fetch_add(&ep->joins_in_flight, 1);    /* olfa_post_join */
 	ret = lfa_join_collective(ep->le, paddr, ranks, n, flags, &m->lmc, context);
+	olfa_test_join_delay();
 	pthread_mutex_lock(&ep->lock);
 	if (!ret) {
 		m->laddr = lfa_mc_addr(m->lmc);
 		olfa_mc_register(ep, m);
 	}
 	pthread_mutex_unlock(&ep->lock);
+	atomic_fetch_sub(&ep->joins_in_flight, 1);
 	free(ranks);
 	ranks = NULL;
 	if (ret)

@@ -128,6 +128,14 @@ struct olfa_ep {
 	pthread_mutex_t plock;             /* one progress pass at a time */
 	struct olfa_mc *mcs;
 	struct olfa_mc *world;             /* world group, after bootstrap */
+	/* joins between their lfa_join_* call and their registration: a join
+	 * that completes at once (a one-member group) can post its event
+	 * before its group is registered, and progress holds such an event
+	 * (under plock) until the group is there instead of posting it
+	 * fid-less (olfa_post_join) */
+	atomic_int joins_in_flight;
+	int have_held;
+	struct lfa_eq_entry held;
 
 	/* bootstrap */
 	int device;

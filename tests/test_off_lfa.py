@@ -437,3 +437,23 @@ def test_reference_multinode_suite(tmp_path, n, mode):
     assert r.returncode == 0, r.stdout + r.stderr
     passed = [x.split()[1] for x in r.stdout.splitlines() if x.startswith("CORE ")]
     assert tuple(passed) == CORE_TESTS, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_join_event_waits_for_its_group(tmp_path, n):
+    """A join that completes inside its lfa_join_* call (a one-member group)
+    posts its event before off_lfa has registered the group.  The progress
+    thread used to hand it to the owner's EQ with no fid, so the owner never
+    matched it and the join timed out (seen once in the serial CPU suite:
+    test_reference_multinode_suite[1-thread]).  LFA_TEST_JOIN_DELAY_US holds
+    every join 20 ms between the call and the registration, so the thread
+    always drains the event inside that window: the event must still reach
+    the owner with its group's fid (olfa_post_join holds it until then)."""
+    if build.have_fabric_headers():
+        build.build_all()
+    env = dict(os.environ, LFA_TEST_JOIN_DELAY_US="20000")
+    r = subprocess.run([build.OFF_PEER, build.LIB_OFF, str(n), str(tmp_path), "core"],
+                       capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    passed = [x.split()[1] for x in r.stdout.splitlines() if x.startswith("CORE ")]
+    assert tuple(passed) == CORE_TESTS, r.stdout + r.stderr
