@@ -405,6 +405,13 @@ static int olfa_mc_close(struct fid *fid)
 	struct olfa_ep *ep = m->ep;
 
 	if (ep) {
+		/* a held join event of this group goes with it: its lfa handle is
+		 * freed below, and a later join's could reuse the address (plock
+		 * before the registry lock, as in olfa_progress) */
+		pthread_mutex_lock(&ep->plock);
+		if (ep->have_held && m->lmc && ep->held.fid == (void *)m->lmc)
+			ep->have_held = 0;
+		pthread_mutex_unlock(&ep->plock);
 		pthread_mutex_lock(&ep->lock);
 		olfa_mc_unregister(ep, m);
 		if (ep->world == m)
