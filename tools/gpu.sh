@@ -139,6 +139,11 @@ for stage in "$@"; do
       # the same at 4 ranks sharing this GPU (one-shots and trees at n = 4)
       LFA_BENCH_REHEARSE=1 $S rehearse4 900 python3 -u bench.py --gpus 4 --steps 5 \
         --warmup 2 --no-cpu --extras-timeout 800 || exit 99 ;;
+    rehearse8)
+      # the N = 8 flow with its 8 ranks and their 8 isolated extras children
+      # on this one GPU (16 processes: the box's limit)
+      LFA_BENCH_REHEARSE=1 $S rehearse8 1100 python3 -u bench.py --gpus 8 --steps 5 \
+        --warmup 2 --no-cpu --extras-timeout 900 || exit 99 ;;
     treeputx)
       # the bench extra (fresh buffer sets rotated, median + range)
       $S treeput_extra 300 python3 -u bench.py --only-extra tree_put || exit 99 ;;
