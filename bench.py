@@ -1361,6 +1361,12 @@ def extra_oneshot_crossover(rank, world, emit=None):
                                     "LFA_OS_RS_BYTES": os.environ.get("LFA_OS_RS_BYTES")},
            "defaults": {"LFA_OS_AG_BYTES": 2 << 20, "LFA_OS_RS_BYTES": 4 << 20},
            "tuned_on": "2-4 processes sharing one MI355X (DESIGN.md §5b)"}
+    # the second child of the pair runs with both bounds at 1 byte: there
+    # LFA_ALGO_P2P is the two-barrier schedule at every size, AUTO's bulk
+    # choice since round 6 (LFA_AUTO_BULK) — timed as "p2p_bulk"
+    bulk = os.environ.get("LFA_OS_AG_BYTES") == "1"
+    algos = ((("p2p_bulk", coll.ALGO_P2P),) if bulk else
+             (("tree", coll.ALGO_TREE), ("oneshot", coll.ALGO_P2P)))
     ep = _provider_ep(rank, world)
     try:
         for coll_name, sizes in (("allreduce", (16 << 10, 64 << 10, 256 << 10, 1 << 20,
@@ -1387,7 +1393,7 @@ def extra_oneshot_crossover(rank, world, emit=None):
                 torch.cuda.synchronize()
                 row = {}
                 reps = 30 if nbytes <= (1 << 20) else 10
-                for name, algo in (("tree", coll.ALGO_TREE), ("oneshot", coll.ALGO_P2P)):
+                for name, algo in algos:
                     try:
                         ep.set_algo(algo)
                         ep.wait(op())
@@ -1418,6 +1424,37 @@ def extra_oneshot_crossover(rank, world, emit=None):
     finally:
         ep.close()
     return out
+
+
+def merge_crossover(out: dict, bulk: dict, world: int) -> None:
+    """Fold the bulk child's P2P two-barrier times into the crossover rows
+    and set `suggested_bound` against AUTO's choice above the bounds
+    (LFA_AUTO_BULK: p2p by default, so the one-shot is priced against the
+    two-barrier schedule; the tree when it is set to "tree")."""
+    from libfabric_amd import coll
+    if not isinstance(out, dict) or not isinstance(bulk, dict):
+        return
+    if "isolated_status" in bulk:
+        out["bulk_isolated_status"] = bulk["isolated_status"]
+    alt = "p2p_bulk" if coll.auto_bulk() == coll.ALGO_P2P else "tree"
+    out["auto_above_bound"] = alt
+    for name in ("allreduce", "reduce_scatter"):
+        rows = (out.get(name) or {}).get("by_bucket_bytes_per_rank")
+        brows = (bulk.get(name) or {}).get("by_bucket_bytes_per_rank") or {}
+        if not rows:
+            continue
+        win, lost = 0, False
+        for size in sorted(rows, key=int):
+            if "p2p_bulk_us" in brows.get(size, {}):
+                rows[size]["p2p_bulk_us"] = brows[size]["p2p_bulk_us"]
+            other = rows[size].get(alt + "_us")
+            if not lost and other is not None and rows[size].get("oneshot_us", 1e30) < other:
+                win = int(size)
+            else:
+                lost = True
+        out[name]["oneshot_wins_up_to_bytes_per_rank"] = win
+        out[name]["suggested_bound"] = win * world if name == "allreduce" else win
+        out[name]["priced_against"] = alt
 
 
 def extra_collectives(rank, world, stream, emit=None):
@@ -2174,6 +2211,16 @@ def main() -> None:
                     ex["oneshot_crossover"] = res.get("oneshot_crossover", res)
                     if "isolated_status" in res:
                         ex["oneshot_crossover"]["isolated_status"] = res["isolated_status"]
+                    # the same buckets through P2P's two-barrier schedule
+                    # (both bounds at 1 byte), AUTO's choice above the bounds
+                    budget = args.extras_timeout - (time.time() - t_extras) - 20.0
+                    if budget > 20.0:
+                        bres = run_isolated(
+                            [sys.executable, os.path.abspath(__file__), "--gpus", str(world),
+                             "--only-extra", "crossover"], rank, world, budget,
+                            {"LFA_OS_AG_BYTES": "1", "LFA_OS_RS_BYTES": "1"})
+                        merge_crossover(ex["oneshot_crossover"],
+                                        bres.get("oneshot_crossover", bres), world)
             elif not args.no_extras_coll:
                 ex.update(extra_collectives(rank, world, stream))
         except Exception as e:  # noqa: BLE001 — extras must not hide the metric

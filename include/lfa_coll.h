@@ -87,21 +87,27 @@ enum lfa_coll_algo {
 	/* the default on device domains: per operation, LFA_ALGO_P2P's
 	 * one-kernel path for small buckets (allreduce / reduce of <= 2 MiB
 	 * summed over the members, reduce_scatter of <= 4 MiB, 2..8 members)
-	 * and LFA_ALGO_TREE above.  The choice depends only on (collective,
-	 * count, members, datatype size) — lfa_coll_auto_algo — and on the
-	 * group's P2P state, itself agreed by every member: the first small
-	 * bucket sets up the IPC workspaces with a MIN agreement over the
-	 * members, and if any member cannot map a peer's workspace every member
-	 * runs TREE from then on.  Same bits either way.  Peer domains run
-	 * LFA_ALGO_TREE. */
+	 * and, above them, LFA_ALGO_P2P's two-barrier schedule for groups of
+	 * 2..32 (since round 6; lfa_coll_auto_bulk, LFA_AUTO_BULK=tree for
+	 * LFA_ALGO_TREE as in rounds 3-5).  The choice depends only on
+	 * (collective, count, members, datatype size) — lfa_coll_auto_algo —
+	 * and on the group's P2P state, itself agreed by every member: the
+	 * first P2P operation sets up the IPC workspaces with a MIN agreement
+	 * over the members, and if any member cannot map a peer's workspace
+	 * every member runs TREE from then on.  Same bits either way.  Peer
+	 * domains run LFA_ALGO_TREE. */
 	LFA_ALGO_AUTO = 5,
 };
 
 /* LFA_ALGO_AUTO's choice for one operation: LFA_ALGO_P2P or LFA_ALGO_TREE.
  * p2p_ok: the group's agreed P2P state (0 once the workspace agreement
- * failed).  Pure; every member computes the same. */
+ * failed).  Pure; every member computes the same (LFA_AUTO_BULK must agree
+ * across the members, as every knob that shapes a schedule). */
 int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
 		       size_t esz, int p2p_ok);
+/* AUTO's choice above the one-shot bounds: LFA_ALGO_P2P (default) or
+ * LFA_ALGO_TREE (LFA_AUTO_BULK=tree, FI_OFF_LFA_AUTO_BULK). */
+int lfa_coll_auto_bulk(void);
 
 /* ---- bootstrap (replaces fi_getinfo/fi_fabric/fi_domain/fi_endpoint
  *      and AV insertion for this path) ---------------------------------- */

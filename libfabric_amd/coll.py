@@ -144,6 +144,8 @@ def lib() -> ctypes.CDLL:
     L.lfa_coll_ep_set_group_chunk.argtypes = [c_void_p, c_size_t]
     L.lfa_coll_auto_algo.restype = c_int
     L.lfa_coll_auto_algo.argtypes = [c_int, c_size_t, c_int, c_size_t, c_int]
+    L.lfa_coll_auto_bulk.restype = c_int
+    L.lfa_coll_auto_bulk.argtypes = []
     L.lfa_coll_member_chunk.restype = c_size_t
     L.lfa_coll_member_chunk.argtypes = [c_int, c_int, c_size_t, c_size_t]
     L.lfa_coll_group_chunk.restype = c_size_t
@@ -262,6 +264,12 @@ def plan(coll: int, algo: int, rank: int, nranks: int, root: int, count: int,
 def auto_algo(coll: int, count: int, nranks: int, esz: int, p2p_ok: bool = True) -> int:
     """lfa_coll_auto_algo: LFA_ALGO_AUTO's choice for one operation."""
     return lib().lfa_coll_auto_algo(coll, count, nranks, esz, int(p2p_ok))
+
+
+def auto_bulk() -> int:
+    """lfa_coll_auto_bulk: AUTO's choice above the one-shot bounds
+    (ALGO_P2P by default, ALGO_TREE with LFA_AUTO_BULK=tree)."""
+    return lib().lfa_coll_auto_bulk()
 
 
 def group_chunk(setting: int, nranks: int, nbytes: int) -> int:

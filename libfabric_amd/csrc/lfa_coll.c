@@ -770,21 +770,46 @@ static int rccl_op(enum lfa_op op, ncclRedOp_t *o)
 	}
 }
 
+/*
+ * LFA_ALGO_AUTO above the one-shot bounds (LFA_AUTO_BULK, round 6): the P2P
+ * two-barrier schedule (default) or the tree.  A device domain's members sit
+ * on distinct GPUs (RCCL takes one rank per device), here the 8 of an xGMI
+ * mesh: the P2P schedule pulls every other member's block of the input and
+ * pushes the reduced block back, about 2·S/n over each link, where the tree
+ * (prov/coll's recursive doubling) sends the whole S over one link in each
+ * of its log2(n) rounds — and both reduce in the same order, bit for bit
+ * (DESIGN.md §6b).  Provisional until the driver's 8-GPU run prices it:
+ * LFA_AUTO_BULK=tree restores the rounds-3-5 choice.
+ */
+int lfa_coll_auto_bulk(void)
+{
+	static int v = -1;
+
+	if (v < 0) {
+		const char *e = lfa_param("LFA_AUTO_BULK");
+
+		v = e && !strcmp(e, "tree") ? LFA_ALGO_TREE : LFA_ALGO_P2P;
+	}
+	return v;
+}
+
 int lfa_coll_auto_algo(enum lfa_collective_op coll, size_t count, int nranks,
 		       size_t esz, int p2p_ok)
 {
 	const size_t bytes = count * esz;
+	const int os = nranks <= LFA_OS_MAX_RANKS;
+	int bulk;
 
-	if (!p2p_ok || nranks < 2 || nranks > LFA_OS_MAX_RANKS || !count)
+	if (!p2p_ok || nranks < 2 || nranks > LFA_SIG_MAX || !count)
 		return LFA_ALGO_TREE;
+	bulk = lfa_coll_auto_bulk();
 	switch (coll) {
 	case LFA_ALLREDUCE:
 	case LFA_REDUCE:
 		/* the planner's one-shot rule (plan_p2p): one kernel */
-		return bytes * (size_t)nranks <= lfa_os_ag_bytes() ? LFA_ALGO_P2P :
-								     LFA_ALGO_TREE;
+		return os && bytes * (size_t)nranks <= lfa_os_ag_bytes() ? LFA_ALGO_P2P : bulk;
 	case LFA_REDUCE_SCATTER:
-		return bytes <= lfa_os_rs_bytes() ? LFA_ALGO_P2P : LFA_ALGO_TREE;
+		return os && bytes <= lfa_os_rs_bytes() ? LFA_ALGO_P2P : bulk;
 	default:
 		return LFA_ALGO_TREE;
 	}

@@ -92,6 +92,8 @@ static const struct olfa_param {
 	  "allreduce/reduce buckets up to this many bytes summed over the members run as one one-shot kernel (default 2 MiB; provisional)" },
 	{ "oneshot_rs_bytes", FI_PARAM_SIZE_T, "LFA_OS_RS_BYTES",
 	  "reduce_scatter buckets up to this many bytes per member run as one one-shot kernel (default 4 MiB; provisional)" },
+	{ "auto_bulk", FI_PARAM_STRING, "LFA_AUTO_BULK",
+	  "algo auto above the one-shot bounds: p2p (default: the two-barrier schedule over the xGMI mesh, the tree's bits) or tree; provisional" },
 	{ "group_chunk_bytes", FI_PARAM_SIZE_T, "LFA_GROUP_CHUNK_BYTES",
 	  "chunk every member of a group splits large operations into (0 off; default: 32 MiB chunks from 64 MiB per member)" },
 	{ "stage_pool_bytes", FI_PARAM_SIZE_T, "LFA_STAGE_POOL_BYTES",

@@ -219,3 +219,37 @@ def test_isolated_extras_child_job(mode):
     else:
         assert "overran" in out0["isolated_status"] or "stopped" in out0["isolated_status"]
         assert max(dt0, dt1) < 40
+
+
+def test_crossover_prices_the_one_shot_against_autos_bulk_choice():
+    """The N > 1 crossover: the one-shot child's
+    tree / one-shot times and the bulk child's P2P two-barrier times per
+    bucket are merged, and `suggested_bound` is the largest bucket up to
+    which the one-shot beats what AUTO runs above the bound — the two-barrier
+    schedule by default (LFA_AUTO_BULK), not the tree."""
+    out = {"allreduce": {"by_bucket_bytes_per_rank": {
+               "16384": {"tree_us": 30.0, "oneshot_us": 9.0},
+               "65536": {"tree_us": 40.0, "oneshot_us": 14.0},
+               "262144": {"tree_us": 60.0, "oneshot_us": 20.0}}},
+           "reduce_scatter": {"by_bucket_bytes_per_rank": {
+               "65536": {"tree_us": 30.0, "oneshot_us": 11.0},
+               "262144": {"tree_us": 9.0, "oneshot_us": 12.0}}}}
+    bulk = {"allreduce": {"by_bucket_bytes_per_rank": {
+                "16384": {"p2p_bulk_us": 12.0}, "65536": {"p2p_bulk_us": 13.0},
+                "262144": {"p2p_bulk_us": 15.0}}},
+            "reduce_scatter": {"by_bucket_bytes_per_rank": {
+                "65536": {"p2p_bulk_us": 12.0}, "262144": {"p2p_bulk_us": 13.0}}},
+            "isolated_status": "ok"}
+    bench.merge_crossover(out, bulk, 8)
+    assert out["auto_above_bound"] == "p2p_bulk"
+    ar, rs = out["allreduce"], out["reduce_scatter"]
+    assert ar["by_bucket_bytes_per_rank"]["65536"]["p2p_bulk_us"] == 13.0
+    # allreduce: the one-shot wins at 16 KiB only (14 > 13 at 64 KiB), although
+    # it beats the tree everywhere; the knob is summed over the 8 members
+    assert ar["oneshot_wins_up_to_bytes_per_rank"] == 16384
+    assert ar["suggested_bound"] == 8 * 16384 and ar["priced_against"] == "p2p_bulk"
+    # reduce_scatter: the one-shot beats the two-barrier schedule at 256 KiB
+    # too (12 < 13), even where the tree is faster still
+    assert rs["oneshot_wins_up_to_bytes_per_rank"] == 262144
+    assert rs["suggested_bound"] == 262144
+    assert out["bulk_isolated_status"] == "ok"

@@ -502,8 +502,10 @@ def test_auto_algo_same_choice_on_every_member(n):
     datatype size) and the group's agreed P2P state only — no rank-local
     input — so every member of N = 1..10 selects the same algorithm; and the
     algorithm it picks for a small bucket is exactly the one-kernel path:
-    every member's P2P schedule is ONE one-shot step.  Above the thresholds,
-    outside 2..8 members, or once the P2P agreement failed: the tree."""
+    every member's P2P schedule is ONE one-shot step.  Above the thresholds
+    (round 6, LFA_AUTO_BULK's default): P2P's two-barrier schedule for 2..32
+    members, with no one-shot step in it.  Allgather, one member, or once the
+    P2P agreement failed: the tree."""
     for kind, esz in ((ALLREDUCE, 4), (REDUCE, 8), (REDUCE_SCATTER, 8), (ALLGATHER, 4)):
         for count in (1, 1000, OS_AG_BYTES // (4 * max(n, 1)), OS_AG_BYTES // (4 * max(n, 1)) + 1,
                       OS_RS_BYTES // 8, OS_RS_BYTES // 8 + 1, 1 << 24):
@@ -511,13 +513,50 @@ def test_auto_algo_same_choice_on_every_member(n):
             nb = count * esz
             small = (nb * n <= OS_AG_BYTES if kind in (ALLREDUCE, REDUCE) else
                      nb <= OS_RS_BYTES if kind == REDUCE_SCATTER else False)
-            want = coll.ALGO_P2P if (2 <= n <= 8 and small) else coll.ALGO_TREE
+            reducing = kind in (ALLREDUCE, REDUCE, REDUCE_SCATTER)
+            one_shot = 2 <= n <= 8 and small
+            want = coll.ALGO_P2P if (reducing and 2 <= n <= 32) else coll.ALGO_TREE
             assert a == want, (kind, count, n, esz)
             assert coll.auto_algo(kind, count, n, esz, p2p_ok=False) == coll.ALGO_TREE
             if a == coll.ALGO_P2P:
                 for r in range(n):
                     p = coll.plan(kind, a, r, n, n - 1 if kind == REDUCE else -1, count, esz)
-                    assert [s["type"] for s in p.steps] == [coll.STEP_ONESHOT], (kind, n, r)
+                    types = [s["type"] for s in p.steps]
+                    if one_shot:
+                        assert types == [coll.STEP_ONESHOT], (kind, n, r)
+                    else:
+                        assert coll.STEP_ONESHOT not in types and coll.STEP_BARRIER in types, \
+                            (kind, count, n, r, types)
+
+
+def test_auto_bulk_knob():
+    """LFA_AUTO_BULK (FI_OFF_LFA_AUTO_BULK): AUTO above the one-shot bounds
+    takes P2P's two-barrier schedule by default and the tree with "tree";
+    the one-shot-sized buckets stay P2P either way.  Read once per process,
+    so each setting runs in its own interpreter."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import json\n"
+        "from libfabric_amd import coll\n"
+        "print(json.dumps([coll.auto_algo(3, c, 8, 4) for c in (1024, 1 << 22, 1 << 26)]"
+        " + [coll.auto_algo(5, c, 8, 8) for c in (1024, 1 << 22)]))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(val):
+        e = {k: v for k, v in os.environ.items() if k != "LFA_AUTO_BULK"}
+        if val is not None:
+            e["LFA_AUTO_BULK"] = val
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, env=e, check=True,
+                             capture_output=True, text=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+
+    P2P, TREE = coll.ALGO_P2P, coll.ALGO_TREE
+    assert run(None) == [P2P, P2P, P2P, P2P, P2P]
+    assert run("p2p") == [P2P, P2P, P2P, P2P, P2P]
+    assert run("tree") == [P2P, TREE, TREE, P2P, TREE]
 
 
 def test_one_shot_bounds_follow_their_knobs():
@@ -540,6 +579,9 @@ def test_one_shot_bounds_follow_their_knobs():
     def run(env):
         e = {k: v for k, v in os.environ.items()
              if k not in ("LFA_OS_AG_BYTES", "LFA_OS_RS_BYTES")}
+        # the bounds alone: above them the tree (test_auto_bulk_knob covers
+        # AUTO's bulk default)
+        e["LFA_AUTO_BULK"] = "tree"
         e.update(env)
         out = subprocess.run([sys.executable, "-c", code], cwd=root, env=e, check=True,
                              capture_output=True, text=True).stdout
