@@ -1436,13 +1436,17 @@ def merge_crossover(out: dict, bulk: dict, world: int) -> None:
         return
     if "isolated_status" in bulk:
         out["bulk_isolated_status"] = bulk["isolated_status"]
-    alt = "p2p_bulk" if coll.auto_bulk() == coll.ALGO_P2P else "tree"
-    out["auto_above_bound"] = alt
+    auto = "p2p_bulk" if coll.auto_bulk() == coll.ALGO_P2P else "tree"
+    out["auto_above_bound"] = auto
     for name in ("allreduce", "reduce_scatter"):
         rows = (out.get(name) or {}).get("by_bucket_bytes_per_rank")
         brows = (bulk.get(name) or {}).get("by_bucket_bytes_per_rank") or {}
         if not rows:
             continue
+        # without the bulk child's times (it failed or ran out of budget)
+        # the first child's pricing against the tree stands
+        alt = auto if auto == "tree" or any("p2p_bulk_us" in r for r in brows.values()) \
+            else "tree"
         win, lost = 0, False
         for size in sorted(rows, key=int):
             if "p2p_bulk_us" in brows.get(size, {}):

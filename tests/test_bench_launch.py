@@ -253,3 +253,17 @@ def test_crossover_prices_the_one_shot_against_autos_bulk_choice():
     assert rs["oneshot_wins_up_to_bytes_per_rank"] == 262144
     assert rs["suggested_bound"] == 262144
     assert out["bulk_isolated_status"] == "ok"
+
+
+def test_crossover_keeps_the_tree_pricing_without_the_bulk_child():
+    """A bulk child that failed (no two-barrier rows) leaves the first
+    child's tree-priced bound as it was, with its status on the line."""
+    out = {"allreduce": {"by_bucket_bytes_per_rank": {
+               "16384": {"tree_us": 30.0, "oneshot_us": 9.0},
+               "65536": {"tree_us": 40.0, "oneshot_us": 14.0}}}}
+    bench.merge_crossover(out, {"isolated_status": "rank 1: child exited with code 1"}, 4)
+    ar = out["allreduce"]
+    assert ar["priced_against"] == "tree"
+    assert ar["oneshot_wins_up_to_bytes_per_rank"] == 65536
+    assert ar["suggested_bound"] == 4 * 65536
+    assert out["bulk_isolated_status"].startswith("rank 1")
