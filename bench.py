@@ -1660,7 +1660,8 @@ def extra_collectives(rank, world, stream, emit=None):
             ep.set_algo(coll.ALGO_TREE)
             emit(out)
             # the device-domain default (LFA_ALGO_AUTO): one-shot P2P for
-            # small buckets, TREE above — the chosen algorithm per bucket
+            # small buckets, P2P's two-barrier schedule above (LFA_AUTO_BULK;
+            # TREE before round 6) — the chosen algorithm per bucket
             try:
                 out["reduce_scatter_double_prod_auto"] = _rs_sweep(ep, rank, world,
                                                                    coll.ALGO_AUTO, egress)
