@@ -219,4 +219,54 @@ __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds(F f, size_t nvec) {
   }
 }
 
+// The drained fetch body with a tapered tail (round 6): the
+// combine's taper (combine_lds_taper) applied to the fetch / compare kernel.
+// Workgroups [0, head) run the drained U-KiB tiles up to vector `split`; the
+// rest — dispatched last — take UT-KiB tiles, so the waves that end the
+// launch are short ones.  The product runs it from kSc1Bytes (launch_fetch).
+template <int U, int UT, int SAUX, typename F>
+__global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds_taper(F f, size_t nvec,
+                                                                 size_t split, unsigned head) {
+  __shared__ u32x4 lds[F::kIn][kLdsWaves][U][64];
+  const unsigned w = wave_id(), l = threadIdx.x % 64, b = blockIdx.x;
+  if (b < head) {
+    // split is a multiple of a workgroup's tile: every head tile is whole
+    const size_t base = (size_t)b * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int k = 0; k < F::kIn; k++)
+        __builtin_amdgcn_global_load_lds((const void *)(f.in(k) + base + u * 64 + l),
+                                         (lds_void *)&lds[k][w][u][0], 16, 0, 2);
+    fetch_drain<U, SAUX, F, 0>(
+        f, lds, w, l, base,
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * U * 16, 0x00020000),
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * U * 16, 0x00020000));
+    return;
+  }
+  const size_t base = split + (size_t)(b - head) * (kLdsWaves * 64 * UT) + (size_t)w * 64 * UT;
+  if (base + 64 * UT <= nvec) {
+#pragma unroll
+    for (int u = 0; u < UT; u++)
+#pragma unroll
+      for (int k = 0; k < F::kIn; k++)
+        __builtin_amdgcn_global_load_lds((const void *)(f.in(k) + base + u * 64 + l),
+                                         (lds_void *)&lds[k][w][u][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < UT; u++) {
+      const u32x4 a = lds[0][w][u][l];
+      const u32x4 bb = F::kIn > 1 ? lds[F::kIn > 1 ? 1 : 0][w][u][l] : a;
+      const u32x4 c = F::kIn > 2 ? lds[F::kIn > 2 ? 2 : 0][w][u][l] : a;
+      st<true>(f.rv + base + u * 64 + l, a);
+      if constexpr (F::kWriteDst) st<true>(f.dv + base + u * 64 + l, f.op(a, bb, c));
+    }
+  } else {
+    for (int u = 0; u < UT; u++) {
+      const size_t i = base + (size_t)u * 64 + l;
+      if (i < nvec) f.vec(i);
+    }
+  }
+}
+
 }  // namespace lfa

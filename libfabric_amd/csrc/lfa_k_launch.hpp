@@ -622,13 +622,24 @@ static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
     // readwrite pair (tools/probe_fetch.py --tune, profiles/r06_tune_fetch_*.jsonl);
     // cmp loaded into VGPRs instead of LDS (5 workgroups per CU instead of 3)
     // measured 213.7 us, no better.
+    // From kSc1Bytes the last quarter of the vectors goes to 1-KiB tiles
+    // (fetch_lds_taper, tune variant 17): 256 MiB float SUM readwrite
+    // 167.0-167.3 -> 165.0-166.5 us, float CSWAP 215.6-215.9 -> 213.0-214.9 us,
+    // three interleaved runs of 20 rounds on one box; UT 1 / 2 with the last
+    // 1/16 .. 1/2 tapered measured within that (profiles/r06_tune_fetch_taper_*.jsonl).
     constexpr int U = 4;
     constexpr bool D = FF::kIn == 2;
     const dim3 grid(grid_for(nvec, (size_t)kLdsWaves * 64 * U, 0x7fffffffu));
     const bool nt = nvec * 16 >= kSc1Bytes;
-    if (nt)
-      hipLaunchKernelGGL((fetch_lds<U, kStoreNt, FF, true>), grid, dim3(kLdsWaves * 64), 0, s,
-                         f, nvec);
+    if (nt) {
+      constexpr size_t hv = (size_t)kLdsWaves * 64 * U, tv = (size_t)kLdsWaves * 64;
+      size_t split = nvec - nvec / 4;
+      split -= split % hv;
+      const unsigned nhead = (unsigned)(split / hv);
+      const unsigned ntail = (unsigned)((nvec - split + tv - 1) / tv);
+      hipLaunchKernelGGL((fetch_lds_taper<U, 1, kStoreNt, FF>), dim3(nhead + ntail),
+                         dim3(kLdsWaves * 64), 0, s, f, nvec, split, nhead);
+    }
     if (nvec && !nt)
       hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF, D>), grid, dim3(kLdsWaves * 64), 0, s,
                          f, nvec);

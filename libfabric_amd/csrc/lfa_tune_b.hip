@@ -67,7 +67,8 @@ __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds3r(F f, size_t nvec) 
 // readwrite (swap = 0) or float CSWAP (swap = 1) over nvec co-aligned 16-B
 // vectors.  0 = the round-1 register form (fetch_vec, 2 vectors per lane),
 // 1..3 = fetch_lds U = 4 / 2 / 1 with nt stores, 4..5 = U = 4 / 2 with sc1
-// write-through stores, 6 / 7 = U = 4 drained step by step (sc1 / nt).
+// write-through stores, 6 / 7 = U = 4 drained step by step (sc1 / nt),
+// 12 / 13 drained nt U = 2 / 3, 14..17 drained nt U = 4 with a tapered tail.
 // ---------------------------------------------------------------------------
 extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void *src,
                                    const void *cmp, void *res, size_t nvec,
@@ -105,6 +106,27 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
       case 7: lds(I4(), NT(), YES()); break;
       case 12: lds(I2(), NT(), YES()); break;   // drained nt, U = 2 / 3
       case 13: lds(std::integral_constant<int, 3>(), NT(), YES()); break;
+      case 14: case 15: case 16: case 17: case 18: case 19: {
+        // drained nt U = 4 with a tapered tail (fetch_lds_taper, lfa_k_fetch.hpp;
+        // 17 is the product's form from kSc1Bytes since round 6): the last 1/div of the
+        // vectors in UT-KiB tiles (14: UT 1, div 8; 15: UT 2, div 8;
+        // 16: UT 1, div 16; 17: UT 1, div 4; 18: UT 1, div 2; 19: UT 2, div 4)
+        const size_t div = variant == 16 ? 16 : variant == 17 || variant == 19 ? 4 :
+                           variant == 18 ? 2 : 8;
+        auto taper = [&](auto ut) {
+          constexpr int UT = decltype(ut)::value;
+          const size_t hv = (size_t)kLdsWaves * 64 * 4, tv = (size_t)kLdsWaves * 64 * UT;
+          size_t split = nvec - nvec / div;
+          split -= split % hv;
+          const unsigned head = (unsigned)(split / hv);
+          const unsigned tail = (unsigned)((nvec - split + tv - 1) / tv);
+          hipLaunchKernelGGL((fetch_lds_taper<4, UT, kStoreNt, FF>), dim3(head + tail),
+                             dim3(kLdsWaves * 64), 0, s, f, nvec, split, head);
+        };
+        if (variant == 15 || variant == 19) taper(I2());
+        else taper(I1());
+        break;
+      }
       case 8: case 9: case 10: case 11:   // compare: cmp in registers
         if constexpr (FF::kIn == 3) {
           auto r3 = [&](auto u, auto aux) {

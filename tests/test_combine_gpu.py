@@ -388,8 +388,9 @@ def test_fetch_compare_nt_path(lfa, table, op, dt):
     nt-store drained body (round 6 moved the three-input compare there too):
     float SUM / double ATOMIC_READ / int64 BAND readwrite and float CSWAP /
     double CSWAP_GE / int64 MSWAP at 200 MiB + a ragged tail, against the
-    oracle on windows at both ends, the middle and across the last tile.
-    cmp equals dst on half the lanes, so both outcomes of every compare run."""
+    oracle on windows at both ends, the middle, across the tapered tail's
+    first tile (round 6) and across the last tile.  cmp equals dst on half
+    the lanes, so both outcomes of every compare run."""
     nd = oracle.DT_NP[dt]
     e = nd.itemsize
     n = ((200 << 20) + 4 * 1000 + e * 3) // e
@@ -410,7 +411,10 @@ def test_fetch_compare_nt_path(lfa, table, op, dt):
         lfa.swap(op, dt, d, sv, cm, res, n)
     torch.cuda.synchronize()
     tile = 16 * 1024 // e
-    for lo in (0, n // 2, (n // tile - 1) * tile - 777, n - 5000):
+    # ... and across the tapered tail's start (round 6: the last quarter of
+    # the vectors in 1-KiB tiles, from a 16-KiB tile boundary below 3/4)
+    for lo in (0, n // 2, 3 * n // 4 - 5000, 3 * n // 4 - 2500,
+               (n // tile - 1) * tile - 777, n - 5000):
         hi = min(n, lo + 5000)
         wd = d0[lo:hi].cpu().numpy().copy()
         wr = np.empty_like(wd)

@@ -76,7 +76,7 @@ def tune():
                 for _ in range(2)]
         for t in sets:                      # cmp == dst on half the lanes
             t[3][::2] = t[0][::2]
-        vs = [v for v in variants if swap or v < 8]    # 8..11: compare only
+        vs = [v for v in variants if swap or not 8 <= v <= 11]    # 8..11: compare only
         ref = None
         for v in vs:                        # correctness on a fresh copy
             d, sr, c, r = (x.clone() for x in sets[0])
@@ -89,7 +89,7 @@ def tune():
                 raise SystemExit(f"fetch variant {v} swap={swap} WRONG")
         del ref
         times = {v: [] for v in vs}
-        for _ in range(8):
+        for _ in range(int(os.environ.get("FETCH_ROUNDS", "8"))):
             for v in vs:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
