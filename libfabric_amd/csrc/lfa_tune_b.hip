@@ -555,6 +555,51 @@ static void launch_taper(u32x4 *d, const u32x4 *v, size_t nvec, unsigned tail_di
                        dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
 }
 
+// The product's drained nt body (combine_lds<..., DRAIN>) with a tapered tail
+// (round 6): round 4's taper variants 85-89 ran their head tiles on the
+// undrained body, so their +1 % at 256 MiB mixed two changes; the fetch
+// kernel's drained head + 1-KiB tail at div 4 gained ~1 % (fetch_lds_taper).
+template <int U, int SAUX>
+__global__ __launch_bounds__(kLdsWaves * 64) void combine_taper_drained(
+    u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, size_t nvec, size_t split,
+    unsigned head_blocks) {
+  __shared__ u32x4 lds[2][kLdsWaves][U][64];
+  const unsigned w = wave_id<true>(), l = threadIdx.x % 64;
+  const unsigned b = blockIdx.x;
+  if (b < head_blocks) {
+    const size_t base = (size_t)b * (kLdsWaves * 64 * U) + (size_t)w * 64 * U;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      __builtin_amdgcn_global_load_lds((const void *)(dst + base + u * 64 + l),
+                                       (lds_void *)&lds[0][w][u][0], 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(src + base + u * 64 + l),
+                                       (lds_void *)&lds[1][w][u][0], 16, 0, 2);
+    }
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, 64 * U * 16, 0x00020000);
+    combine_drain<OP_SUM, float, U, SAUX, 0>(lds, w, l, dst + base, r);
+    return;
+  }
+  taper_tile<U, 1, SAUX>(dst, src, nvec,
+                         split + (size_t)(b - head_blocks) * (kLdsWaves * 64) + (size_t)w * 64,
+                         lds, w, l);
+}
+
+static void launch_taper_drained(u32x4 *d, const u32x4 *v, size_t nvec, size_t div,
+                                 hipStream_t s) {
+  const size_t hv = (size_t)kLdsWaves * 64 * 4, tv = (size_t)kLdsWaves * 64;
+  size_t split = nvec - nvec / div;
+  split -= split % hv;
+  const unsigned head = (unsigned)(split / hv);
+  const unsigned tail = (unsigned)((nvec - split + tv - 1) / tv);
+  if (nvec * 16 < kSc1Bytes)
+    hipLaunchKernelGGL((combine_taper_drained<4, kStoreSc1>), dim3(head + tail),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
+  else
+    hipLaunchKernelGGL((combine_taper_drained<4, kStoreNt>), dim3(head + tail),
+                       dim3(kLdsWaves * 64), 0, s, d, v, nvec, split, head);
+}
+
 // Statically balanced resident grid: exactly one round of
 // workgroups (the occupancy limit per CU times the CUs, so the dispatcher
 // gives every CU the same number), each wave owning a contiguous run of
@@ -788,6 +833,9 @@ extern "C" int lfa__tune3_sum_f32(int variant, void *dst, const void *src, size_
     case 95: lfa::launch_static_pipe<2>(d, v, nvec, 1, s); break;
     case 96: lfa::launch_static_pipe<4>(d, v, nvec, 1, s); break;
     case 97: lfa::launch_static_pipe<1>(d, v, nvec, 1, s); break;
+    // the drained body with a 1-KiB tapered tail: the last 1/4 (98), 1/8 (99)
+    case 98: lfa::launch_taper_drained(d, v, nvec, 4, s); break;
+    case 99: lfa::launch_taper_drained(d, v, nvec, 8, s); break;
     case 85: lfa::launch_taper<4, 2>(d, v, nvec, 8, s); break;
     case 86: lfa::launch_taper<4, 2>(d, v, nvec, 4, s); break;
     case 87: lfa::launch_taper<4, 1>(d, v, nvec, 8, s); break;
