@@ -770,6 +770,46 @@ __global__ __launch_bounds__(NW * 64) void tp_r5(PutArgs a, size_t nvec) {
   }
 }
 
+// Round 6: the product's wide fan-out form (U = 2 KiB per input per wave,
+// one workgroup per CU through the dynamic LDS it reserves, the product's
+// cache policy) with a tapered tail: workgroups past `head` take 1-KiB tiles
+// from vector `split` on, so the waves that end the launch are short — the
+// form that gained ~1 % on the five-stream compare kernel (fetch_lds_taper).
+template <int U>
+__device__ __forceinline__ void tp_tile(const PutArgs &a, size_t wbase, size_t lim,
+                                        unsigned l) {
+  if (wbase >= lim) return;
+  const size_t left = lim - wbase;
+  const unsigned bytes = (unsigned)((left < 64 * U ? left : 64 * U) * 16);
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const unsigned off = (unsigned)(u * 64 + l) * 16;
+    v[u] = tree_eval_with<OP_SUM, float, u32x4, 8>(a.t, [&](int k) {
+      return __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     tile_rsrc((const u32x4 *)a.t.in[k] + wbase, bytes), off, 0, kSysLoadAux));
+    });
+  }
+  for (int j = 0; j < a.nout; j++) {
+    __amdgpu_buffer_rsrc_t r = tile_rsrc((u32x4 *)a.out[j] + wbase, bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[u]), r,
+                                             (unsigned)(u * 64 + l) * 16, 0, kSysAux);
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void tp_taper(PutArgs a, size_t nvec, size_t split,
+                                                   unsigned head) {
+  const unsigned b = blockIdx.x, w = wave_id<true>(), l = threadIdx.x % 64;
+  if (b < head)
+    tp_tile<U>(a, (size_t)b * (kBlock * U) + (size_t)w * 64 * U, split, l);
+  else
+    tp_tile<1>(a, split + (size_t)(b - head) * kBlock + (size_t)w * 64, nvec, l);
+}
+
 // Round 5: a resident grid whose waves walk tiles strided by the number of
 // waves and keep the NEXT tile's loads in flight while they reduce and
 // store the current one (two register buffers, ping-pong), so a wave's store
@@ -996,6 +1036,16 @@ extern "C" int lfa__tune_treeput_f32(int variant, void *const *dsts, int ndst,
     case 57: TPX(4, 17, 8); break;
     case 58: TPX(4, 19, 1); break;        // G = 1: the remap alone
 #undef TPX
+    case 64: case 65: {                   // the wide form with a 1-KiB tail: 1/4, 1/8
+      const size_t div = variant == 64 ? 4 : 8, hv = (size_t)kBlock * 2;
+      size_t split = nvec - nvec / div;
+      split -= split % hv;
+      const unsigned head = (unsigned)(split / hv);
+      const unsigned tail = (unsigned)((nvec - split + kBlock - 1) / kBlock);
+      hipLaunchKernelGGL((tp_taper<2>), dim3(head + tail), dim3(kBlock), kPutNarrowLds, s, a,
+                         nvec, split, head);
+      break;
+    }
     default: return -LFA_EINVAL;
   }
 #undef TP
