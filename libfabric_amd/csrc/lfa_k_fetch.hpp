@@ -253,13 +253,24 @@ __global__ __launch_bounds__(kLdsWaves * 64) void fetch_lds_taper(F f, size_t nv
         __builtin_amdgcn_global_load_lds((const void *)(f.in(k) + base + u * 64 + l),
                                          (lds_void *)&lds[k][w][u][0], 16, 0, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(f.rv + base, 0, 64 * UT * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(f.dv + base, 0, 64 * UT * 16, 0x00020000);
 #pragma unroll
     for (int u = 0; u < UT; u++) {
       const u32x4 a = lds[0][w][u][l];
       const u32x4 bb = F::kIn > 1 ? lds[F::kIn > 1 ? 1 : 0][w][u][l] : a;
       const u32x4 c = F::kIn > 2 ? lds[F::kIn > 2 ? 2 : 0][w][u][l] : a;
-      st<true>(f.rv + base + u * 64 + l, a);
-      if constexpr (F::kWriteDst) st<true>(f.dv + base + u * 64 + l, f.op(a, bb, c));
+      if constexpr (SAUX == kStoreNt) {
+        st<true>(f.rv + base + u * 64 + l, a);
+        if constexpr (F::kWriteDst) st<true>(f.dv + base + u * 64 + l, f.op(a, bb, c));
+      } else {
+        const unsigned off = (unsigned)(u * 64 + l) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(a, rr, off, 0, SAUX);
+        if constexpr (F::kWriteDst)
+          __builtin_amdgcn_raw_buffer_store_b128(f.op(a, bb, c), rd, off, 0, SAUX);
+      }
     }
   } else {
     for (int u = 0; u < UT; u++) {

@@ -640,7 +640,22 @@ static int launch_fetch(const void *const *ptrs, int nptr, size_t cnt,
       hipLaunchKernelGGL((fetch_lds_taper<U, 1, kStoreNt, FF>), dim3(nhead + ntail),
                          dim3(kLdsWaves * 64), 0, s, f, nvec, split, nhead);
     }
-    if (nvec && !nt)
+    // Below kSc1Bytes the two-input readwrite takes the same tail from
+    // kFetchTaperBytes, on its write-through drained body (tune variant 21 vs
+    // 6: 64 MiB 39.1 / 38.6 -> 38.5 / 38.4 us, 128 MiB 83.0 -> 81.7 us); the
+    // compare body keeps its undrained form there, which the tapered one
+    // trailed at 64 MiB (48.5 vs 49.5-50.1 us) and tied at 128
+    // (profiles/r06_tune_fetch_taper_sc1.jsonl).
+    constexpr size_t kFetchTaperBytes = (size_t)64 << 20;
+    if (nvec && !nt && FF::kIn == 2 && nvec * 16 >= kFetchTaperBytes) {
+      constexpr size_t hv = (size_t)kLdsWaves * 64 * U, tv = (size_t)kLdsWaves * 64;
+      size_t split = nvec - nvec / 4;
+      split -= split % hv;
+      const unsigned nhead = (unsigned)(split / hv);
+      const unsigned ntail = (unsigned)((nvec - split + tv - 1) / tv);
+      hipLaunchKernelGGL((fetch_lds_taper<U, 1, kStoreSc1, FF>), dim3(nhead + ntail),
+                         dim3(kLdsWaves * 64), 0, s, f, nvec, split, nhead);
+    } else if (nvec && !nt)
       hipLaunchKernelGGL((fetch_lds<U, kStoreSc1, FF, D>), grid, dim3(kLdsWaves * 64), 0, s,
                          f, nvec);
     if (head + tail)

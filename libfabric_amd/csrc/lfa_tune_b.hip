@@ -106,6 +106,19 @@ extern "C" int lfa__tune_fetch_f32(int variant, int swap, void *dst, const void 
       case 7: lds(I4(), NT(), YES()); break;
       case 12: lds(I2(), NT(), YES()); break;   // drained nt, U = 2 / 3
       case 13: lds(std::integral_constant<int, 3>(), NT(), YES()); break;
+      case 20: case 21: {
+        // the write-through (sc1) body with a 1-KiB tapered tail, as the
+        // combine has from 32 MiB: the last 1/8 (20) or 1/4 (21)
+        const size_t div = variant == 20 ? 8 : 4;
+        const size_t hv = (size_t)kLdsWaves * 64 * 4, tv = (size_t)kLdsWaves * 64;
+        size_t split = nvec - nvec / div;
+        split -= split % hv;
+        const unsigned head = (unsigned)(split / hv);
+        const unsigned tail = (unsigned)((nvec - split + tv - 1) / tv);
+        hipLaunchKernelGGL((fetch_lds_taper<4, 1, kStoreSc1, FF>), dim3(head + tail),
+                           dim3(kLdsWaves * 64), 0, s, f, nvec, split, head);
+        break;
+      }
       case 14: case 15: case 16: case 17: case 18: case 19: {
         // drained nt U = 4 with a tapered tail (fetch_lds_taper, lfa_k_fetch.hpp;
         // 17 is the product's form from kSc1Bytes since round 6): the last 1/div of the

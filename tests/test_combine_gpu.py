@@ -381,19 +381,22 @@ def test_nt_store_path_every_op_family(lfa, op, dt):
         assert_parity(dt, d[lo * e:hi * e].cpu().numpy(), want.view(np.uint8), f"[{lo},{hi})")
 
 
+@pytest.mark.parametrize("mib", [200, 80])
 @pytest.mark.parametrize("table,op,dt", [("rw", 2, 8), ("rw", 10, 9), ("rw", 7, 6),
                                          ("swap", 12, 8), ("swap", 16, 9), ("swap", 18, 6)])
-def test_fetch_compare_nt_path(lfa, table, op, dt):
+def test_fetch_compare_nt_path(lfa, table, op, dt, mib):
     """From 192 MiB per operand the fetch and the compare tables run the
     nt-store drained body (round 6 moved the three-input compare there too):
     float SUM / double ATOMIC_READ / int64 BAND readwrite and float CSWAP /
     double CSWAP_GE / int64 MSWAP at 200 MiB + a ragged tail, against the
     oracle on windows at both ends, the middle, across the tapered tail's
     first tile (round 6) and across the last tile.  cmp equals dst on half
-    the lanes, so both outcomes of every compare run."""
+    the lanes, so both outcomes of every compare run.  At 80 MiB (round 6)
+    the write-through bodies: readwrite with the tapered tail from 64 MiB,
+    the compare body untapered."""
     nd = oracle.DT_NP[dt]
     e = nd.itemsize
-    n = ((200 << 20) + 4 * 1000 + e * 3) // e
+    n = ((mib << 20) + 4 * 1000 + e * 3) // e
     g = torch.Generator(device=DEV).manual_seed(op * 11 + dt)
     tdt = {4: torch.float32, 8: torch.float64}.get(e) if nd.kind == "f" else torch.int64
 

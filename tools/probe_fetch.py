@@ -16,7 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from libfabric_amd import atomic  # noqa: E402
 
-S = 256 << 20
+S = int(os.environ.get("FETCH_MIB", "256")) << 20   # bytes per operand
 
 
 def run(name, fn, nbytes_per_launch):
